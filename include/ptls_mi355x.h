@@ -1,0 +1,172 @@
+/*
+ * ptls_mi355x.h -- MI355X (gfx950) AES-GCM engine behind picotls' AEAD slot.
+ *
+ * Drop-in boundary: the picotls crypto-binding ABI, include/picotls.h:308-400 of the
+ * reference (mpiraux/rapido @ 2024-08-07).  The engine exports the same kind of objects
+ * as the x86 "fusion" engine (include/picotls/fusion.h:87-88, lib/fusion.c:974-1005):
+ *
+ *     ptls_aead_algorithm_t   ptls_mi355x_aes128gcm, ptls_mi355x_aes256gcm;
+ *     ptls_cipher_algorithm_t ptls_mi355x_aes128ctr, ptls_mi355x_aes256ctr;
+ *
+ * so the TLS 1.3 record layer (lib/picotls.c:630-654) and through it rapido's TCPLS
+ * send/receive path (lib/rapido.c:2083-2113, 1929-2026) call it unchanged via
+ * ptls_aead_new_direct()/ptls_aead_encrypt()/ptls_aead_decrypt() and the streaming
+ * init/update/final trio.  All slot entry points are synchronous and leave nothing
+ * retained after return, as the slot contract requires.
+ *
+ * Throughput comes from the batch extension (ptls_mi355x_seal_batch/open_batch) which
+ * seals or opens a whole array of independent records resident in GPU memory with one
+ * kernel launch; it is called only by new code (a batched record layer), never by picotls.
+ *
+ * Include picotls.h BEFORE this header when both are used; otherwise this header declares
+ * layout-identical copies of the five picotls types it needs.
+ */
+#ifndef PTLS_MI355X_H
+#define PTLS_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#ifndef picotls_h
+/* ---- picotls crypto-binding ABI (field order and types of include/picotls.h:311-400) ---- */
+typedef struct st_ptls_cipher_context_t {
+    const struct st_ptls_cipher_algorithm_t *algo;
+    void (*do_dispose)(struct st_ptls_cipher_context_t *ctx);
+    void (*do_init)(struct st_ptls_cipher_context_t *ctx, const void *iv);
+    void (*do_transform)(struct st_ptls_cipher_context_t *ctx, void *output, const void *input, size_t len);
+} ptls_cipher_context_t;
+
+typedef const struct st_ptls_cipher_algorithm_t {
+    const char *name;
+    size_t key_size;
+    size_t block_size;
+    size_t iv_size;
+    size_t context_size;
+    int (*setup_crypto)(ptls_cipher_context_t *ctx, int is_enc, const void *key);
+} ptls_cipher_algorithm_t;
+
+typedef struct st_ptls_aead_supplementary_encryption_t {
+    ptls_cipher_context_t *ctx;
+    const void *input;
+    uint8_t output[16];
+} ptls_aead_supplementary_encryption_t;
+
+typedef struct st_ptls_aead_context_t {
+    const struct st_ptls_aead_algorithm_t *algo;
+    void (*dispose_crypto)(struct st_ptls_aead_context_t *ctx);
+    void (*do_xor_iv)(struct st_ptls_aead_context_t *ctx, const void *bytes, size_t len);
+    void (*do_encrypt_init)(struct st_ptls_aead_context_t *ctx, uint64_t seq, const void *aad, size_t aadlen);
+    size_t (*do_encrypt_update)(struct st_ptls_aead_context_t *ctx, void *output, const void *input, size_t inlen);
+    size_t (*do_encrypt_final)(struct st_ptls_aead_context_t *ctx, void *output);
+    void (*do_encrypt)(struct st_ptls_aead_context_t *ctx, void *output, const void *input, size_t inlen, uint64_t seq,
+                       const void *aad, size_t aadlen, ptls_aead_supplementary_encryption_t *supp);
+    size_t (*do_decrypt)(struct st_ptls_aead_context_t *ctx, void *output, const void *input, size_t inlen, uint64_t seq,
+                         const void *aad, size_t aadlen);
+} ptls_aead_context_t;
+
+typedef const struct st_ptls_aead_algorithm_t {
+    const char *name;
+    const uint64_t confidentiality_limit;
+    const uint64_t integrity_limit;
+    ptls_cipher_algorithm_t *ctr_cipher;
+    ptls_cipher_algorithm_t *ecb_cipher;
+    size_t key_size;
+    size_t iv_size;
+    size_t tag_size;
+    size_t context_size;
+    int (*setup_crypto)(ptls_aead_context_t *ctx, int is_enc, const void *key, const void *iv);
+} ptls_aead_algorithm_t;
+#endif /* picotls_h */
+
+/* ======================================================================================
+ * 1. AEAD slot objects -- replace ptls_fusion_aes{128,256}gcm (lib/fusion.c:986-1005) and
+ *    ptls_fusion_aes{128,256}ctr (lib/fusion.c:974-985).
+ *    - setup_crypto(ctx, is_enc, key, iv): like aesgcm_setup (lib/fusion.c:942-962): key == NULL
+ *      only (re)loads the static IV; both the encrypt and decrypt halves are populated.
+ *    - do_encrypt writes inlen + 16 bytes (output == input allowed); supp, when given, receives
+ *      AES-ECB(supp->ctx key, 16 bytes at supp->input) computed after the record is written
+ *      (lib/fusion.c:472-487).
+ *    - do_decrypt returns inlen - 16, or SIZE_MAX for a bad tag or inlen < 16
+ *      (lib/fusion.c:917-932).  Unlike fusion, a failed open leaves the output zeroed.
+ *    - do_encrypt_init/update/final are implemented (fusion asserts, lib/fusion.c:881-896):
+ *      update buffers the plaintext and returns 0, final emits ciphertext || tag and returns
+ *      inlen + 16, as picotls' record layer (lib/picotls.c:637-640) permits.
+ *    - do_xor_iv XORs persistently into the leading static-IV bytes (lib/fusion.c:934-940).
+ * ====================================================================================== */
+extern ptls_cipher_algorithm_t ptls_mi355x_aes128ctr, ptls_mi355x_aes256ctr;
+extern ptls_aead_algorithm_t ptls_mi355x_aes128gcm, ptls_mi355x_aes256gcm;
+
+/* Capability probe -- replaces ptls_fusion_is_supported_by_cpu (lib/fusion.c:1041-1065):
+ * 1 when a gfx950 device is visible to the HIP runtime, else 0. */
+int ptls_mi355x_is_supported(void);
+
+/* ======================================================================================
+ * 2. Direct engine API -- mirrors ptls_fusion_aesgcm_new/_free/_encrypt/_decrypt
+ *    (include/picotls/fusion.h:48-88).  A context owns the device-resident key image
+ *    (round keys + GHASH tables) on the device that was current at creation time.
+ *    The x86 __m128i counter argument is replaced by the 12-byte nonce.
+ * ====================================================================================== */
+typedef struct st_ptls_mi355x_aesgcm_context ptls_mi355x_aesgcm_context_t;
+
+/* capacity is accepted for API parity (lib/fusion.c:775); tables do not depend on it. */
+ptls_mi355x_aesgcm_context_t *ptls_mi355x_aesgcm_new(const void *key, size_t key_size, size_t capacity);
+void ptls_mi355x_aesgcm_free(ptls_mi355x_aesgcm_context_t *ctx);
+/* HIP device ordinal the context lives on */
+int ptls_mi355x_aesgcm_device(const ptls_mi355x_aesgcm_context_t *ctx);
+
+/* Host-memory, synchronous, one record: output = ciphertext || tag (inlen + 16 bytes). */
+int ptls_mi355x_aesgcm_encrypt(ptls_mi355x_aesgcm_context_t *ctx, void *output, const void *input, size_t inlen,
+                               const void *nonce12, const void *aad, size_t aadlen);
+/* returns 1 if the tag verified (plaintext written), 0 if not (output zeroed), <0 on error */
+int ptls_mi355x_aesgcm_decrypt(ptls_mi355x_aesgcm_context_t *ctx, void *output, const void *input, size_t inlen,
+                               const void *nonce12, const void *aad, size_t aadlen, const void *tag);
+
+/* AES-ECB encryption of nblocks 16-byte blocks in host memory (header protection, H, ...). */
+int ptls_mi355x_aesecb_encrypt(ptls_mi355x_aesgcm_context_t *ctx, void *output, const void *input, size_t nblocks);
+
+/* ======================================================================================
+ * 3. Batch extension (the hot path).  Seals or opens n independent records in ONE launch.
+ *    All buffers are DEVICE pointers on the context's device; `stream` is a hipStream_t
+ *    (NULL = the null stream).  The call is asynchronous.
+ *
+ *    Record i: nonce = static_iv XOR (0^32 || BE64(recs[i].seq))   (lib/picotls.c:5291-5305)
+ *      seal: reads src[recs[i].src .. +len), aad[recs[i].aad .. +aadlen);
+ *            writes dst[recs[i].dst .. +len+16) = ciphertext || tag
+ *      open: reads src[recs[i].src .. +len+16) = ciphertext || tag;
+ *            writes dst[recs[i].dst .. +len) = plaintext (zeroed on failure) and
+ *            status[i] = len, or 0xffffffff when the tag does not verify
+ *    In-place (dst == src with equal offsets) is allowed.  Records may start at any byte
+ *    offset; 16-byte aligned starts are the fast path.
+ * ====================================================================================== */
+typedef struct st_ptls_mi355x_record_t {
+    uint64_t src;    /* byte offset of the record's input in the src arena */
+    uint64_t dst;    /* byte offset of the record's output in the dst arena */
+    uint64_t aad;    /* byte offset of the AAD in the aad arena */
+    uint64_t seq;    /* record sequence number */
+    uint32_t len;    /* payload bytes (open: ciphertext bytes, tag excluded) */
+    uint32_t aadlen; /* AAD bytes */
+} ptls_mi355x_record_t;
+
+int ptls_mi355x_seal_batch(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12, const ptls_mi355x_record_t *recs,
+                           size_t n, const uint8_t *src, uint8_t *dst, const uint8_t *aad, void *stream);
+int ptls_mi355x_open_batch(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12, const ptls_mi355x_record_t *recs,
+                           size_t n, const uint8_t *src, uint8_t *dst, const uint8_t *aad, uint32_t *status, void *stream);
+
+/* ---- tuning / introspection ---- */
+/* lanes per record used by the batch kernels (1, 2, 4 or 8); returns the previous value, or -1 */
+int ptls_mi355x_set_lanes_per_record(int k);
+int ptls_mi355x_get_lanes_per_record(void);
+/* name of the kernel symbol the next batch launch with these parameters uses (for profiling) */
+const char *ptls_mi355x_kernel_name(int is_seal, size_t key_size);
+/* last HIP error string seen by the engine ("" if none) */
+const char *ptls_mi355x_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PTLS_MI355X_H */

@@ -1,0 +1,322 @@
+"""rapido_amd -- MI355X (gfx950) AES-GCM engine for picotls' AEAD slot.
+
+The product is the C-ABI library ``rapido_amd/_lib/libptls_mi355x.so`` (HIP kernels +
+host C adapter, declared in ``include/ptls_mi355x.h``).  This module is a thin ctypes
+mirror used by the tests and the benchmark; it mirrors the reference's own entry points
+so the parity tests read like the reference's tests:
+
+* :func:`aead_new_direct` / :class:`Aead` -- ``ptls_aead_new_direct`` + the inline
+  dispatchers ``ptls_aead_encrypt/_s/_decrypt/_xor_iv/_encrypt_init/_update/_final``
+  (lib/picotls.c:5268-5289, include/picotls.h:1513-1564), called through the
+  engine's exported ``ptls_aead_algorithm_t`` vtables exactly as picotls does.
+* :func:`cipher_new` / :class:`Cipher` -- ``ptls_cipher_new/_init/_encrypt``.
+* :class:`Engine` -- the direct engine API (mirror of ``ptls_fusion_aesgcm_*``,
+  include/picotls/fusion.h:48-88) and the batch extension (the hot path).
+
+There is no fallback: if the library is missing or no gfx950 GPU is present, the
+calls fail loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+try:  # load torch's bundled HIP runtime first: same SONAME, so one runtime serves both
+    import torch as _torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is optional for the C-ABI itself
+    _torch = None
+
+import numpy as np
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "_lib", "libptls_mi355x.so")
+SIZE_MAX = (1 << 64) - 1
+
+#: numpy mirror of ptls_mi355x_record_t (include/ptls_mi355x.h)
+RECORD_DTYPE = np.dtype([("src", "<u8"), ("dst", "<u8"), ("aad", "<u8"), ("seq", "<u8"), ("len", "<u4"),
+                         ("aadlen", "<u4")])
+assert RECORD_DTYPE.itemsize == 40
+
+#: every symbol include/ptls_mi355x.h declares
+EXPORTED_FUNCTIONS = (
+    "ptls_mi355x_is_supported", "ptls_mi355x_aesgcm_new", "ptls_mi355x_aesgcm_free", "ptls_mi355x_aesgcm_device",
+    "ptls_mi355x_aesgcm_encrypt", "ptls_mi355x_aesgcm_decrypt", "ptls_mi355x_aesecb_encrypt",
+    "ptls_mi355x_seal_batch", "ptls_mi355x_open_batch", "ptls_mi355x_set_lanes_per_record",
+    "ptls_mi355x_get_lanes_per_record", "ptls_mi355x_kernel_name", "ptls_mi355x_last_error",
+)
+EXPORTED_OBJECTS = ("ptls_mi355x_aes128gcm", "ptls_mi355x_aes256gcm", "ptls_mi355x_aes128ctr",
+                    "ptls_mi355x_aes256ctr")
+
+# ----------------------------------------------------------------- picotls ABI (ctypes) ---
+vp, sz, u64 = C.c_void_p, C.c_size_t, C.c_uint64
+
+_DISPOSE = C.CFUNCTYPE(None, vp)
+_XOR_IV = C.CFUNCTYPE(None, vp, vp, sz)
+_ENC_INIT = C.CFUNCTYPE(None, vp, u64, vp, sz)
+_ENC_UPDATE = C.CFUNCTYPE(sz, vp, vp, vp, sz)
+_ENC_FINAL = C.CFUNCTYPE(sz, vp, vp)
+_ENCRYPT = C.CFUNCTYPE(None, vp, vp, vp, sz, u64, vp, sz, vp)
+_DECRYPT = C.CFUNCTYPE(sz, vp, vp, vp, sz, u64, vp, sz)
+_AEAD_SETUP = C.CFUNCTYPE(C.c_int, vp, C.c_int, vp, vp)
+_CIPHER_SETUP = C.CFUNCTYPE(C.c_int, vp, C.c_int, vp)
+_C_DISPOSE = C.CFUNCTYPE(None, vp)
+_C_INIT = C.CFUNCTYPE(None, vp, vp)
+_C_TRANSFORM = C.CFUNCTYPE(None, vp, vp, vp, sz)
+
+
+class CipherContext(C.Structure):  # include/picotls.h:311-317
+    _fields_ = [("algo", vp), ("do_dispose", _C_DISPOSE), ("do_init", _C_INIT), ("do_transform", _C_TRANSFORM)]
+
+
+class CipherAlgorithm(C.Structure):  # include/picotls.h:322-329
+    _fields_ = [("name", C.c_char_p), ("key_size", sz), ("block_size", sz), ("iv_size", sz), ("context_size", sz),
+                ("setup_crypto", _CIPHER_SETUP)]
+
+
+class SupplementaryEncryption(C.Structure):  # include/picotls.h:331-335
+    _fields_ = [("ctx", vp), ("input", vp), ("output", C.c_uint8 * 16)]
+
+
+class AeadContext(C.Structure):  # include/picotls.h:341-353
+    _fields_ = [("algo", vp), ("dispose_crypto", _DISPOSE), ("do_xor_iv", _XOR_IV), ("do_encrypt_init", _ENC_INIT),
+                ("do_encrypt_update", _ENC_UPDATE), ("do_encrypt_final", _ENC_FINAL), ("do_encrypt", _ENCRYPT),
+                ("do_decrypt", _DECRYPT)]
+
+
+class AeadAlgorithm(C.Structure):  # include/picotls.h:358-400
+    _fields_ = [("name", C.c_char_p), ("confidentiality_limit", u64), ("integrity_limit", u64),
+                ("ctr_cipher", C.POINTER(CipherAlgorithm)), ("ecb_cipher", C.POINTER(CipherAlgorithm)),
+                ("key_size", sz), ("iv_size", sz), ("tag_size", sz), ("context_size", sz),
+                ("setup_crypto", _AEAD_SETUP)]
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """The engine library (built by rapido_amd.build); raises if it is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} not built: run `python -m rapido_amd.build` (or __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        L.ptls_mi355x_is_supported.restype = C.c_int
+        L.ptls_mi355x_aesgcm_new.argtypes = [vp, sz, sz]
+        L.ptls_mi355x_aesgcm_new.restype = vp
+        L.ptls_mi355x_aesgcm_free.argtypes = [vp]
+        L.ptls_mi355x_aesgcm_device.argtypes = [vp]
+        L.ptls_mi355x_aesgcm_encrypt.argtypes = [vp, vp, vp, sz, vp, vp, sz]
+        L.ptls_mi355x_aesgcm_decrypt.argtypes = [vp, vp, vp, sz, vp, vp, sz, vp]
+        L.ptls_mi355x_aesecb_encrypt.argtypes = [vp, vp, vp, sz]
+        L.ptls_mi355x_seal_batch.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp]
+        L.ptls_mi355x_open_batch.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]
+        L.ptls_mi355x_set_lanes_per_record.argtypes = [C.c_int]
+        L.ptls_mi355x_kernel_name.argtypes = [C.c_int, sz]
+        L.ptls_mi355x_kernel_name.restype = C.c_char_p
+        L.ptls_mi355x_last_error.restype = C.c_char_p
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    return lib().ptls_mi355x_last_error().decode()
+
+
+def is_supported() -> bool:
+    return bool(lib().ptls_mi355x_is_supported())
+
+
+def require_gpu() -> None:
+    if not is_supported():
+        raise RuntimeError("ptls_mi355x: no gfx950 (MI355X) device visible -- the engine has no CPU fallback")
+
+
+def algorithm(name: str):
+    """Pointer to one of the exported algorithm objects, e.g. 'aes128gcm' or 'aes256ctr'."""
+    sym = "ptls_mi355x_" + name
+    typ = AeadAlgorithm if name.endswith("gcm") else CipherAlgorithm
+    return typ.in_dll(lib(), sym)
+
+
+def _cbuf(b: bytes):
+    return C.create_string_buffer(bytes(b), max(len(b), 1))
+
+
+# ------------------------------------------------------------------ picotls API mirror ----
+class Aead:
+    """An AEAD context created exactly like ptls_aead_new_direct (lib/picotls.c:5268-5283)."""
+
+    def __init__(self, algo: AeadAlgorithm, is_enc: bool, key: bytes, iv: bytes):
+        self.algo = algo
+        self._mem = C.create_string_buffer(algo.context_size)  # zeroed: *ctx = (ptls_aead_context_t){aead}
+        self.ctx = AeadContext.from_buffer(self._mem)
+        self.ctx.algo = C.cast(C.pointer(algo), vp)
+        self._key, self._iv = _cbuf(key), _cbuf(iv)
+        rc = algo.setup_crypto(C.addressof(self._mem), 1 if is_enc else 0, self._key, self._iv)
+        if rc != 0:
+            raise RuntimeError(f"setup_crypto failed ({rc:#x}): {last_error()}")
+        self.tag_size = algo.tag_size
+
+    @property
+    def ptr(self) -> int:
+        return C.addressof(self._mem)
+
+    def free(self) -> None:  # ptls_aead_free (lib/picotls.c:5285-5289)
+        if self._mem is not None:
+            self.ctx.dispose_crypto(self.ptr)
+            self._mem = None
+
+    def xor_iv(self, b: bytes) -> None:
+        self.ctx.do_xor_iv(self.ptr, _cbuf(b), len(b))
+
+    def encrypt(self, pt: bytes, seq: int, aad: bytes = b"", supp: SupplementaryEncryption | None = None,
+                inplace: bool = False) -> bytes:
+        out = C.create_string_buffer(len(pt) + self.tag_size)
+        if inplace:
+            C.memmove(out, bytes(pt), len(pt))
+            src = out
+        else:
+            src = _cbuf(pt)
+        self.ctx.do_encrypt(self.ptr, out, src, len(pt), seq, _cbuf(aad) if aad else None, len(aad),
+                            C.byref(supp) if supp is not None else None)
+        return out.raw
+
+    def decrypt(self, ct: bytes, seq: int, aad: bytes = b""):
+        out = C.create_string_buffer(max(len(ct), 1))
+        n = self.ctx.do_decrypt(self.ptr, out, _cbuf(ct), len(ct), seq, _cbuf(aad) if aad else None, len(aad))
+        return None if n == SIZE_MAX else out.raw[:n]
+
+    # streaming trio (include/picotls.h:1531-1544)
+    def encrypt_init(self, seq: int, aad: bytes = b"") -> None:
+        self._aad_keep = _cbuf(aad) if aad else None
+        self.ctx.do_encrypt_init(self.ptr, seq, self._aad_keep, len(aad))
+
+    def encrypt_update(self, out, out_off: int, data: bytes) -> int:
+        return self.ctx.do_encrypt_update(self.ptr, C.addressof(out) + out_off, _cbuf(data), len(data))
+
+    def encrypt_final(self, out, out_off: int) -> int:
+        return self.ctx.do_encrypt_final(self.ptr, C.addressof(out) + out_off)
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def aead_new_direct(name_or_algo, is_enc: bool, key: bytes, iv: bytes) -> Aead:
+    algo = algorithm(name_or_algo) if isinstance(name_or_algo, str) else name_or_algo
+    return Aead(algo, is_enc, key, iv)
+
+
+class Cipher:
+    """ptls_cipher_new / ptls_cipher_init / ptls_cipher_encrypt / ptls_cipher_free."""
+
+    def __init__(self, algo: CipherAlgorithm, is_enc: bool, key: bytes):
+        self._mem = C.create_string_buffer(algo.context_size)
+        self.ctx = CipherContext.from_buffer(self._mem)
+        self.ctx.algo = C.cast(C.pointer(algo), vp)
+        rc = algo.setup_crypto(C.addressof(self._mem), 1 if is_enc else 0, _cbuf(key))
+        if rc != 0:
+            raise RuntimeError(f"cipher setup failed ({rc:#x}): {last_error()}")
+
+    @property
+    def ptr(self) -> int:
+        return C.addressof(self._mem)
+
+    def init(self, iv: bytes) -> None:
+        self._iv = _cbuf(iv)
+        self.ctx.do_init(self.ptr, self._iv)
+
+    def encrypt(self, data: bytes) -> bytes:
+        out = C.create_string_buffer(max(len(data), 1))
+        self.ctx.do_transform(self.ptr, out, _cbuf(data), len(data))
+        return out.raw[:len(data)]
+
+    def free(self) -> None:
+        if self._mem is not None:
+            self.ctx.do_dispose(self.ptr)
+            self._mem = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def cipher_new(name: str, is_enc: bool, key: bytes) -> Cipher:
+    return Cipher(algorithm(name), is_enc, key)
+
+
+# ------------------------------------------------------------------ direct + batch API -----
+class Engine:
+    """ptls_mi355x_aesgcm_context_t: the device-resident key image + batch launches."""
+
+    def __init__(self, key: bytes, capacity: int = 16384):
+        if len(key) not in (16, 32):
+            raise ValueError("key must be 16 or 32 bytes")
+        self.key_size = len(key)
+        self.handle = lib().ptls_mi355x_aesgcm_new(_cbuf(key), len(key), capacity)
+        if not self.handle:
+            raise RuntimeError("ptls_mi355x_aesgcm_new failed: " + last_error())
+
+    def close(self) -> None:
+        if self.handle:
+            lib().ptls_mi355x_aesgcm_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def device(self) -> int:
+        return lib().ptls_mi355x_aesgcm_device(self.handle)
+
+    def encrypt(self, nonce: bytes, aad: bytes, pt: bytes) -> bytes:
+        out = C.create_string_buffer(len(pt) + 16)
+        if lib().ptls_mi355x_aesgcm_encrypt(self.handle, out, _cbuf(pt), len(pt), _cbuf(nonce), _cbuf(aad), len(aad)):
+            raise RuntimeError("encrypt failed: " + last_error())
+        return out.raw
+
+    def decrypt(self, nonce: bytes, aad: bytes, ct: bytes, tag: bytes):
+        out = C.create_string_buffer(max(len(ct), 1))
+        r = lib().ptls_mi355x_aesgcm_decrypt(self.handle, out, _cbuf(ct), len(ct), _cbuf(nonce), _cbuf(aad), len(aad),
+                                             _cbuf(tag))
+        if r < 0:
+            raise RuntimeError("decrypt failed: " + last_error())
+        return out.raw[:len(ct)] if r == 1 else None
+
+    def ecb(self, blocks: bytes) -> bytes:
+        assert len(blocks) % 16 == 0
+        out = C.create_string_buffer(max(len(blocks), 1))
+        if lib().ptls_mi355x_aesecb_encrypt(self.handle, out, _cbuf(blocks), len(blocks) // 16):
+            raise RuntimeError("ecb failed: " + last_error())
+        return out.raw[:len(blocks)]
+
+    # batch: all pointers are device addresses (ints), stream a hipStream_t handle (int) or 0
+    def seal_batch(self, static_iv: bytes, recs_ptr: int, n: int, src_ptr: int, dst_ptr: int, aad_ptr: int,
+                   stream: int = 0) -> None:
+        if lib().ptls_mi355x_seal_batch(self.handle, _cbuf(static_iv), recs_ptr, n, src_ptr, dst_ptr, aad_ptr,
+                                        stream or None):
+            raise RuntimeError("seal_batch failed: " + last_error())
+
+    def open_batch(self, static_iv: bytes, recs_ptr: int, n: int, src_ptr: int, dst_ptr: int, aad_ptr: int,
+                   status_ptr: int, stream: int = 0) -> None:
+        if lib().ptls_mi355x_open_batch(self.handle, _cbuf(static_iv), recs_ptr, n, src_ptr, dst_ptr, aad_ptr,
+                                        status_ptr, stream or None):
+            raise RuntimeError("open_batch failed: " + last_error())
+
+
+def set_lanes_per_record(k: int) -> int:
+    prev = lib().ptls_mi355x_set_lanes_per_record(k)
+    if prev < 0:
+        raise ValueError("lanes per record must be 1, 2, 4 or 8")
+    return prev
+
+
+def kernel_name(is_seal: bool, key_size: int) -> str:
+    return lib().ptls_mi355x_kernel_name(1 if is_seal else 0, key_size).decode()

@@ -1,0 +1,81 @@
+"""Builds the MI355X engine library in-tree (no JIT cache, so the .so travels with the repo).
+
+    rapido_amd/_lib/libptls_mi355x.so  <- csrc/gcm_engine.hip (hipcc, --offload-arch=gfx950)
+                                         + csrc/aead_slot.c   (host C, gcc)
+    tests/cpp/_build/libkernel_model.so <- tests/cpp/kernel_model.cpp (host clang++, test only)
+
+Rebuilds only when a source or header is newer than the output.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIBDIR = os.path.join(PKG, "_lib")
+OBJDIR = os.path.join(PKG, "_lib", "obj")
+LIB = os.path.join(LIBDIR, "libptls_mi355x.so")
+MODEL_SRC = os.path.join(ROOT, "tests", "cpp", "kernel_model.cpp")
+MODEL_LIB = os.path.join(ROOT, "tests", "cpp", "_build", "libkernel_model.so")
+ARCH = os.environ.get("PTLS_MI355X_ARCH", "gfx950")
+
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+CLANGXX = "/opt/rocm/llvm/bin/clang++" if os.path.exists("/opt/rocm/llvm/bin/clang++") else (shutil.which("clang++") or "clang++")
+CC = shutil.which("gcc") or "cc"
+
+HEADERS = [os.path.join(CSRC, "gcm_core.h"), os.path.join(ROOT, "include", "ptls_mi355x.h")]
+
+
+def _newer(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("build failed: " + " ".join(cmd) + "\n" + r.stdout + r.stderr)
+    return r
+
+
+def build_engine(verbose: bool = False, force: bool = False) -> str:
+    os.makedirs(OBJDIR, exist_ok=True)
+    hip_src = os.path.join(CSRC, "gcm_engine.hip")
+    c_src = os.path.join(CSRC, "aead_slot.c")
+    hip_obj = os.path.join(OBJDIR, "gcm_engine.o")
+    c_obj = os.path.join(OBJDIR, "aead_slot.o")
+    if force or _newer(hip_obj, [hip_src] + HEADERS):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-c", hip_src, "-o", hip_obj],
+             verbose)
+    if force or _newer(c_obj, [c_src] + HEADERS):
+        _run([CC, "-std=gnu99", "-O2", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter", "-c", c_src, "-o", c_obj],
+             verbose)
+    if force or _newer(LIB, [hip_obj, c_obj]):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, hip_obj, c_obj], verbose)
+    return LIB
+
+
+def build_model(verbose: bool = False, force: bool = False) -> str:
+    """Host build of the kernel code for the CPU test suite (not part of the product)."""
+    os.makedirs(os.path.dirname(MODEL_LIB), exist_ok=True)
+    if force or _newer(MODEL_LIB, [MODEL_SRC] + HEADERS):
+        _run([CLANGXX, "-std=c++17", "-O2", "-fPIC", "-shared", "-Wall", "-o", MODEL_LIB, MODEL_SRC], verbose)
+    return MODEL_LIB
+
+
+def build_all(verbose: bool = False, force: bool = False) -> None:
+    build_engine(verbose, force)
+    build_model(verbose, force)
+
+
+if __name__ == "__main__":
+    build_all(verbose=True, force="--force" in sys.argv)
+    print(LIB)

@@ -1,0 +1,484 @@
+/*
+ * gcm_engine.hip -- MI355X (gfx950) AES-GCM kernels and the engine half of the C ABI
+ * declared in include/ptls_mi355x.h.
+ *
+ * Replaces, for the TLS/TCPLS record path, the x86 engine lib/fusion.c of the reference:
+ *   ptls_fusion_aesgcm_new   (lib/fusion.c:775-795)  -> ptls_mi355x_aesgcm_new + mi355x_gcm_setup
+ *   ptls_fusion_aesgcm_encrypt (lib/fusion.c:239-495) -> mi355x_gcm_seal_* batch kernels
+ *   ptls_fusion_aesgcm_decrypt (lib/fusion.c:497-679) -> mi355x_gcm_open_* batch kernels
+ *   ptls_fusion_aesecb_encrypt (lib/fusion.c:747-752) -> mi355x_aes_ecb
+ *
+ * Kernel design: one persistent workgroup of 16 waves per CU; LDS holds a
+ * bank-replicated AES T-table image (64 KiB) and the K nibble tables of H^K..H^1 (8 KiB
+ * each); round keys are wave-uniform and live in SGPRs.  A wave processes 64/K records at a
+ * time, K lanes per record; lane j hashes padded GHASH positions j, j+K, ... (Horner with
+ * H^K), runs the AES-CTR block of the ciphertext position it hashes, and the K partial sums
+ * are scaled by H^(K-j) and XOR-reduced with cross-lane shuffles.  Every 16-byte block is
+ * read once from HBM and written once.
+ */
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include "gcm_core.h"
+#include "../../include/ptls_mi355x.h"
+
+using namespace mi355x;
+
+static_assert(sizeof(Record) == sizeof(ptls_mi355x_record_t), "descriptor layout");
+static_assert(sizeof(Record) == 40, "descriptor layout");
+
+__constant__ AesTables c_tabs = AesTables();
+
+namespace {
+
+constexpr int WG_THREADS = 1024; /* 16 waves: 4 per SIMD */
+
+__device__ __forceinline__ uint32_t shfl_xor_u32(uint32_t v, int mask) { return (uint32_t)__shfl_xor((int)v, mask, 64); }
+
+__device__ __forceinline__ u32x4 shfl_xor_u32x4(u32x4 v, int mask)
+{
+    u32x4 r;
+    r[0] = shfl_xor_u32(v[0], mask);
+    r[1] = shfl_xor_u32(v[1], mask);
+    r[2] = shfl_xor_u32(v[2], mask);
+    r[3] = shfl_xor_u32(v[3], mask);
+    return r;
+}
+
+template <int NR, int K, bool SEAL>
+__device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2,
+                                               const Record *__restrict__ recs, uint32_t nrecs, const uint8_t *src,
+                                               uint8_t *dst, const uint8_t *__restrict__ aad, uint32_t *__restrict__ status)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_AES_BYTES + K * GH_TABLE_BYTES];
+    constexpr uint32_t R = 64 / K; /* records per wave step */
+
+    fill_lds(lds, c_tabs.t0, ki, K, threadIdx.x, blockDim.x);
+
+    uint32_t rk[4 * (NR + 1)];
+#pragma unroll
+    for (int i = 0; i < 4 * (NR + 1); ++i)
+        rk[i] = ki->rk[i];
+    __syncthreads();
+
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t j = lane % K, slot = lane / K;
+    const uint32_t lanesel = (lane & 31u) * 4u;
+    const uint32_t waves_per_block = blockDim.x >> 6;
+    const uint64_t ngroups = ((uint64_t)nrecs + R - 1) / R;
+    const uint64_t stride = (uint64_t)gridDim.x * waves_per_block;
+
+    for (uint64_t g = (uint64_t)blockIdx.x * waves_per_block + wave; g < ngroups; g += stride) {
+        const uint64_t r = g * R + slot;
+        const bool valid = r < nrecs;
+        Record rec = {0, 0, 0, 0, 0, 0};
+        if (valid)
+            rec = recs[r];
+        uint32_t T = valid ? make_walk(rec.len, rec.aadlen, K).T : 0u;
+        uint32_t Tmax = T;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1)
+            Tmax = max(Tmax, shfl_xor_u32(Tmax, o));
+
+        const uint32_t n1 = iv1 ^ bswap32((uint32_t)(rec.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)rec.seq);
+        u32x4 part = lane_walk<NR, K, SEAL>(lds, lanesel, rk, j, rec, valid, Tmax, iv0, n1, n2, src, dst, aad);
+#pragma unroll
+        for (int o = 1; o < K; o <<= 1)
+            part ^= shfl_xor_u32x4(part, o);
+
+        if (SEAL) {
+            if (j == 0 && valid)
+                *(u32x4_u *)(dst + rec.dst + rec.len) = part;
+        } else {
+            uint32_t bad = 0;
+            if (valid) {
+                u32x4 rx = *(const u32x4_u *)(src + rec.src + rec.len);
+                u32x4 d = part ^ rx;
+                bad = (d[0] | d[1] | d[2] | d[3]) != 0u;
+                if (j == 0)
+                    status[r] = bad ? 0xffffffffu : rec.len;
+            }
+            if (valid && bad) {
+                /* failed open: do not release plaintext (fusion leaves it, lib/fusion.c:656-679) */
+                uint8_t *out = dst + rec.dst;
+                for (uint32_t off = 16u * j; off < rec.len; off += 16u * K) {
+                    uint32_t n = rec.len - off;
+                    u32x4 z = {0u, 0u, 0u, 0u};
+                    if (n >= 16)
+                        *(u32x4_u *)(out + off) = z;
+                    else
+                        store_partial(out + off, n, z);
+                }
+            }
+        }
+    }
+}
+
+} // namespace
+
+/* Named kernel instances (readable in rocprofv3 traces). */
+#define MI355X_GCM_KERNEL(NAME, NR, K, SEAL)                                                                           \
+    extern "C" __global__ __launch_bounds__(WG_THREADS) void NAME(                                                     \
+        const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2, const Record *__restrict__ recs,    \
+        uint32_t nrecs, const uint8_t *src, uint8_t *dst, const uint8_t *__restrict__ aad, uint32_t *__restrict__ st)  \
+    {                                                                                                                  \
+        gcm_batch_body<NR, K, SEAL>(ki, iv0, iv1, iv2, recs, nrecs, src, dst, aad, st);                                \
+    }
+
+MI355X_GCM_KERNEL(mi355x_gcm_seal_aes128_k1, 10, 1, true)
+MI355X_GCM_KERNEL(mi355x_gcm_seal_aes128_k2, 10, 2, true)
+MI355X_GCM_KERNEL(mi355x_gcm_seal_aes128_k4, 10, 4, true)
+MI355X_GCM_KERNEL(mi355x_gcm_seal_aes128_k8, 10, 8, true)
+MI355X_GCM_KERNEL(mi355x_gcm_seal_aes256_k1, 14, 1, true)
+MI355X_GCM_KERNEL(mi355x_gcm_seal_aes256_k2, 14, 2, true)
+MI355X_GCM_KERNEL(mi355x_gcm_seal_aes256_k4, 14, 4, true)
+MI355X_GCM_KERNEL(mi355x_gcm_seal_aes256_k8, 14, 8, true)
+MI355X_GCM_KERNEL(mi355x_gcm_open_aes128_k1, 10, 1, false)
+MI355X_GCM_KERNEL(mi355x_gcm_open_aes128_k2, 10, 2, false)
+MI355X_GCM_KERNEL(mi355x_gcm_open_aes128_k4, 10, 4, false)
+MI355X_GCM_KERNEL(mi355x_gcm_open_aes128_k8, 10, 8, false)
+MI355X_GCM_KERNEL(mi355x_gcm_open_aes256_k1, 14, 1, false)
+MI355X_GCM_KERNEL(mi355x_gcm_open_aes256_k2, 14, 2, false)
+MI355X_GCM_KERNEL(mi355x_gcm_open_aes256_k4, 14, 4, false)
+MI355X_GCM_KERNEL(mi355x_gcm_open_aes256_k8, 14, 8, false)
+
+/* key image: round keys, H and the nibble tables of H^1..H^8 (cold path, one thread) */
+extern "C" __global__ void mi355x_gcm_setup(const uint8_t *key, uint32_t keylen, KeyImage *ki, int *rc)
+{
+    if (threadIdx.x == 0 && blockIdx.x == 0)
+        *rc = build_key_image(c_tabs.sbox, key, keylen, ki);
+}
+
+/* AES-ECB, one thread per block (cold path: header protection, ctr cipher) */
+extern "C" __global__ void mi355x_aes_ecb(const KeyImage *__restrict__ ki, const uint8_t *in, uint8_t *out, uint32_t nblocks)
+{
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nblocks)
+        aes_encrypt_bytes(c_tabs.sbox, ki->rk, ki->rounds, in + 16u * i, out + 16u * i);
+}
+
+/* ================================================================== host side ============ */
+
+typedef void (*batch_kernel_t)(const KeyImage *, uint32_t, uint32_t, uint32_t, const Record *, uint32_t, const uint8_t *,
+                               uint8_t *, const uint8_t *, uint32_t *);
+
+struct st_ptls_mi355x_aesgcm_context {
+    int device;
+    int num_cu;
+    uint32_t key_size;
+    KeyImage *d_ki;
+    hipStream_t stream;  /* private stream for the synchronous single-record calls */
+    uint8_t *d_stage;    /* device staging for single-record calls */
+    uint8_t *h_stage;    /* pinned host staging */
+    size_t stage_cap;
+};
+
+static thread_local char g_err[256];
+static int g_lanes = 4;
+
+static int fail(const char *what, hipError_t e)
+{
+    snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
+    return -1;
+}
+
+#define HIPCHK(call)                                                                                                   \
+    do {                                                                                                               \
+        hipError_t e_ = (call);                                                                                        \
+        if (e_ != hipSuccess)                                                                                          \
+            return fail(#call, e_);                                                                                    \
+    } while (0)
+
+/* runs `body` with the context's device current, restoring the caller's device */
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) == hipSuccess && prev != dev)
+            (void)hipSetDevice(dev);
+        else if (prev == dev)
+            prev = -1;
+    }
+    ~DeviceGuard()
+    {
+        if (prev >= 0)
+            (void)hipSetDevice(prev);
+    }
+};
+
+static batch_kernel_t pick_kernel(bool seal, uint32_t rounds, int k, const char **name)
+{
+#define PICK(NAME)                                                                                                     \
+    do {                                                                                                               \
+        if (name)                                                                                                      \
+            *name = #NAME;                                                                                             \
+        return NAME;                                                                                                   \
+    } while (0)
+    if (seal && rounds == 10) {
+        if (k == 1) PICK(mi355x_gcm_seal_aes128_k1);
+        if (k == 2) PICK(mi355x_gcm_seal_aes128_k2);
+        if (k == 4) PICK(mi355x_gcm_seal_aes128_k4);
+        if (k == 8) PICK(mi355x_gcm_seal_aes128_k8);
+    } else if (seal && rounds == 14) {
+        if (k == 1) PICK(mi355x_gcm_seal_aes256_k1);
+        if (k == 2) PICK(mi355x_gcm_seal_aes256_k2);
+        if (k == 4) PICK(mi355x_gcm_seal_aes256_k4);
+        if (k == 8) PICK(mi355x_gcm_seal_aes256_k8);
+    } else if (!seal && rounds == 10) {
+        if (k == 1) PICK(mi355x_gcm_open_aes128_k1);
+        if (k == 2) PICK(mi355x_gcm_open_aes128_k2);
+        if (k == 4) PICK(mi355x_gcm_open_aes128_k4);
+        if (k == 8) PICK(mi355x_gcm_open_aes128_k8);
+    } else if (!seal && rounds == 14) {
+        if (k == 1) PICK(mi355x_gcm_open_aes256_k1);
+        if (k == 2) PICK(mi355x_gcm_open_aes256_k2);
+        if (k == 4) PICK(mi355x_gcm_open_aes256_k4);
+        if (k == 8) PICK(mi355x_gcm_open_aes256_k8);
+    }
+#undef PICK
+    if (name)
+        *name = "";
+    return nullptr;
+}
+
+static inline uint32_t le32(const uint8_t *p) { return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24; }
+
+static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void *static_iv12, const Record *recs, size_t n,
+                        const uint8_t *src, uint8_t *dst, const uint8_t *aad, uint32_t *status, hipStream_t stream)
+{
+    if (n == 0)
+        return 0;
+    if (n > 0xffffffffull) {
+        snprintf(g_err, sizeof(g_err), "batch of %zu records exceeds 2^32-1", n);
+        return -1;
+    }
+    const int k = g_lanes;
+    batch_kernel_t kern = pick_kernel(seal, ctx->key_size == 32 ? 14u : 10u, k, nullptr);
+    if (kern == nullptr) {
+        snprintf(g_err, sizeof(g_err), "no kernel for lanes-per-record %d", k);
+        return -1;
+    }
+    const uint8_t *iv = (const uint8_t *)static_iv12;
+    const uint64_t ngroups = (n + (64 / k) - 1) / (64 / k);
+    const uint64_t waves = WG_THREADS / 64;
+    uint64_t blocks = (ngroups + waves - 1) / waves;
+    if (blocks > (uint64_t)ctx->num_cu)
+        blocks = (uint64_t)ctx->num_cu;
+    DeviceGuard guard(ctx->device);
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(WG_THREADS), 0, stream, ctx->d_ki, le32(iv), le32(iv + 4),
+                       le32(iv + 8), recs, (uint32_t)n, src, dst, aad, status);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+static int ensure_stage(ptls_mi355x_aesgcm_context_t *ctx, size_t need)
+{
+    if (need <= ctx->stage_cap)
+        return 0;
+    size_t cap = ctx->stage_cap ? ctx->stage_cap : 4096;
+    while (cap < need)
+        cap *= 2;
+    if (ctx->d_stage)
+        (void)hipFree(ctx->d_stage);
+    if (ctx->h_stage)
+        (void)hipHostFree(ctx->h_stage);
+    ctx->d_stage = nullptr;
+    ctx->h_stage = nullptr;
+    ctx->stage_cap = 0;
+    HIPCHK(hipMalloc(&ctx->d_stage, cap));
+    HIPCHK(hipHostMalloc(&ctx->h_stage, cap, hipHostMallocDefault));
+    ctx->stage_cap = cap;
+    return 0;
+}
+
+static inline size_t up16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+extern "C" {
+
+const char *ptls_mi355x_last_error(void) { return g_err; }
+
+int ptls_mi355x_is_supported(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return 0;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, 0) != hipSuccess)
+        return 0;
+    return strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+}
+
+int ptls_mi355x_set_lanes_per_record(int k)
+{
+    if (k != 1 && k != 2 && k != 4 && k != 8)
+        return -1;
+    int prev = g_lanes;
+    g_lanes = k;
+    return prev;
+}
+
+int ptls_mi355x_get_lanes_per_record(void) { return g_lanes; }
+
+const char *ptls_mi355x_kernel_name(int is_seal, size_t key_size)
+{
+    const char *name = "";
+    pick_kernel(is_seal != 0, key_size == 32 ? 14u : 10u, g_lanes, &name);
+    return name;
+}
+
+ptls_mi355x_aesgcm_context_t *ptls_mi355x_aesgcm_new(const void *key, size_t key_size, size_t capacity)
+{
+    (void)capacity;
+    if (key_size != 16 && key_size != 32) {
+        snprintf(g_err, sizeof(g_err), "unsupported key size %zu", key_size);
+        return nullptr;
+    }
+    ptls_mi355x_aesgcm_context_t *ctx = (ptls_mi355x_aesgcm_context_t *)calloc(1, sizeof(*ctx));
+    if (ctx == nullptr)
+        return nullptr;
+    ctx->key_size = (uint32_t)key_size;
+    hipDeviceProp_t prop;
+    int *d_rc = nullptr, rc = -1;
+    if (hipGetDevice(&ctx->device) != hipSuccess || hipGetDeviceProperties(&prop, ctx->device) != hipSuccess)
+        goto Fail;
+    ctx->num_cu = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess)
+        goto Fail;
+    if (hipMalloc(&ctx->d_ki, sizeof(KeyImage)) != hipSuccess || ensure_stage(ctx, 4096) != 0)
+        goto Fail;
+    memcpy(ctx->h_stage, key, key_size);
+    d_rc = (int *)(ctx->d_stage + 64);
+    if (hipMemcpyAsync(ctx->d_stage, ctx->h_stage, key_size, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+        goto Fail;
+    hipLaunchKernelGGL(mi355x_gcm_setup, dim3(1), dim3(64), 0, ctx->stream, ctx->d_stage, (uint32_t)key_size, ctx->d_ki, d_rc);
+    if (hipGetLastError() != hipSuccess)
+        goto Fail;
+    if (hipMemcpyAsync(&rc, d_rc, sizeof(int), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+        hipStreamSynchronize(ctx->stream) != hipSuccess || rc != 0)
+        goto Fail;
+    memset(ctx->h_stage, 0, key_size);
+    return ctx;
+Fail:
+    if (g_err[0] == 0)
+        snprintf(g_err, sizeof(g_err), "context setup failed: %s", hipGetErrorString(hipGetLastError()));
+    ptls_mi355x_aesgcm_free(ctx);
+    return nullptr;
+}
+
+void ptls_mi355x_aesgcm_free(ptls_mi355x_aesgcm_context_t *ctx)
+{
+    if (ctx == nullptr)
+        return;
+    DeviceGuard guard(ctx->device);
+    if (ctx->stream)
+        (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->d_ki) {
+        (void)hipMemset(ctx->d_ki, 0, sizeof(KeyImage)); /* clear key material, as ptls_fusion_aesgcm_free does */
+        (void)hipFree(ctx->d_ki);
+    }
+    if (ctx->d_stage)
+        (void)hipFree(ctx->d_stage);
+    if (ctx->h_stage) {
+        memset(ctx->h_stage, 0, ctx->stage_cap);
+        (void)hipHostFree(ctx->h_stage);
+    }
+    if (ctx->stream)
+        (void)hipStreamDestroy(ctx->stream);
+    free(ctx);
+}
+
+int ptls_mi355x_aesgcm_device(const ptls_mi355x_aesgcm_context_t *ctx) { return ctx->device; }
+
+int ptls_mi355x_seal_batch(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12, const ptls_mi355x_record_t *recs,
+                           size_t n, const uint8_t *src, uint8_t *dst, const uint8_t *aad, void *stream)
+{
+    return launch_batch(ctx, true, static_iv12, (const Record *)recs, n, src, dst, aad, nullptr, (hipStream_t)stream);
+}
+
+int ptls_mi355x_open_batch(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12, const ptls_mi355x_record_t *recs,
+                           size_t n, const uint8_t *src, uint8_t *dst, const uint8_t *aad, uint32_t *status, void *stream)
+{
+    return launch_batch(ctx, false, static_iv12, (const Record *)recs, n, src, dst, aad, status, (hipStream_t)stream);
+}
+
+/*
+ * Single record in host memory.  Stage layout (device and pinned host alike):
+ *   [0, 64) descriptor | [64, 64 + A) aad | [D, D + inlen + 16) data (in place) | status
+ */
+static int single_record(ptls_mi355x_aesgcm_context_t *ctx, bool seal, void *output, const void *input, size_t inlen,
+                         const void *nonce12, const void *aad, size_t aadlen, const void *tag)
+{
+    if (inlen > 0xffffffffu || aadlen > 0xffffffffu) {
+        snprintf(g_err, sizeof(g_err), "record too large");
+        return -1;
+    }
+    DeviceGuard guard(ctx->device);
+    const size_t off_aad = 64, off_data = off_aad + up16(aadlen), off_status = off_data + up16(inlen + 16);
+    const size_t total = off_status + 16;
+    if (ensure_stage(ctx, total) != 0)
+        return -1;
+    Record rec = {off_data, off_data, off_aad, 0, (uint32_t)inlen, (uint32_t)aadlen};
+    memcpy(ctx->h_stage, &rec, sizeof(rec));
+    if (aadlen)
+        memcpy(ctx->h_stage + off_aad, aad, aadlen);
+    if (inlen)
+        memcpy(ctx->h_stage + off_data, input, inlen);
+    if (!seal)
+        memcpy(ctx->h_stage + off_data + inlen, tag, 16);
+    HIPCHK(hipMemcpyAsync(ctx->d_stage, ctx->h_stage, off_status, hipMemcpyHostToDevice, ctx->stream));
+    if (launch_batch(ctx, seal, nonce12, (const Record *)ctx->d_stage, 1, ctx->d_stage, ctx->d_stage, ctx->d_stage,
+                     (uint32_t *)(ctx->d_stage + off_status), ctx->stream) != 0)
+        return -1;
+    const size_t outlen = seal ? inlen + 16 : inlen;
+    HIPCHK(hipMemcpyAsync(ctx->h_stage + off_data, ctx->d_stage + off_data, outlen, hipMemcpyDeviceToHost, ctx->stream));
+    if (!seal)
+        HIPCHK(hipMemcpyAsync(ctx->h_stage + off_status, ctx->d_stage + off_status, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (outlen)
+        memcpy(output, ctx->h_stage + off_data, outlen);
+    memset(ctx->h_stage + off_aad, 0, off_status - off_aad);
+    if (seal)
+        return 0;
+    uint32_t st;
+    memcpy(&st, ctx->h_stage + off_status, 4);
+    return st == (uint32_t)inlen ? 1 : 0;
+}
+
+int ptls_mi355x_aesgcm_encrypt(ptls_mi355x_aesgcm_context_t *ctx, void *output, const void *input, size_t inlen,
+                               const void *nonce12, const void *aad, size_t aadlen)
+{
+    return single_record(ctx, true, output, input, inlen, nonce12, aad, aadlen, nullptr);
+}
+
+int ptls_mi355x_aesgcm_decrypt(ptls_mi355x_aesgcm_context_t *ctx, void *output, const void *input, size_t inlen,
+                               const void *nonce12, const void *aad, size_t aadlen, const void *tag)
+{
+    return single_record(ctx, false, output, input, inlen, nonce12, aad, aadlen, tag);
+}
+
+int ptls_mi355x_aesecb_encrypt(ptls_mi355x_aesgcm_context_t *ctx, void *output, const void *input, size_t nblocks)
+{
+    if (nblocks == 0)
+        return 0;
+    if (nblocks > 0xffffffffu / 16) {
+        snprintf(g_err, sizeof(g_err), "too many blocks");
+        return -1;
+    }
+    DeviceGuard guard(ctx->device);
+    const size_t bytes = 16 * nblocks;
+    if (ensure_stage(ctx, 2 * bytes) != 0)
+        return -1;
+    memcpy(ctx->h_stage, input, bytes);
+    HIPCHK(hipMemcpyAsync(ctx->d_stage, ctx->h_stage, bytes, hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(mi355x_aes_ecb, dim3((unsigned)((nblocks + 255) / 256)), dim3(256), 0, ctx->stream, ctx->d_ki,
+                       ctx->d_stage, ctx->d_stage + bytes, (uint32_t)nblocks);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(ctx->h_stage + bytes, ctx->d_stage + bytes, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    memcpy(output, ctx->h_stage + bytes, bytes);
+    memset(ctx->h_stage, 0, 2 * bytes);
+    return 0;
+}
+
+} /* extern "C" */

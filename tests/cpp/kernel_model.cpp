@@ -1,0 +1,84 @@
+/*
+ * tests/cpp/kernel_model.cpp -- host execution of the engine's kernel code (test only).
+ *
+ * Runs rapido_amd/csrc/gcm_core.h -- the very functions the HIP kernels are built from --
+ * on the CPU, lane by lane, with v_perm_b32 and the LDS image emulated.  It lets the CPU test
+ * suite check the algorithmic pieces of the kernels (T-table AES with bank-replicated
+ * addressing, nibble-table GHASH, the K-lane record walk with front padding, the H^(K-j)
+ * scaling) against the oracle without a GPU.  It is NOT part of the product library and the
+ * product never calls it.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include "../../rapido_amd/csrc/gcm_core.h"
+
+using namespace mi355x;
+
+static constexpr AesTables kTabs{};
+
+template <int NR, int K, bool SEAL>
+static void run(const KeyImage *ki, const uint8_t *lds, const uint8_t *static_iv, const Record *recs, size_t n,
+                const uint8_t *src, uint8_t *dst, const uint8_t *aad, uint32_t *status)
+{
+    uint32_t iv0, iv1, iv2;
+    memcpy(&iv0, static_iv, 4);
+    memcpy(&iv1, static_iv + 4, 4);
+    memcpy(&iv2, static_iv + 8, 4);
+    for (size_t i = 0; i < n; ++i) {
+        const Record &r = recs[i];
+        Walk wk = make_walk(r.len, r.aadlen, K);
+        uint32_t n1 = iv1 ^ bswap32((uint32_t)(r.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)r.seq);
+        /* received tag first: open may run in place */
+        u32x4 rx = {0, 0, 0, 0};
+        if (!SEAL)
+            memcpy(&rx, src + r.src + r.len, 16);
+        u32x4 tag = {0, 0, 0, 0};
+        for (uint32_t j = 0; j < (uint32_t)K; ++j)
+            tag ^= lane_walk<NR, K, SEAL>(lds, 4u * (j & 31u), ki->rk, j, r, true, wk.T, iv0, n1, n2, src, dst, aad);
+        if (SEAL) {
+            memcpy(dst + r.dst + r.len, &tag, 16);
+        } else {
+            u32x4 d = tag ^ rx;
+            status[i] = (d[0] | d[1] | d[2] | d[3]) ? 0xffffffffu : r.len;
+        }
+    }
+}
+
+extern "C" int model_batch(int is_seal, int K, const uint8_t *key, size_t keylen, const uint8_t *static_iv,
+                           const Record *recs, size_t n, const uint8_t *src, uint8_t *dst, const uint8_t *aad,
+                           uint32_t *status)
+{
+    KeyImage *ki = (KeyImage *)aligned_alloc(64, sizeof(KeyImage));
+    uint8_t *lds = (uint8_t *)aligned_alloc(256, LDS_AES_BYTES + MAX_K * GH_TABLE_BYTES);
+    if (build_key_image(kTabs.sbox, key, (uint32_t)keylen, ki) != 0) {
+        free(ki);
+        free(lds);
+        return -1;
+    }
+    fill_lds(lds, kTabs.t0, ki, (uint32_t)K, 0, 1);
+    int nr = (int)ki->rounds, rc = 0;
+#define MODEL_CASE(NRV, KV)                                                                                            \
+    if (nr == NRV && K == KV) {                                                                                        \
+        if (is_seal)                                                                                                   \
+            run<NRV, KV, true>(ki, lds, static_iv, recs, n, src, dst, aad, status);                                    \
+        else                                                                                                           \
+            run<NRV, KV, false>(ki, lds, static_iv, recs, n, src, dst, aad, status);                                   \
+    } else
+    MODEL_CASE(10, 1) MODEL_CASE(10, 2) MODEL_CASE(10, 4) MODEL_CASE(10, 8) MODEL_CASE(14, 1) MODEL_CASE(14, 2)
+        MODEL_CASE(14, 4) MODEL_CASE(14, 8) rc = -2;
+#undef MODEL_CASE
+    free(ki);
+    free(lds);
+    return rc;
+}
+
+/* exposes the key image (round keys, H, tables) for table-level tests */
+extern "C" int model_key_image(const uint8_t *key, size_t keylen, void *out, size_t outlen)
+{
+    if (outlen < sizeof(KeyImage))
+        return -(int)sizeof(KeyImage);
+    return build_key_image(kTabs.sbox, key, (uint32_t)keylen, (KeyImage *)out);
+}
+
+extern "C" size_t model_key_image_size(void) { return sizeof(KeyImage); }
