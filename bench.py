@@ -1,0 +1,270 @@
+"""Benchmark of the MI355X AES-GCM engine (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload 1400|16k|16k-aes128|ragged]
+
+One step = one pass of the hot path over one batch resident in HBM: seal every record
+of the batch (ptls_mi355x_seal_batch), then open the sealed batch
+(ptls_mi355x_open_batch).  `value` = payload bytes sealed + payload bytes opened by all
+ranks / max-over-ranks wall time of the K timed steps, in GiB/s.
+
+Default workload (N=1) is BASELINE.json configs[1]: AES-128-GCM seal+open of 1 M x 1400 B
+TLS records (5-byte TLS header AAD, seq = record index, 256-B aligned records).  With
+N > 1 (torchrun, one rank per GPU) every rank seals/opens its own 1 M-record shard --
+configs[4], 8 M x 1400 B over 8 GPUs -- with no collective on the data path ("weak").
+
+The JSON line also carries
+  roofline      -- the dominant kernel's algorithmic HBM bytes per launch / its mean launch
+                   time (HIP events on the launch stream) against the 8 TB/s HBM3E peak;
+                   `traffic` from rocprofv3 PMC counters when a profiles/ summary exists;
+  cpu_baseline  -- the reference engine (lib/fusion.c, built unmodified into oracle/_ref)
+                   on this host's cores with the t/ptlsbench.c methodology, bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+DESC_BYTES = 40         # sizeof(ptls_mi355x_record_t)
+GIB = float(1 << 30)
+
+WORKLOADS = {
+    "1400": dict(name="AES-128-GCM seal+open, 1M x 1400 B TLS records", key=16, n=1 << 20, length=1400),
+    "16k": dict(name="AES-256-GCM seal+open, 256K x 16 KiB TLS records", key=32, n=1 << 18, length=16384),
+    "16k-aes128": dict(name="AES-128-GCM seal+open, 256K x 16 KiB TLS records", key=16, n=1 << 18, length=16384),
+    "ragged": dict(name="AES-128-GCM seal+open, 1M records U{64..16384} B", key=16, n=1 << 20, length=None),
+}
+
+
+def algorithmic_bytes(lengths_sum: int, n: int, aad_sum: int, seal: bool) -> int:
+    """seal: read L + aad + descriptor, write L + 16; open: read L + 16 + aad + descriptor, write L + 4."""
+    if seal:
+        return lengths_sum + aad_sum + DESC_BYTES * n + lengths_sum + 16 * n
+    return lengths_sum + 16 * n + aad_sum + DESC_BYTES * n + lengths_sum + 4 * n
+
+
+def cpu_baseline(wl: dict, threads: int) -> dict:
+    """Reference fusion on host cores, t/ptlsbench.c methodology, ~10-30 s of CPU work."""
+    import oracle
+
+    length = wl["length"] or 8224  # ragged: the mean record size
+    try:
+        ref = oracle.Reference()
+        if not ref.supported():
+            raise RuntimeError("CPU lacks AES-NI/PCLMUL/AVX2")
+        per_thread = max(2000, int(1.5e9 / length))  # ~1.5 GB sealed (+ opened) per thread
+        s1, o1, _, f1 = ref.bench(wl["key"], length, 5, per_thread, 1)
+        sN, oN, wall, fN = ref.bench(wl["key"], length, 5, per_thread, threads)
+        if f1 or fN:
+            raise RuntimeError("reference open failed")
+        # seal+open bytes per second (harmonic combination: each record is sealed then opened)
+        one = 2.0 / (1.0 / s1 + 1.0 / o1) / GIB
+        alln = 2.0 / (1.0 / sN + 1.0 / oN) / GIB
+        cpu = open("/proc/cpuinfo").read().split("model name")[1].split("\n")[0].strip(" :\t")
+        return {"value": round(alln, 3), "unit": "GiB/s", "cores": threads, "kind": "reference",
+                "value_1core": round(one, 3), "cpu": cpu,
+                "sample": f"lib/fusion.c AES-{8 * wl['key']}-GCM, {per_thread} x {length} B records per thread, "
+                          f"AAD 5 B, seal then open in 1000-record batches (t/ptlsbench.c:80-165), "
+                          f"{threads} threads each with its own context; 1-core run separately"}
+    except (FileNotFoundError, OSError, RuntimeError) as e:
+        # the CPU restatement (scalar, bit-serial GHASH): a much slower "port" baseline
+        import numpy as np
+        from rapido_amd import records
+
+        n = 256
+        recs, src, aad = records.tls_batch(np.full(n, length, dtype=np.uint64), seed=5)
+        dst = np.zeros_like(src)
+        t0 = time.perf_counter()
+        oracle.batch(True, bytes(wl["key"]), bytes(12), recs, src, dst, aad, nthreads=threads)
+        dt = time.perf_counter() - t0
+        return {"value": round(n * length / dt / GIB, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+                "sample": f"oracle/aesgcm_oracle.c seal only, {n} x {length} B ({e})"}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="1400", choices=sorted(WORKLOADS))
+    ap.add_argument("--lanes", type=int, default=0, help="lanes per record (1/2/4/8); 0 = engine default")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--e2e", action="store_true", help="also time the PCIe-inclusive path (pinned host in/out)")
+    ap.add_argument("--check", type=int, default=64, help="records re-checked against the CPU oracle after timing")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import rapido_amd as ra
+    from rapido_amd import records
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank if world > 1 else 0)
+    torch.cuda.set_device(dev)
+    ra.require_gpu()
+    if args.lanes:
+        ra.set_lanes_per_record(args.lanes)
+
+    wl = WORKLOADS[args.workload]
+    n = wl["n"]
+    rng = np.random.default_rng(1 + rank)
+    if wl["length"] is None:
+        lengths = rng.integers(64, 16385, n).astype(np.uint64)
+    else:
+        lengths = np.full(n, wl["length"], dtype=np.uint64)
+    recs, src_bytes, aad_bytes = records.layout(lengths, np.full(n, 5, dtype=np.uint64), align=256)
+    recs["seq"] = np.arange(n, dtype=np.uint64) + np.uint64(rank) * np.uint64(n)
+    aad = np.zeros(aad_bytes, dtype=np.uint8)
+    aad[: 5 * n] = records.tls_aad(lengths)
+
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1234 + rank)
+    d_src = torch.randint(0, 256, (src_bytes,), dtype=torch.uint8, device=dev, generator=gen)
+    d_ct = torch.zeros_like(d_src)
+    d_pt = torch.zeros_like(d_src)
+    d_recs = torch.from_numpy(recs.view(np.uint8)).to(dev)
+    d_aad = torch.from_numpy(aad).to(dev)
+    d_st = torch.zeros(n, dtype=torch.int32, device=dev)
+    key = bytes(range(wl["key"]))
+    iv = bytes(range(0xA0, 0xAC))
+    eng = ra.Engine(key)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        eng.seal_batch(iv, d_recs.data_ptr(), n, d_src.data_ptr(), d_ct.data_ptr(), d_aad.data_ptr(), sh)
+        if ev is not None:
+            ev[1].record(stream)
+        eng.open_batch(iv, d_recs.data_ptr(), n, d_ct.data_ptr(), d_pt.data_ptr(), d_aad.data_ptr(),
+                       d_st.data_ptr(), sh)
+        if ev is not None:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(events[i])
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    seal_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
+    open_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in events]))
+
+    # correctness after timing: every status verifies; a sample of records bit-exact vs the oracle
+    st = d_st.cpu().numpy().view(np.uint32)
+    if not (st == recs["len"]).all():
+        raise SystemExit("bench: open status mismatch -- results invalid")
+    if args.check and rank == 0:
+        import oracle
+
+        idx = rng.choice(n, size=min(args.check, n), replace=False)
+        sub = recs[idx].copy()
+        spans = [(int(r["src"]), int(r["len"])) for r in sub]
+        srcs = [d_src[a:a + ln].cpu().numpy() for a, ln in spans]
+        cts = [d_ct[a:a + ln + 16].cpu().numpy() for a, ln in spans]
+        for r, s_, c_ in zip(sub, srcs, cts):
+            want = oracle.seal(key, oracle.build_iv(iv, int(r["seq"])), aad[int(r["aad"]):int(r["aad"]) + 5].tobytes(),
+                               s_.tobytes())
+            if want != c_.tobytes():
+                raise SystemExit("bench: sealed record differs from the oracle -- results invalid")
+
+    payload = float(lengths.sum())
+    total_bytes = 2.0 * payload * world  # sealed + opened, all ranks
+    value = total_bytes * args.steps / elapsed / GIB
+    seal_b = algorithmic_bytes(int(payload), n, 5 * n, True)
+    open_b = algorithmic_bytes(int(payload), n, 5 * n, False)
+    dom_is_seal = seal_ms >= open_ms
+    dom_ms = seal_ms if dom_is_seal else open_ms
+    dom_bytes = seal_b if dom_is_seal else open_b
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    kname = ra.kernel_name(dom_is_seal, wl["key"])
+
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        try:
+            pmc = json.load(open(pmc_path))
+            ent = pmc.get(args.workload, {}).get(kname)
+            if ent:
+                traffic = ent["hbm_bytes_per_launch"]
+        except (ValueError, KeyError):
+            traffic = None
+
+    out = {
+        "metric": "device-resident AES-GCM GiB/s, 1.4 KB & 16 KiB record batches, 1/2/4/8 GPU",
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (device-generated random payload, TLS 1.3 record headers as AAD)",
+        "config": {"workload": wl["name"], "records_per_gpu": n,
+                   "record_bytes": wl["length"] if wl["length"] else "U{64..16384}",
+                   "aad_bytes": 5, "key_bits": 8 * wl["key"], "lanes_per_record": ra.lib().ptls_mi355x_get_lanes_per_record(),
+                   "parallelism": f"records sharded per GPU x{world}, no collective"},
+        "seal_gibps": round(payload / (seal_ms * 1e-3) / GIB, 2),
+        "open_gibps": round(payload / (open_ms * 1e-3) / GIB, 2),
+        "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                     "algorithmic_bytes_per_launch": dom_bytes, "launch_ms": round(dom_ms, 4)},
+    }
+
+    if args.e2e:
+        # PCIe-inclusive: records start and end in pinned host memory (one H2D, seal, one D2H)
+        h_src = torch.empty(src_bytes, dtype=torch.uint8, pin_memory=True)
+        h_dst = torch.empty(src_bytes, dtype=torch.uint8, pin_memory=True)
+        h_src.copy_(d_src.cpu())
+        torch.cuda.synchronize(dev)
+        reps = max(2, args.steps // 4)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            d_src.copy_(h_src, non_blocking=True)
+            eng.seal_batch(iv, d_recs.data_ptr(), n, d_src.data_ptr(), d_ct.data_ptr(), d_aad.data_ptr(), sh)
+            h_dst.copy_(d_ct, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        dt = (time.perf_counter() - t0) / reps
+        out["e2e_pcie"] = {"seal_gibps": round(payload / dt / GIB, 2), "note": "pinned H2D + seal + D2H, serial"}
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(wl, args.cpu_threads)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -157,7 +157,7 @@ int ptls_mi355x_open_batch(ptls_mi355x_aesgcm_context_t *ctx, const void *static
                            size_t n, const uint8_t *src, uint8_t *dst, const uint8_t *aad, uint32_t *status, void *stream);
 
 /* ---- tuning / introspection ---- */
-/* lanes per record used by the batch kernels (1, 2, 4 or 8); returns the previous value, or -1 */
+/* lanes per record used by the batch kernels (1, 2, 4 or 8; default 4); returns the previous value, or -1 */
 int ptls_mi355x_set_lanes_per_record(int k);
 int ptls_mi355x_get_lanes_per_record(void);
 /* name of the kernel symbol the next batch launch with these parameters uses (for profiling) */

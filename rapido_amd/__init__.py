@@ -29,7 +29,7 @@ except Exception:  # pragma: no cover - torch is optional for the C-ABI itself
 import numpy as np
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "_lib", "libptls_mi355x.so")
+LIB_PATH = os.environ.get("PTLS_MI355X_LIB") or os.path.join(PKG, "_lib", "libptls_mi355x.so")
 SIZE_MAX = (1 << 64) - 1
 
 #: numpy mirror of ptls_mi355x_record_t (include/ptls_mi355x.h)

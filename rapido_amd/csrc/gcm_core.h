@@ -19,13 +19,19 @@
  *     constant c uses 32 nibble tables Tab_c[t][v] (t = 8*d + n is nibble n of
  *     dword d, v its value) so that X*c = XOR_t Tab_c[t][nibble_t(X)].
  *
- * LDS map used by the batch kernels (one workgroup per CU):
- *   [0x00000, 0x10000)  AES T-table image: row x (256 B) = T0[x] replicated in
- *                       32 banks, then T1[x] = rotl8(T0[x]) replicated in 32
- *                       banks.  Lane l reads bank (l & 31): conflict-free
- *                       ds_read_b32 for any mix of indices.
- *   [0x10000, ...)      GHASH nibble tables, 8 KiB each; slot j holds
+ * LDS map used by the batch kernels (one workgroup per CU; struct Layout<K>):
+ *   K <= 4 ("four tables", 128 KiB AES + K x 8 KiB = 160 KiB at K = 4):
+ *   [0x00000, 0x10000)  AES T-table image A: row x (256 B) = T0[x] replicated in 32
+ *                       banks, then T1[x] = rotl8(T0[x]) replicated in 32 banks.
+ *   [0x10000, 0x20000)  image B: the same rows for T2 = rotl16(T0) and T3 = rotl24(T0).
+ *                       Lane l reads bank (l & 31): conflict-free ds_read_b32 for any
+ *                       mix of indices, and no rotates in the round function.
+ *   [0x20000, ...)      GHASH nibble tables, 8 KiB each; slot j holds
  *                       Tab_{H^(K-j)} (slot 0 = H^K is also the Horner factor).
+ *   K = 8 ("two tables", 64 KiB AES + 8 x 8 KiB = 128 KiB): only image A; T2 and T3 are
+ *                       rotl16 of the T0/T1 reads (one XOR + one rotate per column), and
+ *                       the GHASH tables start at 0x10000.  K = 8 makes every wave-wide
+ *                       load/store cover whole 128-byte lines of 8 records.
  *                       A table is 32 rows of 256 B (one bank row per nibble
  *                       position), so a ds_read_b128 of any 64 nibbles from one
  *                       table is conflict-free.
@@ -43,6 +49,18 @@
 #define GCM_HDC constexpr
 #endif
 
+/*
+ * Profiling ablations (scripts/ablate.py builds them as separate libraries; the product
+ * build never defines these): GCM_ABLATE_GHASH skips the GHASH multiplies, GCM_ABLATE_AES
+ * skips the AES rounds.  Outputs are wrong in those builds; only their timings are used.
+ */
+#ifndef GCM_ABLATE_GHASH
+#define GCM_ABLATE_GHASH 0
+#endif
+#ifndef GCM_ABLATE_AES
+#define GCM_ABLATE_AES 0
+#endif
+
 namespace mi355x {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -50,10 +68,20 @@ typedef u32x4 u32x4_u __attribute__((aligned(1)));
 
 enum : uint32_t {
     LDS_AES_BASE = 0x00000u,
-    LDS_AES_BYTES = 0x10000u,
-    LDS_GH_BASE = 0x10000u,
+    LDS_AES_BYTES = 0x20000u,         /* two 64 KiB images: (T0|T1) and (T2|T3) */
+    LDS_GH_BASE = 0x20000u,
     GH_TABLE_BYTES = 32u * 16u * 16u, /* 8 KiB */
-    MAX_K = 8,                        /* lanes per record, upper bound */
+    MAX_K = 8,                        /* tables kept in the key image: H^1..H^8 */
+    MAX_KERNEL_K = 8,
+};
+
+template <int K>
+struct Layout {
+    static constexpr bool four_tables = K <= 4;
+    static constexpr uint32_t aes_bytes = four_tables ? 0x20000u : 0x10000u;
+    static constexpr uint32_t gh_base = aes_bytes;
+    static constexpr uint32_t total = aes_bytes + (uint32_t)K * GH_TABLE_BYTES;
+    static_assert(total <= 160u * 1024u, "LDS budget");
 };
 
 /* ------------------------------------------------------------------ constant tables ------ */
@@ -91,6 +119,29 @@ struct AesTables {
 
 GCM_HD uint32_t rotl32(uint32_t x, int s) { return (x << s) | (x >> (32 - s)); }
 
+/* a ^ b ^ c in one v_bitop3_b32 (gfx950 has no v_xor3_b32) */
+GCM_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+    return a ^ b ^ c;
+#endif
+}
+
+/* xor3 that the optimizer may not move: pins a GHASH accumulation step right behind its
+ * LDS reads (the IR passes otherwise sink the chain past the AES rounds and spill) */
+GCM_HD uint32_t xor3_pinned(uint32_t a, uint32_t b, uint32_t c)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t r;
+    asm volatile("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+#else
+    return a ^ b ^ c;
+#endif
+}
+
 GCM_HD uint32_t bswap32(uint32_t x)
 {
     return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
@@ -119,36 +170,54 @@ GCM_HD uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
 #endif
 }
 
+/* scheduling fence: keeps the compiler from hoisting one round's independent LDS reads into
+ * another (which it otherwise does, spilling registers at 16 waves per CU) */
+#if defined(__HIP_DEVICE_COMPILE__)
+#define GCM_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define GCM_SCHED_FENCE() ((void)0)
+#endif
+
 GCM_HD uint32_t lds_u32(const uint8_t *lds, uint32_t addr) { return *(const uint32_t *)(lds + addr); }
 GCM_HD u32x4 lds_u32x4(const uint8_t *lds, uint32_t addr) { return *(const u32x4 *)(lds + addr); }
 
 /*
- * One AES encryption of w[4] with the replicated T-table image at lds[0, 64K).
- * lanesel = 4 * (lane & 31): each lane reads its own bank.  rk = 4*(NR+1) round-key dwords.
- * Per column and round: 4 v_perm (address), 4 ds_read_b32, 2 rotates, 2 xor3.
+ * One AES encryption of w[4] with the replicated T-table images at lds[0, 128K).
+ * lanesel = 4 * (lane & 31) | 0x10000: bits 0-7 pick the lane's bank, byte 2 selects image B.
+ * rk = 4*(NR+1) round-key dwords (wave-uniform: SGPRs).
+ * Per column and round: 4 v_perm (addresses), 4 ds_read_b32, 2 v_bitop3 (xor3).
  */
-template <int NR>
+/* one full AES round column: T0[a] ^ T1[b] ^ T2[c] ^ T3[d] ^ k, from 4 or 2 tables */
+template <bool FOUR>
+GCM_HD uint32_t aes_col(const uint8_t *lds, uint32_t lanesel, uint32_t sa, uint32_t sb, uint32_t sc, uint32_t sd, uint32_t k)
+{
+#define GCM_TA(x, kk) perm((x), lanesel, 0x0c0c0400u | ((4u + (kk)) << 8))
+#define GCM_TB(x, kk) perm((x), lanesel, 0x0c020400u | ((4u + (kk)) << 8))
+    if (FOUR)
+        return xor3(xor3(lds_u32(lds, GCM_TA(sa, 0)), lds_u32(lds, GCM_TA(sb, 1) + 128), k), lds_u32(lds, GCM_TB(sc, 2)),
+                    lds_u32(lds, GCM_TB(sd, 3) + 128));
+    /* T2 = rotl16(T0), T3 = rotl16(T1): rotate the XOR of the two reads once */
+    return xor3(lds_u32(lds, GCM_TA(sa, 0)), lds_u32(lds, GCM_TA(sb, 1) + 128),
+                k ^ rotl32(lds_u32(lds, GCM_TA(sc, 2)) ^ lds_u32(lds, GCM_TA(sd, 3) + 128), 16));
+#undef GCM_TA
+#undef GCM_TB
+}
+
+template <int NR, bool FOUR = true>
 GCM_HD void aes_encrypt_tt(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk, uint32_t w[4])
 {
-    /* address of byte k of word x: (x.b_k << 8) | lanesel */
-#define GCM_TADDR(x, k) perm((x), lanesel, 0x0c0c0400u | ((4u + (k)) << 8))
+    /* address of byte k of word x in image A: (x.b_k << 8) | lane bank; image B adds byte 2 of lanesel */
+#define GCM_TA(x, k) perm((x), lanesel, 0x0c0c0400u | ((4u + (k)) << 8))
+#define GCM_TB(x, k) perm((x), lanesel, 0x0c020400u | ((4u + (k)) << 8))
     uint32_t s0 = w[0] ^ rk[0], s1 = w[1] ^ rk[1], s2 = w[2] ^ rk[2], s3 = w[3] ^ rk[3];
 #pragma unroll
     for (int r = 1; r < NR; ++r) {
         const uint32_t *k = rk + 4 * r;
-        uint32_t a0 = GCM_TADDR(s0, 0), a1 = GCM_TADDR(s1, 1), a2 = GCM_TADDR(s2, 2), a3 = GCM_TADDR(s3, 3);
-        uint32_t b0 = GCM_TADDR(s1, 0), b1 = GCM_TADDR(s2, 1), b2 = GCM_TADDR(s3, 2), b3 = GCM_TADDR(s0, 3);
-        uint32_t c0 = GCM_TADDR(s2, 0), c1 = GCM_TADDR(s3, 1), c2 = GCM_TADDR(s0, 2), c3 = GCM_TADDR(s1, 3);
-        uint32_t d0 = GCM_TADDR(s3, 0), d1 = GCM_TADDR(s0, 1), d2 = GCM_TADDR(s1, 2), d3 = GCM_TADDR(s2, 3);
-        /* T0 at +0, T1 at +128 within a row; T2 = rotl16(T0), T3 = rotl16(T1) */
-        uint32_t n0 = lds_u32(lds, a0) ^ lds_u32(lds, a1 + 128) ^ rotl32(lds_u32(lds, a2), 16) ^
-                      rotl32(lds_u32(lds, a3 + 128), 16) ^ k[0];
-        uint32_t n1 = lds_u32(lds, b0) ^ lds_u32(lds, b1 + 128) ^ rotl32(lds_u32(lds, b2), 16) ^
-                      rotl32(lds_u32(lds, b3 + 128), 16) ^ k[1];
-        uint32_t n2 = lds_u32(lds, c0) ^ lds_u32(lds, c1 + 128) ^ rotl32(lds_u32(lds, c2), 16) ^
-                      rotl32(lds_u32(lds, c3 + 128), 16) ^ k[2];
-        uint32_t n3 = lds_u32(lds, d0) ^ lds_u32(lds, d1 + 128) ^ rotl32(lds_u32(lds, d2), 16) ^
-                      rotl32(lds_u32(lds, d3 + 128), 16) ^ k[3];
+        /* column j: T0[s_j.b0] ^ T1[s_{j+1}.b1] ^ T2[s_{j+2}.b2] ^ T3[s_{j+3}.b3] ^ rk */
+        uint32_t n0 = aes_col<FOUR>(lds, lanesel, s0, s1, s2, s3, k[0]);
+        uint32_t n1 = aes_col<FOUR>(lds, lanesel, s1, s2, s3, s0, k[1]);
+        uint32_t n2 = aes_col<FOUR>(lds, lanesel, s2, s3, s0, s1, k[2]);
+        uint32_t n3 = aes_col<FOUR>(lds, lanesel, s3, s0, s1, s2, k[3]);
         s0 = n0;
         s1 = n1;
         s2 = n2;
@@ -160,21 +229,86 @@ GCM_HD void aes_encrypt_tt(const uint8_t *lds, uint32_t lanesel, const uint32_t 
         uint32_t x[4] = {s0, s1, s2, s3};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            uint32_t ra = lds_u32(lds, GCM_TADDR(x[j], 0));
-            uint32_t rb = lds_u32(lds, GCM_TADDR(x[(j + 1) & 3], 1));
-            uint32_t rc = lds_u32(lds, GCM_TADDR(x[(j + 2) & 3], 2));
-            uint32_t rd = lds_u32(lds, GCM_TADDR(x[(j + 3) & 3], 3));
+            uint32_t ra = lds_u32(lds, GCM_TA(x[j], 0));
+            uint32_t rb = lds_u32(lds, GCM_TA(x[(j + 1) & 3], 1));
+            uint32_t rc = lds_u32(lds, GCM_TA(x[(j + 2) & 3], 2));
+            uint32_t rd = lds_u32(lds, GCM_TA(x[(j + 3) & 3], 3));
             uint32_t lo = perm(rb, ra, 0x0c0c0501u); /* S_a -> byte 0, S_b -> byte 1 */
             uint32_t hi = perm(rd, rc, 0x06020c0cu); /* S_c -> byte 2, S_d -> byte 3 */
-            w[j] = lo ^ hi ^ k[j];
+            w[j] = xor3(lo, hi, k[j]);
         }
     }
-#undef GCM_TADDR
+#undef GCM_TA
+#undef GCM_TB
+}
+
+/*
+ * Four of the 32 nibble-table reads of a GHASH multiply (dword d, nibble pairs m0, m0+1):
+ * P ^= Tab[8d+2m][lo.b_m] ^ Tab[8d+2m+1][hi.b_m].  Used to spread one multiply over the
+ * AES rounds so a wave always has independent LDS reads in flight.
+ */
+GCM_HD void ghash_quarter(const uint8_t *lds, uint32_t basereg, uint32_t w, int d, int m0, u32x4 &P)
+{
+    uint32_t lo = (w << 4) & 0xf0f0f0f0u, hi = w & 0xf0f0f0f0u;
+#pragma unroll
+    for (int m = m0; m < m0 + 2; ++m) {
+        uint32_t sel = 0x0c020100u | (4u + (uint32_t)m);
+        u32x4 e = lds_u32x4(lds, perm(lo, basereg, sel) + (uint32_t)(8 * d + 2 * m) * 256u);
+        u32x4 f = lds_u32x4(lds, perm(hi, basereg, sel) + (uint32_t)(8 * d + 2 * m + 1) * 256u);
+        P[0] = xor3_pinned(P[0], e[0], f[0]);
+        P[1] = xor3_pinned(P[1], e[1], f[1]);
+        P[2] = xor3_pinned(P[2], e[2], f[2]);
+        P[3] = xor3_pinned(P[3], e[3], f[3]);
+    }
+}
+
+/*
+ * AES of w (in place) fused with P = A * c (nibble tables of c at basereg): the GHASH reads are
+ * independent of the AES chain and are issued in rounds 1..8, four per round, so each wave keeps
+ * ~20 LDS reads in flight per round instead of 16.  Bit-identical to aes_encrypt_tt + ghash_mul_lds.
+ */
+template <int NR, bool FOUR = true>
+GCM_HD u32x4 aes_ghash_fused(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk, uint32_t w[4], uint32_t basereg, u32x4 A)
+{
+#define GCM_TA(x, k) perm((x), lanesel, 0x0c0c0400u | ((4u + (k)) << 8))
+#define GCM_TB(x, k) perm((x), lanesel, 0x0c020400u | ((4u + (k)) << 8))
+    u32x4 P = {0u, 0u, 0u, 0u};
+    uint32_t s0 = w[0] ^ rk[0], s1 = w[1] ^ rk[1], s2 = w[2] ^ rk[2], s3 = w[3] ^ rk[3];
+#pragma unroll
+    for (int r = 1; r < NR; ++r) {
+        const uint32_t *k = rk + 4 * r;
+        uint32_t n0 = aes_col<FOUR>(lds, lanesel, s0, s1, s2, s3, k[0]);
+        uint32_t n1 = aes_col<FOUR>(lds, lanesel, s1, s2, s3, s0, k[1]);
+        uint32_t n2 = aes_col<FOUR>(lds, lanesel, s2, s3, s0, s1, k[2]);
+        uint32_t n3 = aes_col<FOUR>(lds, lanesel, s3, s0, s1, s2, k[3]);
+        if (r <= 8)
+            ghash_quarter(lds, basereg, A[(r - 1) >> 1], (r - 1) >> 1, ((r - 1) & 1) * 2, P);
+        GCM_SCHED_FENCE();
+        s0 = n0;
+        s1 = n1;
+        s2 = n2;
+        s3 = n3;
+    }
+    {
+        const uint32_t *k = rk + 4 * NR;
+        uint32_t x[4] = {s0, s1, s2, s3};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint32_t ra = lds_u32(lds, GCM_TA(x[j], 0));
+            uint32_t rb = lds_u32(lds, GCM_TA(x[(j + 1) & 3], 1));
+            uint32_t rc = lds_u32(lds, GCM_TA(x[(j + 2) & 3], 2));
+            uint32_t rd = lds_u32(lds, GCM_TA(x[(j + 3) & 3], 3));
+            w[j] = xor3(perm(rb, ra, 0x0c0c0501u), perm(rd, rc, 0x06020c0cu), k[j]);
+        }
+    }
+    return P;
+#undef GCM_TA
+#undef GCM_TB
 }
 
 /*
  * r = x * c with the nibble tables of c at LDS byte offset (base: bytes 1..2 of basereg, a multiple of
- * 256 in [64K, 128K)).  32 conflict-free ds_read_b128 + ~110 VALU.
+ * 256 in [128K, 160K)).  32 conflict-free ds_read_b128 + ~108 VALU.
  */
 GCM_HD u32x4 ghash_mul_lds(const uint8_t *lds, uint32_t basereg, u32x4 x)
 {
@@ -188,8 +322,12 @@ GCM_HD u32x4 ghash_mul_lds(const uint8_t *lds, uint32_t basereg, u32x4 x)
         for (int m = 0; m < 4; ++m) {
             uint32_t sel = 0x0c020100u | (4u + (uint32_t)m);
             uint32_t alo = perm(lo, basereg, sel), ahi = perm(hi, basereg, sel);
-            r ^= lds_u32x4(lds, alo + (uint32_t)(8 * d + 2 * m) * 256u);
-            r ^= lds_u32x4(lds, ahi + (uint32_t)(8 * d + 2 * m + 1) * 256u);
+            u32x4 e = lds_u32x4(lds, alo + (uint32_t)(8 * d + 2 * m) * 256u);
+            u32x4 f = lds_u32x4(lds, ahi + (uint32_t)(8 * d + 2 * m + 1) * 256u);
+            r[0] = xor3(r[0], e[0], f[0]);
+            r[1] = xor3(r[1], e[1], f[1]);
+            r[2] = xor3(r[2], e[2], f[2]);
+            r[3] = xor3(r[3], e[3], f[3]);
         }
     }
     return r;
@@ -391,11 +529,14 @@ GCM_HD int build_key_image(const uint8_t *sbox, const uint8_t *key, uint32_t key
  */
 GCM_HD void fill_lds(uint8_t *lds, const uint32_t *t0, const KeyImage *ki, uint32_t K, uint32_t tid, uint32_t nthr)
 {
-    for (uint32_t i = tid; i < LDS_AES_BYTES / 16; i += nthr) {
-        uint32_t off = i * 16, x = off >> 8;
+    const uint32_t aes_bytes = K <= 4 ? 0x20000u : 0x10000u, gh_base = aes_bytes;
+    for (uint32_t i = tid; i < aes_bytes / 16; i += nthr) {
+        uint32_t off = i * 16, x = (off >> 8) & 0xffu;
         uint32_t v = t0[x];
-        if (off & 128)
-            v = rotl32(v, 8);
+        /* image A: T0 | T1, image B: T2 | T3;  T_i = rotl(T0, 8 i) */
+        uint32_t rot = ((off & 0x10000u) ? 16u : 0u) + ((off & 128u) ? 8u : 0u);
+        if (rot)
+            v = rotl32(v, (int)rot);
         u32x4 q = {v, v, v, v};
         *(u32x4 *)(lds + LDS_AES_BASE + off) = q;
     }
@@ -403,7 +544,7 @@ GCM_HD void fill_lds(uint8_t *lds, const uint32_t *t0, const KeyImage *ki, uint3
     for (uint32_t i = tid; i < nvec; i += nthr) {
         uint32_t slot = i / (GH_TABLE_BYTES / 16), within = i % (GH_TABLE_BYTES / 16);
         const u32x4 *srcv = (const u32x4 *)ki->gh[K - slot - 1];
-        *(u32x4 *)(lds + LDS_GH_BASE + slot * GH_TABLE_BYTES + within * 16) = srcv[within];
+        *(u32x4 *)(lds + gh_base + slot * GH_TABLE_BYTES + within * 16) = srcv[within];
     }
 }
 
@@ -436,25 +577,92 @@ GCM_HD u32x4 mask_tail(u32x4 v, uint32_t n)
     return v;
 }
 
+/* byte shift of a 16-byte block towards byte 0: out.b_i = v.b_(i+n), zero-filled; 0 <= n < 16 */
+GCM_HD u32x4 shr_bytes(u32x4 v, uint32_t n)
+{
+    const uint32_t q = n >> 2, r = n & 3u;
+    uint32_t w0 = q == 0 ? v[0] : q == 1 ? v[1] : q == 2 ? v[2] : v[3];
+    uint32_t w1 = q == 0 ? v[1] : q == 1 ? v[2] : q == 2 ? v[3] : 0u;
+    uint32_t w2 = q == 0 ? v[2] : q == 1 ? v[3] : 0u;
+    uint32_t w3 = q == 0 ? v[3] : 0u;
+#if defined(__HIP_DEVICE_COMPILE__)
+    u32x4 o = {__builtin_amdgcn_alignbyte(w1, w0, r), __builtin_amdgcn_alignbyte(w2, w1, r),
+               __builtin_amdgcn_alignbyte(w3, w2, r), __builtin_amdgcn_alignbyte(0u, w3, r)};
+#else
+    auto ab = [](uint32_t hi, uint32_t lo, uint32_t rr) {
+        return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * rr));
+    };
+    u32x4 o = {ab(w1, w0, r), ab(w2, w1, r), ab(w3, w2, r), ab(0u, w3, r)};
+#endif
+    return o;
+}
+
 /*
  * One lane's share of one record (see struct Walk).  Returns the lane's partial GHASH already
  * scaled by H^(K-j); the lane holding the length block has E_K(J0) folded in, so the XOR of the
  * K returned values is the tag.  Lanes with valid == false run the same instruction stream
  * without touching memory (Tmax is the wave-wide trip count).
  * iv0..iv2: the record's 96-bit nonce as LE dwords.
+ *
+ * Memory pipeline: every step issues at most ONE full 16-byte load (the block of the NEXT
+ * step, so its latency hides under this step's AES + GHASH) and at most one 16-byte store.
+ * Byte-granular reads happen only at record setup: a partial AAD block, and a sealed
+ * payload shorter than 16 bytes.  A partial last payload block of a longer record is read
+ * as the record's last 16 bytes and shifted in registers (seal), or read directly since the
+ * tag follows it (open) -- nothing is ever read outside [src, src + len (+16 for open)).
  */
 template <int NR, int K, bool SEAL>
 GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk, uint32_t j, const Record &rec, bool valid,
                        uint32_t Tmax, uint32_t iv0, uint32_t iv1, uint32_t iv2, const uint8_t *src, uint8_t *dst,
-                       const uint8_t *aad)
+                       const uint8_t *aad, const uint8_t *dummy)
 {
     const Walk wk = make_walk(rec.len, rec.aadlen, K);
     const uint8_t *in = src + rec.src;
     uint8_t *out = dst + rec.dst;
     const uint8_t *ad = aad + rec.aad;
+    const uint32_t arem = rec.aadlen & 15u;
     u32x4 acc = {0u, 0u, 0u, 0u}, ek0 = {0u, 0u, 0u, 0u};
 
-    for (uint32_t t = 0; t < Tmax; ++t) {
+    /* step at which this lane meets position p, or ~0 */
+    auto step_of = [&](uint32_t pos) -> uint32_t {
+        uint32_t q = pos + wk.pad;
+        return (q % K == j) ? q / K : 0xffffffffu;
+    };
+    /* setup-time byte reads (the only ones) */
+    u32x4 aad_tail = {0u, 0u, 0u, 0u}, short_pay = {0u, 0u, 0u, 0u};
+    if (valid && arem != 0u && step_of(wk.A - 1u) != 0xffffffffu)
+        aad_tail = load_partial(ad + 16u * (wk.A - 1u), arem);
+    if (SEAL && valid && rec.len != 0u && rec.len < 16u && step_of(wk.A) != 0xffffffffu)
+        short_pay = load_partial(in, rec.len);
+
+    /*
+     * Address of the 16-byte load of step t.  The load is issued unconditionally (steps with
+     * nothing to read load 16 harmless bytes at `dummy`): with a load in every step the
+     * compiler can wait with vmcnt(1) for the current block while the next one is in flight,
+     * instead of vmcnt(0).
+     */
+    auto fetch_ptr = [&](uint32_t t) -> const uint8_t * {
+        if (!valid || t >= wk.T)
+            return dummy;
+        const int32_t p = (int32_t)(j + K * t) - (int32_t)wk.pad;
+        if (p < 0)
+            return dummy;
+        if ((uint32_t)p < wk.A)
+            return 16u * (uint32_t)p + 16u <= rec.aadlen ? ad + 16u * (uint32_t)p : dummy;
+        const uint32_t c = (uint32_t)p - wk.A;
+        if (c >= wk.C)
+            return dummy;
+        if (!SEAL || 16u * c + 16u <= rec.len)
+            return in + 16u * c;
+        return rec.len >= 16u ? in + rec.len - 16u : dummy;
+    };
+
+    /*
+     * Horner with factor H^K, software-pipelined: in step t the multiply of the previous
+     * value, P = A_(t-1) * H^K, runs inside the AES of step t (aes_ghash_fused), then
+     * A_t = P ^ X_t.  A_(-1) = 0, and A_(T-1) is the lane's sum.
+     */
+    auto step = [&](uint32_t t, u32x4 cur) {
         const bool active = valid && t < wk.T;
         const int32_t p = (int32_t)(j + K * t) - (int32_t)wk.pad;
         const bool is_aad = active && p >= 0 && (uint32_t)p < wk.A;
@@ -463,35 +671,37 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
         const uint32_t c = (uint32_t)p - wk.A;
         const uint32_t clen = rec.len - 16u * c; /* bytes of this payload block if < 16 */
 
-        u32x4 X = {0u, 0u, 0u, 0u}, data = {0u, 0u, 0u, 0u};
-        if (is_pay) {
-            if (clen >= 16)
-                data = *(const u32x4_u *)(in + 16u * c);
-            else
-                data = load_partial(in + 16u * c, clen);
-        } else if (is_aad) {
-            uint32_t alen = rec.aadlen - 16u * (uint32_t)p;
-            if (alen >= 16)
-                X = *(const u32x4_u *)(ad + 16u * (uint32_t)p);
-            else
-                X = load_partial(ad + 16u * (uint32_t)p, alen);
-        }
-
         /* one AES per lane per step: payload counter c + 2, otherwise J0 (counter 1) */
         uint32_t ctr = is_pay ? c + 2u : 1u;
         uint32_t w[4] = {iv0, iv1, iv2, bswap32(ctr)};
-        aes_encrypt_tt<NR>(lds, lanesel, rk, w);
-        u32x4 ks = {w[0], w[1], w[2], w[3]};
+#if GCM_ABLATE_AES && GCM_ABLATE_GHASH
+        const u32x4 P = acc;
+#elif GCM_ABLATE_AES
+        const u32x4 P = ghash_mul_lds(lds, Layout<K>::gh_base, acc);
+#elif GCM_ABLATE_GHASH
+        aes_encrypt_tt<NR, Layout<K>::four_tables>(lds, lanesel, rk, w);
+        const u32x4 P = acc;
+#else
+        const u32x4 P = aes_ghash_fused<NR, Layout<K>::four_tables>(lds, lanesel, rk, w, Layout<K>::gh_base, acc);
+#endif
+        const u32x4 ks = {w[0], w[1], w[2], w[3]};
 
+        u32x4 X = {0u, 0u, 0u, 0u};
         if (is_pay) {
-            u32x4 o = data ^ ks;
-            if (clen >= 16) {
+            u32x4 data = cur;
+            if (clen >= 16u) {
+                const u32x4 o = data ^ ks;
                 *(u32x4_u *)(out + 16u * c) = o;
                 X = SEAL ? o : data;
             } else {
+                if (SEAL)
+                    data = rec.len >= 16u ? shr_bytes(data, 16u - clen) : short_pay;
+                const u32x4 o = data ^ ks;
                 store_partial(out + 16u * c, clen, o);
-                X = SEAL ? mask_tail(o, clen) : data;
+                X = mask_tail(SEAL ? o : data, clen);
             }
+        } else if (is_aad) {
+            X = 16u * (uint32_t)p + 16u <= rec.aadlen ? cur : aad_tail;
         } else if (is_len) {
             uint64_t abits = (uint64_t)rec.aadlen * 8u, cbits = (uint64_t)rec.len * 8u;
             X[0] = bswap32((uint32_t)(abits >> 32));
@@ -500,14 +710,25 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
             X[3] = bswap32((uint32_t)cbits);
             ek0 = ks;
         }
-        if (active) {
-            acc ^= X;
-            if (t + 1 < wk.T)
-                acc = ghash_mul_lds(lds, LDS_GH_BASE, acc);
-        }
+        if (active)
+            acc = P ^ X;
+    };
+
+    /*
+     * Two steps per trip with two load buffers: the block of step t+1 is in flight during step
+     * t and the load of step t+2 reuses the registers step t has just consumed, so no register
+     * copy (and no vmcnt(0) behind the step's own store) sits on the loop back-edge.
+     */
+    u32x4 bufA = *(const u32x4_u *)fetch_ptr(0);
+    for (uint32_t t = 0; t < Tmax; t += 2u) {
+        const u32x4 bufB = *(const u32x4_u *)fetch_ptr(t + 1u);
+        step(t, bufA);
+        bufA = *(const u32x4_u *)fetch_ptr(t + 2u);
+        if (t + 1u < Tmax)
+            step(t + 1u, bufB);
     }
     /* scale by H^(K-j): table slot j */
-    acc = ghash_mul_lds(lds, LDS_GH_BASE + j * GH_TABLE_BYTES, acc);
+    acc = ghash_mul_lds(lds, Layout<K>::gh_base + j * GH_TABLE_BYTES, acc);
     return acc ^ ek0;
 }
 

@@ -9,8 +9,9 @@
  *   ptls_fusion_aesecb_encrypt (lib/fusion.c:747-752) -> mi355x_aes_ecb
  *
  * Kernel design: one persistent workgroup of 16 waves per CU; LDS holds a
- * bank-replicated AES T-table image (64 KiB) and the K nibble tables of H^K..H^1 (8 KiB
- * each); round keys are wave-uniform and live in SGPRs.  A wave processes 64/K records at a
+ * bank-replicated AES T-table image and the K nibble tables of H^K..H^1 (8 KiB each); K = 8
+ * makes each wave-wide load/store cover whole 128-byte lines (K = 4, 64-byte pieces, is
+ * the default: its four-table AES needs fewer VALU ops); round keys are wave-uniform and live in SGPRs.  A wave processes 64/K records at a
  * time, K lanes per record; lane j hashes padded GHASH positions j, j+K, ... (Horner with
  * H^K), runs the AES-CTR block of the ciphertext position it hashes, and the K partial sums
  * are scaled by H^(K-j) and XOR-reduced with cross-lane shuffles.  Every 16-byte block is
@@ -32,7 +33,10 @@ __constant__ AesTables c_tabs = AesTables();
 
 namespace {
 
-constexpr int WG_THREADS = 1024; /* 16 waves: 4 per SIMD */
+#ifndef MI355X_WG_THREADS
+#define MI355X_WG_THREADS 1024
+#endif
+constexpr int WG_THREADS = MI355X_WG_THREADS; /* 16 waves: 4 per SIMD */
 
 __device__ __forceinline__ uint32_t shfl_xor_u32(uint32_t v, int mask) { return (uint32_t)__shfl_xor((int)v, mask, 64); }
 
@@ -51,7 +55,8 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
                                                const Record *__restrict__ recs, uint32_t nrecs, const uint8_t *src,
                                                uint8_t *dst, const uint8_t *__restrict__ aad, uint32_t *__restrict__ status)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_AES_BYTES + K * GH_TABLE_BYTES];
+    static_assert(K <= MAX_KERNEL_K, "LDS holds at most MAX_KERNEL_K GHASH tables");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[Layout<K>::total];
     constexpr uint32_t R = 64 / K; /* records per wave step */
 
     fill_lds(lds, c_tabs.t0, ki, K, threadIdx.x, blockDim.x);
@@ -64,7 +69,7 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
 
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t j = lane % K, slot = lane / K;
-    const uint32_t lanesel = (lane & 31u) * 4u;
+    const uint32_t lanesel = (lane & 31u) * 4u | 0x10000u; /* bank + image-B select (gcm_core.h) */
     const uint32_t waves_per_block = blockDim.x >> 6;
     const uint64_t ngroups = ((uint64_t)nrecs + R - 1) / R;
     const uint64_t stride = (uint64_t)gridDim.x * waves_per_block;
@@ -82,7 +87,9 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
             Tmax = max(Tmax, shfl_xor_u32(Tmax, o));
 
         const uint32_t n1 = iv1 ^ bswap32((uint32_t)(rec.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)rec.seq);
-        u32x4 part = lane_walk<NR, K, SEAL>(lds, lanesel, rk, j, rec, valid, Tmax, iv0, n1, n2, src, dst, aad);
+        /* 16 always-readable bytes for idle prefetch slots: the first descriptor (40 B, nrecs >= 1) */
+        const uint8_t *dummy = (const uint8_t *)recs;
+        u32x4 part = lane_walk<NR, K, SEAL>(lds, lanesel, rk, j, rec, valid, Tmax, iv0, n1, n2, src, dst, aad, dummy);
 #pragma unroll
         for (int o = 1; o < K; o <<= 1)
             part ^= shfl_xor_u32x4(part, o);

@@ -1,0 +1,114 @@
+"""Kernel ablations / variants, timed in ONE process with interleaved rounds.
+
+    python scripts/ablate.py build            # CPU: builds the variant libraries (hipcc)
+    python scripts/ablate.py run [--workload 1400|16k-aes128] [--rounds 5]   # GPU
+
+Each variant is the engine library compiled with extra -D flags (see VARIANTS).  Ablated
+variants (no AES / no GHASH) produce wrong output; only their kernel times are used, to
+locate the bottleneck (cdna_hip_programming.md sec. 7, "The diagnostic loop").
+"""
+import ctypes as C
+import json
+import os
+import statistics
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+VDIR = os.path.join(ROOT, "rapido_amd", "_lib", "variants")
+
+VARIANTS = {
+    "base": [],
+    "wg512": ["-DMI355X_WG_THREADS=512"],
+    "no_ghash": ["-DGCM_ABLATE_GHASH=1"],
+    "no_aes": ["-DGCM_ABLATE_AES=1"],
+    "no_both": ["-DGCM_ABLATE_AES=1", "-DGCM_ABLATE_GHASH=1"],
+}
+if os.environ.get("ABLATE_VARIANTS"):
+    VARIANTS = {k: v for k, v in VARIANTS.items() if k in os.environ["ABLATE_VARIANTS"].split(",")}
+
+
+def build():
+    from rapido_amd import build as b
+    os.makedirs(VDIR, exist_ok=True)
+    b.build_engine()
+    c_obj = os.path.join(b.OBJDIR, "aead_slot.o")
+    for name, flags in VARIANTS.items():
+        obj = os.path.join(VDIR, name + ".o")
+        so = os.path.join(VDIR, name + ".so")
+        src = os.path.join(b.CSRC, "gcm_engine.hip")
+        subprocess.run([b.HIPCC, f"--offload-arch={b.ARCH}", "-O3", "-std=c++17", "-fPIC", *flags, "-c", src, "-o", obj],
+                       check=True)
+        subprocess.run([b.HIPCC, f"--offload-arch={b.ARCH}", "-shared", "-fPIC", "-o", so, obj, c_obj], check=True)
+        print("built", so)
+
+
+def run(workload="1400", rounds=5, lanes=4):
+    import numpy as np
+    import torch
+    from rapido_amd import records
+
+    n, length, keylen = {"1400": (1 << 20, 1400, 16), "16k-aes128": (1 << 18, 16384, 16),
+                         "16k": (1 << 18, 16384, 32)}[workload]
+    lengths = np.full(n, length, dtype=np.uint64)
+    recs, src_bytes, aad_bytes = records.layout(lengths, np.full(n, 5, dtype=np.uint64), align=256)
+    aad = np.zeros(aad_bytes, dtype=np.uint8)
+    aad[: 5 * n] = records.tls_aad(lengths)
+    dev = torch.device("cuda:0")
+    d_src = torch.randint(0, 256, (src_bytes,), dtype=torch.uint8, device=dev)
+    d_ct, d_pt = torch.zeros_like(d_src), torch.zeros_like(d_src)
+    d_recs = torch.from_numpy(recs.view(np.uint8)).to(dev)
+    d_aad = torch.from_numpy(aad).to(dev)
+    d_st = torch.zeros(n, dtype=torch.int32, device=dev)
+    iv = C.create_string_buffer(bytes(range(12)), 12)
+    key = C.create_string_buffer(bytes(range(keylen)), keylen)
+    vp, sz = C.c_void_p, C.c_size_t
+    libs = {}
+    for name in VARIANTS:
+        L = C.CDLL(os.path.join(VDIR, name + ".so"), mode=C.RTLD_LOCAL)
+        L.ptls_mi355x_aesgcm_new.argtypes = [vp, sz, sz]
+        L.ptls_mi355x_aesgcm_new.restype = vp
+        L.ptls_mi355x_seal_batch.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp]
+        L.ptls_mi355x_open_batch.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]
+        L.ptls_mi355x_set_lanes_per_record(lanes)
+        libs[name] = (L, L.ptls_mi355x_aesgcm_new(key, keylen, 0))
+    stream = torch.cuda.current_stream().cuda_stream
+    res = {name: {"seal": [], "open": []} for name in VARIANTS}
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    for r in range(rounds + 1):
+        for name, (L, ctx) in libs.items():
+            ev[0].record()
+            L.ptls_mi355x_seal_batch(ctx, iv, d_recs.data_ptr(), n, d_src.data_ptr(), d_ct.data_ptr(), d_aad.data_ptr(),
+                                     stream)
+            ev[1].record()
+            L.ptls_mi355x_open_batch(ctx, iv, d_recs.data_ptr(), n, d_ct.data_ptr(), d_pt.data_ptr(), d_aad.data_ptr(),
+                                     d_st.data_ptr(), stream)
+            ev[2].record()
+            torch.cuda.synchronize()
+            if r:  # round 0 is warmup
+                res[name]["seal"].append(ev[0].elapsed_time(ev[1]))
+                res[name]["open"].append(ev[1].elapsed_time(ev[2]))
+    out = {}
+    for name, d in res.items():
+        s, o = statistics.median(d["seal"]), statistics.median(d["open"])
+        gib = n * length / 2 ** 30
+        out[name] = {"seal_ms": round(s, 4), "open_ms": round(o, 4), "seal_gibps": round(gib / (s / 1e3), 1),
+                     "open_gibps": round(gib / (o / 1e3), 1)}
+        print(f"{workload:10s} K={lanes} {name:12s} seal {s:7.3f} ms {gib / (s / 1e3):8.1f} GiB/s   open {o:7.3f} ms "
+              f"{gib / (o / 1e3):8.1f} GiB/s", flush=True)
+    return out
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "build":
+        build()
+    else:
+        import argparse
+        ap = argparse.ArgumentParser()
+        ap.add_argument("cmd")
+        ap.add_argument("--workload", default="1400")
+        ap.add_argument("--rounds", type=int, default=5)
+        ap.add_argument("--lanes", type=int, default=4)
+        a = ap.parse_args()
+        print(json.dumps(run(a.workload, a.rounds, a.lanes)))

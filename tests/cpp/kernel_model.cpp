@@ -35,7 +35,8 @@ static void run(const KeyImage *ki, const uint8_t *lds, const uint8_t *static_iv
             memcpy(&rx, src + r.src + r.len, 16);
         u32x4 tag = {0, 0, 0, 0};
         for (uint32_t j = 0; j < (uint32_t)K; ++j)
-            tag ^= lane_walk<NR, K, SEAL>(lds, 4u * (j & 31u), ki->rk, j, r, true, wk.T, iv0, n1, n2, src, dst, aad);
+            tag ^= lane_walk<NR, K, SEAL>(lds, 4u * (j & 31u) | 0x10000u, ki->rk, j, r, true, wk.T, iv0, n1, n2, src, dst, aad,
+                                          (const uint8_t *)recs);
         if (SEAL) {
             memcpy(dst + r.dst + r.len, &tag, 16);
         } else {
@@ -50,7 +51,7 @@ extern "C" int model_batch(int is_seal, int K, const uint8_t *key, size_t keylen
                            uint32_t *status)
 {
     KeyImage *ki = (KeyImage *)aligned_alloc(64, sizeof(KeyImage));
-    uint8_t *lds = (uint8_t *)aligned_alloc(256, LDS_AES_BYTES + MAX_K * GH_TABLE_BYTES);
+    uint8_t *lds = (uint8_t *)aligned_alloc(256, 160u * 1024u);
     if (build_key_image(kTabs.sbox, key, (uint32_t)keylen, ki) != 0) {
         free(ki);
         free(lds);
