@@ -42,6 +42,26 @@ WORKLOADS = {
 }
 
 
+def rank_shard(rank: int, world: int, n_per_rank: int):
+    """Weak-scaling shard of rank `rank`: records [rank*n, (rank+1)*n) of the global batch (configs[4]:
+    8 M x 1400 B over 8 GPUs = 1 M per GPU).  Returns (first global record index == first seq, count).
+    Records are independent, so shards need no exchange."""
+    if not 0 <= rank < world:
+        raise ValueError("bad rank")
+    return rank * n_per_rank, n_per_rank
+
+
+def max_over_ranks(value: float, device=None) -> float:
+    """Max of a per-rank float over the process group (the contract's max-over-ranks timing)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def algorithmic_bytes(lengths_sum: int, n: int, aad_sum: int, seal: bool) -> int:
     """seal: read L + aad + descriptor, write L + 16; open: read L + 16 + aad + descriptor, write L + 4."""
     if seal:
@@ -127,7 +147,8 @@ def main() -> None:
     else:
         lengths = np.full(n, wl["length"], dtype=np.uint64)
     recs, src_bytes, aad_bytes = records.layout(lengths, np.full(n, 5, dtype=np.uint64), align=256)
-    recs["seq"] = np.arange(n, dtype=np.uint64) + np.uint64(rank) * np.uint64(n)
+    first, n = rank_shard(rank, world, n)
+    recs["seq"] = np.arange(n, dtype=np.uint64) + np.uint64(first)
     aad = np.zeros(aad_bytes, dtype=np.uint8)
     aad[: 5 * n] = records.tls_aad(lengths)
 
@@ -170,9 +191,7 @@ def main() -> None:
     elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = max_over_ranks(elapsed, dev)
 
     seal_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
     open_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in events]))

@@ -1,0 +1,117 @@
+"""CPU execution of the kernels' own code (rapido_amd/csrc/gcm_core.h via tests/cpp/kernel_model.cpp)
+against the oracle: T-table AES with bank-replicated v_perm addressing, nibble-table GHASH, the K-lane
+record walk with front padding, software-pipelined Horner, tail handling.  No GPU needed."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from rapido_amd import RECORD_DTYPE, records
+
+
+@pytest.fixture(scope="module")
+def model():
+    from rapido_amd import build
+    path = build.build_model()
+    lib = C.CDLL(path)
+    vp = C.c_void_p
+    lib.model_batch.argtypes = [C.c_int, C.c_int, vp, C.c_size_t, vp, vp, C.c_size_t, vp, vp, vp, vp]
+    lib.model_key_image.argtypes = [vp, C.c_size_t, vp, C.c_size_t]
+    lib.model_key_image_size.restype = C.c_size_t
+    return lib
+
+
+def run(lib, is_seal, K, key, iv, recs, src, dst, aad, st):
+    rc = lib.model_batch(1 if is_seal else 0, K, key, len(key), iv, recs.ctypes.data, len(recs), src.ctypes.data,
+                         dst.ctypes.data, aad.ctypes.data, st.ctypes.data)
+    assert rc == 0
+
+
+def batch(rng, n, max_len, max_aad, shift=True):
+    lens = rng.integers(0, max_len, n).astype(np.uint64)
+    aadlens = rng.integers(0, max_aad, n).astype(np.uint64)
+    for i, (l, a) in enumerate([(0, 0), (1, 0), (15, 1), (16, 16), (17, 15), (31, 17), (32, 32), (33, 5), (0, 13)]):
+        if i < n:
+            lens[i], aadlens[i] = l, a
+    recs, src_bytes, aad_bytes = records.layout(lens + 8, aadlens, align=1)
+    recs["len"] = lens.astype(np.uint32)
+    if shift:
+        recs["src"] += np.arange(n, dtype=np.uint64) % 7
+        recs["dst"] = recs["src"]
+    recs["seq"] = rng.integers(0, 2 ** 63, n, dtype=np.uint64)
+    return recs, rng.integers(0, 256, src_bytes, dtype=np.uint8), rng.integers(0, 256, aad_bytes, dtype=np.uint8)
+
+
+def spans(buf, recs, extra):
+    return [bytes(buf[int(r["dst"]): int(r["dst"]) + int(r["len"]) + extra]) for r in recs]
+
+
+@pytest.mark.parametrize("K", [1, 2, 4, 8])
+@pytest.mark.parametrize("keylen", [16, 32])
+def test_model_matches_oracle(model, K, keylen):
+    rng = np.random.default_rng(K * 100 + keylen)
+    recs, src, aad = batch(rng, 150, 700, 48)
+    key = rng.integers(0, 256, keylen, dtype=np.uint8).tobytes()
+    iv = rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    got, want = np.zeros_like(src), np.zeros_like(src)
+    st = np.zeros(len(recs), np.uint32)
+    run(model, True, K, key, iv, recs, src, got, aad, st)
+    oracle.batch(True, key, iv, recs, src, want, aad)
+    assert spans(got, recs, 16) == spans(want, recs, 16)
+    pt = np.zeros_like(src)
+    run(model, False, K, key, iv, recs, got, pt, aad, st)
+    assert (st == recs["len"]).all()
+    assert spans(pt, recs, 0) == [bytes(src[int(r["src"]): int(r["src"]) + int(r["len"])]) for r in recs]
+    got[int(recs[20]["dst"]) + 1] ^= 0x40
+    run(model, False, K, key, iv, recs, got, pt, aad, st)
+    assert st[20] == 0xFFFFFFFF and (np.delete(st, 20) == np.delete(recs["len"], 20)).all()
+
+
+def test_model_tls_records_all_sizes(model):
+    """Every TLS-ish length around block and lane boundaries, in place."""
+    lens = np.array(list(range(0, 70)) + [1399, 1400, 1401, 4095, 4096, 4097, 16383, 16384, 16385], dtype=np.uint64)
+    recs, src, aad = records.tls_batch(lens, seed=3, align=16)
+    key, iv = bytes(range(16)), bytes(range(12))
+    for K in (4, 8):
+        got = src.copy()
+        st = np.zeros(len(recs), np.uint32)
+        run(model, True, K, key, iv, recs, got, got, aad, st)  # in place
+        want = np.zeros_like(src)
+        oracle.batch(True, key, iv, recs, src, want, aad)
+        assert spans(got, recs, 16) == spans(want, recs, 16)
+
+
+def test_key_image_tables(model):
+    """The nibble tables in the key image equal H^p * (nibble basis element), via the oracle's multiply."""
+    size = model.model_key_image_size()
+    buf = C.create_string_buffer(size)
+    key = bytes(range(3, 19))
+    assert model.model_key_image(key, 16, buf, size) == 0
+    raw = buf.raw
+    H = raw[240 + 16: 240 + 32]
+    assert H == oracle.ecb(key, bytes(16))
+    gh = raw[272:]
+    rng = np.random.default_rng(1)
+    hp = H
+    for p in range(1, 9):
+        if p > 1:
+            hp = oracle.gf128_mul(hp, H)
+        tab = np.frombuffer(gh[(p - 1) * 8192: p * 8192], dtype=np.uint8).reshape(32, 16, 16)
+        for _ in range(8):
+            x = rng.integers(0, 256, 16, dtype=np.uint8)
+            acc = np.zeros(16, np.uint8)
+            words = x.view("<u4")
+            for t in range(32):
+                nib = (int(words[t // 8]) >> (4 * (t % 8))) & 0xF
+                acc ^= tab[t, nib]
+            assert acc.tobytes() == oracle.gf128_mul(x.tobytes(), hp)
+
+
+def test_record_dtype_matches_header():
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(__file__)), "include", "ptls_mi355x.h")).read()
+    body = hdr[hdr.index("typedef struct st_ptls_mi355x_record_t"):]
+    body = body[: body.index("}")]
+    fields = [ln.split(";")[0].split()[-1] for ln in body.splitlines() if ";" in ln]
+    assert fields == list(RECORD_DTYPE.names)
