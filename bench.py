@@ -166,14 +166,27 @@ def main() -> None:
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
 
+    ragged = wl["length"] is None
+    d_order = torch.zeros(n, dtype=torch.int32, device=dev)
+
     def step(ev=None):
         if ev is not None:
             ev[0].record(stream)
-        eng.seal_batch(iv, d_recs.data_ptr(), n, d_src.data_ptr(), d_ct.data_ptr(), d_aad.data_ptr(), sh)
+        if ragged:
+            # length-binned, longest-first schedule; the device sort is inside the timed step
+            eng.order_by_length(d_recs.data_ptr(), n, d_order.data_ptr(), sh)
+            eng.seal_batch_ordered(iv, d_recs.data_ptr(), d_order.data_ptr(), n, d_src.data_ptr(), d_ct.data_ptr(),
+                                   d_aad.data_ptr(), sh)
+        else:
+            eng.seal_batch(iv, d_recs.data_ptr(), n, d_src.data_ptr(), d_ct.data_ptr(), d_aad.data_ptr(), sh)
         if ev is not None:
             ev[1].record(stream)
-        eng.open_batch(iv, d_recs.data_ptr(), n, d_ct.data_ptr(), d_pt.data_ptr(), d_aad.data_ptr(),
-                       d_st.data_ptr(), sh)
+        if ragged:
+            eng.open_batch_ordered(iv, d_recs.data_ptr(), d_order.data_ptr(), n, d_ct.data_ptr(), d_pt.data_ptr(),
+                                   d_aad.data_ptr(), d_st.data_ptr(), sh)
+        else:
+            eng.open_batch(iv, d_recs.data_ptr(), n, d_ct.data_ptr(), d_pt.data_ptr(), d_aad.data_ptr(),
+                           d_st.data_ptr(), sh)
         if ev is not None:
             ev[2].record(stream)
 

@@ -156,6 +156,20 @@ int ptls_mi355x_seal_batch(ptls_mi355x_aesgcm_context_t *ctx, const void *static
 int ptls_mi355x_open_batch(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12, const ptls_mi355x_record_t *recs,
                            size_t n, const uint8_t *src, uint8_t *dst, const uint8_t *aad, uint32_t *status, void *stream);
 
+/* Ragged batches: same as above, but record i of the launch is recs[order[i]] (status is still
+ * indexed by descriptor).  ptls_mi355x_order_by_length() fills `order` (n device uint32) with the
+ * descriptor indices sorted by decreasing work (device radix sort on the stream), so each wave's
+ * records have similar lengths and the longest go first (the kernels hand out record groups
+ * dynamically).  The order can be reused for the matching open batch. */
+int ptls_mi355x_order_by_length(ptls_mi355x_aesgcm_context_t *ctx, const ptls_mi355x_record_t *recs, size_t n,
+                                uint32_t *order, void *stream);
+int ptls_mi355x_seal_batch_ordered(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12,
+                                   const ptls_mi355x_record_t *recs, const uint32_t *order, size_t n, const uint8_t *src,
+                                   uint8_t *dst, const uint8_t *aad, void *stream);
+int ptls_mi355x_open_batch_ordered(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12,
+                                   const ptls_mi355x_record_t *recs, const uint32_t *order, size_t n, const uint8_t *src,
+                                   uint8_t *dst, const uint8_t *aad, uint32_t *status, void *stream);
+
 /* ---- tuning / introspection ---- */
 /* lanes per record used by the batch kernels (1, 2, 4 or 8; default 4); returns the previous value, or -1 */
 int ptls_mi355x_set_lanes_per_record(int k);

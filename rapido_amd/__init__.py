@@ -41,7 +41,8 @@ assert RECORD_DTYPE.itemsize == 40
 EXPORTED_FUNCTIONS = (
     "ptls_mi355x_is_supported", "ptls_mi355x_aesgcm_new", "ptls_mi355x_aesgcm_free", "ptls_mi355x_aesgcm_device",
     "ptls_mi355x_aesgcm_encrypt", "ptls_mi355x_aesgcm_decrypt", "ptls_mi355x_aesecb_encrypt",
-    "ptls_mi355x_seal_batch", "ptls_mi355x_open_batch", "ptls_mi355x_set_lanes_per_record",
+    "ptls_mi355x_seal_batch", "ptls_mi355x_open_batch", "ptls_mi355x_order_by_length",
+    "ptls_mi355x_seal_batch_ordered", "ptls_mi355x_open_batch_ordered", "ptls_mi355x_set_lanes_per_record",
     "ptls_mi355x_get_lanes_per_record", "ptls_mi355x_kernel_name", "ptls_mi355x_last_error",
 )
 EXPORTED_OBJECTS = ("ptls_mi355x_aes128gcm", "ptls_mi355x_aes256gcm", "ptls_mi355x_aes128ctr",
@@ -110,6 +111,9 @@ def lib() -> C.CDLL:
         L.ptls_mi355x_aesecb_encrypt.argtypes = [vp, vp, vp, sz]
         L.ptls_mi355x_seal_batch.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp]
         L.ptls_mi355x_open_batch.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]
+        L.ptls_mi355x_order_by_length.argtypes = [vp, vp, sz, vp, vp]
+        L.ptls_mi355x_seal_batch_ordered.argtypes = [vp, vp, vp, vp, sz, vp, vp, vp, vp]
+        L.ptls_mi355x_open_batch_ordered.argtypes = [vp, vp, vp, vp, sz, vp, vp, vp, vp, vp]
         L.ptls_mi355x_set_lanes_per_record.argtypes = [C.c_int]
         L.ptls_mi355x_kernel_name.argtypes = [C.c_int, sz]
         L.ptls_mi355x_kernel_name.restype = C.c_char_p
@@ -303,6 +307,22 @@ class Engine:
         if lib().ptls_mi355x_seal_batch(self.handle, _cbuf(static_iv), recs_ptr, n, src_ptr, dst_ptr, aad_ptr,
                                         stream or None):
             raise RuntimeError("seal_batch failed: " + last_error())
+
+    def order_by_length(self, recs_ptr: int, n: int, order_ptr: int, stream: int = 0) -> None:
+        if lib().ptls_mi355x_order_by_length(self.handle, recs_ptr, n, order_ptr, stream or None):
+            raise RuntimeError("order_by_length failed: " + last_error())
+
+    def seal_batch_ordered(self, static_iv: bytes, recs_ptr: int, order_ptr: int, n: int, src_ptr: int, dst_ptr: int,
+                           aad_ptr: int, stream: int = 0) -> None:
+        if lib().ptls_mi355x_seal_batch_ordered(self.handle, _cbuf(static_iv), recs_ptr, order_ptr, n, src_ptr, dst_ptr,
+                                                aad_ptr, stream or None):
+            raise RuntimeError("seal_batch_ordered failed: " + last_error())
+
+    def open_batch_ordered(self, static_iv: bytes, recs_ptr: int, order_ptr: int, n: int, src_ptr: int, dst_ptr: int,
+                           aad_ptr: int, status_ptr: int, stream: int = 0) -> None:
+        if lib().ptls_mi355x_open_batch_ordered(self.handle, _cbuf(static_iv), recs_ptr, order_ptr, n, src_ptr, dst_ptr,
+                                                aad_ptr, status_ptr, stream or None):
+            raise RuntimeError("open_batch_ordered failed: " + last_error())
 
     def open_batch(self, static_iv: bytes, recs_ptr: int, n: int, src_ptr: int, dst_ptr: int, aad_ptr: int,
                    status_ptr: int, stream: int = 0) -> None:

@@ -21,6 +21,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <hipcub/hipcub.hpp>
 #include "gcm_core.h"
 #include "../../include/ptls_mi355x.h"
 
@@ -52,8 +53,10 @@ __device__ __forceinline__ u32x4 shfl_xor_u32x4(u32x4 v, int mask)
 
 template <int NR, int K, bool SEAL>
 __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2,
-                                               const Record *__restrict__ recs, uint32_t nrecs, const uint8_t *src,
-                                               uint8_t *dst, const uint8_t *__restrict__ aad, uint32_t *__restrict__ status)
+                                               const Record *__restrict__ recs, const uint32_t *__restrict__ order,
+                                               uint32_t nrecs, const uint8_t *src, uint8_t *dst,
+                                               const uint8_t *__restrict__ aad, uint32_t *__restrict__ status,
+                                               uint32_t *__restrict__ work)
 {
     static_assert(K <= MAX_KERNEL_K, "LDS holds at most MAX_KERNEL_K GHASH tables");
     __shared__ __attribute__((aligned(16))) uint8_t lds[Layout<K>::total];
@@ -71,12 +74,26 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
     const uint32_t j = lane % K, slot = lane / K;
     const uint32_t lanesel = (lane & 31u) * 4u | 0x10000u; /* bank + image-B select (gcm_core.h) */
     const uint32_t waves_per_block = blockDim.x >> 6;
-    const uint64_t ngroups = ((uint64_t)nrecs + R - 1) / R;
-    const uint64_t stride = (uint64_t)gridDim.x * waves_per_block;
+    const uint32_t ngroups = (nrecs + R - 1) / R;
+    (void)wave;
+    (void)waves_per_block;
 
-    for (uint64_t g = (uint64_t)blockIdx.x * waves_per_block + wave; g < ngroups; g += stride) {
-        const uint64_t r = g * R + slot;
-        const bool valid = r < nrecs;
+    /*
+     * Record groups (64/K records) are handed out dynamically: one returning atomic per group
+     * (MI355X_MICROARCH.md "dequeue": ~1 us under load, against ~100 us of work per group).
+     * With `order` sorted by length (ptls_mi355x_order_by_length) this is longest-first
+     * scheduling, and each group holds records of similar length.
+     */
+    for (;;) {
+        uint32_t g = 0;
+        if (lane == 0)
+            g = atomicAdd(work, 1u);
+        g = (uint32_t)__shfl((int)g, 0, 64);
+        if (g >= ngroups)
+            break;
+        const uint32_t idx = g * R + slot;
+        const bool valid = idx < nrecs;
+        const uint32_t r = valid ? (order ? order[idx] : idx) : 0u;
         Record rec = {0, 0, 0, 0, 0, 0};
         if (valid)
             rec = recs[r];
@@ -128,9 +145,10 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
 #define MI355X_GCM_KERNEL(NAME, NR, K, SEAL)                                                                           \
     extern "C" __global__ __launch_bounds__(WG_THREADS) void NAME(                                                     \
         const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2, const Record *__restrict__ recs,    \
-        uint32_t nrecs, const uint8_t *src, uint8_t *dst, const uint8_t *__restrict__ aad, uint32_t *__restrict__ st)  \
+        const uint32_t *__restrict__ order, uint32_t nrecs, const uint8_t *src, uint8_t *dst,                          \
+        const uint8_t *__restrict__ aad, uint32_t *__restrict__ st, uint32_t *__restrict__ work)                       \
     {                                                                                                                  \
-        gcm_batch_body<NR, K, SEAL>(ki, iv0, iv1, iv2, recs, nrecs, src, dst, aad, st);                                \
+        gcm_batch_body<NR, K, SEAL>(ki, iv0, iv1, iv2, recs, order, nrecs, src, dst, aad, st, work);                   \
     }
 
 MI355X_GCM_KERNEL(mi355x_gcm_seal_aes128_k1, 10, 1, true)
@@ -167,8 +185,10 @@ extern "C" __global__ void mi355x_aes_ecb(const KeyImage *__restrict__ ki, const
 
 /* ================================================================== host side ============ */
 
-typedef void (*batch_kernel_t)(const KeyImage *, uint32_t, uint32_t, uint32_t, const Record *, uint32_t, const uint8_t *,
-                               uint8_t *, const uint8_t *, uint32_t *);
+typedef void (*batch_kernel_t)(const KeyImage *, uint32_t, uint32_t, uint32_t, const Record *, const uint32_t *, uint32_t,
+                               const uint8_t *, uint8_t *, const uint8_t *, uint32_t *, uint32_t *);
+
+constexpr uint32_t WORK_SLOTS = 256; /* per-context ring of work counters: one per launch in flight */
 
 struct st_ptls_mi355x_aesgcm_context {
     int device;
@@ -179,6 +199,10 @@ struct st_ptls_mi355x_aesgcm_context {
     uint8_t *d_stage;    /* device staging for single-record calls */
     uint8_t *h_stage;    /* pinned host staging */
     size_t stage_cap;
+    uint32_t *d_work;    /* WORK_SLOTS dynamic-scheduling counters, zeroed per launch */
+    uint32_t work_next;
+    void *d_sort;        /* ptls_mi355x_order_by_length workspace */
+    size_t sort_cap;
 };
 
 static thread_local char g_err[256];
@@ -251,8 +275,9 @@ static batch_kernel_t pick_kernel(bool seal, uint32_t rounds, int k, const char 
 
 static inline uint32_t le32(const uint8_t *p) { return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24; }
 
-static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void *static_iv12, const Record *recs, size_t n,
-                        const uint8_t *src, uint8_t *dst, const uint8_t *aad, uint32_t *status, hipStream_t stream)
+static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void *static_iv12, const Record *recs,
+                        const uint32_t *order, size_t n, const uint8_t *src, uint8_t *dst, const uint8_t *aad,
+                        uint32_t *status, hipStream_t stream)
 {
     if (n == 0)
         return 0;
@@ -273,8 +298,10 @@ static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void
     if (blocks > (uint64_t)ctx->num_cu)
         blocks = (uint64_t)ctx->num_cu;
     DeviceGuard guard(ctx->device);
+    uint32_t *work = ctx->d_work + (ctx->work_next++ % WORK_SLOTS);
+    HIPCHK(hipMemsetAsync(work, 0, sizeof(uint32_t), stream));
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(WG_THREADS), 0, stream, ctx->d_ki, le32(iv), le32(iv + 4),
-                       le32(iv + 8), recs, (uint32_t)n, src, dst, aad, status);
+                       le32(iv + 8), recs, order, (uint32_t)n, src, dst, aad, status, work);
     HIPCHK(hipGetLastError());
     return 0;
 }
@@ -352,7 +379,8 @@ ptls_mi355x_aesgcm_context_t *ptls_mi355x_aesgcm_new(const void *key, size_t key
     ctx->num_cu = prop.multiProcessorCount;
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess)
         goto Fail;
-    if (hipMalloc(&ctx->d_ki, sizeof(KeyImage)) != hipSuccess || ensure_stage(ctx, 4096) != 0)
+    if (hipMalloc(&ctx->d_ki, sizeof(KeyImage)) != hipSuccess || ensure_stage(ctx, 4096) != 0 ||
+        hipMalloc(&ctx->d_work, WORK_SLOTS * sizeof(uint32_t)) != hipSuccess)
         goto Fail;
     memcpy(ctx->h_stage, key, key_size);
     d_rc = (int *)(ctx->d_stage + 64);
@@ -386,6 +414,10 @@ void ptls_mi355x_aesgcm_free(ptls_mi355x_aesgcm_context_t *ctx)
     }
     if (ctx->d_stage)
         (void)hipFree(ctx->d_stage);
+    if (ctx->d_work)
+        (void)hipFree(ctx->d_work);
+    if (ctx->d_sort)
+        (void)hipFree(ctx->d_sort);
     if (ctx->h_stage) {
         memset(ctx->h_stage, 0, ctx->stage_cap);
         (void)hipHostFree(ctx->h_stage);
@@ -400,13 +432,77 @@ int ptls_mi355x_aesgcm_device(const ptls_mi355x_aesgcm_context_t *ctx) { return 
 int ptls_mi355x_seal_batch(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12, const ptls_mi355x_record_t *recs,
                            size_t n, const uint8_t *src, uint8_t *dst, const uint8_t *aad, void *stream)
 {
-    return launch_batch(ctx, true, static_iv12, (const Record *)recs, n, src, dst, aad, nullptr, (hipStream_t)stream);
+    return launch_batch(ctx, true, static_iv12, (const Record *)recs, nullptr, n, src, dst, aad, nullptr,
+                        (hipStream_t)stream);
 }
 
 int ptls_mi355x_open_batch(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12, const ptls_mi355x_record_t *recs,
                            size_t n, const uint8_t *src, uint8_t *dst, const uint8_t *aad, uint32_t *status, void *stream)
 {
-    return launch_batch(ctx, false, static_iv12, (const Record *)recs, n, src, dst, aad, status, (hipStream_t)stream);
+    return launch_batch(ctx, false, static_iv12, (const Record *)recs, nullptr, n, src, dst, aad, status,
+                        (hipStream_t)stream);
+}
+
+int ptls_mi355x_seal_batch_ordered(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12,
+                                   const ptls_mi355x_record_t *recs, const uint32_t *order, size_t n, const uint8_t *src,
+                                   uint8_t *dst, const uint8_t *aad, void *stream)
+{
+    return launch_batch(ctx, true, static_iv12, (const Record *)recs, order, n, src, dst, aad, nullptr,
+                        (hipStream_t)stream);
+}
+
+int ptls_mi355x_open_batch_ordered(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12,
+                                   const ptls_mi355x_record_t *recs, const uint32_t *order, size_t n, const uint8_t *src,
+                                   uint8_t *dst, const uint8_t *aad, uint32_t *status, void *stream)
+{
+    return launch_batch(ctx, false, static_iv12, (const Record *)recs, order, n, src, dst, aad, status,
+                        (hipStream_t)stream);
+}
+
+/* keys = GHASH steps of each record (its work), values = record index */
+extern "C" __global__ void mi355x_sort_keys(const Record *__restrict__ recs, uint32_t n, uint32_t *keys, uint32_t *vals)
+{
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        Record r = recs[i];
+        uint64_t blocks = ((uint64_t)r.len + 15) / 16 + ((uint64_t)r.aadlen + 15) / 16 + 1;
+        keys[i] = blocks > 0xffffffu ? 0xffffffu : (uint32_t)blocks;
+        vals[i] = i;
+    }
+}
+
+int ptls_mi355x_order_by_length(ptls_mi355x_aesgcm_context_t *ctx, const ptls_mi355x_record_t *recs, size_t n,
+                                uint32_t *order, void *stream_)
+{
+    if (n == 0)
+        return 0;
+    if (n > 0x7fffffffull) {
+        snprintf(g_err, sizeof(g_err), "batch too large to order");
+        return -1;
+    }
+    DeviceGuard guard(ctx->device);
+    hipStream_t stream = (hipStream_t)stream_;
+    size_t temp = 0;
+    HIPCHK(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, temp, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                                        (uint32_t *)nullptr, (uint32_t *)nullptr, (int)n, 0, 24, stream));
+    const size_t arr = ((n * sizeof(uint32_t)) + 255) & ~(size_t)255;
+    const size_t need = 3 * arr + temp;
+    if (need > ctx->sort_cap) {
+        if (ctx->d_sort)
+            (void)hipFree(ctx->d_sort);
+        ctx->d_sort = nullptr;
+        ctx->sort_cap = 0;
+        HIPCHK(hipMalloc(&ctx->d_sort, need));
+        ctx->sort_cap = need;
+    }
+    uint8_t *base = (uint8_t *)ctx->d_sort;
+    uint32_t *keys_in = (uint32_t *)base, *keys_out = (uint32_t *)(base + arr), *vals_in = (uint32_t *)(base + 2 * arr);
+    hipLaunchKernelGGL(mi355x_sort_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, (const Record *)recs,
+                       (uint32_t)n, keys_in, vals_in);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipcub::DeviceRadixSort::SortPairsDescending(base + 3 * arr, temp, keys_in, keys_out, vals_in, order, (int)n, 0,
+                                                        24, stream));
+    return 0;
 }
 
 /*
@@ -434,7 +530,7 @@ static int single_record(ptls_mi355x_aesgcm_context_t *ctx, bool seal, void *out
     if (!seal)
         memcpy(ctx->h_stage + off_data + inlen, tag, 16);
     HIPCHK(hipMemcpyAsync(ctx->d_stage, ctx->h_stage, off_status, hipMemcpyHostToDevice, ctx->stream));
-    if (launch_batch(ctx, seal, nonce12, (const Record *)ctx->d_stage, 1, ctx->d_stage, ctx->d_stage, ctx->d_stage,
+    if (launch_batch(ctx, seal, nonce12, (const Record *)ctx->d_stage, nullptr, 1, ctx->d_stage, ctx->d_stage, ctx->d_stage,
                      (uint32_t *)(ctx->d_stage + off_status), ctx->stream) != 0)
         return -1;
     const size_t outlen = seal ? inlen + 16 : inlen;

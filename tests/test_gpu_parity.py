@@ -230,3 +230,45 @@ def test_ctr_cipher_kat(gpu):
     c = ra.cipher_new("aes128ctr", True, key)
     c.init(iv)
     assert c.encrypt(bytes(16)).hex() == "3ad77bb40d7a3660a89ecaf32466ef97"
+
+
+@pytest.mark.parametrize("lanes", [4, 8])
+def test_ordered_ragged_batch(gpu, lanes):
+    """ptls_mi355x_order_by_length + *_batch_ordered: descending work, every record sealed once, status per descriptor."""
+    import torch
+    rng = np.random.default_rng(55 + lanes)
+    n = 2000
+    lens = rng.integers(0, 5000, n).astype(np.uint64)
+    recs, src_bytes, aad_bytes = records.layout(lens, rng.integers(0, 40, n).astype(np.uint64), align=16)
+    recs["seq"] = rng.integers(0, 2 ** 63, n, dtype=np.uint64)
+    src = rng.integers(0, 256, src_bytes, dtype=np.uint8)
+    aad = rng.integers(0, 256, aad_bytes, dtype=np.uint8)
+    key, iv = bytes(range(40, 56)), bytes(range(12))
+    prev = ra.set_lanes_per_record(lanes)
+    try:
+        eng = ra.Engine(key)
+        d_recs, d_src, d_aad = to_dev(recs.view(np.uint8)), to_dev(src), to_dev(aad)
+        d_dst = torch.zeros_like(d_src)
+        d_order = torch.zeros(n, dtype=torch.int32, device="cuda")
+        eng.order_by_length(d_recs.data_ptr(), n, d_order.data_ptr())
+        eng.seal_batch_ordered(iv, d_recs.data_ptr(), d_order.data_ptr(), n, d_src.data_ptr(), d_dst.data_ptr(),
+                               d_aad.data_ptr())
+        torch.cuda.synchronize()
+        order = d_order.cpu().numpy().view(np.uint32)
+        assert sorted(order.tolist()) == list(range(n))
+        work = (recs["len"].astype(np.int64) + 15) // 16 + (recs["aadlen"].astype(np.int64) + 15) // 16
+        assert (np.diff(work[order]) <= 0).all()
+        want = np.zeros_like(src)
+        oracle.batch(True, key, iv, recs, src, want, aad)
+        got = d_dst.cpu().numpy()
+        assert slices(got, recs, 16) == slices(want, recs, 16)
+        d_pt = torch.zeros_like(d_src)
+        d_st = torch.zeros(n, dtype=torch.int32, device="cuda")
+        eng.open_batch_ordered(iv, d_recs.data_ptr(), d_order.data_ptr(), n, d_dst.data_ptr(), d_pt.data_ptr(),
+                               d_aad.data_ptr(), d_st.data_ptr())
+        torch.cuda.synchronize()
+        assert (d_st.cpu().numpy().view(np.uint32) == recs["len"]).all()
+        assert slices(d_pt.cpu().numpy(), recs, 0) == [bytes(src[int(r["src"]): int(r["src"]) + int(r["len"])])
+                                                        for r in recs]
+    finally:
+        ra.set_lanes_per_record(prev)
