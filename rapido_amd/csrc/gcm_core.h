@@ -306,6 +306,91 @@ GCM_HD u32x4 aes_ghash_fused(const uint8_t *lds, uint32_t lanesel, const uint32_
 #undef GCM_TB
 }
 
+/* T_t[byte kk of x] from the 4-table or the 2-table image */
+template <bool FOUR>
+GCM_HD uint32_t tlook(const uint8_t *lds, uint32_t lanesel, uint32_t x, uint32_t kk, int t)
+{
+    const uint32_t a = perm(x, lanesel, 0x0c0c0400u | ((4u + kk) << 8));
+    if (t == 0)
+        return lds_u32(lds, a);
+    if (t == 1)
+        return lds_u32(lds, a + 128);
+    if (FOUR) {
+        const uint32_t b = perm(x, lanesel, 0x0c020400u | ((4u + kk) << 8));
+        return lds_u32(lds, t == 2 ? b : b + 128);
+    }
+    return rotl32(lds_u32(lds, t == 2 ? a : a + 128), 16);
+}
+
+/*
+ * CTR-mode round-1 hoisting.  The AES input of every block of a record is nonce || BE32(ctr): the
+ * first 12 bytes never change, and inside a 2^16-block window neither do ctr's two high bytes
+ * (every TLS record lies in the first window).  Round 1 then has only two table reads that depend
+ * on the block (T3 of the counter's low byte for column 0, T2 of its next byte for column 1);
+ * everything else of round 1 is folded into four constants c[0..3], recomputed when the window
+ * changes.
+ */
+template <bool FOUR>
+GCM_HD void aes_round1_consts(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk, uint32_t iv0, uint32_t iv1,
+                              uint32_t iv2, uint32_t ctr_hi, uint32_t c[4])
+{
+    /* ctr_hi = ctr & 0xffff0000: the two counter bytes that are constant inside a 2^16-block window */
+    const uint32_t s0 = iv0 ^ rk[0], s1 = iv1 ^ rk[1], s2 = iv2 ^ rk[2], s3 = bswap32(ctr_hi) ^ rk[3];
+    const uint32_t *k = rk + 4;
+    c[0] = xor3(tlook<FOUR>(lds, lanesel, s0, 0, 0), tlook<FOUR>(lds, lanesel, s1, 1, 1),
+                tlook<FOUR>(lds, lanesel, s2, 2, 2) ^ k[0]);
+    c[1] = xor3(tlook<FOUR>(lds, lanesel, s1, 0, 0), tlook<FOUR>(lds, lanesel, s2, 1, 1),
+                tlook<FOUR>(lds, lanesel, s0, 3, 3) ^ k[1]);
+    c[2] = xor3(xor3(tlook<FOUR>(lds, lanesel, s2, 0, 0), tlook<FOUR>(lds, lanesel, s3, 1, 1), k[2]),
+                tlook<FOUR>(lds, lanesel, s0, 2, 2), tlook<FOUR>(lds, lanesel, s1, 3, 3));
+    c[3] = xor3(xor3(tlook<FOUR>(lds, lanesel, s3, 0, 0), tlook<FOUR>(lds, lanesel, s0, 1, 1), k[3]),
+                tlook<FOUR>(lds, lanesel, s1, 2, 2), tlook<FOUR>(lds, lanesel, s2, 3, 3));
+}
+
+/*
+ * aes_ghash_fused for a block whose round 1 is hoisted (c from the block's 2^16 window): 2 table reads in round 1
+ * instead of 16; the GHASH reads go to rounds 2..9.  Writes the keystream to w[4].
+ */
+template <int NR, bool FOUR = true>
+GCM_HD u32x4 aes_ghash_fused_h(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk, const uint32_t c[4],
+                               uint32_t ctr, uint32_t w[4], uint32_t basereg, u32x4 A)
+{
+#define GCM_TA(x, k) perm((x), lanesel, 0x0c0c0400u | ((4u + (k)) << 8))
+    u32x4 P = {0u, 0u, 0u, 0u};
+    const uint32_t s3 = bswap32(ctr) ^ rk[3];
+    uint32_t s0 = c[0] ^ tlook<FOUR>(lds, lanesel, s3, 3, 3), s1 = c[1] ^ tlook<FOUR>(lds, lanesel, s3, 2, 2);
+    uint32_t s2 = c[2], s3r = c[3];
+#pragma unroll
+    for (int r = 2; r < NR; ++r) {
+        const uint32_t *k = rk + 4 * r;
+        uint32_t n0 = aes_col<FOUR>(lds, lanesel, s0, s1, s2, s3r, k[0]);
+        uint32_t n1 = aes_col<FOUR>(lds, lanesel, s1, s2, s3r, s0, k[1]);
+        uint32_t n2 = aes_col<FOUR>(lds, lanesel, s2, s3r, s0, s1, k[2]);
+        uint32_t n3 = aes_col<FOUR>(lds, lanesel, s3r, s0, s1, s2, k[3]);
+        if (r <= 9)
+            ghash_quarter(lds, basereg, A[(r - 2) >> 1], (r - 2) >> 1, ((r - 2) & 1) * 2, P);
+        GCM_SCHED_FENCE();
+        s0 = n0;
+        s1 = n1;
+        s2 = n2;
+        s3r = n3;
+    }
+    {
+        const uint32_t *k = rk + 4 * NR;
+        uint32_t x[4] = {s0, s1, s2, s3r};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint32_t ra = lds_u32(lds, GCM_TA(x[j], 0));
+            uint32_t rb = lds_u32(lds, GCM_TA(x[(j + 1) & 3], 1));
+            uint32_t rc = lds_u32(lds, GCM_TA(x[(j + 2) & 3], 2));
+            uint32_t rd = lds_u32(lds, GCM_TA(x[(j + 3) & 3], 3));
+            w[j] = xor3(perm(rb, ra, 0x0c0c0501u), perm(rd, rc, 0x06020c0cu), k[j]);
+        }
+    }
+    return P;
+#undef GCM_TA
+}
+
 /*
  * r = x * c with the nibble tables of c at LDS byte offset (base: bytes 1..2 of basereg, a multiple of
  * 256 in [128K, 160K)).  32 conflict-free ds_read_b128 + ~108 VALU.
@@ -622,6 +707,9 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
     const uint8_t *ad = aad + rec.aad;
     const uint32_t arem = rec.aadlen & 15u;
     u32x4 acc = {0u, 0u, 0u, 0u}, ek0 = {0u, 0u, 0u, 0u};
+    /* hoisted round-1 constants of the current 2^16-counter window (aes_round1_consts) */
+    uint32_t c1[4] = {0u, 0u, 0u, 0u}, c1_hi = 0u;
+    aes_round1_consts<Layout<K>::four_tables>(lds, lanesel, rk, iv0, iv1, iv2, 0u, c1);
 
     /* step at which this lane meets position p, or ~0 */
     auto step_of = [&](uint32_t pos) -> uint32_t {
@@ -682,7 +770,12 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
         aes_encrypt_tt<NR, Layout<K>::four_tables>(lds, lanesel, rk, w);
         const u32x4 P = acc;
 #else
-        const u32x4 P = aes_ghash_fused<NR, Layout<K>::four_tables>(lds, lanesel, rk, w, Layout<K>::gh_base, acc);
+        if ((ctr & 0xffff0000u) != c1_hi) { /* records beyond 2^16 blocks only */
+            c1_hi = ctr & 0xffff0000u;
+            aes_round1_consts<Layout<K>::four_tables>(lds, lanesel, rk, iv0, iv1, iv2, c1_hi, c1);
+        }
+        const u32x4 P =
+            aes_ghash_fused_h<NR, Layout<K>::four_tables>(lds, lanesel, rk, c1, ctr, w, Layout<K>::gh_base, acc);
 #endif
         const u32x4 ks = {w[0], w[1], w[2], w[3]};
 

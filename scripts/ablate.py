@@ -21,6 +21,7 @@ VDIR = os.path.join(ROOT, "rapido_amd", "_lib", "variants")
 VARIANTS = {
     "base": [],
     "wg512": ["-DMI355X_WG_THREADS=512"],
+    "wg768": ["-DMI355X_WG_THREADS=768"],
     "no_ghash": ["-DGCM_ABLATE_GHASH=1"],
     "no_aes": ["-DGCM_ABLATE_AES=1"],
     "no_both": ["-DGCM_ABLATE_AES=1", "-DGCM_ABLATE_GHASH=1"],

@@ -272,3 +272,22 @@ def test_ordered_ragged_batch(gpu, lanes):
                                                         for r in recs]
     finally:
         ra.set_lanes_per_record(prev)
+
+
+@pytest.mark.parametrize("lanes", [4, 8])
+def test_record_beyond_2p16_blocks(gpu, lanes):
+    """Counters past 2^16 (records > 1 MiB): round-1 constants are recomputed per 2^16 window."""
+    lens = np.array([70000 * 16 + 5, 1400, 200000 * 16], dtype=np.uint64)
+    recs, src, aad = records.tls_batch(lens, seed=21, align=256)
+    key, iv = bytes(range(7, 39)), bytes(range(12))
+    prev = ra.set_lanes_per_record(lanes)
+    try:
+        eng = ra.Engine(key)
+        got, _ = run_batch(eng, True, iv, recs, src, len(src), aad)
+        want = np.zeros_like(src)
+        oracle.batch(True, key, iv, recs, src, want, aad)
+        assert slices(got, recs, 16) == slices(want, recs, 16)
+        pt, st = run_batch(eng, False, iv, recs, got, len(src), aad)
+        assert (st == recs["len"]).all()
+    finally:
+        ra.set_lanes_per_record(prev)

@@ -115,3 +115,16 @@ def test_record_dtype_matches_header():
     body = body[: body.index("}")]
     fields = [ln.split(";")[0].split()[-1] for ln in body.splitlines() if ";" in ln]
     assert fields == list(RECORD_DTYPE.names)
+
+
+@pytest.mark.parametrize("K", [4, 8])
+def test_model_record_beyond_2p16_blocks(model, K):
+    """A 1.1 MB record: counters cross 2^16, so the hoisted round-1 constants must be recomputed."""
+    lens = np.array([70000 * 16 + 5, 33], dtype=np.uint64)
+    recs, src, aad = records.tls_batch(lens, seed=9, align=16)
+    key, iv = bytes(range(1, 17)), bytes(range(12))
+    got, want = np.zeros_like(src), np.zeros_like(src)
+    st = np.zeros(len(recs), np.uint32)
+    run(model, True, K, key, iv, recs, src, got, aad, st)
+    oracle.batch(True, key, iv, recs, src, want, aad)
+    assert spans(got, recs, 16) == spans(want, recs, 16)
