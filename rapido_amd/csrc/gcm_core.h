@@ -65,6 +65,7 @@ namespace mi355x {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef u32x4 u32x4_u __attribute__((aligned(1)));
+typedef uint32_t uint32_t_u __attribute__((aligned(1)));
 
 enum : uint32_t {
     LDS_AES_BASE = 0x00000u,
@@ -177,6 +178,12 @@ GCM_HD uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
 #else
 #define GCM_SCHED_FENCE() ((void)0)
 #endif
+/* value the optimiser cannot see through (blocks hoisting of rare-path work out of the loop) */
+#if defined(__HIP_DEVICE_COMPILE__)
+#define GCM_OPAQUE(x) asm volatile("" : "+v"(x))
+#else
+#define GCM_OPAQUE(x) ((void)0)
+#endif
 
 GCM_HD uint32_t lds_u32(const uint8_t *lds, uint32_t addr) { return *(const uint32_t *)(lds + addr); }
 GCM_HD u32x4 lds_u32x4(const uint8_t *lds, uint32_t addr) { return *(const u32x4 *)(lds + addr); }
@@ -261,6 +268,102 @@ GCM_HD void ghash_quarter(const uint8_t *lds, uint32_t basereg, uint32_t w, int 
         P[3] = xor3_pinned(P[3], e[3], f[3]);
     }
 }
+
+/* ghash_quarter split in two: the four table reads, and their accumulation into P */
+GCM_HD void ghash_quarter_issue(const uint8_t *lds, uint32_t basereg, uint32_t w, int d, int m0, u32x4 g[4])
+{
+    uint32_t lo = (w << 4) & 0xf0f0f0f0u, hi = w & 0xf0f0f0f0u;
+#pragma unroll
+    for (int m = m0; m < m0 + 2; ++m) {
+        uint32_t sel = 0x0c020100u | (4u + (uint32_t)m);
+        g[2 * (m - m0)] = lds_u32x4(lds, perm(lo, basereg, sel) + (uint32_t)(8 * d + 2 * m) * 256u);
+        g[2 * (m - m0) + 1] = lds_u32x4(lds, perm(hi, basereg, sel) + (uint32_t)(8 * d + 2 * m + 1) * 256u);
+    }
+}
+
+GCM_HD void ghash_quarter_acc(const u32x4 g[4], u32x4 &P)
+{
+#pragma unroll
+    for (int i = 0; i < 4; i += 2) {
+        P[0] = xor3_pinned(P[0], g[i][0], g[i + 1][0]);
+        P[1] = xor3_pinned(P[1], g[i][1], g[i + 1][1]);
+        P[2] = xor3_pinned(P[2], g[i][2], g[i + 1][2]);
+        P[3] = xor3_pinned(P[3], g[i][3], g[i + 1][3]);
+    }
+}
+
+#ifndef GCM_ROUND_ASM
+#define GCM_ROUND_ASM 1
+#endif
+#if defined(__HIP_DEVICE_COMPILE__)
+/*
+ * One full AES round on the four-table image (aes_col x 4) as a single instruction block:
+ * 16 address perms, the 16 ds_read_b32 back to back, then counted waits feeding the column
+ * XORs, so every wave keeps 16 (+ the GHASH quarter's 4, issued just before) LDS reads in
+ * flight regardless of the compiler's scheduling heuristics.  The block ends with
+ * lgkmcnt(0): no read of it is outstanding afterwards, so the compiler's own counted waits
+ * stay exact (DS reads complete in order).  Bit-identical to the aes_col sequence.
+ */
+__device__ __forceinline__ void aes_round_tt4_asm(uint32_t ls, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3,
+                                                  const uint32_t *k, uint32_t &n0, uint32_t &n1, uint32_t &n2,
+                                                  uint32_t &n3)
+{
+    uint32_t t1, t2, t3, t5, t6, t7, t9, t10, t11, t13, t14, t15;
+    asm volatile(
+        /* column c reads T0[s_c.b0], T1[s_(c+1).b1] (+128), T2[s_(c+2).b2], T3[s_(c+3).b3] (+128) */
+        "v_perm_b32 %[n0], %[s0], %[ls], %[a0]\n\t"
+        "v_perm_b32 %[t1], %[s1], %[ls], %[a1]\n\t"
+        "v_perm_b32 %[t2], %[s2], %[ls], %[b2]\n\t"
+        "v_perm_b32 %[t3], %[s3], %[ls], %[b3]\n\t"
+        "ds_read_b32 %[n0], %[n0]\n\t"
+        "ds_read_b32 %[t1], %[t1] offset:128\n\t"
+        "ds_read_b32 %[t2], %[t2]\n\t"
+        "ds_read_b32 %[t3], %[t3] offset:128\n\t"
+        "v_perm_b32 %[n1], %[s1], %[ls], %[a0]\n\t"
+        "v_perm_b32 %[t5], %[s2], %[ls], %[a1]\n\t"
+        "v_perm_b32 %[t6], %[s3], %[ls], %[b2]\n\t"
+        "v_perm_b32 %[t7], %[s0], %[ls], %[b3]\n\t"
+        "ds_read_b32 %[n1], %[n1]\n\t"
+        "ds_read_b32 %[t5], %[t5] offset:128\n\t"
+        "ds_read_b32 %[t6], %[t6]\n\t"
+        "ds_read_b32 %[t7], %[t7] offset:128\n\t"
+        "v_perm_b32 %[n2], %[s2], %[ls], %[a0]\n\t"
+        "v_perm_b32 %[t9], %[s3], %[ls], %[a1]\n\t"
+        "v_perm_b32 %[t10], %[s0], %[ls], %[b2]\n\t"
+        "v_perm_b32 %[t11], %[s1], %[ls], %[b3]\n\t"
+        "ds_read_b32 %[n2], %[n2]\n\t"
+        "ds_read_b32 %[t9], %[t9] offset:128\n\t"
+        "ds_read_b32 %[t10], %[t10]\n\t"
+        "ds_read_b32 %[t11], %[t11] offset:128\n\t"
+        "v_perm_b32 %[n3], %[s3], %[ls], %[a0]\n\t"
+        "v_perm_b32 %[t13], %[s0], %[ls], %[a1]\n\t"
+        "v_perm_b32 %[t14], %[s1], %[ls], %[b2]\n\t"
+        "v_perm_b32 %[t15], %[s2], %[ls], %[b3]\n\t"
+        "ds_read_b32 %[n3], %[n3]\n\t"
+        "ds_read_b32 %[t13], %[t13] offset:128\n\t"
+        "ds_read_b32 %[t14], %[t14]\n\t"
+        "ds_read_b32 %[t15], %[t15] offset:128\n\t"
+        "s_waitcnt lgkmcnt(12)\n\t"
+        "v_bitop3_b32 %[n0], %[n0], %[t1], %[k0] bitop3:0x96\n\t"
+        "v_bitop3_b32 %[n0], %[n0], %[t2], %[t3] bitop3:0x96\n\t"
+        "s_waitcnt lgkmcnt(8)\n\t"
+        "v_bitop3_b32 %[n1], %[n1], %[t5], %[k1] bitop3:0x96\n\t"
+        "v_bitop3_b32 %[n1], %[n1], %[t6], %[t7] bitop3:0x96\n\t"
+        "s_waitcnt lgkmcnt(4)\n\t"
+        "v_bitop3_b32 %[n2], %[n2], %[t9], %[k2] bitop3:0x96\n\t"
+        "v_bitop3_b32 %[n2], %[n2], %[t10], %[t11] bitop3:0x96\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_bitop3_b32 %[n3], %[n3], %[t13], %[k3] bitop3:0x96\n\t"
+        "v_bitop3_b32 %[n3], %[n3], %[t14], %[t15] bitop3:0x96"
+        : [n0] "=&v"(n0), [n1] "=&v"(n1), [n2] "=&v"(n2), [n3] "=&v"(n3), [t1] "=&v"(t1), [t2] "=&v"(t2),
+          [t3] "=&v"(t3), [t5] "=&v"(t5), [t6] "=&v"(t6), [t7] "=&v"(t7), [t9] "=&v"(t9), [t10] "=&v"(t10),
+          [t11] "=&v"(t11), [t13] "=&v"(t13), [t14] "=&v"(t14), [t15] "=&v"(t15)
+        : [s0] "v"(s0), [s1] "v"(s1), [s2] "v"(s2), [s3] "v"(s3), [ls] "v"(ls), [k0] "s"(k[0]), [k1] "s"(k[1]),
+          [k2] "s"(k[2]), [k3] "s"(k[3]), [a0] "s"(0x0c0c0400u), [a1] "s"(0x0c0c0500u), [b2] "s"(0x0c020600u),
+          [b3] "s"(0x0c020700u)
+        : "memory");
+}
+#endif
 
 /*
  * AES of w (in place) fused with P = A * c (nibble tables of c at basereg): the GHASH reads are
@@ -363,12 +466,26 @@ GCM_HD u32x4 aes_ghash_fused_h(const uint8_t *lds, uint32_t lanesel, const uint3
 #pragma unroll
     for (int r = 2; r < NR; ++r) {
         const uint32_t *k = rk + 4 * r;
-        uint32_t n0 = aes_col<FOUR>(lds, lanesel, s0, s1, s2, s3r, k[0]);
-        uint32_t n1 = aes_col<FOUR>(lds, lanesel, s1, s2, s3r, s0, k[1]);
-        uint32_t n2 = aes_col<FOUR>(lds, lanesel, s2, s3r, s0, s1, k[2]);
-        uint32_t n3 = aes_col<FOUR>(lds, lanesel, s3r, s0, s1, s2, k[3]);
-        if (r <= 9)
-            ghash_quarter(lds, basereg, A[(r - 2) >> 1], (r - 2) >> 1, ((r - 2) & 1) * 2, P);
+        uint32_t n0, n1, n2, n3;
+#if defined(__HIP_DEVICE_COMPILE__) && GCM_ROUND_ASM
+        if (FOUR) {
+            /* GHASH quarter: reads issued ahead of the round, accumulated after it */
+            u32x4 g[4];
+            if (r <= 9)
+                ghash_quarter_issue(lds, basereg, A[(r - 2) >> 1], (r - 2) >> 1, ((r - 2) & 1) * 2, g);
+            aes_round_tt4_asm(lanesel, s0, s1, s2, s3r, k, n0, n1, n2, n3);
+            if (r <= 9)
+                ghash_quarter_acc(g, P);
+        } else
+#endif
+        {
+            n0 = aes_col<FOUR>(lds, lanesel, s0, s1, s2, s3r, k[0]);
+            n1 = aes_col<FOUR>(lds, lanesel, s1, s2, s3r, s0, k[1]);
+            n2 = aes_col<FOUR>(lds, lanesel, s2, s3r, s0, s1, k[2]);
+            n3 = aes_col<FOUR>(lds, lanesel, s3r, s0, s1, s2, k[3]);
+            if (r <= 9)
+                ghash_quarter(lds, basereg, A[(r - 2) >> 1], (r - 2) >> 1, ((r - 2) & 1) * 2, P);
+        }
         GCM_SCHED_FENCE();
         s0 = n0;
         s1 = n1;
@@ -638,16 +755,42 @@ GCM_HD void fill_lds(uint8_t *lds, const uint32_t *t0, const KeyImage *ki, uint3
 /* loads n (< 16) bytes zero-extended */
 GCM_HD u32x4 load_partial(const uint8_t *p, uint32_t n)
 {
+    /* loop-free (n < 16): whole dwords, then up to 3 bytes of dword q = n / 4 */
     u32x4 v = {0u, 0u, 0u, 0u};
-    for (uint32_t i = 0; i < n; ++i)
-        v[i >> 2] |= (uint32_t)p[i] << (8 * (i & 3));
+    const uint32_t q = n >> 2, rem = n & 3u;
+#pragma unroll
+    for (uint32_t d = 0; d < 3; ++d)
+        if (d < q)
+            v[d] = *(const uint32_t_u *)(p + 4u * d);
+    uint32_t t = 0u;
+    if (rem > 0u)
+        t = p[4u * q];
+    if (rem > 1u)
+        t |= (uint32_t)p[4u * q + 1u] << 8;
+    if (rem > 2u)
+        t |= (uint32_t)p[4u * q + 2u] << 16;
+    v[0] = q == 0u ? t : v[0];
+    v[1] = q == 1u ? t : v[1];
+    v[2] = q == 2u ? t : v[2];
+    v[3] = q == 3u ? t : v[3];
     return v;
 }
 
 GCM_HD void store_partial(uint8_t *p, uint32_t n, u32x4 v)
 {
-    for (uint32_t i = 0; i < n; ++i)
-        p[i] = (uint8_t)(v[i >> 2] >> (8 * (i & 3)));
+    /* loop-free (n < 16), mirror of load_partial */
+    const uint32_t q = n >> 2, rem = n & 3u;
+#pragma unroll
+    for (uint32_t d = 0; d < 3; ++d)
+        if (d < q)
+            *(uint32_t_u *)(p + 4u * d) = v[d];
+    const uint32_t t = q == 0u ? v[0] : q == 1u ? v[1] : q == 2u ? v[2] : v[3];
+    if (rem > 0u)
+        p[4u * q] = (uint8_t)t;
+    if (rem > 1u)
+        p[4u * q + 1u] = (uint8_t)(t >> 8);
+    if (rem > 2u)
+        p[4u * q + 2u] = (uint8_t)(t >> 16);
 }
 
 /* bytes of a block at and beyond n zeroed (n < 16) */
@@ -685,16 +828,19 @@ GCM_HD u32x4 shr_bytes(u32x4 v, uint32_t n)
 /*
  * One lane's share of one record (see struct Walk).  Returns the lane's partial GHASH already
  * scaled by H^(K-j); the lane holding the length block has E_K(J0) folded in, so the XOR of the
- * K returned values is the tag.  Lanes with valid == false run the same instruction stream
+ * K returned values is the tag (seal), or the tag XOR the received tag (open: the length
+ * lane fetches the received tag through its prefetch slot, so the record verifies iff the XOR
+ * is zero and nothing has to be read after the walk).  Lanes with valid == false run the same instruction stream
  * without touching memory (Tmax is the wave-wide trip count).
  * iv0..iv2: the record's 96-bit nonce as LE dwords.
  *
  * Memory pipeline: every step issues at most ONE full 16-byte load (the block of the NEXT
  * step, so its latency hides under this step's AES + GHASH) and at most one 16-byte store.
- * Byte-granular reads happen only at record setup: a partial AAD block, and a sealed
- * payload shorter than 16 bytes.  A partial last payload block of a longer record is read
- * as the record's last 16 bytes and shifted in registers (seal), or read directly since the
- * tag follows it (open) -- nothing is ever read outside [src, src + len (+16 for open)).
+ * Byte-granular reads happen only for an AAD shorter than 16 bytes (at setup, into the first
+ * buffer) and a sealed payload shorter than 16 bytes (in its step).  A partial last AAD block
+ * or payload block of a longer AAD/record is read as its last 16 bytes and shifted in
+ * registers (seal), or read directly since the tag follows it (open) -- nothing is ever
+ * read outside [aad, aad + aadlen) and [src, src + len (+16 for open)).
  */
 template <int NR, int K, bool SEAL>
 GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk, uint32_t j, const Record &rec, bool valid,
@@ -711,18 +857,6 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
     uint32_t c1[4] = {0u, 0u, 0u, 0u}, c1_hi = 0u;
     aes_round1_consts<Layout<K>::four_tables>(lds, lanesel, rk, iv0, iv1, iv2, 0u, c1);
 
-    /* step at which this lane meets position p, or ~0 */
-    auto step_of = [&](uint32_t pos) -> uint32_t {
-        uint32_t q = pos + wk.pad;
-        return (q % K == j) ? q / K : 0xffffffffu;
-    };
-    /* setup-time byte reads (the only ones) */
-    u32x4 aad_tail = {0u, 0u, 0u, 0u}, short_pay = {0u, 0u, 0u, 0u};
-    if (valid && arem != 0u && step_of(wk.A - 1u) != 0xffffffffu)
-        aad_tail = load_partial(ad + 16u * (wk.A - 1u), arem);
-    if (SEAL && valid && rec.len != 0u && rec.len < 16u && step_of(wk.A) != 0xffffffffu)
-        short_pay = load_partial(in, rec.len);
-
     /*
      * Address of the 16-byte load of step t.  The load is issued unconditionally (steps with
      * nothing to read load 16 harmless bytes at `dummy`): with a load in every step the
@@ -730,16 +864,20 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
      * instead of vmcnt(0).
      */
     auto fetch_ptr = [&](uint32_t t) -> const uint8_t * {
+        GCM_OPAQUE(t); /* recompute from t: no strength-reduced induction variables (VGPRs) */
         if (!valid || t >= wk.T)
             return dummy;
         const int32_t p = (int32_t)(j + K * t) - (int32_t)wk.pad;
         if (p < 0)
             return dummy;
-        if ((uint32_t)p < wk.A)
-            return 16u * (uint32_t)p + 16u <= rec.aadlen ? ad + 16u * (uint32_t)p : dummy;
+        if ((uint32_t)p < wk.A) { /* a partial last AAD block is read as the AAD's last 16 bytes */
+            if (16u * (uint32_t)p + 16u <= rec.aadlen)
+                return ad + 16u * (uint32_t)p;
+            return rec.aadlen >= 16u ? ad + rec.aadlen - 16u : dummy;
+        }
         const uint32_t c = (uint32_t)p - wk.A;
-        if (c >= wk.C)
-            return dummy;
+        if (c >= wk.C) /* the length block; open fetches the received tag into its slot */
+            return !SEAL && c == wk.C ? in + rec.len : dummy;
         if (!SEAL || 16u * c + 16u <= rec.len)
             return in + 16u * c;
         return rec.len >= 16u ? in + rec.len - 16u : dummy;
@@ -751,6 +889,7 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
      * A_t = P ^ X_t.  A_(-1) = 0, and A_(T-1) is the lane's sum.
      */
     auto step = [&](uint32_t t, u32x4 cur) {
+        GCM_OPAQUE(t);
         const bool active = valid && t < wk.T;
         const int32_t p = (int32_t)(j + K * t) - (int32_t)wk.pad;
         const bool is_aad = active && p >= 0 && (uint32_t)p < wk.A;
@@ -772,7 +911,13 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
 #else
         if ((ctr & 0xffff0000u) != c1_hi) { /* records beyond 2^16 blocks only */
             c1_hi = ctr & 0xffff0000u;
-            aes_round1_consts<Layout<K>::four_tables>(lds, lanesel, rk, iv0, iv1, iv2, c1_hi, c1);
+            /* opaque inputs: keeps LICM from parking this rare path's 16 LDS addresses in VGPRs */
+            uint32_t o0 = iv0, o1 = iv1, o2 = iv2, ol = lanesel;
+            GCM_OPAQUE(o0);
+            GCM_OPAQUE(o1);
+            GCM_OPAQUE(o2);
+            GCM_OPAQUE(ol);
+            aes_round1_consts<Layout<K>::four_tables>(lds, ol, rk, o0, o1, o2, c1_hi, c1);
         }
         const u32x4 P =
             aes_ghash_fused_h<NR, Layout<K>::four_tables>(lds, lanesel, rk, c1, ctr, w, Layout<K>::gh_base, acc);
@@ -787,21 +932,25 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
                 *(u32x4_u *)(out + 16u * c) = o;
                 X = SEAL ? o : data;
             } else {
-                if (SEAL)
-                    data = rec.len >= 16u ? shr_bytes(data, 16u - clen) : short_pay;
+                if (SEAL) {
+                    if (rec.len >= 16u)
+                        data = shr_bytes(data, 16u - clen);
+                    else /* rare: a whole payload under 16 bytes, read in place */
+                        data = load_partial(in, rec.len);
+                }
                 const u32x4 o = data ^ ks;
                 store_partial(out + 16u * c, clen, o);
                 X = mask_tail(SEAL ? o : data, clen);
             }
         } else if (is_aad) {
-            X = 16u * (uint32_t)p + 16u <= rec.aadlen ? cur : aad_tail;
+            X = 16u * (uint32_t)p + 16u <= rec.aadlen || rec.aadlen < 16u ? cur : shr_bytes(cur, 16u - arem);
         } else if (is_len) {
             uint64_t abits = (uint64_t)rec.aadlen * 8u, cbits = (uint64_t)rec.len * 8u;
             X[0] = bswap32((uint32_t)(abits >> 32));
             X[1] = bswap32((uint32_t)abits);
             X[2] = bswap32((uint32_t)(cbits >> 32));
             X[3] = bswap32((uint32_t)cbits);
-            ek0 = ks;
+            ek0 = SEAL ? ks : ks ^ cur; /* open: E(J0) ^ received tag */
         }
         if (active)
             acc = P ^ X;
@@ -812,7 +961,15 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
      * t and the load of step t+2 reuses the registers step t has just consumed, so no register
      * copy (and no vmcnt(0) behind the step's own store) sits on the loop back-edge.
      */
-    u32x4 bufA = *(const u32x4_u *)fetch_ptr(0);
+    /*
+     * An AAD shorter than 16 bytes (TLS: the 5-byte record header) is position 0, which lies in
+     * step 0 (front padding < K): its lane reads it byte-exact into the first buffer.
+     */
+    u32x4 bufA;
+    if (valid && rec.aadlen != 0u && rec.aadlen < 16u && j == wk.pad)
+        bufA = load_partial(ad, rec.aadlen);
+    else
+        bufA = *(const u32x4_u *)fetch_ptr(0);
     for (uint32_t t = 0; t < Tmax; t += 2u) {
         const u32x4 bufB = *(const u32x4_u *)fetch_ptr(t + 1u);
         step(t, bufA);

@@ -115,19 +115,22 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
             if (j == 0 && valid)
                 *(u32x4_u *)(dst + rec.dst + rec.len) = part;
         } else {
-            uint32_t bad = 0;
-            if (valid) {
-                u32x4 rx = *(const u32x4_u *)(src + rec.src + rec.len);
-                u32x4 d = part ^ rx;
-                bad = (d[0] | d[1] | d[2] | d[3]) != 0u;
-                if (j == 0)
-                    status[r] = bad ? 0xffffffffu : rec.len;
-            }
-            if (valid && bad) {
-                /* failed open: do not release plaintext (fusion leaves it, lib/fusion.c:656-679) */
-                uint8_t *out = dst + rec.dst;
-                for (uint32_t off = 16u * j; off < rec.len; off += 16u * K) {
-                    uint32_t n = rec.len - off;
+            /* part = computed tag ^ received tag (lane_walk) */
+            const bool bad = valid && (part[0] | part[1] | part[2] | part[3]) != 0u;
+            if (j == 0 && valid)
+                status[r] = bad ? 0xffffffffu : rec.len;
+            if (bad) {
+                /*
+                 * Failed open: do not release plaintext (fusion leaves it, lib/fusion.c:656-679).
+                 * Rare path: the descriptor is re-read through an opaque pointer so the walk does
+                 * not keep dst/len alive in registers for it.
+                 */
+                const Record *rp = recs + r;
+                asm volatile("" : "+v"(rp));
+                const Record again = *rp;
+                uint8_t *out = dst + again.dst;
+                for (uint32_t off = 16u * j; off < again.len; off += 16u * K) {
+                    uint32_t n = again.len - off;
                     u32x4 z = {0u, 0u, 0u, 0u};
                     if (n >= 16)
                         *(u32x4_u *)(out + off) = z;

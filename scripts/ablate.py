@@ -22,6 +22,10 @@ VARIANTS = {
     "base": [],
     "wg512": ["-DMI355X_WG_THREADS=512"],
     "wg768": ["-DMI355X_WG_THREADS=768"],
+    "ilp": ["-mllvm", "--amdgpu-sched-strategy=iterative-ilp"],
+    "noasm": ["-DGCM_ROUND_ASM=0"],
+    # "@src=DIR": compile gcm_engine.hip from DIR (e.g. a `git show` of an older revision) instead of csrc/
+    "head": ["@src=" + os.path.join(VDIR, "src_head")],
     "no_ghash": ["-DGCM_ABLATE_GHASH=1"],
     "no_aes": ["-DGCM_ABLATE_AES=1"],
     "no_both": ["-DGCM_ABLATE_AES=1", "-DGCM_ABLATE_GHASH=1"],
@@ -38,9 +42,17 @@ def build():
     for name, flags in VARIANTS.items():
         obj = os.path.join(VDIR, name + ".o")
         so = os.path.join(VDIR, name + ".so")
-        src = os.path.join(b.CSRC, "gcm_engine.hip")
-        subprocess.run([b.HIPCC, f"--offload-arch={b.ARCH}", "-O3", "-std=c++17", "-fPIC", *flags, "-c", src, "-o", obj],
-                       check=True)
+        srcdir = next((f[5:] for f in flags if f.startswith("@src=")), b.CSRC)
+        if srcdir != b.CSRC and not os.path.isdir(srcdir):
+            os.makedirs(srcdir)
+            for f in ("gcm_engine.hip", "gcm_core.h"):
+                with open(os.path.join(srcdir, f), "wb") as fh:
+                    fh.write(subprocess.run(["git", "-C", ROOT, "show", "HEAD:rapido_amd/csrc/" + f],
+                                            check=True, capture_output=True).stdout)
+        flags = [f for f in flags if not f.startswith("@src=")]
+        src = os.path.join(srcdir, "gcm_engine.hip")
+        subprocess.run([b.HIPCC, f"--offload-arch={b.ARCH}", "-O3", "-std=c++17", "-fPIC", "-I" + b.CSRC, *flags, "-c",
+                        src, "-o", obj], check=True)
         subprocess.run([b.HIPCC, f"--offload-arch={b.ARCH}", "-shared", "-fPIC", "-o", so, obj, c_obj], check=True)
         print("built", so)
 

@@ -30,9 +30,6 @@ static void run(const KeyImage *ki, const uint8_t *lds, const uint8_t *static_iv
         Walk wk = make_walk(r.len, r.aadlen, K);
         uint32_t n1 = iv1 ^ bswap32((uint32_t)(r.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)r.seq);
         /* received tag first: open may run in place */
-        u32x4 rx = {0, 0, 0, 0};
-        if (!SEAL)
-            memcpy(&rx, src + r.src + r.len, 16);
         u32x4 tag = {0, 0, 0, 0};
         for (uint32_t j = 0; j < (uint32_t)K; ++j)
             tag ^= lane_walk<NR, K, SEAL>(lds, 4u * (j & 31u) | 0x10000u, ki->rk, j, r, true, wk.T, iv0, n1, n2, src, dst, aad,
@@ -40,7 +37,7 @@ static void run(const KeyImage *ki, const uint8_t *lds, const uint8_t *static_iv
         if (SEAL) {
             memcpy(dst + r.dst + r.len, &tag, 16);
         } else {
-            u32x4 d = tag ^ rx;
+            const u32x4 d = tag; /* computed ^ received (lane_walk) */
             status[i] = (d[0] | d[1] | d[2] | d[3]) ? 0xffffffffu : r.len;
         }
     }
