@@ -170,6 +170,66 @@ int ptls_mi355x_open_batch_ordered(ptls_mi355x_aesgcm_context_t *ctx, const void
                                    const ptls_mi355x_record_t *recs, const uint32_t *order, size_t n, const uint8_t *src,
                                    uint8_t *dst, const uint8_t *aad, uint32_t *status, void *stream);
 
+/* ======================================================================================
+ * 4. TLS 1.3 record framing in the batch.  The framing of picotls's
+ *    record layer done by the kernel, so a send window / recv() window of records is ONE launch
+ *    instead of per-record ptls_aead_encrypt/decrypt slot calls.
+ *
+ *    seal -- replaces buffer_push_encrypted_records + aead_encrypt + build_aad
+ *            (lib/picotls.c:621-643,658-684) for one record per descriptor:
+ *        reads  src[recs[i].src .. +len)                      (the fragment, len <= 16384)
+ *        writes dst[recs[i].dst .. +len+22) = 17 03 03 BE16(len+17) || ciphertext(fragment ||
+ *               (uint8)type) || tag, AAD = the 5 header bytes, nonce from recs[i].seq
+ *    open -- replaces aead_decrypt + the padding strip / content-type pop of handle_input_tls13
+ *            (lib/picotls.c:645-654,4779-4791) for one header-framed record per descriptor:
+ *        reads  src[recs[i].src .. +5+len) = header || ciphertext || tag, len = the header's
+ *               length field (AAD rebuilt as 17 03 03 BE16(len), as build_aad does)
+ *        writes dst[recs[i].dst .. +len-16) = plaintext with padding and type, then
+ *               status[i] = inner plaintext length and types[i] = content type, or
+ *               status[i] = PTLS_MI355X_TLS_BAD_RECORD_MAC (tag, or len < 16; plaintext zeroed)
+ *                           PTLS_MI355X_TLS_UNEXPECTED_MESSAGE (no non-zero byte)
+ *    Device pointers, asynchronous on `stream`, like section 3.  Headers are parsed and
+ *    descriptors planned on the host (ptls_mi355x_tls_plan_send / _parse_records below).
+ * ====================================================================================== */
+typedef struct st_ptls_mi355x_tls_record_t {
+    uint64_t src;  /* seal: fragment offset in src;     open: record (header) offset in src */
+    uint64_t dst;  /* seal: record (header) offset in dst; open: plaintext offset in dst */
+    uint64_t seq;  /* record sequence number */
+    uint32_t len;  /* seal: fragment bytes (<= 16384); open: the header's length field */
+    uint32_t type; /* seal: inner content type (23 = application_data); open: unused */
+} ptls_mi355x_tls_record_t;
+
+#define PTLS_MI355X_TLS_HEADER_SIZE 5
+#define PTLS_MI355X_TLS_MAX_FRAGMENT 16384              /* PTLS_MAX_PLAINTEXT_RECORD_SIZE, lib/picotls.c:38 */
+#define PTLS_MI355X_TLS_MAX_RECORD (16384 + 256)        /* PTLS_MAX_ENCRYPTED_RECORD_SIZE, lib/picotls.c:39 */
+#define PTLS_MI355X_TLS_OVERHEAD (5 + 1 + 16)           /* header + content type + tag */
+#define PTLS_MI355X_TLS_BAD_RECORD_MAC 0xffffffffu      /* -> PTLS_ALERT_BAD_RECORD_MAC (20) */
+#define PTLS_MI355X_TLS_UNEXPECTED_MESSAGE 0xfffffffeu  /* -> PTLS_ALERT_UNEXPECTED_MESSAGE (10) */
+
+int ptls_mi355x_tls_seal_records(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12,
+                                 const ptls_mi355x_tls_record_t *recs, size_t n, const uint8_t *src, uint8_t *dst,
+                                 void *stream);
+int ptls_mi355x_tls_open_records(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12,
+                                 const ptls_mi355x_tls_record_t *recs, size_t n, const uint8_t *src, uint8_t *dst,
+                                 uint32_t *status, uint8_t *types, void *stream);
+
+/* Host-side planning (no device access), the loops of the reference record layer:
+ *  plan_send: splits len bytes at src_off into <= 16384-byte fragments with consecutive seq
+ *    from *seq, records laid out back to back from dst_off (buffer_push_encrypted_records,
+ *    lib/picotls.c:664-684).  Returns the number of records (recs may be NULL to count);
+ *    *wire_len = bytes the records occupy; *seq advanced past them.  Writes at most max.
+ *  parse_records: walks the complete records at the start of wire[0..len) (parse_record +
+ *    parse_record_header fast path, lib/picotls.c:4243-4268): type 23 records only, one
+ *    descriptor each (src = src_off + offset, plaintext slots back to back from dst_off,
+ *    consecutive seq from *seq).  Stops before an incomplete record, a record of another
+ *    type (left to the caller's slot path) or after max.  *consumed = bytes parsed,
+ *    *nrecs = descriptors written.  Returns 0, or PTLS_ALERT_DECODE_ERROR (50) for a length
+ *    field above PTLS_MI355X_TLS_MAX_RECORD (parse_record_header :4249-4251). */
+size_t ptls_mi355x_tls_plan_send(size_t len, uint32_t type, uint64_t *seq, uint64_t src_off, uint64_t dst_off,
+                                 ptls_mi355x_tls_record_t *recs, size_t max, size_t *wire_len);
+int ptls_mi355x_tls_parse_records(const uint8_t *wire, size_t len, uint64_t src_off, uint64_t *seq, uint64_t dst_off,
+                                  ptls_mi355x_tls_record_t *recs, size_t max, size_t *nrecs, size_t *consumed);
+
 /* ---- tuning / introspection ---- */
 /* lanes per record used by the batch kernels (1, 2, 4 or 8; default 4); returns the previous value, or -1 */
 int ptls_mi355x_set_lanes_per_record(int k);

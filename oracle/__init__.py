@@ -50,6 +50,10 @@ def _load():
         lib.oracle_gf128_mul.argtypes = [vp, vp, vp]
         lib.oracle_gcm_batch.argtypes = [C.c_int, vp, sz, vp, vp, sz, vp, vp, vp, vp, C.c_int]
         lib.oracle_gcm_batch.restype = C.c_int
+        lib.oracle_tls_seal_record.argtypes = [vp, sz, vp, C.c_uint64, C.c_uint8, vp, sz, sz, vp]
+        lib.oracle_tls_seal_record.restype = C.c_size_t
+        lib.oracle_tls_open_record.argtypes = [vp, sz, vp, C.c_uint64, vp, vp, vp]
+        lib.oracle_tls_open_record.restype = C.c_size_t
         _lib = lib
     return _lib
 
@@ -114,6 +118,31 @@ def batch(is_seal: bool, key: bytes, static_iv: bytes, recs, src, dst, aad, stat
     del np
 
 
+TLS_BAD_MAC = 2 ** 64 - 1  # oracle_tls_open_record: SIZE_MAX -> PTLS_ALERT_BAD_RECORD_MAC
+TLS_NO_TYPE = 2 ** 64 - 2  # all-zero inner plaintext -> PTLS_ALERT_UNEXPECTED_MESSAGE
+
+
+def tls_seal_record(key: bytes, static_iv: bytes, seq: int, content_type: int, fragment: bytes, pad: int = 0) -> bytes:
+    """One TLS 1.3 record: header || seal(fragment || type || 0^pad) (lib/picotls.c:621-684)."""
+    lib = _load()
+    out = C.create_string_buffer(5 + len(fragment) + 1 + pad + 16)
+    n = lib.oracle_tls_seal_record(key, len(key), static_iv, seq, content_type, _buf(fragment), len(fragment), pad, out)
+    assert n == len(out.raw)
+    return out.raw
+
+
+def tls_open_record(key: bytes, static_iv: bytes, seq: int, wire: bytes):
+    """-> (inner plaintext, content type) or TLS_BAD_MAC / TLS_NO_TYPE (lib/picotls.c:645-654,4779-4791)."""
+    lib = _load()
+    L = (wire[3] << 8) | wire[4]
+    out = C.create_string_buffer(max(L, 1))
+    t = C.c_uint8()
+    n = lib.oracle_tls_open_record(key, len(key), static_iv, seq, _buf(wire), out, C.byref(t))
+    if n in (TLS_BAD_MAC, TLS_NO_TYPE):
+        return n
+    return out.raw[:n], t.value
+
+
 class Reference:
     """The reference lib/fusion.c engine (oracle/_ref), for golden vectors and the CPU baseline."""
 
@@ -132,6 +161,12 @@ class Reference:
         lib.ref_ecb.argtypes = [vp, sz, vp, vp]
         lib.ref_bench.argtypes = [sz, sz, sz, sz, C.c_int, C.POINTER(C.c_double)]
         lib.ref_bench.restype = C.c_int
+        lib.ref_tls_send.argtypes = [vp, sz, vp, C.c_uint64, vp, sz, vp, sz, C.POINTER(C.c_size_t),
+                                     C.POINTER(C.c_uint64)]
+        lib.ref_tls_send.restype = C.c_int
+        lib.ref_tls_receive.argtypes = [vp, sz, vp, C.c_uint64, vp, sz, vp, sz, C.POINTER(C.c_size_t),
+                                        C.POINTER(C.c_size_t), C.POINTER(C.c_uint64)]
+        lib.ref_tls_receive.restype = C.c_int
         self.lib = lib
 
     def supported(self) -> bool:
@@ -172,6 +207,26 @@ class Reference:
         out = C.create_string_buffer(16)
         self.lib.ref_ecb(_buf(key), len(key), _buf(block), out)
         return out.raw
+
+    def tls_send(self, key, static_iv, seq0, data):
+        """The reference ptls_send() (lib/picotls.c:4969-4988): -> (wire bytes, next seq)."""
+        cap = len(data) + (len(data) // 16384 + 1) * 22 + 64
+        out = C.create_string_buffer(cap)
+        n, seq = C.c_size_t(), C.c_uint64()
+        rc = self.lib.ref_tls_send(key, len(key), static_iv, seq0, _buf(data), len(data), out, cap, C.byref(n),
+                                   C.byref(seq))
+        if rc != 0:
+            raise RuntimeError(f"ptls_send: {rc}")
+        return out.raw[: n.value], seq.value
+
+    def tls_receive(self, key, static_iv, seq0, wire):
+        """The reference ptls_receive() over a whole buffer: -> (rc, plaintext, consumed, next seq)."""
+        cap = len(wire) + 64
+        out = C.create_string_buffer(cap)
+        n, used, seq = C.c_size_t(), C.c_size_t(), C.c_uint64()
+        rc = self.lib.ref_tls_receive(key, len(key), static_iv, seq0, _buf(wire), len(wire), out, cap, C.byref(n),
+                                      C.byref(used), C.byref(seq))
+        return rc, out.raw[: n.value], used.value, seq.value
 
     def bench(self, keylen: int, length: int, aadlen: int, nrec_per_thread: int, nthreads: int):
         """t/ptlsbench.c methodology; returns (seal B/s, open B/s, wall s, failed)."""

@@ -364,3 +364,57 @@ int oracle_gcm_batch(int is_seal, const uint8_t *key, size_t keylen, const uint8
             pthread_join(th[t], NULL);
     return 0;
 }
+
+/* ------------------------------------------------------- TLS 1.3 records ----- */
+
+/*
+ * TLS 1.3 record framing over the AEAD, restated from picotls's record layer:
+ *   header = 17 03 03 BE16(length)          build_aad (lib/picotls.c:621-628) + buffer_push_record (:658-662)
+ *   body   = seal(fragment || type || 0^pad, aad = header, seq)
+ *                                           aead_encrypt (:630-643), length = fraglen + 1 + pad + 16
+ *   one record per <= 16384-byte fragment, seq + 1 per record   buffer_push_encrypted_records (:664-684)
+ * pad != 0 produces the zero padding picotls never sends but must strip on receive (RFC 8446 5.4).
+ * Writes 5 + fraglen + 1 + pad + 16 bytes to out (returned).  out must not overlap frag.
+ */
+size_t oracle_tls_seal_record(const uint8_t *key, size_t keylen, const uint8_t static_iv[12], uint64_t seq, uint8_t type,
+                              const uint8_t *frag, size_t fraglen, size_t pad, uint8_t *out)
+{
+    size_t body = fraglen + 1 + pad;
+    uint8_t iv[12];
+    out[0] = 23; /* PTLS_CONTENT_TYPE_APPDATA */
+    out[1] = 3;
+    out[2] = 3;
+    out[3] = (uint8_t)((body + 16) >> 8);
+    out[4] = (uint8_t)(body + 16);
+    memcpy(out + 5, frag, fraglen);
+    out[5 + fraglen] = type;
+    memset(out + 5 + fraglen + 1, 0, pad);
+    oracle_build_iv(static_iv, seq, iv);
+    if (oracle_gcm_seal(key, keylen, iv, out, 5, out + 5, body, out + 5) != 0)
+        return 0;
+    return 5 + body + 16;
+}
+
+/*
+ * Receive side of one record whose header is at wire[0..5) (length field L = ciphertext + tag):
+ * aead_decrypt (lib/picotls.c:645-654) with the AAD rebuilt from L (build_aad), then the padding
+ * strip and content-type pop of handle_input_tls13 (:4784-4791).  Returns the inner plaintext
+ * length with *type set; SIZE_MAX for a bad tag or L < 16 (-> PTLS_ALERT_BAD_RECORD_MAC),
+ * SIZE_MAX - 1 for an all-zero plaintext (-> PTLS_ALERT_UNEXPECTED_MESSAGE).  out holds L - 16 bytes.
+ */
+size_t oracle_tls_open_record(const uint8_t *key, size_t keylen, const uint8_t static_iv[12], uint64_t seq,
+                              const uint8_t *wire, uint8_t *out, uint8_t *type)
+{
+    size_t L = ((size_t)wire[3] << 8) | wire[4];
+    uint8_t aad[5] = {23, 3, 3, wire[3], wire[4]}, iv[12];
+    oracle_build_iv(static_iv, seq, iv);
+    size_t n = oracle_gcm_open(key, keylen, iv, aad, 5, wire + 5, L, out);
+    if (n == SIZE_MAX)
+        return SIZE_MAX;
+    while (n != 0 && out[n - 1] == 0)
+        --n;
+    if (n == 0)
+        return SIZE_MAX - 1;
+    *type = out[--n];
+    return n;
+}

@@ -37,6 +37,16 @@ RECORD_DTYPE = np.dtype([("src", "<u8"), ("dst", "<u8"), ("aad", "<u8"), ("seq",
                          ("aadlen", "<u4")])
 assert RECORD_DTYPE.itemsize == 40
 
+#: numpy mirror of ptls_mi355x_tls_record_t (include/ptls_mi355x.h section 4)
+TLS_RECORD_DTYPE = np.dtype([("src", "<u8"), ("dst", "<u8"), ("seq", "<u8"), ("len", "<u4"), ("type", "<u4")])
+assert TLS_RECORD_DTYPE.itemsize == 32
+TLS_HEADER_SIZE = 5
+TLS_MAX_FRAGMENT = 16384
+TLS_MAX_RECORD = 16384 + 256
+TLS_OVERHEAD = 5 + 1 + 16
+TLS_BAD_RECORD_MAC = 0xFFFFFFFF  # -> PTLS_ALERT_BAD_RECORD_MAC (20)
+TLS_UNEXPECTED_MESSAGE = 0xFFFFFFFE  # -> PTLS_ALERT_UNEXPECTED_MESSAGE (10)
+
 #: every symbol include/ptls_mi355x.h declares
 EXPORTED_FUNCTIONS = (
     "ptls_mi355x_is_supported", "ptls_mi355x_aesgcm_new", "ptls_mi355x_aesgcm_free", "ptls_mi355x_aesgcm_device",
@@ -44,6 +54,8 @@ EXPORTED_FUNCTIONS = (
     "ptls_mi355x_seal_batch", "ptls_mi355x_open_batch", "ptls_mi355x_order_by_length",
     "ptls_mi355x_seal_batch_ordered", "ptls_mi355x_open_batch_ordered", "ptls_mi355x_set_lanes_per_record",
     "ptls_mi355x_get_lanes_per_record", "ptls_mi355x_kernel_name", "ptls_mi355x_last_error",
+    "ptls_mi355x_tls_seal_records", "ptls_mi355x_tls_open_records", "ptls_mi355x_tls_plan_send",
+    "ptls_mi355x_tls_parse_records",
 )
 EXPORTED_OBJECTS = ("ptls_mi355x_aes128gcm", "ptls_mi355x_aes256gcm", "ptls_mi355x_aes128ctr",
                     "ptls_mi355x_aes256ctr")
@@ -118,6 +130,13 @@ def lib() -> C.CDLL:
         L.ptls_mi355x_kernel_name.argtypes = [C.c_int, sz]
         L.ptls_mi355x_kernel_name.restype = C.c_char_p
         L.ptls_mi355x_last_error.restype = C.c_char_p
+        L.ptls_mi355x_tls_seal_records.argtypes = [vp, vp, vp, sz, vp, vp, vp]
+        L.ptls_mi355x_tls_open_records.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]
+        L.ptls_mi355x_tls_plan_send.argtypes = [sz, C.c_uint32, C.POINTER(u64), u64, u64, vp, sz, C.POINTER(sz)]
+        L.ptls_mi355x_tls_plan_send.restype = sz
+        L.ptls_mi355x_tls_parse_records.argtypes = [vp, sz, u64, C.POINTER(u64), u64, vp, sz, C.POINTER(sz),
+                                                    C.POINTER(sz)]
+        L.ptls_mi355x_tls_parse_records.restype = C.c_int
         _lib = L
     return _lib
 
@@ -329,6 +348,47 @@ class Engine:
         if lib().ptls_mi355x_open_batch(self.handle, _cbuf(static_iv), recs_ptr, n, src_ptr, dst_ptr, aad_ptr,
                                         status_ptr, stream or None):
             raise RuntimeError("open_batch failed: " + last_error())
+
+
+    # TLS 1.3 record framing in the batch (include/ptls_mi355x.h section 4)
+    def tls_seal_records(self, static_iv: bytes, recs_ptr: int, n: int, src_ptr: int, dst_ptr: int,
+                         stream: int = 0) -> None:
+        if lib().ptls_mi355x_tls_seal_records(self.handle, _cbuf(static_iv), recs_ptr, n, src_ptr, dst_ptr,
+                                              stream or None):
+            raise RuntimeError("tls_seal_records failed: " + last_error())
+
+    def tls_open_records(self, static_iv: bytes, recs_ptr: int, n: int, src_ptr: int, dst_ptr: int, status_ptr: int,
+                         types_ptr: int, stream: int = 0) -> None:
+        if lib().ptls_mi355x_tls_open_records(self.handle, _cbuf(static_iv), recs_ptr, n, src_ptr, dst_ptr, status_ptr,
+                                              types_ptr, stream or None):
+            raise RuntimeError("tls_open_records failed: " + last_error())
+
+
+def tls_plan_send(length: int, seq: int, content_type: int = 23, src_off: int = 0, dst_off: int = 0):
+    """Descriptors for sending `length` bytes as records (buffer_push_encrypted_records, lib/picotls.c:664-684).
+    -> (TLS_RECORD_DTYPE array, wire bytes, next seq)."""
+    L = lib()
+    s = u64(seq)
+    wire = sz()
+    n = L.ptls_mi355x_tls_plan_send(length, content_type, C.byref(s), src_off, dst_off, None, 0, C.byref(wire))
+    recs = np.zeros(n, TLS_RECORD_DTYPE)
+    got = L.ptls_mi355x_tls_plan_send(length, content_type, C.byref(s), src_off, dst_off, recs.ctypes.data, n,
+                                      C.byref(wire))
+    assert got == n
+    return recs, wire.value, s.value
+
+
+def tls_parse_records(wire: bytes, seq: int, src_off: int = 0, dst_off: int = 0, max_records: int = 1 << 20):
+    """Descriptors for the complete type-23 records at the start of `wire` (parse_record, lib/picotls.c:4243-4268).
+    -> (rc, TLS_RECORD_DTYPE array, bytes consumed, next seq); rc 50 = PTLS_ALERT_DECODE_ERROR."""
+    L = lib()
+    cap = min(max_records, len(wire) // TLS_HEADER_SIZE + 1)
+    recs = np.zeros(cap, TLS_RECORD_DTYPE)
+    s, n, used = u64(seq), sz(), sz()
+    buf = np.frombuffer(wire, np.uint8) if wire else np.zeros(1, np.uint8)
+    rc = L.ptls_mi355x_tls_parse_records(buf.ctypes.data, len(wire), src_off, C.byref(s), dst_off, recs.ctypes.data,
+                                         cap, C.byref(n), C.byref(used))
+    return rc, recs[: n.value].copy(), used.value, s.value
 
 
 def set_lanes_per_record(k: int) -> int:

@@ -793,6 +793,17 @@ GCM_HD void store_partial(uint8_t *p, uint32_t n, u32x4 v)
         p[4u * q + 2u] = (uint8_t)(t >> 16);
 }
 
+/* byte n (< 16) of the block set to b; the block's bytes at and beyond n are zero */
+GCM_HD u32x4 insert_byte(u32x4 v, uint32_t n, uint32_t b)
+{
+    const uint32_t bits = (b & 0xffu) << (8u * (n & 3u));
+    v[0] |= (n >> 2) == 0u ? bits : 0u;
+    v[1] |= (n >> 2) == 1u ? bits : 0u;
+    v[2] |= (n >> 2) == 2u ? bits : 0u;
+    v[3] |= (n >> 2) == 3u ? bits : 0u;
+    return v;
+}
+
 /* bytes of a block at and beyond n zeroed (n < 16) */
 GCM_HD u32x4 mask_tail(u32x4 v, uint32_t n)
 {
@@ -842,12 +853,20 @@ GCM_HD u32x4 shr_bytes(u32x4 v, uint32_t n)
  * registers (seal), or read directly since the tag follows it (open) -- nothing is ever
  * read outside [aad, aad + aadlen) and [src, src + len (+16 for open)).
  */
-template <int NR, int K, bool SEAL>
+template <int NR, int K, bool SEAL, bool FRAME = false>
 GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk, uint32_t j, const Record &rec, bool valid,
                        uint32_t Tmax, uint32_t iv0, uint32_t iv1, uint32_t iv2, const uint8_t *src, uint8_t *dst,
-                       const uint8_t *aad, const uint8_t *dummy)
+                       const uint8_t *aad, const uint8_t *dummy, uint32_t ctype = 0u)
 {
-    const Walk wk = make_walk(rec.len, rec.aadlen, K);
+    /*
+     * FRAME (TLS 1.3 record framing, lib/picotls.c:621-684 and :4779-4791): the AAD is the 5-byte
+     * record header 17 03 03 BE16(plen + 16), built here in registers (build_aad), never read;
+     * seal's GCM payload is the fragment (rec.len bytes at src) followed by the content-type byte
+     * ctype, so plen = rec.len + 1 and the block holding the type byte is assembled in registers.
+     */
+    const uint32_t plen = FRAME && SEAL ? rec.len + 1u : rec.len;
+    const uint32_t aadlen = FRAME ? 5u : rec.aadlen;
+    const Walk wk = make_walk(plen, aadlen, K);
     const uint8_t *in = src + rec.src;
     uint8_t *out = dst + rec.dst;
     const uint8_t *ad = aad + rec.aad;
@@ -871,13 +890,15 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
         if (p < 0)
             return dummy;
         if ((uint32_t)p < wk.A) { /* a partial last AAD block is read as the AAD's last 16 bytes */
+            if (FRAME)
+                return dummy;
             if (16u * (uint32_t)p + 16u <= rec.aadlen)
                 return ad + 16u * (uint32_t)p;
             return rec.aadlen >= 16u ? ad + rec.aadlen - 16u : dummy;
         }
         const uint32_t c = (uint32_t)p - wk.A;
         if (c >= wk.C) /* the length block; open fetches the received tag into its slot */
-            return !SEAL && c == wk.C ? in + rec.len : dummy;
+            return !SEAL && c == wk.C ? in + plen : dummy;
         if (!SEAL || 16u * c + 16u <= rec.len)
             return in + 16u * c;
         return rec.len >= 16u ? in + rec.len - 16u : dummy;
@@ -896,7 +917,8 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
         const bool is_pay = active && (uint32_t)p >= wk.A && (uint32_t)p < wk.A + wk.C && p >= 0;
         const bool is_len = active && (uint32_t)p == wk.A + wk.C;
         const uint32_t c = (uint32_t)p - wk.A;
-        const uint32_t clen = rec.len - 16u * c; /* bytes of this payload block if < 16 */
+        const uint32_t clen = plen - 16u * c;    /* bytes of this payload block if < 16 */
+        const uint32_t flen = rec.len - 16u * c; /* of them from the input (FRAME seal: all but the type byte) */
 
         /* one AES per lane per step: payload counter c + 2, otherwise J0 (counter 1) */
         uint32_t ctr = is_pay ? c + 2u : 1u;
@@ -927,7 +949,22 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
         u32x4 X = {0u, 0u, 0u, 0u};
         if (is_pay) {
             u32x4 data = cur;
-            if (clen >= 16u) {
+            if (FRAME && SEAL && flen < 16u) {
+                /* the last block: fb = flen fragment bytes (0..15), then the content type */
+                if (flen == 0u)
+                    data = u32x4{0u, 0u, 0u, 0u};
+                else if (rec.len >= 16u)
+                    data = shr_bytes(data, 16u - flen);
+                else /* rare: a fragment under 16 bytes, read in place */
+                    data = load_partial(in, rec.len);
+                data = insert_byte(data, flen, ctype);
+                const u32x4 o = data ^ ks;
+                if (clen == 16u)
+                    *(u32x4_u *)(out + 16u * c) = o;
+                else
+                    store_partial(out + 16u * c, clen, o);
+                X = mask_tail(o, clen);
+            } else if (clen >= 16u) {
                 const u32x4 o = data ^ ks;
                 *(u32x4_u *)(out + 16u * c) = o;
                 X = SEAL ? o : data;
@@ -943,9 +980,15 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
                 X = mask_tail(SEAL ? o : data, clen);
             }
         } else if (is_aad) {
-            X = 16u * (uint32_t)p + 16u <= rec.aadlen || rec.aadlen < 16u ? cur : shr_bytes(cur, 16u - arem);
+            if (FRAME) { /* 17 03 03 BE16(plen + 16) */
+                const uint32_t reclen = plen + 16u;
+                X[0] = 0x00030317u | ((reclen >> 8) & 0xffu) << 24;
+                X[1] = reclen & 0xffu;
+            } else {
+                X = 16u * (uint32_t)p + 16u <= rec.aadlen || rec.aadlen < 16u ? cur : shr_bytes(cur, 16u - arem);
+            }
         } else if (is_len) {
-            uint64_t abits = (uint64_t)rec.aadlen * 8u, cbits = (uint64_t)rec.len * 8u;
+            uint64_t abits = (uint64_t)aadlen * 8u, cbits = (uint64_t)plen * 8u;
             X[0] = bswap32((uint32_t)(abits >> 32));
             X[1] = bswap32((uint32_t)abits);
             X[2] = bswap32((uint32_t)(cbits >> 32));
@@ -966,7 +1009,7 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
      * step 0 (front padding < K): its lane reads it byte-exact into the first buffer.
      */
     u32x4 bufA;
-    if (valid && rec.aadlen != 0u && rec.aadlen < 16u && j == wk.pad)
+    if (!FRAME && valid && rec.aadlen != 0u && rec.aadlen < 16u && j == wk.pad)
         bufA = load_partial(ad, rec.aadlen);
     else
         bufA = *(const u32x4_u *)fetch_ptr(0);

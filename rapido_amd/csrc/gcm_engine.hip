@@ -51,16 +51,31 @@ __device__ __forceinline__ u32x4 shfl_xor_u32x4(u32x4 v, int mask)
     return r;
 }
 
-template <int NR, int K, bool SEAL>
+/* TLS 1.3 record descriptor of the framing kernels (include/ptls_mi355x.h) */
+struct TlsRecord {
+    uint64_t src, dst, seq;
+    uint32_t len, type;
+};
+static_assert(sizeof(TlsRecord) == sizeof(ptls_mi355x_tls_record_t), "descriptor layout");
+
+/*
+ * FRAME = false: descs are ptls_mi355x_record_t (the AEAD batch API).
+ * FRAME = true:  descs are ptls_mi355x_tls_record_t; seal writes header || ciphertext(fragment ||
+ * type) || tag at dst (lib/picotls.c:630-643,658-684), open verifies header-framed records and
+ * strips padding / pops the content type (lib/picotls.c:4779-4791) into status / types.
+ */
+template <int NR, int K, bool SEAL, bool FRAME>
 __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2,
-                                               const Record *__restrict__ recs, const uint32_t *__restrict__ order,
+                                               const void *__restrict__ descs, const uint32_t *__restrict__ order,
                                                uint32_t nrecs, const uint8_t *src, uint8_t *dst,
                                                const uint8_t *__restrict__ aad, uint32_t *__restrict__ status,
-                                               uint32_t *__restrict__ work)
+                                               uint8_t *__restrict__ types, uint32_t *__restrict__ work)
 {
     static_assert(K <= MAX_KERNEL_K, "LDS holds at most MAX_KERNEL_K GHASH tables");
     __shared__ __attribute__((aligned(16))) uint8_t lds[Layout<K>::total];
     constexpr uint32_t R = 64 / K; /* records per wave step */
+    const Record *__restrict__ recs = (const Record *)descs;
+    const TlsRecord *__restrict__ trecs = (const TlsRecord *)descs;
 
     fill_lds(lds, c_tabs.t0, ki, K, threadIdx.x, blockDim.x);
 
@@ -70,13 +85,10 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
         rk[i] = ki->rk[i];
     __syncthreads();
 
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
     const uint32_t j = lane % K, slot = lane / K;
     const uint32_t lanesel = (lane & 31u) * 4u | 0x10000u; /* bank + image-B select (gcm_core.h) */
-    const uint32_t waves_per_block = blockDim.x >> 6;
     const uint32_t ngroups = (nrecs + R - 1) / R;
-    (void)wave;
-    (void)waves_per_block;
 
     /*
      * Record groups (64/K records) are handed out dynamically: one returning atomic per group
@@ -92,32 +104,60 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
         if (g >= ngroups)
             break;
         const uint32_t idx = g * R + slot;
-        const bool valid = idx < nrecs;
-        const uint32_t r = valid ? (order ? order[idx] : idx) : 0u;
+        const bool in_batch = idx < nrecs;
+        const uint32_t r = in_batch ? (order ? order[idx] : idx) : 0u;
         Record rec = {0, 0, 0, 0, 0, 0};
-        if (valid)
+        uint32_t ctype = 0u;
+        bool valid = in_batch;
+        if (FRAME) {
+            if (in_batch) {
+                const TlsRecord t = trecs[r];
+                rec.seq = t.seq;
+                rec.aadlen = 5u;
+                if (SEAL) { /* header at t.dst, ciphertext after it */
+                    rec.src = t.src;
+                    rec.dst = t.dst + 5u;
+                    rec.len = t.len;
+                    ctype = t.type;
+                } else { /* header at t.src; length field = ciphertext + tag */
+                    rec.src = t.src + 5u;
+                    rec.dst = t.dst;
+                    rec.len = t.len >= 16u ? t.len - 16u : 0u;
+                    valid = t.len >= 16u; /* shorter: bad_record_mac without a walk (aead_do_decrypt) */
+                }
+            }
+        } else if (in_batch) {
             rec = recs[r];
-        uint32_t T = valid ? make_walk(rec.len, rec.aadlen, K).T : 0u;
+        }
+        const uint32_t plen = FRAME && SEAL ? rec.len + 1u : rec.len;
+        uint32_t T = valid ? make_walk(plen, rec.aadlen, K).T : 0u;
         uint32_t Tmax = T;
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1)
             Tmax = max(Tmax, shfl_xor_u32(Tmax, o));
 
         const uint32_t n1 = iv1 ^ bswap32((uint32_t)(rec.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)rec.seq);
-        /* 16 always-readable bytes for idle prefetch slots: the first descriptor (40 B, nrecs >= 1) */
-        const uint8_t *dummy = (const uint8_t *)recs;
-        u32x4 part = lane_walk<NR, K, SEAL>(lds, lanesel, rk, j, rec, valid, Tmax, iv0, n1, n2, src, dst, aad, dummy);
+        /* 16 always-readable bytes for idle prefetch slots: the first descriptor (>= 32 B, nrecs >= 1) */
+        const uint8_t *dummy = (const uint8_t *)descs;
+        u32x4 part = lane_walk<NR, K, SEAL, FRAME>(lds, lanesel, rk, j, rec, valid, Tmax, iv0, n1, n2, src, dst, aad,
+                                                   dummy, ctype);
 #pragma unroll
         for (int o = 1; o < K; o <<= 1)
             part ^= shfl_xor_u32x4(part, o);
 
         if (SEAL) {
-            if (j == 0 && valid)
-                *(u32x4_u *)(dst + rec.dst + rec.len) = part;
+            if (j == 0 && valid) {
+                *(u32x4_u *)(dst + rec.dst + plen) = part;
+                if (FRAME) { /* record header 17 03 03 BE16(plen + 16) (buffer_push_record, lib/picotls.c:658-662) */
+                    const uint32_t reclen = plen + 16u;
+                    store_partial(dst + rec.dst - 5u, 5u, u32x4{0x00030317u | ((reclen >> 8) & 0xffu) << 24, reclen & 0xffu,
+                                                             0u, 0u});
+                }
+            }
         } else {
             /* part = computed tag ^ received tag (lane_walk) */
-            const bool bad = valid && (part[0] | part[1] | part[2] | part[3]) != 0u;
-            if (j == 0 && valid)
+            const bool bad = in_batch && (!valid || (part[0] | part[1] | part[2] | part[3]) != 0u);
+            if (j == 0 && in_batch && !FRAME)
                 status[r] = bad ? 0xffffffffu : rec.len;
             if (bad) {
                 /*
@@ -125,18 +165,59 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
                  * Rare path: the descriptor is re-read through an opaque pointer so the walk does
                  * not keep dst/len alive in registers for it.
                  */
-                const Record *rp = recs + r;
-                asm volatile("" : "+v"(rp));
-                const Record again = *rp;
-                uint8_t *out = dst + again.dst;
-                for (uint32_t off = 16u * j; off < again.len; off += 16u * K) {
-                    uint32_t n = again.len - off;
+                uint64_t odst;
+                uint32_t olen;
+                if (FRAME) {
+                    const TlsRecord *tp = trecs + r;
+                    asm volatile("" : "+v"(tp));
+                    const TlsRecord again = *tp;
+                    odst = again.dst;
+                    olen = again.len >= 16u ? again.len - 16u : 0u;
+                    if (j == 0) {
+                        status[r] = 0xffffffffu; /* PTLS_ALERT_BAD_RECORD_MAC */
+                        types[r] = 0u;
+                    }
+                } else {
+                    const Record *rp = recs + r;
+                    asm volatile("" : "+v"(rp));
+                    const Record again = *rp;
+                    odst = again.dst;
+                    olen = again.len;
+                }
+                uint8_t *out = dst + odst;
+                for (uint32_t off = 16u * j; off < olen; off += 16u * K) {
+                    uint32_t n = olen - off;
                     u32x4 z = {0u, 0u, 0u, 0u};
                     if (n >= 16)
                         *(u32x4_u *)(out + off) = z;
                     else
                         store_partial(out + off, n, z);
                 }
+            } else if (FRAME && in_batch && j == 0) {
+                /*
+                 * Verified record: skip the zero padding and pop the content type
+                 * (handle_input_tls13, lib/picotls.c:4784-4791), reading back the plaintext the
+                 * record's K lanes have just stored (made visible to this lane by the fence).
+                 */
+                __threadfence_block();
+                const uint8_t *pt = dst + rec.dst;
+                uint32_t n = plen, found = 0xfffffffeu; /* PTLS_ALERT_UNEXPECTED_MESSAGE if all zero */
+                uint32_t ty = 0u;
+                while (n != 0u && found == 0xfffffffeu) {
+                    const uint32_t base = n >= 16u ? n - 16u : 0u;
+                    const u32x4 v = n >= 16u ? *(const u32x4_u *)(pt + base) : load_partial(pt, n);
+#pragma unroll
+                    for (int d = 3; d >= 0; --d) {
+                        if (found == 0xfffffffeu && v[d] != 0u) {
+                            const uint32_t b = (31u - (uint32_t)__builtin_clz(v[d])) >> 3; /* highest nonzero byte */
+                            found = base + 4u * (uint32_t)d + b;
+                            ty = (v[d] >> (8u * b)) & 0xffu;
+                        }
+                    }
+                    n = base;
+                }
+                status[r] = found;
+                types[r] = (uint8_t)ty;
             }
         }
     }
@@ -145,14 +226,16 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
 } // namespace
 
 /* Named kernel instances (readable in rocprofv3 traces). */
-#define MI355X_GCM_KERNEL(NAME, NR, K, SEAL)                                                                           \
+#define MI355X_GCM_KERNEL_F(NAME, NR, K, SEAL, FRAME)                                                                  \
     extern "C" __global__ __launch_bounds__(WG_THREADS) void NAME(                                                     \
-        const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2, const Record *__restrict__ recs,    \
+        const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2, const void *__restrict__ descs,     \
         const uint32_t *__restrict__ order, uint32_t nrecs, const uint8_t *src, uint8_t *dst,                          \
-        const uint8_t *__restrict__ aad, uint32_t *__restrict__ st, uint32_t *__restrict__ work)                       \
+        const uint8_t *__restrict__ aad, uint32_t *__restrict__ st, uint8_t *__restrict__ types,                       \
+        uint32_t *__restrict__ work)                                                                                   \
     {                                                                                                                  \
-        gcm_batch_body<NR, K, SEAL>(ki, iv0, iv1, iv2, recs, order, nrecs, src, dst, aad, st, work);                   \
+        gcm_batch_body<NR, K, SEAL, FRAME>(ki, iv0, iv1, iv2, descs, order, nrecs, src, dst, aad, st, types, work);    \
     }
+#define MI355X_GCM_KERNEL(NAME, NR, K, SEAL) MI355X_GCM_KERNEL_F(NAME, NR, K, SEAL, false)
 
 MI355X_GCM_KERNEL(mi355x_gcm_seal_aes128_k1, 10, 1, true)
 MI355X_GCM_KERNEL(mi355x_gcm_seal_aes128_k2, 10, 2, true)
@@ -170,6 +253,11 @@ MI355X_GCM_KERNEL(mi355x_gcm_open_aes256_k1, 14, 1, false)
 MI355X_GCM_KERNEL(mi355x_gcm_open_aes256_k2, 14, 2, false)
 MI355X_GCM_KERNEL(mi355x_gcm_open_aes256_k4, 14, 4, false)
 MI355X_GCM_KERNEL(mi355x_gcm_open_aes256_k8, 14, 8, false)
+/* TLS 1.3 record framing (K = 4: the framing batches are window-sized, see ptls_mi355x_tls_seal_records) */
+MI355X_GCM_KERNEL_F(mi355x_tls_seal_aes128_k4, 10, 4, true, true)
+MI355X_GCM_KERNEL_F(mi355x_tls_seal_aes256_k4, 14, 4, true, true)
+MI355X_GCM_KERNEL_F(mi355x_tls_open_aes128_k4, 10, 4, false, true)
+MI355X_GCM_KERNEL_F(mi355x_tls_open_aes256_k4, 14, 4, false, true)
 
 /* key image: round keys, H and the nibble tables of H^1..H^8 (cold path, one thread) */
 extern "C" __global__ void mi355x_gcm_setup(const uint8_t *key, uint32_t keylen, KeyImage *ki, int *rc)
@@ -188,8 +276,8 @@ extern "C" __global__ void mi355x_aes_ecb(const KeyImage *__restrict__ ki, const
 
 /* ================================================================== host side ============ */
 
-typedef void (*batch_kernel_t)(const KeyImage *, uint32_t, uint32_t, uint32_t, const Record *, const uint32_t *, uint32_t,
-                               const uint8_t *, uint8_t *, const uint8_t *, uint32_t *, uint32_t *);
+typedef void (*batch_kernel_t)(const KeyImage *, uint32_t, uint32_t, uint32_t, const void *, const uint32_t *, uint32_t,
+                               const uint8_t *, uint8_t *, const uint8_t *, uint32_t *, uint8_t *, uint32_t *);
 
 constexpr uint32_t WORK_SLOTS = 256; /* per-context ring of work counters: one per launch in flight */
 
@@ -276,11 +364,18 @@ static batch_kernel_t pick_kernel(bool seal, uint32_t rounds, int k, const char 
     return nullptr;
 }
 
+static batch_kernel_t pick_tls_kernel(bool seal, uint32_t rounds)
+{
+    if (rounds == 10)
+        return seal ? mi355x_tls_seal_aes128_k4 : mi355x_tls_open_aes128_k4;
+    return seal ? mi355x_tls_seal_aes256_k4 : mi355x_tls_open_aes256_k4;
+}
+
 static inline uint32_t le32(const uint8_t *p) { return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24; }
 
-static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void *static_iv12, const Record *recs,
+static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void *static_iv12, const void *recs,
                         const uint32_t *order, size_t n, const uint8_t *src, uint8_t *dst, const uint8_t *aad,
-                        uint32_t *status, hipStream_t stream)
+                        uint32_t *status, hipStream_t stream, bool frame = false, uint8_t *types = nullptr)
 {
     if (n == 0)
         return 0;
@@ -288,8 +383,9 @@ static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void
         snprintf(g_err, sizeof(g_err), "batch of %zu records exceeds 2^32-1", n);
         return -1;
     }
-    const int k = g_lanes;
-    batch_kernel_t kern = pick_kernel(seal, ctx->key_size == 32 ? 14u : 10u, k, nullptr);
+    const int k = frame ? 4 : g_lanes;
+    batch_kernel_t kern = frame ? pick_tls_kernel(seal, ctx->key_size == 32 ? 14u : 10u)
+                                : pick_kernel(seal, ctx->key_size == 32 ? 14u : 10u, k, nullptr);
     if (kern == nullptr) {
         snprintf(g_err, sizeof(g_err), "no kernel for lanes-per-record %d", k);
         return -1;
@@ -304,7 +400,7 @@ static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void
     uint32_t *work = ctx->d_work + (ctx->work_next++ % WORK_SLOTS);
     HIPCHK(hipMemsetAsync(work, 0, sizeof(uint32_t), stream));
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(WG_THREADS), 0, stream, ctx->d_ki, le32(iv), le32(iv + 4),
-                       le32(iv + 8), recs, order, (uint32_t)n, src, dst, aad, status, work);
+                       le32(iv + 8), recs, order, (uint32_t)n, src, dst, aad, status, types, work);
     HIPCHK(hipGetLastError());
     return 0;
 }
@@ -460,6 +556,26 @@ int ptls_mi355x_open_batch_ordered(ptls_mi355x_aesgcm_context_t *ctx, const void
 {
     return launch_batch(ctx, false, static_iv12, (const Record *)recs, order, n, src, dst, aad, status,
                         (hipStream_t)stream);
+}
+
+int ptls_mi355x_tls_seal_records(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12,
+                                 const ptls_mi355x_tls_record_t *recs, size_t n, const uint8_t *src, uint8_t *dst,
+                                 void *stream)
+{
+    return launch_batch(ctx, true, static_iv12, recs, nullptr, n, src, dst, nullptr, nullptr, (hipStream_t)stream,
+                        true, nullptr);
+}
+
+int ptls_mi355x_tls_open_records(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12,
+                                 const ptls_mi355x_tls_record_t *recs, size_t n, const uint8_t *src, uint8_t *dst,
+                                 uint32_t *status, uint8_t *types, void *stream)
+{
+    if (n != 0 && (status == nullptr || types == nullptr)) {
+        snprintf(g_err, sizeof(g_err), "tls_open_records needs status and types");
+        return -1;
+    }
+    return launch_batch(ctx, false, static_iv12, recs, nullptr, n, src, dst, nullptr, status, (hipStream_t)stream,
+                        true, types);
 }
 
 /* keys = GHASH steps of each record (its work), values = record index */

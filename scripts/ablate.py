@@ -38,7 +38,6 @@ def build():
     from rapido_amd import build as b
     os.makedirs(VDIR, exist_ok=True)
     b.build_engine()
-    c_obj = os.path.join(b.OBJDIR, "aead_slot.o")
     for name, flags in VARIANTS.items():
         obj = os.path.join(VDIR, name + ".o")
         so = os.path.join(VDIR, name + ".so")
@@ -53,7 +52,7 @@ def build():
         src = os.path.join(srcdir, "gcm_engine.hip")
         subprocess.run([b.HIPCC, f"--offload-arch={b.ARCH}", "-O3", "-std=c++17", "-fPIC", "-I" + b.CSRC, *flags, "-c",
                         src, "-o", obj], check=True)
-        subprocess.run([b.HIPCC, f"--offload-arch={b.ARCH}", "-shared", "-fPIC", "-o", so, obj, c_obj], check=True)
+        subprocess.run([b.HIPCC, f"--offload-arch={b.ARCH}", "-shared", "-fPIC", "-o", so, obj] + b.C_OBJS, check=True)
         print("built", so)
 
 

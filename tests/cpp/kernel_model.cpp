@@ -29,7 +29,6 @@ static void run(const KeyImage *ki, const uint8_t *lds, const uint8_t *static_iv
         const Record &r = recs[i];
         Walk wk = make_walk(r.len, r.aadlen, K);
         uint32_t n1 = iv1 ^ bswap32((uint32_t)(r.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)r.seq);
-        /* received tag first: open may run in place */
         u32x4 tag = {0, 0, 0, 0};
         for (uint32_t j = 0; j < (uint32_t)K; ++j)
             tag ^= lane_walk<NR, K, SEAL>(lds, 4u * (j & 31u) | 0x10000u, ki->rk, j, r, true, wk.T, iv0, n1, n2, src, dst, aad,
@@ -41,6 +40,88 @@ static void run(const KeyImage *ki, const uint8_t *lds, const uint8_t *static_iv
             status[i] = (d[0] | d[1] | d[2] | d[3]) ? 0xffffffffu : r.len;
         }
     }
+}
+
+/* ptls_mi355x_tls_record_t (include/ptls_mi355x.h section 4) */
+struct TlsRecord {
+    uint64_t src, dst, seq;
+    uint32_t len, type;
+};
+
+/* the FRAME walk (TLS 1.3 record framing) with the framing kernels' prologue/epilogue, K = 4 */
+template <int NR, bool SEAL>
+static void run_tls(const KeyImage *ki, const uint8_t *lds, const uint8_t *static_iv, const TlsRecord *trecs, size_t n,
+                    const uint8_t *src, uint8_t *dst, uint32_t *status, uint8_t *types)
+{
+    constexpr int K = 4;
+    uint32_t iv0, iv1, iv2;
+    memcpy(&iv0, static_iv, 4);
+    memcpy(&iv1, static_iv + 4, 4);
+    memcpy(&iv2, static_iv + 8, 4);
+    for (size_t i = 0; i < n; ++i) {
+        const TlsRecord &t = trecs[i];
+        Record r = {0, 0, 0, t.seq, 0, 5};
+        if (SEAL) {
+            r.src = t.src;
+            r.dst = t.dst + 5;
+            r.len = t.len;
+        } else {
+            if (t.len < 16) {
+                status[i] = 0xffffffffu;
+                types[i] = 0;
+                continue;
+            }
+            r.src = t.src + 5;
+            r.dst = t.dst;
+            r.len = t.len - 16;
+        }
+        const uint32_t plen = SEAL ? r.len + 1 : r.len;
+        Walk wk = make_walk(plen, 5, K);
+        uint32_t n1 = iv1 ^ bswap32((uint32_t)(r.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)r.seq);
+        u32x4 tag = {0, 0, 0, 0};
+        for (uint32_t j = 0; j < (uint32_t)K; ++j)
+            tag ^= lane_walk<NR, K, SEAL, true>(lds, 4u * (j & 31u) | 0x10000u, ki->rk, j, r, true, wk.T, iv0, n1, n2, src,
+                                                dst, nullptr, (const uint8_t *)trecs, t.type);
+        if (SEAL) {
+            memcpy(dst + r.dst + plen, &tag, 16);
+            const uint32_t reclen = plen + 16;
+            const uint8_t hdr[5] = {23, 3, 3, (uint8_t)(reclen >> 8), (uint8_t)reclen};
+            memcpy(dst + t.dst, hdr, 5);
+        } else if (tag[0] | tag[1] | tag[2] | tag[3]) {
+            status[i] = 0xffffffffu;
+            types[i] = 0;
+            memset(dst + r.dst, 0, plen);
+        } else {
+            uint32_t m = plen;
+            while (m != 0 && dst[r.dst + m - 1] == 0)
+                --m;
+            status[i] = m ? m - 1 : 0xfffffffeu;
+            types[i] = m ? dst[r.dst + m - 1] : 0;
+        }
+    }
+}
+
+extern "C" int model_tls_batch(int is_seal, const uint8_t *key, size_t keylen, const uint8_t *static_iv,
+                               const TlsRecord *trecs, size_t n, const uint8_t *src, uint8_t *dst, uint32_t *status,
+                               uint8_t *types)
+{
+    KeyImage *ki = (KeyImage *)aligned_alloc(64, sizeof(KeyImage));
+    uint8_t *lds = (uint8_t *)aligned_alloc(256, 160u * 1024u);
+    if (build_key_image(kTabs.sbox, key, (uint32_t)keylen, ki) != 0) {
+        free(ki);
+        free(lds);
+        return -1;
+    }
+    fill_lds(lds, kTabs.t0, ki, 4u, 0, 1);
+    if (ki->rounds == 10)
+        is_seal ? run_tls<10, true>(ki, lds, static_iv, trecs, n, src, dst, status, types)
+                : run_tls<10, false>(ki, lds, static_iv, trecs, n, src, dst, status, types);
+    else
+        is_seal ? run_tls<14, true>(ki, lds, static_iv, trecs, n, src, dst, status, types)
+                : run_tls<14, false>(ki, lds, static_iv, trecs, n, src, dst, status, types);
+    free(ki);
+    free(lds);
+    return 0;
 }
 
 extern "C" int model_batch(int is_seal, int K, const uint8_t *key, size_t keylen, const uint8_t *static_iv,

@@ -17,6 +17,12 @@ through oracle/ref_fusion_harness.c:
                           rapido's connection-id IV + ptls_aead_encrypt, lib/picotls.c:630-643,
                           lib/rapido.c:127-133), below fusion's slot capacity.
 * fusion_supp.json     -- supplementary (header-protection) outputs, lib/fusion.c:472-487.
+* tls_records.json     -- the reference TLS record layer (ptls_send / ptls_receive of
+                          lib/picotls.c, driven by oracle/ref_record_harness.c over the fusion
+                          core): send = wire bytes (SHA-256, full hex when small) for a stream of
+                          xorshift64star(seed, len) application data from seq0; receive = the
+                          reference's return code and plaintext for padded / tampered / all-zero
+                          records (their wire bytes built by oracle.tls_seal_record).
 
 The known-answer vectors transcribed from the reference's own tests (t/fusion.c,
 t/picotls.c, deps/cifra/src/testmodes.c) live in kats.json and are data only.
@@ -112,6 +118,42 @@ def main():
                      "ct": ct.hex(), "sample_off": off, "supp_out": so.hex()})
     with open(os.path.join(HERE, "fusion_supp.json"), "w") as f:
         json.dump({"source": "reference ptls_fusion_aesgcm_encrypt with supp", "cases": supp}, f, indent=0)
+    tls = {"send": [], "receive": []}
+    trng = np.random.default_rng(8446)
+    for keylen in (16, 32):
+        for ln in (1, 15, 16, 17, 255, 1400, 16383, 16384, 16385, 40000):
+            seed = 5000 + ln + keylen
+            key, iv = xorshift_bytes(seed + 1, keylen), xorshift_bytes(seed + 2, 12)
+            seq0 = int(trng.integers(0, 2 ** 20))
+            data = xorshift_bytes(seed, ln)
+            wire, seq_after = ref.tls_send(key, iv, seq0, data)
+            rc, pt, used, _ = ref.tls_receive(key, iv, seq0, wire)
+            assert rc == 0 and pt == data and used == len(wire)
+            case = {"keylen": keylen, "len": ln, "seed": seed, "seq0": seq0, "seq_after": seq_after,
+                    "wire_len": len(wire), "wire_sha256": hashlib.sha256(wire).hexdigest()}
+            if len(wire) <= 128:
+                case["wire"] = wire.hex()
+            tls["send"].append(case)
+    for i, (ln, ctype, pad, tamper) in enumerate([(50, 23, 0, False), (50, 23, 1, False), (50, 23, 15, False),
+                                                  (50, 23, 16, False), (0, 23, 40, False), (300, 23, 333, False),
+                                                  (16000, 23, 384, False), (10, 23, 0, True), (0, 0, 7, False),
+                                                  (0, 0, 0, False)]):
+        keylen = 16 if i % 2 == 0 else 32
+        key = trng.integers(0, 256, keylen, dtype=np.uint8).tobytes()
+        iv = trng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+        seq = int(trng.integers(0, 2 ** 24))
+        frag = trng.integers(1, 256, ln, dtype=np.uint8).tobytes()
+        wire = bytearray(oracle.tls_seal_record(key, iv, seq, ctype, frag, pad))
+        if tamper:
+            wire[-1] ^= 0x80
+        rc, pt, used, _ = ref.tls_receive(key, iv, seq, bytes(wire))
+        tls["receive"].append({"key": key.hex(), "iv": iv.hex(), "seq": seq, "wire": bytes(wire).hex(), "rc": rc,
+                               "plaintext": pt.hex()})
+    with open(os.path.join(HERE, "tls_records.json"), "w") as f:
+        json.dump({"source": "reference lib/picotls.c ptls_send / ptls_receive via oracle/ref_record_harness.c",
+                   "inputs": "send: key=xorshift64star(seed+1,keylen) iv=xorshift64star(seed+2,12) "
+                             "data=xorshift64star(seed,len); receive: wire from oracle.tls_seal_record",
+                   "rc": "0 ok, 20 PTLS_ALERT_BAD_RECORD_MAC, 10 PTLS_ALERT_UNEXPECTED_MESSAGE", **tls}, f, indent=0)
     print("golden fixtures written to", HERE)
 
 

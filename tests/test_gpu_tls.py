@@ -1,0 +1,211 @@
+"""GPU parity of the TLS 1.3 record-framing kernels (include/ptls_mi355x.h section 4, SURVEY.md 8(f)
+rows 1-3) through the C-ABI: against the reference record layer's own outputs
+(tests/golden/tls_records.json: ptls_send / ptls_receive of lib/picotls.c) and the oracle's
+restatement of it.  Bit-exact wire bytes, plaintext, status and content types."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import rapido_amd as ra
+from rapido_amd.records import xorshift64star
+
+pytestmark = pytest.mark.gpu
+GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "tls_records.json")))
+
+
+def dev(a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def seal(eng, iv, trecs, src, wire_size, dst=None):
+    import torch
+    d_src = dev(src)
+    d_dst = torch.zeros(wire_size, dtype=torch.uint8, device="cuda") if dst is None else dst
+    d_recs = dev(trecs.view(np.uint8))
+    eng.tls_seal_records(iv, d_recs.data_ptr(), len(trecs), d_src.data_ptr(), d_dst.data_ptr())
+    torch.cuda.synchronize()
+    return d_dst.cpu().numpy()
+
+
+def open_(eng, iv, orecs, wire, pt_size, inplace=False):
+    import torch
+    d_wire = dev(wire)
+    d_pt = d_wire if inplace else torch.zeros(max(pt_size, 1), dtype=torch.uint8, device="cuda")
+    d_recs = dev(orecs.view(np.uint8))
+    d_st = torch.zeros(max(len(orecs), 1), dtype=torch.int32, device="cuda")
+    d_ty = torch.zeros(max(len(orecs), 1), dtype=torch.uint8, device="cuda")
+    eng.tls_open_records(iv, d_recs.data_ptr(), len(orecs), d_wire.data_ptr(), d_pt.data_ptr(), d_st.data_ptr(),
+                         d_ty.data_ptr())
+    torch.cuda.synchronize()
+    return d_pt.cpu().numpy(), d_st.cpu().numpy().view(np.uint32), d_ty.cpu().numpy()
+
+
+def xs(seed, n):
+    return xorshift64star(seed, n).tobytes()
+
+
+@pytest.mark.parametrize("case", GOLDEN["send"], ids=lambda c: f"aes{c['keylen'] * 8}-{c['len']}")
+def test_send_matches_reference_ptls_send(gpu, case):
+    """ptls_send's wire bytes (lib/picotls.c:4969-4988) from one framing launch per stream."""
+    key, iv = xs(case["seed"] + 1, case["keylen"]), xs(case["seed"] + 2, 12)
+    data = np.frombuffer(xs(case["seed"], case["len"]), np.uint8)
+    trecs, wire_len, seq = ra.tls_plan_send(case["len"], case["seq0"])
+    assert wire_len == case["wire_len"] and seq == case["seq_after"]
+    eng = ra.Engine(key)
+    wire = seal(eng, iv, trecs, data, wire_len).tobytes()
+    assert hashlib.sha256(wire).hexdigest() == case["wire_sha256"]
+    if "wire" in case:
+        assert wire.hex() == case["wire"]
+    # and back: parse the wire on the host, open every record in one launch
+    rc, orecs, used, seq2 = ra.tls_parse_records(wire, case["seq0"])
+    assert rc == 0 and used == len(wire) and seq2 == seq
+    pt, st, ty = open_(eng, iv, orecs, np.frombuffer(wire, np.uint8), case["len"] + 16 * len(orecs))
+    assert list(st[: len(orecs)]) == list(trecs["len"]) and (ty[: len(orecs)] == 23).all()
+    got = b"".join(pt[int(o["dst"]): int(o["dst"]) + int(s)].tobytes() for o, s in zip(orecs, st))
+    assert got == data.tobytes()
+
+
+@pytest.mark.parametrize("i", range(len(GOLDEN["receive"])))
+def test_receive_matches_reference_ptls_receive(gpu, i):
+    """Padding strip, content-type pop, bad MAC and no-content-type verdicts of handle_input_tls13."""
+    c = GOLDEN["receive"][i]
+    key, iv, wire = bytes.fromhex(c["key"]), bytes.fromhex(c["iv"]), bytes.fromhex(c["wire"])
+    rc, orecs, used, _ = ra.tls_parse_records(wire, c["seq"])
+    assert rc == 0 and len(orecs) == 1
+    pt, st, ty = open_(ra.Engine(key), iv, orecs, np.frombuffer(wire, np.uint8), int(orecs[0]["len"]))
+    if c["rc"] == 20:
+        assert st[0] == ra.TLS_BAD_RECORD_MAC and not pt.any()
+    elif c["rc"] == 10:
+        assert st[0] == ra.TLS_UNEXPECTED_MESSAGE
+    else:
+        assert pt[: st[0]].tobytes() == bytes.fromhex(c["plaintext"]) and ty[0] == 23
+
+
+@pytest.mark.parametrize("keylen", [16, 32])
+def test_framing_edges_vs_oracle(gpu, keylen):
+    """Every fragment length around the block edges, three content types, unaligned offsets, both ways."""
+    rng = np.random.default_rng(100 + keylen)
+    key, iv = rng.integers(0, 256, keylen, dtype=np.uint8).tobytes(), rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    lens = list(range(0, 70)) + [255, 256, 1399, 1400, 1401, 4095, 16383, 16384] + list(rng.integers(0, 16385, 60))
+    n = len(lens)
+    trecs = np.zeros(n, ra.TLS_RECORD_DTYPE)
+    off = woff = 0
+    for i, ln in enumerate(lens):
+        trecs[i] = (off, woff, int(rng.integers(0, 2 ** 48)), ln, [23, 22, 21, 0x40][i % 4])
+        off += int(ln) + 3
+        woff += int(ln) + 22 + (i % 5)
+    src = rng.integers(0, 256, off + 16, dtype=np.uint8)
+    eng = ra.Engine(key)
+    wire = seal(eng, iv, trecs, src, woff + 16)
+    for t in trecs:
+        frag = src[int(t["src"]): int(t["src"]) + int(t["len"])].tobytes()
+        want = oracle.tls_seal_record(key, iv, int(t["seq"]), int(t["type"]), frag)
+        assert wire[int(t["dst"]): int(t["dst"]) + len(want)].tobytes() == want, int(t["len"])
+    orecs = trecs.copy()
+    orecs["src"], orecs["len"] = trecs["dst"], trecs["len"] + 17
+    orecs["dst"] = np.concatenate([[0], np.cumsum((orecs["len"] - 16).astype(np.uint64))[:-1]]).astype(np.uint64)
+    pt, st, ty = open_(eng, iv, orecs, wire, int(orecs["dst"][-1]) + int(orecs["len"][-1]))
+    assert list(st[:n]) == lens and list(ty[:n]) == list(trecs["type"])
+    for t, o in zip(trecs, orecs):
+        assert pt[int(o["dst"]): int(o["dst"]) + int(t["len"])].tobytes() == \
+            src[int(t["src"]): int(t["src"]) + int(t["len"])].tobytes()
+
+
+def test_open_padding_tamper_short(gpu):
+    key, iv = bytes(range(16)), bytes(range(30, 42))
+    cases = [(50, 23, 0), (50, 23, 1), (50, 23, 15), (50, 23, 16), (0, 23, 40), (300, 23, 333), (0, 0, 7),
+             (1000, 22, 2000), (15, 21, 17)]
+    wires = [oracle.tls_seal_record(key, iv, 77 + i, t, bytes(k % 255 + 1 for k in range(n)), p)
+             for i, (n, t, p) in enumerate(cases)]
+    seqs = [77 + i for i in range(len(cases))]
+    for k in (1, 9, -3):  # the header's version byte (not in the AAD: build_aad uses 03 03), ciphertext, tag
+        w = bytearray(oracle.tls_seal_record(key, iv, 1, 23, bytes(range(100))))
+        w[k] ^= 1
+        wires.append(bytes(w))
+        seqs.append(1)
+    w = bytearray(oracle.tls_seal_record(key, iv, 1, 23, bytes(range(100))))
+    wires.append(bytes(w)); seqs.append(2)  # wrong seq
+    wires.append(b"\x17\x03\x03\x00\x0f" + bytes(15)); seqs.append(3)  # shorter than a tag
+    wires.append(b"\x17\x03\x03\x00\x10" + bytes(16)); seqs.append(4)  # empty ciphertext, wrong tag
+    buf = b"".join(wires)
+    rc, orecs, used, _ = ra.tls_parse_records(buf, 0)
+    assert rc == 0 and len(orecs) == len(wires) and used == len(buf)
+    orecs["seq"] = seqs
+    pt, st, ty = open_(ra.Engine(key), iv, orecs, np.frombuffer(buf, np.uint8),
+                       int(orecs["dst"][-1]) + int(orecs["len"][-1]))
+    for i, w in enumerate(wires):
+        want = oracle.tls_open_record(key, iv, seqs[i], w)
+        o = orecs[i]
+        if want == oracle.TLS_BAD_MAC:
+            assert st[i] == ra.TLS_BAD_RECORD_MAC, i
+            assert not pt[int(o["dst"]): int(o["dst"]) + max(int(o["len"]) - 16, 0)].any()
+        elif want == oracle.TLS_NO_TYPE:
+            assert st[i] == ra.TLS_UNEXPECTED_MESSAGE, i
+        else:
+            assert st[i] == len(want[0]) and ty[i] == want[1], i
+            assert pt[int(o["dst"]): int(o["dst"]) + int(st[i])].tobytes() == want[0]
+
+
+def test_rapido_windows_and_retransmission(gpu):
+    """rapido's send window (16 x 16406-B records, lib/rapido.c:2083-2126) sealed in one launch, a recv()
+    window of 32 records (:2030) opened in one launch, and the retransmission path (:1555-1590): a
+    non-contiguous subset of the sent records re-opened with their stored sequence numbers."""
+    key, iv = bytes(range(7, 23)), bytes(range(12))
+    data = xorshift64star(11, 16 * 16384).tobytes()
+    trecs, wire_len, seq = ra.tls_plan_send(len(data), 1000)
+    assert len(trecs) == 16 and wire_len == 16 * 16406
+    eng = ra.Engine(key)
+    wire = seal(eng, iv, trecs, np.frombuffer(data, np.uint8), wire_len)
+    # recv window of 32 records: two send windows back to back
+    wire2 = np.concatenate([wire, seal(eng, iv, ra.tls_plan_send(len(data), seq)[0], np.frombuffer(data, np.uint8),
+                                       wire_len)])
+    rc, orecs, used, _ = ra.tls_parse_records(wire2.tobytes(), 1000)
+    assert rc == 0 and len(orecs) == 32 and used == len(wire2)
+    pt, st, ty = open_(eng, iv, orecs, wire2, 32 * 16401)
+    assert (st[:32] == 16384).all() and (ty[:32] == 23).all()
+    assert b"".join(pt[int(o["dst"]): int(o["dst"]) + 16384].tobytes() for o in orecs) == data + data
+    # retransmission: records 1, 4, 5, 9, 15 of the first window, stored (offset, ciphertext_len, seq)
+    pick = [1, 4, 5, 9, 15]
+    rrecs = np.zeros(len(pick), ra.TLS_RECORD_DTYPE)
+    for k, i in enumerate(pick):
+        rrecs[k] = (int(trecs[i]["dst"]), k * 16401, int(trecs[i]["seq"]), 16384 + 17, 0)
+    pt, st, ty = open_(eng, iv, rrecs, wire, len(pick) * 16401)
+    assert (st[: len(pick)] == 16384).all()
+    for k, i in enumerate(pick):
+        assert pt[k * 16401: k * 16401 + 16384].tobytes() == data[i * 16384: (i + 1) * 16384]
+
+
+def test_in_place(gpu):
+    """Seal a fragment already placed 5 bytes into its record slot, and open a record in place (plaintext
+    over its own header + ciphertext, dst = src + 5), as picotls's buffer_encrypt_record does in its buffer."""
+    import torch
+    key, iv = bytes(range(16)), bytes(range(12))
+    lens = [0, 1, 16, 100, 1400, 16384]
+    slots = [ln + 22 for ln in lens]
+    base = np.cumsum([0] + slots[:-1])
+    buf = np.zeros(sum(slots) + 16, np.uint8)
+    trecs = np.zeros(len(lens), ra.TLS_RECORD_DTYPE)
+    frags = []
+    for i, ln in enumerate(lens):
+        f = xorshift64star(20 + i, ln).tobytes()
+        frags.append(f)
+        buf[base[i] + 5: base[i] + 5 + ln] = np.frombuffer(f, np.uint8)
+        trecs[i] = (base[i] + 5, base[i], 50 + i, ln, 23)
+    eng = ra.Engine(key)
+    d = dev(buf)
+    eng.tls_seal_records(iv, dev(trecs.view(np.uint8)).data_ptr(), len(trecs), d.data_ptr(), d.data_ptr())
+    torch.cuda.synchronize()
+    wire = d.cpu().numpy()
+    for i, ln in enumerate(lens):
+        assert wire[base[i]: base[i] + ln + 22].tobytes() == oracle.tls_seal_record(key, iv, 50 + i, 23, frags[i])
+    orecs = trecs.copy()
+    orecs["src"], orecs["dst"], orecs["len"] = base, base + 5, np.array(lens) + 17
+    pt, st, ty = open_(eng, iv, orecs, wire, 0, inplace=True)
+    assert list(st[: len(lens)]) == lens
+    for i, ln in enumerate(lens):
+        assert pt[base[i] + 5: base[i] + 5 + ln].tobytes() == frags[i]

@@ -128,3 +128,78 @@ def test_model_record_beyond_2p16_blocks(model, K):
     run(model, True, K, key, iv, recs, src, got, aad, st)
     oracle.batch(True, key, iv, recs, src, want, aad)
     assert spans(got, recs, 16) == spans(want, recs, 16)
+
+
+def run_tls(lib, is_seal, key, iv, trecs, src, dst, st=None, ty=None):
+    vp = C.c_void_p
+    lib.model_tls_batch.argtypes = [C.c_int, vp, C.c_size_t, vp, vp, C.c_size_t, vp, vp, vp, vp]
+    st = np.zeros(max(len(trecs), 1), np.uint32) if st is None else st
+    ty = np.zeros(max(len(trecs), 1), np.uint8) if ty is None else ty
+    rc = lib.model_tls_batch(1 if is_seal else 0, key, len(key), iv, trecs.ctypes.data, len(trecs), src.ctypes.data,
+                             dst.ctypes.data, st.ctypes.data, ty.ctypes.data)
+    assert rc == 0
+    return st, ty
+
+
+@pytest.mark.parametrize("keylen", [16, 32])
+def test_model_tls_framing(model, keylen):
+    """The FRAME walk (header AAD in registers, content-type byte spliced into the tail block) vs the oracle's
+    restatement of the picotls record layer, both directions, every fragment length around the block edges."""
+    import rapido_amd as ra
+    rng = np.random.default_rng(keylen)
+    key, iv = rng.integers(0, 256, keylen, dtype=np.uint8).tobytes(), rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    lens = list(range(0, 40)) + [255, 256, 1399, 1400, 4095, 16383, 16384]
+    trecs = np.zeros(len(lens), ra.TLS_RECORD_DTYPE)
+    off = woff = 0
+    for i, n in enumerate(lens):
+        trecs[i] = (off, woff, 1000 + 3 * i, n, [23, 22, 21][i % 3])
+        off += n + 3
+        woff += n + 22 + 1
+    src = rng.integers(0, 256, off + 16, dtype=np.uint8)
+    wire = np.zeros(woff + 16, np.uint8)
+    run_tls(model, True, key, iv, trecs, src, wire)
+    for t in trecs:
+        frag = bytes(src[int(t["src"]): int(t["src"]) + int(t["len"])])
+        want = oracle.tls_seal_record(key, iv, int(t["seq"]), int(t["type"]), frag)
+        assert bytes(wire[int(t["dst"]): int(t["dst"]) + len(want)]) == want, int(t["len"])
+    # receive the same wire: descriptors from the host parser semantics (src = header, len = length field)
+    orecs = trecs.copy()
+    orecs["src"], orecs["len"] = trecs["dst"], trecs["len"] + 17
+    orecs["dst"] = np.cumsum(np.concatenate([[0], (orecs["len"] - 16)[:-1].astype(np.int64)])).astype(np.uint64)
+    pt = np.zeros(int(orecs["dst"][-1]) + int(orecs["len"][-1]), np.uint8)
+    st, ty = run_tls(model, False, key, iv, orecs, wire, pt)
+    assert list(st[: len(lens)]) == lens and list(ty[: len(lens)]) == list(trecs["type"])
+    for t, o in zip(trecs, orecs):
+        assert bytes(pt[int(o["dst"]): int(o["dst"]) + int(t["len"])]) == bytes(src[int(t["src"]): int(t["src"]) +
+                                                                                    int(t["len"])])
+
+
+def test_model_tls_open_padding_and_failures(model):
+    import rapido_amd as ra
+    key, iv = bytes(range(16)), bytes(range(30, 42))
+    cases = [(50, 23, 0), (50, 23, 1), (50, 23, 15), (50, 23, 16), (0, 23, 40), (300, 23, 333), (0, 0, 7)]
+    wires = [oracle.tls_seal_record(key, iv, 77 + i, t, bytes(k % 255 + 1 for k in range(n)), p)
+             for i, (n, t, p) in enumerate(cases)]
+    bad = bytearray(oracle.tls_seal_record(key, iv, 99, 23, b"hello world")); bad[9] ^= 1
+    short = b"\x17\x03\x03\x00\x0f" + bytes(15)
+    wires += [bytes(bad), short]
+    seqs = [77 + i for i in range(len(cases))] + [99, 5]
+    buf = np.frombuffer(b"".join(wires), np.uint8).copy()
+    orecs = np.zeros(len(wires), ra.TLS_RECORD_DTYPE)
+    off = dst = 0
+    for i, w in enumerate(wires):
+        L = (w[3] << 8) | w[4]
+        orecs[i] = (off, dst, seqs[i], L, 0)
+        off += len(w)
+        dst += max(L - 16, 0)
+    pt = np.zeros(dst + 16, np.uint8)
+    st, ty = run_tls(model, False, key, iv, orecs, buf, pt)
+    for i, w in enumerate(wires):
+        want = oracle.tls_open_record(key, iv, seqs[i], w)
+        if want == oracle.TLS_BAD_MAC:
+            assert st[i] == 0xFFFFFFFF
+        elif want == oracle.TLS_NO_TYPE:
+            assert st[i] == 0xFFFFFFFE
+        else:
+            assert st[i] == len(want[0]) and ty[i] == want[1]
+            assert bytes(pt[int(orecs[i]["dst"]): int(orecs[i]["dst"]) + st[i]]) == want[0]
