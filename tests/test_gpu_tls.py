@@ -19,7 +19,7 @@ GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "tls_r
 
 def dev(a):
     import torch
-    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    return torch.from_numpy(np.array(a, copy=True)).cuda()
 
 
 def seal(eng, iv, trecs, src, wire_size, dst=None):
