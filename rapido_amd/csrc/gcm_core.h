@@ -295,6 +295,9 @@ GCM_HD void ghash_quarter_acc(const u32x4 g[4], u32x4 &P)
 #ifndef GCM_ROUND_ASM
 #define GCM_ROUND_ASM 1
 #endif
+#ifndef GCM_R2CACHE
+#define GCM_R2CACHE 1
+#endif
 #if defined(__HIP_DEVICE_COMPILE__)
 /*
  * One full AES round on the four-table image (aes_col x 4) as a single instruction block:
@@ -451,20 +454,68 @@ GCM_HD void aes_round1_consts(const uint8_t *lds, uint32_t lanesel, const uint32
 }
 
 /*
+ * CTR caching over rounds 1 AND 2 (GCM_R2CACHE): inside a 2^8-block window only the counter's low
+ * byte (state byte 15: row 3 of column 3) changes.  ShiftRows moves it to column 0, so after round 1
+ * only column 0 varies (n0 = c[0] ^ T3[x]); in round 2 every output column takes exactly one byte of
+ * that column (m0 <- n0.b0 via T0, m3 <- n0.b1 via T1, m2 <- n0.b2 via T2, m1 <- n0.b3 via T3), and
+ * its three other terms plus the round key are constants c[4..7].  Per block: 1 + 4 table reads for
+ * rounds 1-2 instead of 2 + 16.  c[0..7] are recomputed when ctr & 0xffffff00 changes.
+ */
+template <bool FOUR>
+GCM_HD void aes_round12_consts(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk, uint32_t iv0, uint32_t iv1,
+                               uint32_t iv2, uint32_t ctr_hi, uint32_t c[8])
+{
+    /* ctr_hi = ctr & 0xffffff00 */
+    const uint32_t s0 = iv0 ^ rk[0], s1 = iv1 ^ rk[1], s2 = iv2 ^ rk[2], s3 = bswap32(ctr_hi) ^ rk[3];
+    const uint32_t *k = rk + 4;
+    c[0] = xor3(tlook<FOUR>(lds, lanesel, s0, 0, 0), tlook<FOUR>(lds, lanesel, s1, 1, 1),
+                tlook<FOUR>(lds, lanesel, s2, 2, 2) ^ k[0]); /* + T3[s3.b3] per block */
+    const uint32_t n1 = xor3(xor3(tlook<FOUR>(lds, lanesel, s1, 0, 0), tlook<FOUR>(lds, lanesel, s2, 1, 1), k[1]),
+                             tlook<FOUR>(lds, lanesel, s3, 2, 2), tlook<FOUR>(lds, lanesel, s0, 3, 3));
+    const uint32_t n2 = xor3(xor3(tlook<FOUR>(lds, lanesel, s2, 0, 0), tlook<FOUR>(lds, lanesel, s3, 1, 1), k[2]),
+                             tlook<FOUR>(lds, lanesel, s0, 2, 2), tlook<FOUR>(lds, lanesel, s1, 3, 3));
+    const uint32_t n3 = xor3(xor3(tlook<FOUR>(lds, lanesel, s3, 0, 0), tlook<FOUR>(lds, lanesel, s0, 1, 1), k[3]),
+                             tlook<FOUR>(lds, lanesel, s1, 2, 2), tlook<FOUR>(lds, lanesel, s2, 3, 3));
+    c[1] = n1;
+    c[2] = n2;
+    c[3] = n3;
+    const uint32_t *k2 = rk + 8;
+    c[4] = xor3(tlook<FOUR>(lds, lanesel, n1, 1, 1), tlook<FOUR>(lds, lanesel, n2, 2, 2),
+                tlook<FOUR>(lds, lanesel, n3, 3, 3) ^ k2[0]); /* + T0[n0.b0] */
+    c[5] = xor3(tlook<FOUR>(lds, lanesel, n1, 0, 0), tlook<FOUR>(lds, lanesel, n2, 1, 1),
+                tlook<FOUR>(lds, lanesel, n3, 2, 2) ^ k2[1]); /* + T3[n0.b3] */
+    c[6] = xor3(tlook<FOUR>(lds, lanesel, n2, 0, 0), tlook<FOUR>(lds, lanesel, n3, 1, 1),
+                tlook<FOUR>(lds, lanesel, n1, 3, 3) ^ k2[2]); /* + T2[n0.b2] */
+    c[7] = xor3(tlook<FOUR>(lds, lanesel, n3, 0, 0), tlook<FOUR>(lds, lanesel, n1, 2, 2),
+                tlook<FOUR>(lds, lanesel, n2, 3, 3) ^ k2[3]); /* + T1[n0.b1] */
+}
+
+/*
  * aes_ghash_fused for a block whose round 1 is hoisted (c from the block's 2^16 window): 2 table reads in round 1
  * instead of 16; the GHASH reads go to rounds 2..9.  Writes the keystream to w[4].
  */
 template <int NR, bool FOUR = true>
-GCM_HD u32x4 aes_ghash_fused_h(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk, const uint32_t c[4],
+GCM_HD u32x4 aes_ghash_fused_h(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk, const uint32_t *c,
                                uint32_t ctr, uint32_t w[4], uint32_t basereg, u32x4 A)
 {
 #define GCM_TA(x, k) perm((x), lanesel, 0x0c0c0400u | ((4u + (k)) << 8))
     u32x4 P = {0u, 0u, 0u, 0u};
     const uint32_t s3 = bswap32(ctr) ^ rk[3];
+#if GCM_R2CACHE
+    /* rounds 1 and 2 from the window constants c[0..7] (aes_round12_consts): 5 reads */
+    const uint32_t n0 = c[0] ^ tlook<FOUR>(lds, lanesel, s3, 3, 3);
+    uint32_t s0 = c[4] ^ tlook<FOUR>(lds, lanesel, n0, 0, 0), s1 = c[5] ^ tlook<FOUR>(lds, lanesel, n0, 3, 3);
+    uint32_t s2 = c[6] ^ tlook<FOUR>(lds, lanesel, n0, 2, 2), s3r = c[7] ^ tlook<FOUR>(lds, lanesel, n0, 1, 1);
+    ghash_quarter(lds, basereg, A[0], 0, 0, P);
+    GCM_SCHED_FENCE();
+    constexpr int R0 = 3;
+#else
     uint32_t s0 = c[0] ^ tlook<FOUR>(lds, lanesel, s3, 3, 3), s1 = c[1] ^ tlook<FOUR>(lds, lanesel, s3, 2, 2);
     uint32_t s2 = c[2], s3r = c[3];
+    constexpr int R0 = 2;
+#endif
 #pragma unroll
-    for (int r = 2; r < NR; ++r) {
+    for (int r = R0; r < NR; ++r) {
         const uint32_t *k = rk + 4 * r;
         uint32_t n0, n1, n2, n3;
 #if defined(__HIP_DEVICE_COMPILE__) && GCM_ROUND_ASM
@@ -872,9 +923,16 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
     const uint8_t *ad = aad + rec.aad;
     const uint32_t arem = rec.aadlen & 15u;
     u32x4 acc = {0u, 0u, 0u, 0u}, ek0 = {0u, 0u, 0u, 0u};
-    /* hoisted round-1 constants of the current 2^16-counter window (aes_round1_consts) */
+    /* hoisted round-1 (and round-2, GCM_R2CACHE) constants of the current counter window */
+#if GCM_R2CACHE
+    constexpr uint32_t WIN = 0xffffff00u; /* 2^8-block windows (aes_round12_consts) */
+    uint32_t c1[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, c1_hi = 0u;
+    aes_round12_consts<Layout<K>::four_tables>(lds, lanesel, rk, iv0, iv1, iv2, 0u, c1);
+#else
+    constexpr uint32_t WIN = 0xffff0000u; /* 2^16-block windows (aes_round1_consts) */
     uint32_t c1[4] = {0u, 0u, 0u, 0u}, c1_hi = 0u;
     aes_round1_consts<Layout<K>::four_tables>(lds, lanesel, rk, iv0, iv1, iv2, 0u, c1);
+#endif
 
     /*
      * Address of the 16-byte load of step t.  The load is issued unconditionally (steps with
@@ -931,15 +989,19 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
         aes_encrypt_tt<NR, Layout<K>::four_tables>(lds, lanesel, rk, w);
         const u32x4 P = acc;
 #else
-        if ((ctr & 0xffff0000u) != c1_hi) { /* records beyond 2^16 blocks only */
-            c1_hi = ctr & 0xffff0000u;
+        if ((ctr & WIN) != c1_hi) { /* a record crossing a counter window (>= 2^8 blocks with GCM_R2CACHE) */
+            c1_hi = ctr & WIN;
             /* opaque inputs: keeps LICM from parking this rare path's 16 LDS addresses in VGPRs */
             uint32_t o0 = iv0, o1 = iv1, o2 = iv2, ol = lanesel;
             GCM_OPAQUE(o0);
             GCM_OPAQUE(o1);
             GCM_OPAQUE(o2);
             GCM_OPAQUE(ol);
+#if GCM_R2CACHE
+            aes_round12_consts<Layout<K>::four_tables>(lds, ol, rk, o0, o1, o2, c1_hi, c1);
+#else
             aes_round1_consts<Layout<K>::four_tables>(lds, ol, rk, o0, o1, o2, c1_hi, c1);
+#endif
         }
         const u32x4 P =
             aes_ghash_fused_h<NR, Layout<K>::four_tables>(lds, lanesel, rk, c1, ctr, w, Layout<K>::gh_base, acc);

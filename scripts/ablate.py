@@ -24,6 +24,7 @@ VARIANTS = {
     "wg768": ["-DMI355X_WG_THREADS=768"],
     "ilp": ["-mllvm", "--amdgpu-sched-strategy=iterative-ilp"],
     "noasm": ["-DGCM_ROUND_ASM=0"],
+    "r1only": ["-DGCM_R2CACHE=0"],
     # "@src=DIR": compile gcm_engine.hip from DIR (e.g. a `git show` of an older revision) instead of csrc/
     "head": ["@src=" + os.path.join(VDIR, "src_head")],
     "no_ghash": ["-DGCM_ABLATE_GHASH=1"],
