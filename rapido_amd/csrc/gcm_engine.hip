@@ -130,7 +130,7 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
             rec = recs[r];
         }
         const uint32_t plen = FRAME && SEAL ? rec.len + 1u : rec.len;
-        uint32_t T = valid ? make_walk(plen, rec.aadlen, K).T : 0u;
+        uint32_t T = valid ? make_walk(plen, rec.aadlen, K, walk_out16(dst + rec.dst)).T : 0u;
         uint32_t Tmax = T;
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1)

@@ -25,6 +25,9 @@ VARIANTS = {
     "ilp": ["-mllvm", "--amdgpu-sched-strategy=iterative-ilp"],
     "noasm": ["-DGCM_ROUND_ASM=0"],
     "r1only": ["-DGCM_R2CACHE=0"],
+    "noalign": ["-DGCM_ALIGN_OUTPUT=0"],
+    "freealign": ["-DGCM_ALIGN_MIN_T=100000u"],
+    "align8": ["-DGCM_ALIGN_MIN_T=8u"],
     # "@src=DIR": compile gcm_engine.hip from DIR (e.g. a `git show` of an older revision) instead of csrc/
     "head": ["@src=" + os.path.join(VDIR, "src_head")],
     "no_ghash": ["-DGCM_ABLATE_GHASH=1"],

@@ -27,7 +27,7 @@ static void run(const KeyImage *ki, const uint8_t *lds, const uint8_t *static_iv
     memcpy(&iv2, static_iv + 8, 4);
     for (size_t i = 0; i < n; ++i) {
         const Record &r = recs[i];
-        Walk wk = make_walk(r.len, r.aadlen, K);
+        Walk wk = make_walk(r.len, r.aadlen, K, walk_out16(dst + r.dst));
         uint32_t n1 = iv1 ^ bswap32((uint32_t)(r.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)r.seq);
         u32x4 tag = {0, 0, 0, 0};
         for (uint32_t j = 0; j < (uint32_t)K; ++j)
@@ -76,7 +76,7 @@ static void run_tls(const KeyImage *ki, const uint8_t *lds, const uint8_t *stati
             r.len = t.len - 16;
         }
         const uint32_t plen = SEAL ? r.len + 1 : r.len;
-        Walk wk = make_walk(plen, 5, K);
+        Walk wk = make_walk(plen, 5, K, walk_out16(dst + r.dst));
         uint32_t n1 = iv1 ^ bswap32((uint32_t)(r.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)r.seq);
         u32x4 tag = {0, 0, 0, 0};
         for (uint32_t j = 0; j < (uint32_t)K; ++j)

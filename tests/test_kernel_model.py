@@ -203,3 +203,26 @@ def test_model_tls_open_padding_and_failures(model):
         else:
             assert st[i] == len(want[0]) and ty[i] == want[1]
             assert bytes(pt[int(orecs[i]["dst"]): int(orecs[i]["dst"]) + st[i]]) == want[0]
+
+
+@pytest.mark.parametrize("K", [2, 4, 8])
+def test_model_every_front_pad(model, K):
+    """The same records at output offsets shifted by 0..K-1 blocks: make_walk picks every front padding
+    (and trailing-pad chain ends with their H^(pad + g - q_last) scaling) for long and short records."""
+    rng = np.random.default_rng(K)
+    lens = np.array([0, 5, 16, 100, 1392, 1400, 1401, 4096, 16384, 16368], dtype=np.uint64)
+    key, iv = bytes(range(16)), bytes(range(12))
+    for shift in range(K):
+        recs, src, aad = records.tls_batch(lens, seed=shift + 1, align=256)
+        recs["dst"] = recs["dst"] + np.uint64(16 * shift)
+        got = np.zeros(len(src) + 256, np.uint8)
+        want = np.zeros_like(got)
+        st = np.zeros(len(recs), np.uint32)
+        run(model, True, K, key, iv, recs, src, got, aad, st)
+        oracle.batch(True, key, iv, recs, src, want, aad)
+        assert spans(got, recs, 16) == spans(want, recs, 16)
+        opened = np.zeros_like(got)
+        orecs = recs.copy()
+        orecs["src"] = recs["dst"]
+        run(model, False, K, key, iv, orecs, got, opened, aad, st)
+        assert (st == recs["len"]).all()
