@@ -27,7 +27,7 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 CLANGXX = "/opt/rocm/llvm/bin/clang++" if os.path.exists("/opt/rocm/llvm/bin/clang++") else (shutil.which("clang++") or "clang++")
 CC = shutil.which("gcc") or "cc"
 
-HEADERS = [os.path.join(CSRC, "gcm_core.h"), os.path.join(ROOT, "include", "ptls_mi355x.h")]
+HEADERS = [os.path.join(CSRC, "gcm_core.h"), os.path.join(CSRC, "gcm_bitslice.h"), os.path.join(ROOT, "include", "ptls_mi355x.h")]
 
 
 def _newer(target: str, deps) -> bool:

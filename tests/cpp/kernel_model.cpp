@@ -12,6 +12,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include "../../rapido_amd/csrc/gcm_core.h"
+#include "../../rapido_amd/csrc/gcm_bitslice.h"
 
 using namespace mi355x;
 
@@ -161,3 +162,35 @@ extern "C" int model_key_image(const uint8_t *key, size_t keylen, void *out, siz
 }
 
 extern "C" size_t model_key_image_size(void) { return sizeof(KeyImage); }
+
+/*
+ * Bitsliced AES-CTR (gcm_bitslice.h) of one quad: blocks nonce || BE32(ctr0 + b), b = 0..7, written
+ * to out[16 b ...] from the lanes that hold them (lane t: blocks t and t + 4).
+ */
+extern "C" int model_bs_keystream(const uint8_t *key, size_t keylen, const uint8_t *nonce12, uint32_t ctr0, uint8_t *out)
+{
+    KeyImage *ki = (KeyImage *)aligned_alloc(64, sizeof(KeyImage));
+    uint8_t *kp = (uint8_t *)aligned_alloc(256, KEYPLANE_BYTES);
+    if (build_key_image(kTabs.sbox, key, (uint32_t)keylen, ki) != 0) {
+        free(ki);
+        free(kp);
+        return -1;
+    }
+    fill_keyplanes(kp, ki->rk, ki->rounds, 0, 1);
+    uint32_t n[3];
+    memcpy(n, nonce12, 12);
+    QuadOpsHost o;
+    Quad4 ka[4], kb[4];
+    if (ki->rounds == 10)
+        ctr_keystream_bs<10>(o, kp, 0u, q4(n[0]), q4(n[1]), q4(n[2]), q4(ctr0), ka, kb);
+    else
+        ctr_keystream_bs<14>(o, kp, 0u, q4(n[0]), q4(n[1]), q4(n[2]), q4(ctr0), ka, kb);
+    for (int t = 0; t < 4; ++t)
+        for (int d = 0; d < 4; ++d) {
+            memcpy(out + 16 * t + 4 * d, &ka[d].v[t], 4);
+            memcpy(out + 16 * (t + 4) + 4 * d, &kb[d].v[t], 4);
+        }
+    free(ki);
+    free(kp);
+    return 0;
+}

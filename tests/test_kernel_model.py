@@ -226,3 +226,29 @@ def test_model_every_front_pad(model, K):
         orecs["src"] = recs["dst"]
         run(model, False, K, key, iv, orecs, got, opened, aad, st)
         assert (st == recs["len"]).all()
+
+
+@pytest.mark.parametrize("keylen", [16, 32])
+def test_model_bitsliced_keystream(model, keylen):
+    """The VALU engine of gcm_bitslice.h (quad layout: Boyar-Peralta S-box as 92 three-input LUTs, DPP
+    MixColumns, plane transposes) for 8 counter blocks, against the oracle's AES, including a counter wrap."""
+    import struct
+    model.model_bs_keystream.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_uint32, C.c_void_p]
+    rng = np.random.default_rng(keylen + 5)
+    for ctr0 in [0, 1, 0xF9, 0xFFFFFFFC] + [int(x) for x in rng.integers(0, 2 ** 32, 6)]:
+        key = rng.integers(0, 256, keylen, dtype=np.uint8).tobytes()
+        nonce = rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+        out = C.create_string_buffer(128)
+        assert model.model_bs_keystream(key, keylen, nonce, ctr0, out) == 0
+        want = b"".join(oracle.ecb(key, nonce + struct.pack(">I", (ctr0 + b) & 0xFFFFFFFF)) for b in range(8))
+        assert out.raw == want
+
+
+def test_sbox_circuit_and_lut3_mapping():
+    """The Boyar-Peralta circuit and its 3-input-LUT cover (the S-box of the VALU engine) on all 256 inputs."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(__file__))
+    for script in ("sbox_circuit.py", "sbox_lut3.py"):
+        r = subprocess.run([sys.executable, os.path.join(root, "scripts", script)], capture_output=True, text=True)
+        assert r.returncode == 0, r.stdout + r.stderr
