@@ -145,13 +145,13 @@ extern "C" int probe_key(const void *d_key, uint32_t keylen, void *d_ki, int *d_
 extern "C" size_t probe_key_image_size(void) { return sizeof(KeyImage); }
 
 extern "C" int probe_run(const void *d_ki, int nr, uint32_t n_tt, uint32_t nunits, uint32_t nblocks, void *d_work,
-                         void *d_out, void *stream)
+                         void *d_out, void *stream, uint32_t threads)
 {
     if (nr == 10)
-        hipLaunchKernelGGL(probe_mix128, dim3(nblocks), dim3(1024), 0, (hipStream_t)stream, (const KeyImage *)d_ki, n_tt,
+        hipLaunchKernelGGL(probe_mix128, dim3(nblocks), dim3(threads), 0, (hipStream_t)stream, (const KeyImage *)d_ki, n_tt,
                            nunits, (uint32_t *)d_work, (uint32_t *)d_out);
     else
-        hipLaunchKernelGGL(probe_mix256, dim3(nblocks), dim3(1024), 0, (hipStream_t)stream, (const KeyImage *)d_ki, n_tt,
+        hipLaunchKernelGGL(probe_mix256, dim3(nblocks), dim3(threads), 0, (hipStream_t)stream, (const KeyImage *)d_ki, n_tt,
                            nunits, (uint32_t *)d_work, (uint32_t *)d_out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

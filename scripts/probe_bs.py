@@ -34,7 +34,7 @@ def run():
     vp, u32 = C.c_void_p, C.c_uint32
     lib.probe_key.argtypes = [vp, u32, vp, vp, vp]
     lib.probe_key_image_size.restype = C.c_size_t
-    lib.probe_run.argtypes = [vp, C.c_int, u32, u32, u32, vp, vp, vp]
+    lib.probe_run.argtypes = [vp, C.c_int, u32, u32, u32, vp, vp, vp, u32]
     lib.probe_check_run.argtypes = [vp, u32, u32, u32, u32, vp, vp]
     dev = torch.device("cuda:0")
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
@@ -67,13 +67,14 @@ def run():
         d_out = torch.zeros(ncu * 1024, dtype=torch.int32, device=dev)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         res = {}
+        threads = int(os.environ.get("PROBE_THREADS", "1024"))
         for n_tt in [int(x) for x in os.environ.get("PROBE_NTT", "16,14,13,12,11,10,8,6,4,0").split(",")]:
             ts = []
             for rep in range(4):
                 d_work.zero_()
                 ev[0].record()
                 assert lib.probe_run(d_ki.data_ptr(), nr, n_tt, nunits, ncu, d_work.data_ptr(), d_out.data_ptr(),
-                                     stream) == 0
+                                     stream, threads) == 0
                 ev[1].record()
                 torch.cuda.synchronize()
                 if rep:
@@ -81,7 +82,7 @@ def run():
             ms = sorted(ts)[len(ts) // 2]
             gbps = nunits * 64 * 16 / (ms * 1e-3) / 1e9
             res[n_tt] = round(gbps, 1)
-            print(f"AES-{8 * keylen} T-table waves {n_tt:2d}/16: {ms:7.3f} ms  {gbps:8.1f} GB/s", flush=True)
+            print(f"AES-{8 * keylen} [{threads // 64} waves/CU] T-table waves {min(n_tt, threads // 64):2d}: {ms:7.3f} ms  {gbps:8.1f} GB/s", flush=True)
         results[f"aes{8 * keylen}"] = res
     print(json.dumps(results))
 
