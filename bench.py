@@ -32,6 +32,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 DESC_BYTES = 40         # sizeof(ptls_mi355x_record_t)
+LDS_CLOCK_GHZ = 2.4     # MI355X peak engine clock (the LDS roofline is priced at it, as HBM at its spec peak)
 GIB = float(1 << 30)
 
 WORKLOADS = {
@@ -273,21 +274,66 @@ def main() -> None:
                      "algorithmic_bytes_per_launch": dom_bytes, "launch_ms": round(dom_ms, 4)},
     }
 
+    # the kernels' binding resource: LDS-array cycles of the T-table AES + nibble-table GHASH reads
+    # (MI355X_MICROARCH.md LDS table: ds_read_b32 2 clk, ds_read_b128 4 clk per wave)
+    b32_reads = 133 if wl["key"] == 16 else 197
+    lds_cycles_per_block = (2.0 * b32_reads + 4.0 * 32) / 64.0
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    lds_ceiling = ncu * LDS_CLOCK_GHZ * 1e9 / lds_cycles_per_block * 16 / 1e9  # payload GB/s
+    dom_payload = payload / (dom_ms * 1e-3) / 1e9
+    out["lds_roofline"] = {"bound": "lds", "kernel": kname, "achieved": round(dom_payload, 1),
+                           "peak": round(lds_ceiling, 1), "unit": "GB/s payload", "frac": round(dom_payload / lds_ceiling, 4),
+                           "model": f"{b32_reads} ds_read_b32 + 32 ds_read_b128 per 16-B block = "
+                                    f"{lds_cycles_per_block:.2f} LDS clk/block/CU, {ncu} CU x {LDS_CLOCK_GHZ} GHz",
+                           "note": "this read mix alone sustains 0.78 of the nominal rate (profiles/r01c_lds_ceiling.json)"}
+
     if args.e2e:
-        # PCIe-inclusive: records start and end in pinned host memory (one H2D, seal, one D2H)
+        # PCIe-inclusive: records start and end in pinned host memory
         h_src = torch.empty(src_bytes, dtype=torch.uint8, pin_memory=True)
         h_dst = torch.empty(src_bytes, dtype=torch.uint8, pin_memory=True)
         h_src.copy_(d_src.cpu())
         torch.cuda.synchronize(dev)
         reps = max(2, args.steps // 4)
         t0 = time.perf_counter()
-        for _ in range(reps):
+        for _ in range(reps):  # serial: one H2D, the seal, one D2H
             d_src.copy_(h_src, non_blocking=True)
             eng.seal_batch(iv, d_recs.data_ptr(), n, d_src.data_ptr(), d_ct.data_ptr(), d_aad.data_ptr(), sh)
             h_dst.copy_(d_ct, non_blocking=True)
         torch.cuda.synchronize(dev)
-        dt = (time.perf_counter() - t0) / reps
-        out["e2e_pcie"] = {"seal_gibps": round(payload / dt / GIB, 2), "note": "pinned H2D + seal + D2H, serial"}
+        serial = (time.perf_counter() - t0) / reps
+        # pipelined: the batch in chunks over 3 streams, so the H2D of chunk i+1 and the D2H of chunk i-1
+        # overlap the seal of chunk i (the copy engines run both directions at once)
+        nchunk = 16
+        bounds = np.linspace(0, n, nchunk + 1).astype(np.int64)
+        streams = [torch.cuda.Stream(dev) for _ in range(3)]
+        starts = recs["src"].astype(np.int64)
+        ends = starts + recs["len"].astype(np.int64) + 16
+
+        def pipelined():
+            for c in range(nchunk):
+                r0, r1 = int(bounds[c]), int(bounds[c + 1])
+                a, b = int(starts[r0]), int(ends[r1 - 1])
+                st = streams[c % 3]
+                with torch.cuda.stream(st):
+                    d_src[a:b].copy_(h_src[a:b], non_blocking=True)
+                    eng.seal_batch(iv, d_recs.data_ptr() + r0 * DESC_BYTES, r1 - r0, d_src.data_ptr(), d_ct.data_ptr(),
+                                   d_aad.data_ptr(), st.cuda_stream)
+                    h_dst[a:b].copy_(d_ct[a:b], non_blocking=True)
+
+        pipelined()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            pipelined()
+        torch.cuda.synchronize(dev)
+        piped = (time.perf_counter() - t0) / reps
+        # the pipelined output is the same ciphertext as the device-resident run
+        if not torch.equal(h_dst[: int(ends[-1])], d_ct[: int(ends[-1])].cpu()):
+            raise SystemExit("bench: pipelined PCIe seal differs from the device-resident seal -- results invalid")
+        out["e2e_pcie"] = {"seal_gibps_serial": round(payload / serial / GIB, 2),
+                           "seal_gibps_pipelined": round(payload / piped / GIB, 2),
+                           "note": "pinned host src -> H2D -> seal -> D2H -> pinned host dst; serial = one copy each way "
+                                   "around one launch; pipelined = 16 chunks over 3 streams"}
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(wl, args.cpu_threads)
