@@ -27,7 +27,7 @@ __device__ void body(uint32_t iters, uint32_t *out)
     uint32_t acc = 0;
     u32x4 acc4 = {0u, 0u, 0u, 0u};
     for (uint32_t it = 0; it < iters; ++it) {
-        if (MODE != 1) {
+        if (MODE == 0 || MODE == 2) {
             uint32_t v[16];
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
@@ -39,7 +39,24 @@ __device__ void body(uint32_t iters, uint32_t *out)
             for (int k = 0; k < 16; k += 2)
                 acc = __builtin_amdgcn_bitop3_b32(acc, v[k], v[k + 1], 0x96);
         }
-        if (MODE == 1 || (MODE == 2 && (it & 3u) == 0u)) {
+        if (MODE == 3 || MODE == 4) {
+            /* 16 T-table style reads as ds_read_b64: lane l reads the 8-byte slot l & 31 of a random row */
+            const uint32_t lanesel8 = (lane & 31u) * 8u | 0x10000u;
+            uint32_t v[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const uint32_t w = (k & 3) == 0 ? s0 : (k & 3) == 1 ? s1 : (k & 3) == 2 ? s2 : s3;
+                const uint32_t sel = ((k & 2) ? 0x0c020400u : 0x0c0c0400u) | ((4u + (uint32_t)(k >> 2)) << 8);
+                const uint32_t a = __builtin_amdgcn_perm(w, lanesel8, sel);
+                typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+                const u32x2 d = *(const u32x2 *)(lds + a);
+                v[k] = (k & 1) ? d[1] : d[0];
+            }
+#pragma unroll
+            for (int k = 0; k < 16; k += 2)
+                acc = __builtin_amdgcn_bitop3_b32(acc, v[k], v[k + 1], 0x96);
+        }
+        if (MODE == 1 || ((MODE == 2 || MODE == 4) && (it & 3u) == 0u)) {
             u32x4 g[16];
             const uint32_t lo = (s0 << 4) & 0xf0f0f0f0u, hi = s0 & 0xf0f0f0f0u;
 #pragma unroll
@@ -66,10 +83,12 @@ __device__ void body(uint32_t iters, uint32_t *out)
 extern "C" __global__ __launch_bounds__(1024) void lds_b32(uint32_t iters, uint32_t *out) { body<0>(iters, out); }
 extern "C" __global__ __launch_bounds__(1024) void lds_b128(uint32_t iters, uint32_t *out) { body<1>(iters, out); }
 extern "C" __global__ __launch_bounds__(1024) void lds_mix(uint32_t iters, uint32_t *out) { body<2>(iters, out); }
+extern "C" __global__ __launch_bounds__(1024) void lds_b64(uint32_t iters, uint32_t *out) { body<3>(iters, out); }
+extern "C" __global__ __launch_bounds__(1024) void lds_mix64(uint32_t iters, uint32_t *out) { body<4>(iters, out); }
 
 extern "C" int lds_bench_run(int mode, uint32_t iters, uint32_t nblocks, uint32_t threads, void *out, void *stream)
 {
-    void (*k)(uint32_t, uint32_t *) = mode == 0 ? lds_b32 : mode == 1 ? lds_b128 : lds_mix;
+    void (*k)(uint32_t, uint32_t *) = mode == 0 ? lds_b32 : mode == 1 ? lds_b128 : mode == 2 ? lds_mix : mode == 3 ? lds_b64 : lds_mix64;
     hipLaunchKernelGGL(k, dim3(nblocks), dim3(threads), 0, (hipStream_t)stream, iters, (uint32_t *)out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
