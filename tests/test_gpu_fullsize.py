@@ -1,0 +1,113 @@
+"""GPU parity at BASELINE.json's full batch sizes, through size-independent properties.
+
+- seal -> open round trip over the whole batch: every status equals the record length, and the
+  opened plaintext equals the source byte-for-byte (compared on the device);
+- a random sample of sealed records is bit-exact against the CPU oracle;
+- flipping one bit in a sample of records (ciphertext, tag) fails exactly those records, zeroes their
+  output, and leaves every other record verified.
+
+Configs (BASELINE.json configs[1..3]): 1 M x 1400 B AES-128, 256 K x 16 KiB AES-256, 1 M ragged
+U{64..16384} AES-128 (ordered launches).  Each case holds ~3 copies of its batch in HBM (<= 24 GB).
+"""
+import zlib
+
+import numpy as np
+import pytest
+
+import oracle
+import rapido_amd as ra
+from rapido_amd import records
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    ("1400", 16, 1 << 20, 1400),
+    ("16k-aes256", 32, 1 << 18, 16384),
+    ("ragged", 16, 1 << 20, None),
+]
+
+
+@pytest.mark.parametrize("name,keylen,n,length", CASES)
+def test_full_size_round_trip(gpu, name, keylen, n, length):
+    import torch
+    rng = np.random.default_rng(zlib.crc32(name.encode()))
+    lengths = rng.integers(64, 16385, n).astype(np.uint64) if length is None else np.full(n, length, np.uint64)
+    recs, src_bytes, aad_bytes = records.layout(lengths, np.full(n, 5, dtype=np.uint64), align=256)
+    recs["seq"] = rng.integers(0, 2 ** 48, n, dtype=np.uint64)
+    aad = np.zeros(aad_bytes, dtype=np.uint8)
+    aad[: 5 * n] = records.tls_aad(lengths)
+    key = rng.integers(0, 256, keylen, dtype=np.uint8).tobytes()
+    iv = rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    dev = gpu
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(77)
+    d_src = torch.randint(0, 256, (src_bytes,), dtype=torch.uint8, device=dev, generator=gen)
+    d_ct = torch.zeros_like(d_src)
+    d_recs = torch.from_numpy(recs.view(np.uint8)).to(dev)
+    d_aad = torch.from_numpy(aad).to(dev)
+    d_st = torch.zeros(n, dtype=torch.int32, device=dev)
+    d_order = torch.zeros(n, dtype=torch.int32, device=dev)
+    eng = ra.Engine(key)
+    ragged = length is None
+
+    def seal(dst):
+        if ragged:
+            eng.order_by_length(d_recs.data_ptr(), n, d_order.data_ptr())
+            eng.seal_batch_ordered(iv, d_recs.data_ptr(), d_order.data_ptr(), n, d_src.data_ptr(), dst.data_ptr(),
+                                   d_aad.data_ptr())
+        else:
+            eng.seal_batch(iv, d_recs.data_ptr(), n, d_src.data_ptr(), dst.data_ptr(), d_aad.data_ptr())
+
+    def open_(src, dst):
+        d_st.zero_()
+        if ragged:
+            eng.open_batch_ordered(iv, d_recs.data_ptr(), d_order.data_ptr(), n, src.data_ptr(), dst.data_ptr(),
+                                   d_aad.data_ptr(), d_st.data_ptr())
+        else:
+            eng.open_batch(iv, d_recs.data_ptr(), n, src.data_ptr(), dst.data_ptr(), d_aad.data_ptr(), d_st.data_ptr())
+        torch.cuda.synchronize()
+        return d_st.cpu().numpy().view(np.uint32)
+
+    seal(d_ct)
+    d_pt = torch.zeros_like(d_src)
+    st = open_(d_ct, d_pt)
+    assert (st == recs["len"]).all()
+    # the payload bytes of every record round-trip (slot padding is not written by open)
+    starts = torch.from_numpy(recs["src"].astype(np.int64)).to(dev)
+    lens = torch.from_numpy(recs["len"].astype(np.int64)).to(dev)
+    mark = torch.zeros(src_bytes + 1, dtype=torch.int32, device=dev)
+    mark.index_add_(0, starts, torch.ones_like(starts, dtype=torch.int32))
+    mark.index_add_(0, starts + lens, -torch.ones_like(starts, dtype=torch.int32))
+    mask = torch.cumsum(mark, 0)[:src_bytes] > 0
+    assert int(mask.sum(dtype=torch.int64).item()) == int(recs["len"].sum())
+    assert not bool(((d_pt != d_src) & mask).any().item())  # elementwise: no >2^32-element boolean gather
+
+    # a sample is bit-exact against the oracle
+    sample = rng.choice(n, size=24, replace=False)
+    for i in sample:
+        r = recs[i]
+        a, ln = int(r["src"]), int(r["len"])
+        want = oracle.seal(key, oracle.build_iv(iv, int(r["seq"])), aad[int(r["aad"]): int(r["aad"]) + 5].tobytes(),
+                           d_src[a: a + ln].cpu().numpy().tobytes())
+        assert d_ct[a: a + ln + 16].cpu().numpy().tobytes() == want
+
+    # tamper: one ciphertext bit in some records, one tag bit in others
+    bad_ct = rng.choice(n, size=8, replace=False)
+    bad_tag = np.setdiff1d(rng.choice(n, size=16, replace=False), bad_ct)[:8]
+    for i in bad_ct:
+        p = int(recs[i]["src"]) + int(rng.integers(0, int(recs[i]["len"])))
+        d_ct[p] ^= 1
+    for i in bad_tag:
+        p = int(recs[i]["src"]) + int(recs[i]["len"]) + int(rng.integers(0, 16))
+        d_ct[p] ^= 0x80
+    d_pt.fill_(0xA5)
+    st = open_(d_ct, d_pt)
+    bad = np.zeros(n, bool)
+    bad[bad_ct] = True
+    bad[bad_tag] = True
+    assert (st[bad] == 0xFFFFFFFF).all()
+    assert (st[~bad] == recs["len"][~bad]).all()
+    for i in np.flatnonzero(bad):
+        a, ln = int(recs[i]["src"]), int(recs[i]["len"])
+        assert not d_pt[a: a + ln].any()
+    eng.close()
