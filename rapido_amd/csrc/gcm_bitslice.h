@@ -190,11 +190,53 @@ static inline Quad4 lut3(Quad4 a, Quad4 b, Quad4 c)
 }
 #endif
 
+/*
+ * Two-input gates pinned to VOP2 encodings.  On gfx950 a VOP2 op (v_xor/v_and/v_xnor_b32) issues in
+ * 2 clk per wave64, while VOP3 three-source ops (v_bitop3_b32, v_perm_b32) and DPP ops take about 4
+ * (scripts/valu_bench.py, profiles/r01c_valu_rates.json).  Left alone, the compiler fuses XOR/AND chains
+ * into v_bitop3_b32, which costs more than the two gates it replaces; the asm keeps the gates separate
+ * (and is not volatile, so the scheduler still orders them freely).
+ */
+#if defined(__HIP_DEVICE_COMPILE__)
+GCM_HD uint32_t gx(uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm("v_xor_b32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+GCM_HD uint32_t ga(uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm("v_and_b32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+GCM_HD uint32_t gxn(uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm("v_xnor_b32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+#else
+GCM_HD uint32_t gx(uint32_t a, uint32_t b) { return a ^ b; }
+GCM_HD uint32_t ga(uint32_t a, uint32_t b) { return a & b; }
+GCM_HD uint32_t gxn(uint32_t a, uint32_t b) { return ~(a ^ b); }
+#endif
+#if !defined(__HIPCC__)
+static inline Quad4 gx(Quad4 a, Quad4 b) { return a ^ b; }
+static inline Quad4 ga(Quad4 a, Quad4 b) { return a & b; }
+static inline Quad4 gxn(Quad4 a, Quad4 b) { return ~(a ^ b); }
+#endif
+
+#ifndef GCM_SBOX_LUT3
+#define GCM_SBOX_LUT3 1
+#endif
+
 /* SubBytes on 8 planes (in place): the Boyar-Peralta circuit; U0 / S0 is the most significant bit */
 template <class V>
 GCM_HD void sbox_bs(V p[8])
 {
     const V U0 = p[7], U1 = p[6], U2 = p[5], U3 = p[4], U4 = p[3], U5 = p[2], U6 = p[1], U7 = p[0];
+#if GCM_SBOX_LUT3
     /* the circuit mapped onto 92 three-input LUTs (scripts/sbox_lut3.py --emit) */
     const V T1 = lut3<0x5a>(U0, U3, U3);
     const V T2 = lut3<0x5a>(U0, U5, U5);
@@ -288,6 +330,41 @@ GCM_HD void sbox_bs(V p[8])
     const V S5 = lut3<0x96>(L6, L10, L29);
     const V S6 = lut3<0x69>(L8, L10, L13);
     const V S7 = lut3<0x69>(L2, L6, L18);
+#else
+    /* the 128 gates as VOP2 ops (2 clk each): cheaper than the 92-LUT cover (4 clk each) */
+    const V T1 = gx(U0, U3); const V T2 = gx(U0, U5); const V T3 = gx(U0, U6); const V T4 = gx(U3, U5);
+    const V T5 = gx(U4, U6); const V T6 = gx(T1, T5); const V T7 = gx(U1, U2); const V T8 = gx(U7, T6);
+    const V T9 = gx(U7, T7); const V T10 = gx(T6, T7); const V T11 = gx(U1, U5); const V T12 = gx(U2, U5);
+    const V T13 = gx(T3, T4); const V T14 = gx(T6, T11); const V T15 = gx(T5, T11); const V T16 = gx(T5, T12);
+    const V T17 = gx(T9, T16); const V T18 = gx(U3, U7); const V T19 = gx(T7, T18); const V T20 = gx(T1, T19);
+    const V T21 = gx(U6, U7); const V T22 = gx(T7, T21); const V T23 = gx(T2, T22); const V T24 = gx(T2, T10);
+    const V T25 = gx(T20, T17); const V T26 = gx(T3, T16); const V T27 = gx(T1, T12); const V M1 = ga(T13, T6);
+    const V M2 = ga(T23, T8); const V M3 = gx(T14, M1); const V M4 = ga(T19, U7); const V M5 = gx(M4, M1);
+    const V M6 = ga(T3, T16); const V M7 = ga(T22, T9); const V M8 = gx(T26, M6); const V M9 = ga(T20, T17);
+    const V M10 = gx(M9, M6); const V M11 = ga(T1, T15); const V M12 = ga(T4, T27); const V M13 = gx(M12, M11);
+    const V M14 = ga(T2, T10); const V M15 = gx(M14, M11); const V M16 = gx(M3, M2); const V M17 = gx(M5, T24);
+    const V M18 = gx(M8, M7); const V M19 = gx(M10, M15); const V M20 = gx(M16, M13); const V M21 = gx(M17, M15);
+    const V M22 = gx(M18, M13); const V M23 = gx(M19, T25); const V M24 = gx(M22, M23); const V M25 = ga(M22, M20);
+    const V M26 = gx(M21, M25); const V M27 = gx(M20, M21); const V M28 = gx(M23, M25); const V M29 = ga(M28, M27);
+    const V M30 = ga(M26, M24); const V M31 = ga(M20, M23); const V M32 = ga(M27, M31); const V M33 = gx(M27, M25);
+    const V M34 = ga(M21, M22); const V M35 = ga(M24, M34); const V M36 = gx(M24, M25); const V M37 = gx(M21, M29);
+    const V M38 = gx(M32, M33); const V M39 = gx(M23, M30); const V M40 = gx(M35, M36); const V M41 = gx(M38, M40);
+    const V M42 = gx(M37, M39); const V M43 = gx(M37, M38); const V M44 = gx(M39, M40); const V M45 = gx(M42, M41);
+    const V M46 = ga(M44, T6); const V M47 = ga(M40, T8); const V M48 = ga(M39, U7); const V M49 = ga(M43, T16);
+    const V M50 = ga(M38, T9); const V M51 = ga(M37, T17); const V M52 = ga(M42, T15); const V M53 = ga(M45, T27);
+    const V M54 = ga(M41, T10); const V M55 = ga(M44, T13); const V M56 = ga(M40, T23); const V M57 = ga(M39, T19);
+    const V M58 = ga(M43, T3); const V M59 = ga(M38, T22); const V M60 = ga(M37, T20); const V M61 = ga(M42, T1);
+    const V M62 = ga(M45, T4); const V M63 = ga(M41, T2); const V L0 = gx(M61, M62); const V L1 = gx(M50, M56);
+    const V L2 = gx(M46, M48); const V L3 = gx(M47, M55); const V L4 = gx(M54, M58); const V L5 = gx(M49, M61);
+    const V L6 = gx(M62, L5); const V L7 = gx(M46, L3); const V L8 = gx(M51, M59); const V L9 = gx(M52, M53);
+    const V L10 = gx(M53, L4); const V L11 = gx(M60, L2); const V L12 = gx(M48, M51); const V L13 = gx(M50, L0);
+    const V L14 = gx(M52, M61); const V L15 = gx(M55, L1); const V L16 = gx(M56, L0); const V L17 = gx(M57, L1);
+    const V L18 = gx(M58, L8); const V L19 = gx(M63, L4); const V L20 = gx(L0, L1); const V L21 = gx(L1, L7);
+    const V L22 = gx(L3, L12); const V L23 = gx(L18, L2); const V L24 = gx(L15, L9); const V L25 = gx(L6, L10);
+    const V L26 = gx(L7, L9); const V L27 = gx(L8, L10); const V L28 = gx(L11, L14); const V L29 = gx(L11, L17);
+    const V S0 = gx(L6, L24); const V S1 = gxn(L16, L26); const V S2 = gxn(L19, L28); const V S3 = gx(L6, L21);
+    const V S4 = gx(L20, L22); const V S5 = gx(L25, L29); const V S6 = gxn(L13, L27); const V S7 = gxn(L6, L23);
+#endif
     p[7] = S0;
     p[6] = S1;
     p[5] = S2;
@@ -298,26 +375,29 @@ GCM_HD void sbox_bs(V p[8])
     p[0] = S7;
 }
 
-/* MixColumns across the quad: out_q = xtime(a_q ^ a_q+1) ^ (a_q+1 ^ a_q+2) ^ a_q-1 */
+/*
+ * MixColumns across the quad: out_q = 2 a_q + 3 a_q+1 + a_q+2 + a_q+3 = xtime(t) + (colsum + a_q) with
+ * t = a_q + a_q+1 and colsum = t + t_q+2 (the XOR of the whole column): two DPP ops per plane.
+ */
 template <class O, class V>
 GCM_HD void mixcolumns_bs(const O &o, V p[8])
 {
-    V t[8], u[8];
+    V t[8], c[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i)
         t[i] = p[i] ^ o.template qperm<QP_NEXT>(p[i]);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
-        u[i] = o.template qperm<QP_NEXT>(t[i]) ^ o.template qperm<QP_PREV>(p[i]);
+        c[i] = gx(t[i] ^ o.template qperm<QP_SWAP2>(t[i]), p[i]); /* colsum + a_q = a_q+1 + a_q+2 + a_q+3 */
     /* xtime on planes: bit i <- bit i-1, bit 7 folds into bits 0, 1, 3, 4 (x^8 = x^4 + x^3 + x + 1) */
-    p[0] = t[7] ^ u[0];
-    p[1] = t[0] ^ t[7] ^ u[1];
-    p[2] = t[1] ^ u[2];
-    p[3] = t[2] ^ t[7] ^ u[3];
-    p[4] = t[3] ^ t[7] ^ u[4];
-    p[5] = t[4] ^ u[5];
-    p[6] = t[5] ^ u[6];
-    p[7] = t[6] ^ u[7];
+    p[0] = gx(t[7], c[0]);
+    p[1] = gx(gx(t[0], t[7]), c[1]);
+    p[2] = gx(t[1], c[2]);
+    p[3] = gx(gx(t[2], t[7]), c[3]);
+    p[4] = gx(gx(t[3], t[7]), c[4]);
+    p[5] = gx(t[4], c[5]);
+    p[6] = gx(t[5], c[6]);
+    p[7] = gx(t[6], c[7]);
 }
 
 /*
@@ -353,6 +433,49 @@ GCM_HD void aes_bs(const O &o, V p[8], const KF &keyplanes)
 #pragma unroll
     for (int i = 0; i < 8; ++i)
         p[i] = p[i] ^ k[i];
+}
+
+/* G independent plane sets through AES-NR at once (instruction-level parallelism for the VALU issue) */
+template <int NR, int G, class O, class V, class KF>
+GCM_HD void aes_bs_multi(const O &o, V (*p)[8], const KF &keyplanes)
+{
+    V k[8];
+    keyplanes(0, k);
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            p[g][i] = p[g][i] ^ k[i];
+#pragma unroll 1
+    for (int r = 1; r < NR; ++r) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            sbox_bs(p[g]);
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                p[g][i] = o.rotr_row(p[g][i]);
+            mixcolumns_bs(o, p[g]);
+        }
+        keyplanes(r, k);
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                p[g][i] = p[g][i] ^ k[i];
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        sbox_bs(p[g]);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            p[g][i] = o.rotr_row(p[g][i]);
+    }
+    keyplanes(NR, k);
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            p[g][i] = p[g][i] ^ k[i];
 }
 
 /* ------------------------------------------------------------------ into and out of planes --- */
@@ -464,6 +587,21 @@ GCM_HD void ctr_keystream_bs(const O &o, const uint8_t *lds, uint32_t kp_base, V
     auto keyplanes = [&](int r, V k[8]) { load_keyplanes(lds, kaddr + (uint32_t)(128 * r), k); };
     aes_bs<NR>(o, p, keyplanes);
     planes_to_blocks_bs(o, p, ks_a, ks_b);
+}
+
+/* two groups of 8 counter blocks (ctr0a.., ctr0b..) at once: lane t receives blocks t and t + 4 of each */
+template <int NR, class O, class V>
+GCM_HD void ctr_keystream_bs2(const O &o, const uint8_t *lds, uint32_t kp_base, V n0, V n1, V n2, V ctr0a, V ctr0b,
+                              V ks[4][4])
+{
+    V p[2][8];
+    ctr_planes_bs(o, n0, n1, n2, ctr0a, p[0]);
+    ctr_planes_bs(o, n0, n1, n2, ctr0b, p[1]);
+    const V kaddr = (o.row() << 5u) + kp_base;
+    auto keyplanes = [&](int r, V k[8]) { load_keyplanes(lds, kaddr + (uint32_t)(128 * r), k); };
+    aes_bs_multi<NR, 2>(o, p, keyplanes);
+    planes_to_blocks_bs(o, p[0], ks[0], ks[1]);
+    planes_to_blocks_bs(o, p[1], ks[2], ks[3]);
 }
 
 } // namespace mi355x

@@ -81,6 +81,16 @@ __device__ void mix_body(const KeyImage *ki, uint32_t n_tt, uint32_t nunits, uin
             g = (uint32_t)__shfl((int)g, 0, 64);
             if (g >= nunits)
                 break;
+#if PROBE_ILP2
+            for (uint32_t s = 0; s < 4u; ++s) {
+                uint32_t ks[4][4];
+                ctr_keystream_bs2<NR>(o, lds, KP, iv0, iv1, iv2, ctr0, ctr0 + 128u, ks);
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    acc = ghash_mul_lds(lds, GH, acc ^ u32x4{ks[b][0], ks[b][1], ks[b][2], ks[b][3]});
+                ctr0 += 256u;
+            }
+#else
             for (uint32_t s = 0; s < 8u; ++s) {
                 uint32_t ka[4], kb[4];
                 ctr_keystream_bs<NR>(o, lds, KP, iv0, iv1, iv2, ctr0, ka, kb);
@@ -88,6 +98,7 @@ __device__ void mix_body(const KeyImage *ki, uint32_t n_tt, uint32_t nunits, uin
                 acc = ghash_mul_lds(lds, GH, acc ^ u32x4{kb[0], kb[1], kb[2], kb[3]});
                 ctr0 += 128u;
             }
+#endif
         }
     }
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;

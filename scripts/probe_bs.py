@@ -15,13 +15,14 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-SO = os.path.join(ROOT, "scripts", "_build", "libprobe_bs.so")
+SO = os.path.join(ROOT, "scripts", "_build", os.environ.get("PROBE_SO", "libprobe_bs.so"))
 
 
 def build():
     os.makedirs(os.path.dirname(SO), exist_ok=True)
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-                    os.path.join(ROOT, "scripts", "probe_bs.hip"), "-o", SO], check=True)
+                    *os.environ.get("PROBE_FLAGS", "").split(), os.path.join(ROOT, "scripts", "probe_bs.hip"), "-o",
+                    SO], check=True)
     print("built", SO)
 
 
