@@ -212,6 +212,18 @@ int ptls_mi355x_tls_seal_records(ptls_mi355x_aesgcm_context_t *ctx, const void *
 int ptls_mi355x_tls_open_records(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12,
                                  const ptls_mi355x_tls_record_t *recs, size_t n, const uint8_t *src, uint8_t *dst,
                                  uint32_t *status, uint8_t *types, void *stream);
+/* Windows of several TCPLS connections of one session in one launch.  rapido gives every connection
+ * the session's key and its own IV: IV bytes 0..3 ^= BE32(connection_id) (derive_connection_aead_iv,
+ * lib/rapido.c:127-133; setup_connection_crypto_context :135-200), with a seq per connection.
+ * conn_ids[i] (device memory, one per descriptor) is that connection_id for record i; conn_ids == NULL
+ * is the single-connection call above. */
+int ptls_mi355x_tls_seal_records_multi(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12,
+                                       const ptls_mi355x_tls_record_t *recs, const uint32_t *conn_ids, size_t n,
+                                       const uint8_t *src, uint8_t *dst, void *stream);
+int ptls_mi355x_tls_open_records_multi(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12,
+                                       const ptls_mi355x_tls_record_t *recs, const uint32_t *conn_ids, size_t n,
+                                       const uint8_t *src, uint8_t *dst, uint32_t *status, uint8_t *types,
+                                       void *stream);
 
 /* Host-side planning (no device access), the loops of the reference record layer:
  *  plan_send: splits len bytes at src_off into <= 16384-byte fragments with consecutive seq

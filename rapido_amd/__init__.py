@@ -54,7 +54,8 @@ EXPORTED_FUNCTIONS = (
     "ptls_mi355x_seal_batch", "ptls_mi355x_open_batch", "ptls_mi355x_order_by_length",
     "ptls_mi355x_seal_batch_ordered", "ptls_mi355x_open_batch_ordered", "ptls_mi355x_set_lanes_per_record",
     "ptls_mi355x_get_lanes_per_record", "ptls_mi355x_kernel_name", "ptls_mi355x_last_error",
-    "ptls_mi355x_tls_seal_records", "ptls_mi355x_tls_open_records", "ptls_mi355x_tls_plan_send",
+    "ptls_mi355x_tls_seal_records", "ptls_mi355x_tls_open_records", "ptls_mi355x_tls_seal_records_multi",
+    "ptls_mi355x_tls_open_records_multi", "ptls_mi355x_tls_plan_send",
     "ptls_mi355x_tls_parse_records",
 )
 EXPORTED_OBJECTS = ("ptls_mi355x_aes128gcm", "ptls_mi355x_aes256gcm", "ptls_mi355x_aes128ctr",
@@ -132,6 +133,8 @@ def lib() -> C.CDLL:
         L.ptls_mi355x_last_error.restype = C.c_char_p
         L.ptls_mi355x_tls_seal_records.argtypes = [vp, vp, vp, sz, vp, vp, vp]
         L.ptls_mi355x_tls_open_records.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]
+        L.ptls_mi355x_tls_seal_records_multi.argtypes = [vp, vp, vp, vp, sz, vp, vp, vp]
+        L.ptls_mi355x_tls_open_records_multi.argtypes = [vp, vp, vp, vp, sz, vp, vp, vp, vp, vp]
         L.ptls_mi355x_tls_plan_send.argtypes = [sz, C.c_uint32, C.POINTER(u64), u64, u64, vp, sz, C.POINTER(sz)]
         L.ptls_mi355x_tls_plan_send.restype = sz
         L.ptls_mi355x_tls_parse_records.argtypes = [vp, sz, u64, C.POINTER(u64), u64, vp, sz, C.POINTER(sz),
@@ -351,16 +354,17 @@ class Engine:
 
 
     # TLS 1.3 record framing in the batch (include/ptls_mi355x.h section 4)
+    # conn_ptr: optional device array of per-record rapido connection ids (the *_multi entry points)
     def tls_seal_records(self, static_iv: bytes, recs_ptr: int, n: int, src_ptr: int, dst_ptr: int,
-                         stream: int = 0) -> None:
-        if lib().ptls_mi355x_tls_seal_records(self.handle, _cbuf(static_iv), recs_ptr, n, src_ptr, dst_ptr,
-                                              stream or None):
+                         stream: int = 0, conn_ptr: int = 0) -> None:
+        if lib().ptls_mi355x_tls_seal_records_multi(self.handle, _cbuf(static_iv), recs_ptr, conn_ptr or None, n,
+                                                    src_ptr, dst_ptr, stream or None):
             raise RuntimeError("tls_seal_records failed: " + last_error())
 
     def tls_open_records(self, static_iv: bytes, recs_ptr: int, n: int, src_ptr: int, dst_ptr: int, status_ptr: int,
-                         types_ptr: int, stream: int = 0) -> None:
-        if lib().ptls_mi355x_tls_open_records(self.handle, _cbuf(static_iv), recs_ptr, n, src_ptr, dst_ptr, status_ptr,
-                                              types_ptr, stream or None):
+                         types_ptr: int, stream: int = 0, conn_ptr: int = 0) -> None:
+        if lib().ptls_mi355x_tls_open_records_multi(self.handle, _cbuf(static_iv), recs_ptr, conn_ptr or None, n,
+                                                    src_ptr, dst_ptr, status_ptr, types_ptr, stream or None):
             raise RuntimeError("tls_open_records failed: " + last_error())
 
 

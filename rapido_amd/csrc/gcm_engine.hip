@@ -69,7 +69,8 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
                                                const void *__restrict__ descs, const uint32_t *__restrict__ order,
                                                uint32_t nrecs, const uint8_t *src, uint8_t *dst,
                                                const uint8_t *__restrict__ aad, uint32_t *__restrict__ status,
-                                               uint8_t *__restrict__ types, uint32_t *__restrict__ work)
+                                               uint8_t *__restrict__ types, uint32_t *__restrict__ work,
+                                               const uint32_t *__restrict__ conn)
 {
     static_assert(K <= MAX_KERNEL_K, "LDS holds at most MAX_KERNEL_K GHASH tables");
     __shared__ __attribute__((aligned(16))) uint8_t lds[Layout<K>::total];
@@ -137,9 +138,11 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
             Tmax = max(Tmax, shfl_xor_u32(Tmax, o));
 
         const uint32_t n1 = iv1 ^ bswap32((uint32_t)(rec.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)rec.seq);
+        /* per-connection IV (rapido derive_connection_aead_iv, lib/rapido.c:127-133): IV bytes 0..3 ^= BE32(id) */
+        const uint32_t n0 = conn != nullptr && in_batch ? iv0 ^ bswap32(conn[r]) : iv0;
         /* 16 always-readable bytes for idle prefetch slots: the first descriptor (>= 32 B, nrecs >= 1) */
         const uint8_t *dummy = (const uint8_t *)descs;
-        u32x4 part = lane_walk<NR, K, SEAL, FRAME>(lds, lanesel, rk, j, rec, valid, Tmax, iv0, n1, n2, src, dst, aad,
+        u32x4 part = lane_walk<NR, K, SEAL, FRAME>(lds, lanesel, rk, j, rec, valid, Tmax, n0, n1, n2, src, dst, aad,
                                                    dummy, ctype);
 #pragma unroll
         for (int o = 1; o < K; o <<= 1)
@@ -231,9 +234,10 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
         const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2, const void *__restrict__ descs,     \
         const uint32_t *__restrict__ order, uint32_t nrecs, const uint8_t *src, uint8_t *dst,                          \
         const uint8_t *__restrict__ aad, uint32_t *__restrict__ st, uint8_t *__restrict__ types,                       \
-        uint32_t *__restrict__ work)                                                                                   \
+        uint32_t *__restrict__ work, const uint32_t *__restrict__ conn)                                                \
     {                                                                                                                  \
-        gcm_batch_body<NR, K, SEAL, FRAME>(ki, iv0, iv1, iv2, descs, order, nrecs, src, dst, aad, st, types, work);    \
+        gcm_batch_body<NR, K, SEAL, FRAME>(ki, iv0, iv1, iv2, descs, order, nrecs, src, dst, aad, st, types, work,     \
+                                           conn);                                                                      \
     }
 #define MI355X_GCM_KERNEL(NAME, NR, K, SEAL) MI355X_GCM_KERNEL_F(NAME, NR, K, SEAL, false)
 
@@ -277,7 +281,8 @@ extern "C" __global__ void mi355x_aes_ecb(const KeyImage *__restrict__ ki, const
 /* ================================================================== host side ============ */
 
 typedef void (*batch_kernel_t)(const KeyImage *, uint32_t, uint32_t, uint32_t, const void *, const uint32_t *, uint32_t,
-                               const uint8_t *, uint8_t *, const uint8_t *, uint32_t *, uint8_t *, uint32_t *);
+                               const uint8_t *, uint8_t *, const uint8_t *, uint32_t *, uint8_t *, uint32_t *,
+                               const uint32_t *);
 
 constexpr uint32_t WORK_SLOTS = 256; /* per-context ring of work counters: one per launch in flight */
 
@@ -375,7 +380,8 @@ static inline uint32_t le32(const uint8_t *p) { return (uint32_t)p[0] | (uint32_
 
 static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void *static_iv12, const void *recs,
                         const uint32_t *order, size_t n, const uint8_t *src, uint8_t *dst, const uint8_t *aad,
-                        uint32_t *status, hipStream_t stream, bool frame = false, uint8_t *types = nullptr)
+                        uint32_t *status, hipStream_t stream, bool frame = false, uint8_t *types = nullptr,
+                        const uint32_t *conn = nullptr)
 {
     if (n == 0)
         return 0;
@@ -400,7 +406,7 @@ static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void
     uint32_t *work = ctx->d_work + (ctx->work_next++ % WORK_SLOTS);
     HIPCHK(hipMemsetAsync(work, 0, sizeof(uint32_t), stream));
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(WG_THREADS), 0, stream, ctx->d_ki, le32(iv), le32(iv + 4),
-                       le32(iv + 8), recs, order, (uint32_t)n, src, dst, aad, status, types, work);
+                       le32(iv + 8), recs, order, (uint32_t)n, src, dst, aad, status, types, work, conn);
     HIPCHK(hipGetLastError());
     return 0;
 }
@@ -562,20 +568,34 @@ int ptls_mi355x_tls_seal_records(ptls_mi355x_aesgcm_context_t *ctx, const void *
                                  const ptls_mi355x_tls_record_t *recs, size_t n, const uint8_t *src, uint8_t *dst,
                                  void *stream)
 {
-    return launch_batch(ctx, true, static_iv12, recs, nullptr, n, src, dst, nullptr, nullptr, (hipStream_t)stream,
-                        true, nullptr);
+    return ptls_mi355x_tls_seal_records_multi(ctx, static_iv12, recs, nullptr, n, src, dst, stream);
 }
 
 int ptls_mi355x_tls_open_records(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12,
                                  const ptls_mi355x_tls_record_t *recs, size_t n, const uint8_t *src, uint8_t *dst,
                                  uint32_t *status, uint8_t *types, void *stream)
 {
+    return ptls_mi355x_tls_open_records_multi(ctx, static_iv12, recs, nullptr, n, src, dst, status, types, stream);
+}
+
+int ptls_mi355x_tls_seal_records_multi(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12,
+                                       const ptls_mi355x_tls_record_t *recs, const uint32_t *conn_ids, size_t n,
+                                       const uint8_t *src, uint8_t *dst, void *stream)
+{
+    return launch_batch(ctx, true, static_iv12, recs, nullptr, n, src, dst, nullptr, nullptr, (hipStream_t)stream,
+                        true, nullptr, conn_ids);
+}
+
+int ptls_mi355x_tls_open_records_multi(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12,
+                                       const ptls_mi355x_tls_record_t *recs, const uint32_t *conn_ids, size_t n,
+                                       const uint8_t *src, uint8_t *dst, uint32_t *status, uint8_t *types, void *stream)
+{
     if (n != 0 && (status == nullptr || types == nullptr)) {
         snprintf(g_err, sizeof(g_err), "tls_open_records needs status and types");
         return -1;
     }
     return launch_batch(ctx, false, static_iv12, recs, nullptr, n, src, dst, nullptr, status, (hipStream_t)stream,
-                        true, types);
+                        true, types, conn_ids);
 }
 
 /* keys = GHASH steps of each record (its work), values = record index */

@@ -52,7 +52,7 @@ struct TlsRecord {
 /* the FRAME walk (TLS 1.3 record framing) with the framing kernels' prologue/epilogue, K = 4 */
 template <int NR, bool SEAL>
 static void run_tls(const KeyImage *ki, const uint8_t *lds, const uint8_t *static_iv, const TlsRecord *trecs, size_t n,
-                    const uint8_t *src, uint8_t *dst, uint32_t *status, uint8_t *types)
+                    const uint8_t *src, uint8_t *dst, uint32_t *status, uint8_t *types, const uint32_t *conn)
 {
     constexpr int K = 4;
     uint32_t iv0, iv1, iv2;
@@ -79,9 +79,10 @@ static void run_tls(const KeyImage *ki, const uint8_t *lds, const uint8_t *stati
         const uint32_t plen = SEAL ? r.len + 1 : r.len;
         Walk wk = make_walk(plen, 5, K, walk_out16(dst + r.dst));
         uint32_t n1 = iv1 ^ bswap32((uint32_t)(r.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)r.seq);
+        const uint32_t n0 = conn ? iv0 ^ bswap32(conn[i]) : iv0; /* rapido's per-connection IV */
         u32x4 tag = {0, 0, 0, 0};
         for (uint32_t j = 0; j < (uint32_t)K; ++j)
-            tag ^= lane_walk<NR, K, SEAL, true>(lds, 4u * (j & 31u) | 0x10000u, ki->rk, j, r, true, wk.T, iv0, n1, n2, src,
+            tag ^= lane_walk<NR, K, SEAL, true>(lds, 4u * (j & 31u) | 0x10000u, ki->rk, j, r, true, wk.T, n0, n1, n2, src,
                                                 dst, nullptr, (const uint8_t *)trecs, t.type);
         if (SEAL) {
             memcpy(dst + r.dst + plen, &tag, 16);
@@ -104,7 +105,7 @@ static void run_tls(const KeyImage *ki, const uint8_t *lds, const uint8_t *stati
 
 extern "C" int model_tls_batch(int is_seal, const uint8_t *key, size_t keylen, const uint8_t *static_iv,
                                const TlsRecord *trecs, size_t n, const uint8_t *src, uint8_t *dst, uint32_t *status,
-                               uint8_t *types)
+                               uint8_t *types, const uint32_t *conn)
 {
     KeyImage *ki = (KeyImage *)aligned_alloc(64, sizeof(KeyImage));
     uint8_t *lds = (uint8_t *)aligned_alloc(256, 160u * 1024u);
@@ -115,11 +116,11 @@ extern "C" int model_tls_batch(int is_seal, const uint8_t *key, size_t keylen, c
     }
     fill_lds(lds, kTabs.t0, ki, 4u, 0, 1);
     if (ki->rounds == 10)
-        is_seal ? run_tls<10, true>(ki, lds, static_iv, trecs, n, src, dst, status, types)
-                : run_tls<10, false>(ki, lds, static_iv, trecs, n, src, dst, status, types);
+        is_seal ? run_tls<10, true>(ki, lds, static_iv, trecs, n, src, dst, status, types, conn)
+                : run_tls<10, false>(ki, lds, static_iv, trecs, n, src, dst, status, types, conn);
     else
-        is_seal ? run_tls<14, true>(ki, lds, static_iv, trecs, n, src, dst, status, types)
-                : run_tls<14, false>(ki, lds, static_iv, trecs, n, src, dst, status, types);
+        is_seal ? run_tls<14, true>(ki, lds, static_iv, trecs, n, src, dst, status, types, conn)
+                : run_tls<14, false>(ki, lds, static_iv, trecs, n, src, dst, status, types, conn);
     free(ki);
     free(lds);
     return 0;

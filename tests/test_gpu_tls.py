@@ -197,8 +197,8 @@ def test_in_place(gpu):
         buf[base[i] + 5: base[i] + 5 + ln] = np.frombuffer(f, np.uint8)
         trecs[i] = (base[i] + 5, base[i], 50 + i, ln, 23)
     eng = ra.Engine(key)
-    d = dev(buf)
-    eng.tls_seal_records(iv, dev(trecs.view(np.uint8)).data_ptr(), len(trecs), d.data_ptr(), d.data_ptr())
+    d, d_recs = dev(buf), dev(trecs.view(np.uint8))  # descriptors held until the launch completes
+    eng.tls_seal_records(iv, d_recs.data_ptr(), len(trecs), d.data_ptr(), d.data_ptr())
     torch.cuda.synchronize()
     wire = d.cpu().numpy()
     for i, ln in enumerate(lens):
@@ -209,3 +209,70 @@ def test_in_place(gpu):
     assert list(st[: len(lens)]) == lens
     for i, ln in enumerate(lens):
         assert pt[base[i] + 5: base[i] + 5 + ln].tobytes() == frags[i]
+
+
+def conn_iv(iv: bytes, conn_id: int) -> bytes:
+    """rapido's derive_connection_aead_iv (lib/rapido.c:127-133): IV bytes 0..3 ^= BE32(connection_id)."""
+    return (int.from_bytes(iv[:4], "big") ^ conn_id).to_bytes(4, "big") + iv[4:]
+
+
+@pytest.mark.parametrize("keylen", [16, 32])
+def test_multi_connection_windows(gpu, keylen):
+    """The 16-record send windows of several TCPLS connections of one session (same key; per-connection IV and
+    seq, lib/rapido.c:135-200) sealed in ONE launch through tls_seal_records_multi, then received in one
+    tls_open_records_multi launch; every record matches the oracle's record layer under its connection's IV,
+    and a record opened under the wrong connection id fails alone."""
+    import torch
+    key = bytes(range(90, 90 + keylen))
+    iv = bytes(range(200, 212))
+    conns = [0, 1, 2, 3, 5, 0x01020304, 0xFFFFFFFF]
+    lens = [16384] * 14 + [1, 777]
+    trecs = np.zeros(len(conns) * len(lens), ra.TLS_RECORD_DTYPE)
+    conn = np.zeros(len(trecs), np.uint32)
+    off = woff = 0
+    k = 0
+    for ci, c in enumerate(conns):
+        for j, n in enumerate(lens):
+            trecs[k] = (off, woff, 1000 * ci + j, n, 23 if j % 5 else 22)
+            conn[k] = c
+            off += n
+            woff += n + 22
+            k += 1
+    src = np.frombuffer(xs(33, off + 16), np.uint8)
+    d_src, d_recs, d_conn = dev(src), dev(trecs.view(np.uint8)), dev(conn.view(np.int32))
+    d_wire = torch.zeros(woff + 16, dtype=torch.uint8, device="cuda")
+    eng = ra.Engine(key)
+    eng.tls_seal_records(iv, d_recs.data_ptr(), len(trecs), d_src.data_ptr(), d_wire.data_ptr(), conn_ptr=d_conn.data_ptr())
+    torch.cuda.synchronize()
+    wire = d_wire.cpu().numpy()
+    for t, c in zip(trecs, conn):
+        frag = bytes(src[int(t["src"]): int(t["src"]) + int(t["len"])])
+        want = oracle.tls_seal_record(key, conn_iv(iv, int(c)), int(t["seq"]), int(t["type"]), frag)
+        assert bytes(wire[int(t["dst"]): int(t["dst"]) + len(want)]) == want
+    # receive: plaintext slots of len + 1 bytes each (fragment + type), back to back
+    orecs = trecs.copy()
+    orecs["src"], orecs["len"] = trecs["dst"], trecs["len"] + 17
+    orecs["dst"] = np.concatenate([[0], np.cumsum(trecs["len"].astype(np.int64) + 1)[:-1]]).astype(np.uint64)
+    pt_size = int(orecs["dst"][-1]) + int(trecs["len"][-1]) + 1
+
+    def receive(conn_ids):
+        d_pt = torch.zeros(pt_size, dtype=torch.uint8, device="cuda")
+        d_st = torch.zeros(len(orecs), dtype=torch.int32, device="cuda")
+        d_ty = torch.zeros(len(orecs), dtype=torch.uint8, device="cuda")
+        d_orecs, d_ids = dev(orecs.view(np.uint8)), dev(conn_ids.view(np.int32))  # held until the launch completes
+        eng.tls_open_records(iv, d_orecs.data_ptr(), len(orecs), d_wire.data_ptr(), d_pt.data_ptr(), d_st.data_ptr(),
+                             d_ty.data_ptr(), conn_ptr=d_ids.data_ptr())
+        torch.cuda.synchronize()
+        return d_pt.cpu().numpy(), d_st.cpu().numpy().view(np.uint32), d_ty.cpu().numpy()
+
+    pt, st, ty = receive(conn)
+    assert (st == trecs["len"]).all() and (ty == trecs["type"]).all()
+    for t, o in zip(trecs, orecs):
+        assert bytes(pt[int(o["dst"]): int(o["dst"]) + int(t["len"])]) == bytes(src[int(t["src"]): int(t["src"]) +
+                                                                                  int(t["len"])])
+    wrong = conn.copy()
+    wrong[20] ^= 0x10
+    _, st, _ = receive(wrong)
+    assert st[20] == 0xFFFFFFFF
+    assert (np.delete(st, 20) == np.delete(trecs["len"], 20)).all()
+    eng.close()

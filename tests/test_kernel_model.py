@@ -130,13 +130,14 @@ def test_model_record_beyond_2p16_blocks(model, K):
     assert spans(got, recs, 16) == spans(want, recs, 16)
 
 
-def run_tls(lib, is_seal, key, iv, trecs, src, dst, st=None, ty=None):
+def run_tls(lib, is_seal, key, iv, trecs, src, dst, st=None, ty=None, conn=None):
     vp = C.c_void_p
-    lib.model_tls_batch.argtypes = [C.c_int, vp, C.c_size_t, vp, vp, C.c_size_t, vp, vp, vp, vp]
+    lib.model_tls_batch.argtypes = [C.c_int, vp, C.c_size_t, vp, vp, C.c_size_t, vp, vp, vp, vp, vp]
     st = np.zeros(max(len(trecs), 1), np.uint32) if st is None else st
     ty = np.zeros(max(len(trecs), 1), np.uint8) if ty is None else ty
     rc = lib.model_tls_batch(1 if is_seal else 0, key, len(key), iv, trecs.ctypes.data, len(trecs), src.ctypes.data,
-                             dst.ctypes.data, st.ctypes.data, ty.ctypes.data)
+                             dst.ctypes.data, st.ctypes.data, ty.ctypes.data,
+                             None if conn is None else conn.ctypes.data)
     assert rc == 0
     return st, ty
 
@@ -252,3 +253,45 @@ def test_sbox_circuit_and_lut3_mapping():
     for script in ("sbox_circuit.py", "sbox_lut3.py"):
         r = subprocess.run([sys.executable, os.path.join(root, "scripts", script)], capture_output=True, text=True)
         assert r.returncode == 0, r.stdout + r.stderr
+
+
+def conn_iv(iv: bytes, conn_id: int) -> bytes:
+    """rapido's derive_connection_aead_iv (lib/rapido.c:127-133): IV bytes 0..3 ^= BE32(connection_id)."""
+    head = (int.from_bytes(iv[:4], "big") ^ conn_id).to_bytes(4, "big")
+    return head + iv[4:]
+
+
+def test_model_tls_multi_connection_window(model):
+    """One batch holding the send windows of several connections of a session (same key, per-connection IV and
+    seq), sealed and opened in one pass, against the oracle's record layer with each connection's derived IV."""
+    import rapido_amd as ra
+    key, iv = bytes(range(50, 66)), bytes(range(12))
+    conns = [0, 1, 2, 7, 0xFFFFFFFF]
+    lens = [16384, 1, 1399, 16384, 300]
+    trecs = np.zeros(len(conns) * len(lens), ra.TLS_RECORD_DTYPE)
+    conn = np.zeros(len(trecs), np.uint32)
+    off = woff = 0
+    for k, (c, n) in enumerate((c, n) for c in conns for n in lens):
+        trecs[k] = (off, woff, 5 + k % len(lens), n, 23)
+        conn[k] = c
+        off += n
+        woff += n + 22
+    src = np.frombuffer(bytes((i * 7 + 3) & 0xFF for i in range(off + 16)), np.uint8).copy()
+    wire = np.zeros(woff + 16, np.uint8)
+    run_tls(model, True, key, iv, trecs, src, wire, conn=conn)
+    for t, c in zip(trecs, conn):
+        frag = bytes(src[int(t["src"]): int(t["src"]) + int(t["len"])])
+        want = oracle.tls_seal_record(key, conn_iv(iv, int(c)), int(t["seq"]), 23, frag)
+        assert bytes(wire[int(t["dst"]): int(t["dst"]) + len(want)]) == want
+    orecs = trecs.copy()
+    orecs["src"], orecs["len"] = trecs["dst"], trecs["len"] + 17
+    orecs["dst"] = trecs["src"]
+    pt = np.zeros_like(src)
+    st, ty = run_tls(model, False, key, iv, orecs, wire, pt, conn=conn)
+    assert (st[: len(trecs)] == trecs["len"]).all() and (ty[: len(trecs)] == 23).all()
+    assert bytes(pt[:off]) == bytes(src[:off])
+    # a record opened under another connection's IV fails
+    wrong = conn.copy()
+    wrong[3] ^= 1
+    st, _ = run_tls(model, False, key, iv, orecs, wire, pt, conn=wrong)
+    assert st[3] == 0xFFFFFFFF and (np.delete(st[: len(trecs)], 3) == np.delete(trecs["len"], 3)).all()
