@@ -246,6 +246,10 @@ int ptls_mi355x_tls_parse_records(const uint8_t *wire, size_t len, uint64_t src_
 /* lanes per record used by the batch kernels (1, 2, 4 or 8; default 4); returns the previous value, or -1 */
 int ptls_mi355x_set_lanes_per_record(int k);
 int ptls_mi355x_get_lanes_per_record(void);
+/* framing batches (section 4) of at most n records run on the window kernels, which cut every record into
+ * 64-block GHASH segments walked in parallel (latency of rapido-sized windows); larger batches run on the
+ * batch kernels (throughput).  Default 16384; returns the previous value.  Results are identical. */
+size_t ptls_mi355x_set_tls_window_records(size_t n);
 /* name of the kernel symbol the next batch launch with these parameters uses (for profiling) */
 const char *ptls_mi355x_kernel_name(int is_seal, size_t key_size);
 /* last HIP error string seen by the engine ("" if none) */

@@ -55,7 +55,7 @@ EXPORTED_FUNCTIONS = (
     "ptls_mi355x_seal_batch_ordered", "ptls_mi355x_open_batch_ordered", "ptls_mi355x_set_lanes_per_record",
     "ptls_mi355x_get_lanes_per_record", "ptls_mi355x_kernel_name", "ptls_mi355x_last_error",
     "ptls_mi355x_tls_seal_records", "ptls_mi355x_tls_open_records", "ptls_mi355x_tls_seal_records_multi",
-    "ptls_mi355x_tls_open_records_multi", "ptls_mi355x_tls_plan_send",
+    "ptls_mi355x_tls_open_records_multi", "ptls_mi355x_set_tls_window_records", "ptls_mi355x_tls_plan_send",
     "ptls_mi355x_tls_parse_records",
 )
 EXPORTED_OBJECTS = ("ptls_mi355x_aes128gcm", "ptls_mi355x_aes256gcm", "ptls_mi355x_aes128ctr",
@@ -134,6 +134,8 @@ def lib() -> C.CDLL:
         L.ptls_mi355x_tls_seal_records.argtypes = [vp, vp, vp, sz, vp, vp, vp]
         L.ptls_mi355x_tls_open_records.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]
         L.ptls_mi355x_tls_seal_records_multi.argtypes = [vp, vp, vp, vp, sz, vp, vp, vp]
+        L.ptls_mi355x_set_tls_window_records.argtypes = [sz]
+        L.ptls_mi355x_set_tls_window_records.restype = sz
         L.ptls_mi355x_tls_open_records_multi.argtypes = [vp, vp, vp, vp, sz, vp, vp, vp, vp, vp]
         L.ptls_mi355x_tls_plan_send.argtypes = [sz, C.c_uint32, C.POINTER(u64), u64, u64, vp, sz, C.POINTER(sz)]
         L.ptls_mi355x_tls_plan_send.restype = sz
@@ -400,6 +402,11 @@ def set_lanes_per_record(k: int) -> int:
     if prev < 0:
         raise ValueError("lanes per record must be 1, 2, 4 or 8")
     return prev
+
+
+def set_tls_window_records(n: int) -> int:
+    """Framing batches of at most n records run on the window kernels (0: never); returns the previous value."""
+    return lib().ptls_mi355x_set_tls_window_records(n)
 
 
 def kernel_name(is_seal: bool, key_size: int) -> str:

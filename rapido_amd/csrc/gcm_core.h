@@ -642,6 +642,7 @@ struct KeyImage {
     uint32_t pad_[2];
     uint8_t H[16];      /* E_K(0^128) */
     uint8_t gh[MAX_K][32][16][16]; /* gh[p-1] = nibble tables of H^p, p = 1..MAX_K */
+    uint8_t gh64[32][16][16];      /* nibble tables of H^64: joins the 64-position segments of the window kernels */
 };
 
 /* ------------------------------------------------------------------ record walk ----------- */
@@ -698,10 +699,15 @@ GCM_HD Walk make_walk(uint32_t len, uint32_t aadlen, uint32_t K, uint32_t out16 
     return w;
 }
 
-/* table slot (H^(K - slot)) that scales lane j's chain: exponent pad + g - q_last(j) */
-GCM_HD uint32_t walk_scale_slot(const Walk &w, uint32_t j, uint32_t K)
+/*
+ * table slot (H^(K - slot)) that scales lane j's chain: exponent pad + g - q_last(j).  end_cap bounds the
+ * chain to the first end_cap padded positions (a segment of the window kernels, see lane_walk).
+ */
+GCM_HD uint32_t walk_scale_slot(const Walk &w, uint32_t j, uint32_t K, uint32_t end_cap = 0xffffffffu)
 {
-    const uint32_t end = w.pad + w.A + w.C + 1u; /* one past the last real position */
+    uint32_t end = w.pad + w.A + w.C + 1u; /* one past the last real position */
+    if (end > end_cap)
+        end = end_cap;
     if (end <= j)
         return 0u; /* no real position: the chain is 0 */
     const uint32_t q_last = j + K * ((end - 1u - j) / K);
@@ -769,7 +775,31 @@ GCM_HD void aes_encrypt_bytes(const uint8_t *sbox, const uint32_t *rk, uint32_t 
         out[i] = s[i];
 }
 
-/* Builds the whole KeyImage (round keys, H, nibble tables of H^1..H^MAX_K) sequentially. */
+/* the 32 nibble tables of multiplication by c: tab[t][v] = (nibble t of the element = v) * c */
+GCM_HD void nibble_tables(const uint8_t c[16], uint8_t (*tab)[16][16])
+{
+    for (int t = 0; t < 32; ++t)
+        for (int k = 0; k < 16; ++k)
+            tab[t][0][k] = 0;
+    /* single-bit entries: the element with GCM bit k set, times c, is c * x^k */
+    uint8_t v[16];
+    for (int k = 0; k < 16; ++k)
+        v[k] = c[k];
+    for (int bit = 0; bit < 128; ++bit) {
+        int byte = bit >> 3, q = 7 - (bit & 7);
+        int t = 8 * (byte >> 2) + 2 * (byte & 3) + (q >= 4 ? 1 : 0), s = q & 3;
+        for (int k = 0; k < 16; ++k)
+            tab[t][1 << s][k] = v[k];
+        gf128_mulx_bytes(v);
+    }
+    for (int t = 0; t < 32; ++t)
+        for (int e = 3; e < 16; ++e)
+            if (e & (e - 1))
+                for (int k = 0; k < 16; ++k)
+                    tab[t][e][k] = (uint8_t)(tab[t][e & (e - 1)][k] ^ tab[t][e & -e][k]);
+}
+
+/* Builds the whole KeyImage (round keys, H, nibble tables of H^1..H^MAX_K and H^64) sequentially. */
 GCM_HD int build_key_image(const uint8_t *sbox, const uint8_t *key, uint32_t keylen, KeyImage *ki)
 {
     if (keylen != 16 && keylen != 32)
@@ -788,27 +818,12 @@ GCM_HD int build_key_image(const uint8_t *sbox, const uint8_t *key, uint32_t key
     for (int p = 1; p <= MAX_K; ++p) {
         if (p > 1)
             gf128_mul_bytes(hp, ki->H, hp);
-        uint8_t(*tab)[16][16] = ki->gh[p - 1];
-        for (int t = 0; t < 32; ++t)
-            for (int k = 0; k < 16; ++k)
-                tab[t][0][k] = 0;
-        /* single-bit entries: the element with GCM bit k set, times H^p, is H^p * x^k */
-        uint8_t v[16];
-        for (int k = 0; k < 16; ++k)
-            v[k] = hp[k];
-        for (int bit = 0; bit < 128; ++bit) {
-            int byte = bit >> 3, q = 7 - (bit & 7);
-            int t = 8 * (byte >> 2) + 2 * (byte & 3) + (q >= 4 ? 1 : 0), s = q & 3;
-            for (int k = 0; k < 16; ++k)
-                tab[t][1 << s][k] = v[k];
-            gf128_mulx_bytes(v);
-        }
-        for (int t = 0; t < 32; ++t)
-            for (int e = 3; e < 16; ++e)
-                if (e & (e - 1))
-                    for (int k = 0; k < 16; ++k)
-                        tab[t][e][k] = (uint8_t)(tab[t][e & (e - 1)][k] ^ tab[t][e & -e][k]);
+        nibble_tables(hp, ki->gh[p - 1]);
     }
+    /* H^64 = ((H^8)^2)^2)^2 */
+    for (int sq = 0; sq < 3; ++sq)
+        gf128_mul_bytes(hp, hp, hp);
+    nibble_tables(hp, ki->gh64);
     return 0;
 }
 
@@ -835,6 +850,55 @@ GCM_HD void fill_lds(uint8_t *lds, const uint32_t *t0, const KeyImage *ki, uint3
         const u32x4 *srcv = (const u32x4 *)ki->gh[K - slot - 1];
         *(u32x4 *)(lds + gh_base + slot * GH_TABLE_BYTES + within * 16) = srcv[within];
     }
+}
+
+/* ------------------------------------------------------------------ window kernels --------- */
+
+/*
+ * LDS map of the window kernels (small framing batches, gcm_engine.hip tls_window_body): the two-table
+ * AES image, the tables of H^4..H^1 (slot j = H^(4-j), the lane scaling of a K = 4 walk), the tables of
+ * H^64 (joining 64-position segments), then the segment sums.
+ */
+struct LayoutWin {
+    static constexpr bool four_tables = false;
+    static constexpr uint32_t gh_base = 0x10000u;
+    static constexpr uint32_t gh64 = gh_base + 4u * GH_TABLE_BYTES;
+    static constexpr uint32_t parts = gh64 + GH_TABLE_BYTES;
+};
+enum : uint32_t {
+    WIN_SEG = 64,    /* GHASH positions per segment: 4 lanes x 16 steps */
+    WIN_MAXSEG = 17, /* segments of the largest TLS record (16640-byte record: 1 + 1039 + 1 positions) */
+};
+
+GCM_HD void fill_lds_window(uint8_t *lds, const uint32_t *t0, const KeyImage *ki, uint32_t tid, uint32_t nthr)
+{
+    for (uint32_t i = tid; i < 0x10000u / 16u; i += nthr) { /* image A: T0 | T1 rows, 32 bank replicas each */
+        const uint32_t off = i * 16u, x = (off >> 8) & 0xffu;
+        const uint32_t v = (off & 128u) ? rotl32(t0[x], 8) : t0[x];
+        *(u32x4 *)(lds + off) = u32x4{v, v, v, v};
+    }
+    for (uint32_t i = tid; i < 5u * GH_TABLE_BYTES / 16u; i += nthr) {
+        const uint32_t slot = i / (GH_TABLE_BYTES / 16u), within = i % (GH_TABLE_BYTES / 16u);
+        const u32x4 *srcv = slot < 4u ? (const u32x4 *)ki->gh[3u - slot] : (const u32x4 *)ki->gh64;
+        *(u32x4 *)(lds + LayoutWin::gh_base + slot * GH_TABLE_BYTES + within * 16u) = srcv[within];
+    }
+}
+
+/*
+ * Segment seg of a framed record with GHASH payload plen (AAD = the 5-byte header, one block): the record's
+ * g = 1 + ceil(plen/16) + 1 positions are front-padded to nseg * 64; the returned walk covers padded
+ * positions [64 seg, 64 seg + 64) (its pad is negative as int32 after the first segment).
+ */
+GCM_HD Walk window_segment(uint32_t plen, uint32_t seg, uint32_t *nseg)
+{
+    const uint32_t g = 1u + (plen + 15u) / 16u + 1u;
+    *nseg = (g + WIN_SEG - 1u) / WIN_SEG;
+    Walk w;
+    w.A = 1u;
+    w.C = (plen + 15u) / 16u;
+    w.T = WIN_SEG / 4u;
+    w.pad = WIN_SEG * *nseg - g - WIN_SEG * seg;
+    return w;
 }
 
 /* ------------------------------------------------------------------ per-lane record walk -- */
@@ -940,10 +1004,16 @@ GCM_HD u32x4 shr_bytes(u32x4 v, uint32_t n)
  * registers (seal), or read directly since the tag follows it (open) -- nothing is ever
  * read outside [aad, aad + aadlen) and [src, src + len (+16 for open)).
  */
-template <int NR, int K, bool SEAL, bool FRAME = false>
+/*
+ * seg (window kernels): walk only one 64-position segment of the record.  The record's GHASH positions are
+ * front-padded to a multiple of K*T (T = seg->T) and seg->pad is that padding minus the segment's first
+ * padded position (negative as int32 for later segments); the lane's chain is scaled to the segment's end.
+ * LY: the LDS layout (T-table image count and GHASH table base).
+ */
+template <int NR, int K, bool SEAL, bool FRAME = false, class LY = Layout<K>>
 GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk, uint32_t j, const Record &rec, bool valid,
                        uint32_t Tmax, uint32_t iv0, uint32_t iv1, uint32_t iv2, const uint8_t *src, uint8_t *dst,
-                       const uint8_t *aad, const uint8_t *dummy, uint32_t ctype = 0u)
+                       const uint8_t *aad, const uint8_t *dummy, uint32_t ctype = 0u, const Walk *seg = nullptr)
 {
     /*
      * FRAME (TLS 1.3 record framing, lib/picotls.c:621-684 and :4779-4791): the AAD is the 5-byte
@@ -953,7 +1023,8 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
      */
     const uint32_t plen = FRAME && SEAL ? rec.len + 1u : rec.len;
     const uint32_t aadlen = FRAME ? 5u : rec.aadlen;
-    const Walk wk = make_walk(plen, aadlen, K, walk_out16(dst + rec.dst));
+    const Walk wk = seg != nullptr ? *seg : make_walk(plen, aadlen, K, walk_out16(dst + rec.dst));
+    const uint32_t end_cap = seg != nullptr ? (uint32_t)K * seg->T : 0xffffffffu;
     const uint32_t gend = wk.A + wk.C + 1u; /* positions p >= gend are trailing pads */
     const uint8_t *in = src + rec.src;
     uint8_t *out = dst + rec.dst;
@@ -964,11 +1035,11 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
 #if GCM_R2CACHE
     constexpr uint32_t WIN = 0xffffff00u; /* 2^8-block windows (aes_round12_consts) */
     uint32_t c1[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, c1_hi = 0u;
-    aes_round12_consts<Layout<K>::four_tables>(lds, lanesel, rk, iv0, iv1, iv2, 0u, c1);
+    aes_round12_consts<LY::four_tables>(lds, lanesel, rk, iv0, iv1, iv2, 0u, c1);
 #else
     constexpr uint32_t WIN = 0xffff0000u; /* 2^16-block windows (aes_round1_consts) */
     uint32_t c1[4] = {0u, 0u, 0u, 0u}, c1_hi = 0u;
-    aes_round1_consts<Layout<K>::four_tables>(lds, lanesel, rk, iv0, iv1, iv2, 0u, c1);
+    aes_round1_consts<LY::four_tables>(lds, lanesel, rk, iv0, iv1, iv2, 0u, c1);
 #endif
 
     /*
@@ -1021,9 +1092,9 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
 #if GCM_ABLATE_AES && GCM_ABLATE_GHASH
         const u32x4 P = acc;
 #elif GCM_ABLATE_AES
-        const u32x4 P = ghash_mul_lds(lds, Layout<K>::gh_base, acc);
+        const u32x4 P = ghash_mul_lds(lds, LY::gh_base, acc);
 #elif GCM_ABLATE_GHASH
-        aes_encrypt_tt<NR, Layout<K>::four_tables>(lds, lanesel, rk, w);
+        aes_encrypt_tt<NR, LY::four_tables>(lds, lanesel, rk, w);
         const u32x4 P = acc;
 #else
         if ((ctr & WIN) != c1_hi) { /* a record crossing a counter window (>= 2^8 blocks with GCM_R2CACHE) */
@@ -1035,13 +1106,13 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
             GCM_OPAQUE(o2);
             GCM_OPAQUE(ol);
 #if GCM_R2CACHE
-            aes_round12_consts<Layout<K>::four_tables>(lds, ol, rk, o0, o1, o2, c1_hi, c1);
+            aes_round12_consts<LY::four_tables>(lds, ol, rk, o0, o1, o2, c1_hi, c1);
 #else
-            aes_round1_consts<Layout<K>::four_tables>(lds, ol, rk, o0, o1, o2, c1_hi, c1);
+            aes_round1_consts<LY::four_tables>(lds, ol, rk, o0, o1, o2, c1_hi, c1);
 #endif
         }
         const u32x4 P =
-            aes_ghash_fused_h<NR, Layout<K>::four_tables>(lds, lanesel, rk, c1, ctr, w, Layout<K>::gh_base, acc);
+            aes_ghash_fused_h<NR, LY::four_tables>(lds, lanesel, rk, c1, ctr, w, LY::gh_base, acc);
 #endif
         const u32x4 ks = {w[0], w[1], w[2], w[3]};
 
@@ -1120,7 +1191,7 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
             step(t + 1u, bufB);
     }
     /* scale the chain by H^(pad + g - q_last(j)) (make_walk) */
-    acc = ghash_mul_lds(lds, Layout<K>::gh_base + walk_scale_slot(wk, j, K) * GH_TABLE_BYTES, acc);
+    acc = ghash_mul_lds(lds, LY::gh_base + walk_scale_slot(wk, j, K, end_cap) * GH_TABLE_BYTES, acc);
     return acc ^ ek0;
 }
 

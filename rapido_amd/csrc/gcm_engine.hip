@@ -226,6 +226,134 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
     }
 }
 
+/*
+ * Window kernels for SMALL framing batches (rapido's 16-record send / 32-record recv windows, a few
+ * connections' windows at once).  The batch kernels above give a record 4 lanes, so a 16-record window
+ * is one wave walking 257 steps.  Here every record is cut into 64-position GHASH segments (its
+ * positions front-padded to a multiple of 64 with zero blocks, which leaves GHASH unchanged), each
+ * segment walked by its own 4-lane slot (16 steps), and the segment sums joined by Horner with H^64:
+ *   GHASH = (..((P_0 H^64 + P_1) H^64 + P_2) ..) H^64 + P_{S-1}
+ * (E_K(J0), folded into the length lane of the last segment, is added unmultiplied).  A 256-thread
+ * workgroup holds WIN_RECS records x 17 segments; its LDS holds the two-table AES image, the tables of
+ * H^4..H^1 (lane scaling) and of H^64.  A record of more than WIN_MAXSEG segments (larger than a TLS
+ * record) is walked whole by its first slot instead.  Results are bit-identical to the batch kernels.
+ */
+template <int NR, bool SEAL, int THREADS>
+__device__ __forceinline__ void tls_window_body(const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2,
+                                                const TlsRecord *__restrict__ trecs, uint32_t nrecs, const uint8_t *src,
+                                                uint8_t *dst, uint32_t *__restrict__ status, uint8_t *__restrict__ types,
+                                                const uint32_t *__restrict__ conn)
+{
+    constexpr uint32_t SLOTS = THREADS / 4, RECS = SLOTS / WIN_MAXSEG; /* records per workgroup pass */
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LayoutWin::parts + RECS * WIN_MAXSEG * 16u];
+    fill_lds_window(lds, c_tabs.t0, ki, threadIdx.x, blockDim.x);
+    uint32_t rk[4 * (NR + 1)];
+#pragma unroll
+    for (int i = 0; i < 4 * (NR + 1); ++i)
+        rk[i] = ki->rk[i];
+    __syncthreads();
+
+    const uint32_t lane = threadIdx.x & 63u, slot = threadIdx.x >> 2, j = lane & 3u;
+    const uint32_t lanesel = (lane & 31u) * 4u | 0x10000u;
+    const uint32_t rl = slot / WIN_MAXSEG, seg = slot % WIN_MAXSEG;
+    const uint32_t ngroups = (nrecs + RECS - 1u) / RECS;
+    /* persistent: the workgroup fills its LDS once and takes record groups with a grid stride */
+    for (uint32_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+        const uint32_t r = grp * RECS + rl;
+        const bool in_batch = rl < RECS && r < nrecs;
+        Record rec = {0, 0, 0, 0, 0, 5};
+        uint32_t ctype = 0u;
+        bool valid = in_batch;
+        if (in_batch) {
+            const TlsRecord t = trecs[r];
+            rec.seq = t.seq;
+            if (SEAL) {
+                rec.src = t.src;
+                rec.dst = t.dst + 5u;
+                rec.len = t.len;
+                ctype = t.type;
+            } else {
+                rec.src = t.src + 5u;
+                rec.dst = t.dst;
+                rec.len = t.len >= 16u ? t.len - 16u : 0u;
+                valid = t.len >= 16u;
+            }
+        }
+        const uint32_t plen = SEAL ? rec.len + 1u : rec.len;
+        uint32_t nseg;
+        const Walk sw = window_segment(plen, seg, &nseg);
+        const bool whole = nseg > WIN_MAXSEG; /* not a TLS-sized record: its first slot walks it all */
+        const bool active = valid && (whole ? seg == 0u : seg < nseg);
+        uint32_t Tw = active ? (whole ? make_walk(plen, 5u, 4u, walk_out16(dst + rec.dst)).T : sw.T) : 0u;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1)
+            Tw = max(Tw, shfl_xor_u32(Tw, o));
+        const uint32_t n1 = iv1 ^ bswap32((uint32_t)(rec.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)rec.seq);
+        const uint32_t n0 = conn != nullptr && in_batch ? iv0 ^ bswap32(conn[r]) : iv0;
+        u32x4 part = lane_walk<NR, 4, SEAL, true, LayoutWin>(lds, lanesel, rk, j, rec, active, Tw, n0, n1, n2, src, dst,
+                                                             nullptr, (const uint8_t *)trecs, ctype, whole ? nullptr : &sw);
+        part ^= shfl_xor_u32x4(part, 1);
+        part ^= shfl_xor_u32x4(part, 2);
+        if (active && j == 0u)
+            *(u32x4 *)(lds + LayoutWin::parts + (rl * WIN_MAXSEG + seg) * 16u) = part;
+        __syncthreads();
+        if (in_batch && seg == 0u) {
+            /* the record's first slot joins the segment sums: tag (seal) or tag ^ received tag (open) */
+            u32x4 acc = {0u, 0u, 0u, 0u};
+            if (valid) {
+                const uint32_t ns = whole ? 1u : nseg;
+                acc = *(const u32x4 *)(lds + LayoutWin::parts + rl * WIN_MAXSEG * 16u);
+                for (uint32_t k = 1; k < ns; ++k)
+                    acc = ghash_mul_lds(lds, LayoutWin::gh64, acc) ^
+                          *(const u32x4 *)(lds + LayoutWin::parts + (rl * WIN_MAXSEG + k) * 16u);
+            }
+            if (SEAL) {
+                if (j == 0u) {
+                    *(u32x4_u *)(dst + rec.dst + plen) = acc;
+                    const uint32_t reclen = plen + 16u; /* 17 03 03 BE16(plen + 16) (lib/picotls.c:658-662) */
+                    store_partial(dst + rec.dst - 5u, 5u,
+                                  u32x4{0x00030317u | ((reclen >> 8) & 0xffu) << 24, reclen & 0xffu, 0u, 0u});
+                }
+            } else if (!valid || (acc[0] | acc[1] | acc[2] | acc[3]) != 0u) {
+                /* no unverified plaintext is released (fusion leaves it, lib/fusion.c:656-679) */
+                uint8_t *out = dst + rec.dst;
+                for (uint32_t off = 16u * j; off < rec.len; off += 64u) {
+                    const uint32_t n = rec.len - off;
+                    if (n >= 16u)
+                        *(u32x4_u *)(out + off) = u32x4{0u, 0u, 0u, 0u};
+                    else
+                        store_partial(out + off, n, u32x4{0u, 0u, 0u, 0u});
+                }
+                if (j == 0u) {
+                    status[r] = 0xffffffffu; /* PTLS_ALERT_BAD_RECORD_MAC */
+                    types[r] = 0u;
+                }
+            } else if (j == 0u) {
+                /* padding strip + content-type pop (lib/picotls.c:4784-4791) over plaintext the other slots wrote */
+                __threadfence();
+                const uint8_t *pt = dst + rec.dst;
+                uint32_t n = plen, found = 0xfffffffeu, ty = 0u; /* PTLS_ALERT_UNEXPECTED_MESSAGE if all zero */
+                while (n != 0u && found == 0xfffffffeu) {
+                    const uint32_t base = n >= 16u ? n - 16u : 0u;
+                    const u32x4 v = n >= 16u ? *(const u32x4_u *)(pt + base) : load_partial(pt, n);
+#pragma unroll
+                    for (int d = 3; d >= 0; --d) {
+                        if (found == 0xfffffffeu && v[d] != 0u) {
+                            const uint32_t b = (31u - (uint32_t)__builtin_clz(v[d])) >> 3;
+                            found = base + 4u * (uint32_t)d + b;
+                            ty = (v[d] >> (8u * b)) & 0xffu;
+                        }
+                    }
+                    n = base;
+                }
+                status[r] = found;
+                types[r] = (uint8_t)ty;
+            }
+        }
+        __syncthreads(); /* the segment sums of this pass are consumed before the next pass writes them */
+    }
+}
+
 } // namespace
 
 /* Named kernel instances (readable in rocprofv3 traces). */
@@ -263,7 +391,26 @@ MI355X_GCM_KERNEL_F(mi355x_tls_seal_aes256_k4, 14, 4, true, true)
 MI355X_GCM_KERNEL_F(mi355x_tls_open_aes128_k4, 10, 4, false, true)
 MI355X_GCM_KERNEL_F(mi355x_tls_open_aes256_k4, 14, 4, false, true)
 
-/* key image: round keys, H and the nibble tables of H^1..H^8 (cold path, one thread) */
+#define MI355X_TLS_WIN_KERNEL(NAME, NR, SEAL, THREADS)                                                                 \
+    extern "C" __global__ __launch_bounds__(THREADS) void NAME(                                                        \
+        const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2, const TlsRecord *__restrict__ trecs, \
+        uint32_t nrecs, const uint8_t *src, uint8_t *dst, uint32_t *__restrict__ st, uint8_t *__restrict__ types,       \
+        const uint32_t *__restrict__ conn)                                                                             \
+    {                                                                                                                  \
+        tls_window_body<NR, SEAL, THREADS>(ki, iv0, iv1, iv2, trecs, nrecs, src, dst, st, types, conn);                \
+    }
+/* 256 threads (3 records per pass): one window spread over many CUs; 1024 threads (15 records per pass,
+ * persistent): batches of hundreds of windows */
+MI355X_TLS_WIN_KERNEL(mi355x_tls_win_seal_aes128, 10, true, 256)
+MI355X_TLS_WIN_KERNEL(mi355x_tls_win_seal_aes256, 14, true, 256)
+MI355X_TLS_WIN_KERNEL(mi355x_tls_win_open_aes128, 10, false, 256)
+MI355X_TLS_WIN_KERNEL(mi355x_tls_win_open_aes256, 14, false, 256)
+MI355X_TLS_WIN_KERNEL(mi355x_tls_winw_seal_aes128, 10, true, 1024)
+MI355X_TLS_WIN_KERNEL(mi355x_tls_winw_seal_aes256, 14, true, 1024)
+MI355X_TLS_WIN_KERNEL(mi355x_tls_winw_open_aes128, 10, false, 1024)
+MI355X_TLS_WIN_KERNEL(mi355x_tls_winw_open_aes256, 14, false, 1024)
+
+/* key image: round keys, H and the nibble tables of H^1..H^8 and H^64 (cold path, one thread) */
 extern "C" __global__ void mi355x_gcm_setup(const uint8_t *key, uint32_t keylen, KeyImage *ki, int *rc)
 {
     if (threadIdx.x == 0 && blockIdx.x == 0)
@@ -303,6 +450,8 @@ struct st_ptls_mi355x_aesgcm_context {
 
 static thread_local char g_err[256];
 static int g_lanes = 4;
+/* framing batches of at most this many records go to the window kernels (ptls_mi355x_set_tls_window_records) */
+static size_t g_window_records = 16384;
 
 static int fail(const char *what, hipError_t e)
 {
@@ -389,6 +538,33 @@ static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void
         snprintf(g_err, sizeof(g_err), "batch of %zu records exceeds 2^32-1", n);
         return -1;
     }
+    if (frame && n <= g_window_records) {
+        /*
+         * small framing batch: the window kernels (segments of 64 GHASH positions in parallel).  Up to 3 records
+         * per CU: 256-thread groups of 3 records, so a window spreads over many CUs; above that, persistent
+         * 1024-thread groups of 15 records, one per CU.
+         */
+        typedef void (*win_kernel_t)(const KeyImage *, uint32_t, uint32_t, uint32_t, const TlsRecord *, uint32_t,
+                                     const uint8_t *, uint8_t *, uint32_t *, uint8_t *, const uint32_t *);
+        const bool k256 = ctx->key_size == 32, wide = n > 3u * (uint64_t)ctx->num_cu;
+        win_kernel_t wk;
+        if (wide)
+            wk = seal ? (k256 ? mi355x_tls_winw_seal_aes256 : mi355x_tls_winw_seal_aes128)
+                      : (k256 ? mi355x_tls_winw_open_aes256 : mi355x_tls_winw_open_aes128);
+        else
+            wk = seal ? (k256 ? mi355x_tls_win_seal_aes256 : mi355x_tls_win_seal_aes128)
+                      : (k256 ? mi355x_tls_win_open_aes256 : mi355x_tls_win_open_aes128);
+        const uint32_t threads = wide ? 1024u : 256u, per = (threads / 4u) / WIN_MAXSEG;
+        uint64_t blocks = (n + per - 1) / per;
+        if (wide && blocks > (uint64_t)ctx->num_cu)
+            blocks = (uint64_t)ctx->num_cu;
+        const uint8_t *wiv = (const uint8_t *)static_iv12;
+        DeviceGuard guard(ctx->device);
+        hipLaunchKernelGGL(wk, dim3((unsigned)blocks), dim3(threads), 0, stream, ctx->d_ki, le32(wiv), le32(wiv + 4),
+                           le32(wiv + 8), (const TlsRecord *)recs, (uint32_t)n, src, dst, status, types, conn);
+        HIPCHK(hipGetLastError());
+        return 0;
+    }
     const int k = frame ? 4 : g_lanes;
     batch_kernel_t kern = frame ? pick_tls_kernel(seal, ctx->key_size == 32 ? 14u : 10u)
                                 : pick_kernel(seal, ctx->key_size == 32 ? 14u : 10u, k, nullptr);
@@ -458,6 +634,13 @@ int ptls_mi355x_set_lanes_per_record(int k)
 }
 
 int ptls_mi355x_get_lanes_per_record(void) { return g_lanes; }
+
+size_t ptls_mi355x_set_tls_window_records(size_t n)
+{
+    const size_t prev = g_window_records;
+    g_window_records = n;
+    return prev;
+}
 
 const char *ptls_mi355x_kernel_name(int is_seal, size_t key_size)
 {

@@ -103,6 +103,98 @@ static void run_tls(const KeyImage *ki, const uint8_t *lds, const uint8_t *stati
     }
 }
 
+/* the window kernels' math (tls_window_body): per record, every 64-position segment walked by 4 lanes, sums
+ * joined by Horner with H^64 (records above WIN_MAXSEG segments walked whole, as the kernel does) */
+template <int NR, bool SEAL>
+static void run_tls_window(const KeyImage *ki, const uint8_t *lds, const uint8_t *static_iv, const TlsRecord *trecs,
+                           size_t n, const uint8_t *src, uint8_t *dst, uint32_t *status, uint8_t *types,
+                           const uint32_t *conn)
+{
+    uint32_t iv0, iv1, iv2;
+    memcpy(&iv0, static_iv, 4);
+    memcpy(&iv1, static_iv + 4, 4);
+    memcpy(&iv2, static_iv + 8, 4);
+    for (size_t i = 0; i < n; ++i) {
+        const TlsRecord &t = trecs[i];
+        Record r = {0, 0, 0, t.seq, 0, 5};
+        if (SEAL) {
+            r.src = t.src;
+            r.dst = t.dst + 5;
+            r.len = t.len;
+        } else {
+            if (t.len < 16) {
+                status[i] = 0xffffffffu;
+                types[i] = 0;
+                continue;
+            }
+            r.src = t.src + 5;
+            r.dst = t.dst;
+            r.len = t.len - 16;
+        }
+        const uint32_t plen = SEAL ? r.len + 1 : r.len;
+        const uint32_t n1 = iv1 ^ bswap32((uint32_t)(r.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)r.seq);
+        const uint32_t n0 = conn ? iv0 ^ bswap32(conn[i]) : iv0;
+        uint32_t nseg;
+        window_segment(plen, 0, &nseg);
+        u32x4 acc = {0, 0, 0, 0};
+        if (nseg > WIN_MAXSEG) {
+            const Walk wk = make_walk(plen, 5, 4, walk_out16(dst + r.dst));
+            for (uint32_t j = 0; j < 4; ++j)
+                acc ^= lane_walk<NR, 4, SEAL, true, LayoutWin>(lds, 4u * j | 0x10000u, ki->rk, j, r, true, wk.T, n0, n1, n2,
+                                                               src, dst, nullptr, (const uint8_t *)trecs, t.type);
+        } else {
+            for (uint32_t sg = 0; sg < nseg; ++sg) {
+                const Walk sw = window_segment(plen, sg, &nseg);
+                u32x4 part = {0, 0, 0, 0};
+                for (uint32_t j = 0; j < 4; ++j)
+                    part ^= lane_walk<NR, 4, SEAL, true, LayoutWin>(lds, 4u * j | 0x10000u, ki->rk, j, r, true, sw.T, n0, n1,
+                                                                    n2, src, dst, nullptr, (const uint8_t *)trecs, t.type,
+                                                                    &sw);
+                acc = sg == 0 ? part : ghash_mul_lds(lds, LayoutWin::gh64, acc) ^ part;
+            }
+        }
+        if (SEAL) {
+            memcpy(dst + r.dst + plen, &acc, 16);
+            const uint32_t reclen = plen + 16;
+            const uint8_t hdr[5] = {23, 3, 3, (uint8_t)(reclen >> 8), (uint8_t)reclen};
+            memcpy(dst + t.dst, hdr, 5);
+        } else if (acc[0] | acc[1] | acc[2] | acc[3]) {
+            status[i] = 0xffffffffu;
+            types[i] = 0;
+            memset(dst + r.dst, 0, plen);
+        } else {
+            uint32_t m = plen;
+            while (m != 0 && dst[r.dst + m - 1] == 0)
+                --m;
+            status[i] = m ? m - 1 : 0xfffffffeu;
+            types[i] = m ? dst[r.dst + m - 1] : 0;
+        }
+    }
+}
+
+extern "C" int model_tls_window(int is_seal, const uint8_t *key, size_t keylen, const uint8_t *static_iv,
+                                const TlsRecord *trecs, size_t n, const uint8_t *src, uint8_t *dst, uint32_t *status,
+                                uint8_t *types, const uint32_t *conn)
+{
+    KeyImage *ki = (KeyImage *)aligned_alloc(64, sizeof(KeyImage));
+    uint8_t *lds = (uint8_t *)aligned_alloc(256, 160u * 1024u);
+    if (build_key_image(kTabs.sbox, key, (uint32_t)keylen, ki) != 0) {
+        free(ki);
+        free(lds);
+        return -1;
+    }
+    fill_lds_window(lds, kTabs.t0, ki, 0, 1);
+    if (ki->rounds == 10)
+        is_seal ? run_tls_window<10, true>(ki, lds, static_iv, trecs, n, src, dst, status, types, conn)
+                : run_tls_window<10, false>(ki, lds, static_iv, trecs, n, src, dst, status, types, conn);
+    else
+        is_seal ? run_tls_window<14, true>(ki, lds, static_iv, trecs, n, src, dst, status, types, conn)
+                : run_tls_window<14, false>(ki, lds, static_iv, trecs, n, src, dst, status, types, conn);
+    free(ki);
+    free(lds);
+    return 0;
+}
+
 extern "C" int model_tls_batch(int is_seal, const uint8_t *key, size_t keylen, const uint8_t *static_iv,
                                const TlsRecord *trecs, size_t n, const uint8_t *src, uint8_t *dst, uint32_t *status,
                                uint8_t *types, const uint32_t *conn)

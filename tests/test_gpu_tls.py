@@ -17,6 +17,15 @@ pytestmark = pytest.mark.gpu
 GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "tls_records.json")))
 
 
+@pytest.fixture(autouse=True, params=["window", "batch"])
+def framing_kernels(request, engine_lib):
+    """Every framing test runs on both kernel families: the window kernels (64-block segments in parallel, the
+    default for batches up to 16384 records) and the batch kernels (4 lanes per record)."""
+    prev = ra.set_tls_window_records(1 << 30 if request.param == "window" else 0)
+    yield request.param
+    ra.set_tls_window_records(prev)
+
+
 def dev(a):
     import torch
     return torch.from_numpy(np.array(a, copy=True)).cuda()
@@ -275,4 +284,51 @@ def test_multi_connection_windows(gpu, keylen):
     _, st, _ = receive(wrong)
     assert st[20] == 0xFFFFFFFF
     assert (np.delete(st, 20) == np.delete(trecs["len"], 20)).all()
+    eng.close()
+
+
+def test_many_windows_one_launch(gpu, framing_kernels):
+    """1200 framed records of random lengths in one launch each way: above 3 records per CU, so the window path
+    takes its persistent 1024-thread kernels (15 records per pass); every record vs the oracle's record layer."""
+    import torch
+    rng = np.random.default_rng(4242)
+    n = 1200
+    lens = rng.integers(0, 16385, n)
+    lens[:5] = [0, 1, 16383, 16384, 15]
+    trecs = np.zeros(n, ra.TLS_RECORD_DTYPE)
+    conn = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
+    off = woff = 0
+    for i, ln in enumerate(lens):
+        trecs[i] = (off, woff, int(rng.integers(0, 2 ** 40)), int(ln), int(rng.choice([21, 22, 23])))
+        off += int(ln)
+        woff += int(ln) + 22
+    key, iv = bytes(range(7, 23)), bytes(range(60, 72))
+    src = np.frombuffer(xs(77, off + 16), np.uint8)
+    d_src, d_recs, d_conn = dev(src), dev(trecs.view(np.uint8)), dev(conn.view(np.int32))
+    d_wire = torch.zeros(woff + 16, dtype=torch.uint8, device="cuda")
+    eng = ra.Engine(key)
+    eng.tls_seal_records(iv, d_recs.data_ptr(), n, d_src.data_ptr(), d_wire.data_ptr(), conn_ptr=d_conn.data_ptr())
+    torch.cuda.synchronize()
+    wire = d_wire.cpu().numpy()
+    for i in range(n):
+        t = trecs[i]
+        frag = bytes(src[int(t["src"]): int(t["src"]) + int(t["len"])])
+        civ = (int.from_bytes(iv[:4], "big") ^ int(conn[i])).to_bytes(4, "big") + iv[4:]
+        want = oracle.tls_seal_record(key, civ, int(t["seq"]), int(t["type"]), frag)
+        assert bytes(wire[int(t["dst"]): int(t["dst"]) + len(want)]) == want, i
+    orecs = trecs.copy()
+    orecs["src"], orecs["len"] = trecs["dst"], trecs["len"] + 17
+    orecs["dst"] = np.concatenate([[0], np.cumsum(trecs["len"].astype(np.int64) + 1)[:-1]]).astype(np.uint64)
+    d_orecs = dev(orecs.view(np.uint8))
+    d_pt = torch.zeros(int(orecs["dst"][-1]) + int(trecs["len"][-1]) + 17, dtype=torch.uint8, device="cuda")
+    d_st = torch.zeros(n, dtype=torch.int32, device="cuda")
+    d_ty = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    eng.tls_open_records(iv, d_orecs.data_ptr(), n, d_wire.data_ptr(), d_pt.data_ptr(), d_st.data_ptr(), d_ty.data_ptr(),
+                         conn_ptr=d_conn.data_ptr())
+    torch.cuda.synchronize()
+    st, ty, pt = d_st.cpu().numpy().view(np.uint32), d_ty.cpu().numpy(), d_pt.cpu().numpy()
+    assert (st == trecs["len"]).all() and (ty == trecs["type"]).all()
+    for i in range(n):
+        a, b = int(orecs["dst"][i]), int(trecs["src"][i])
+        assert bytes(pt[a: a + int(lens[i])]) == bytes(src[b: b + int(lens[i])]), i
     eng.close()

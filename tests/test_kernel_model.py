@@ -130,20 +130,22 @@ def test_model_record_beyond_2p16_blocks(model, K):
     assert spans(got, recs, 16) == spans(want, recs, 16)
 
 
-def run_tls(lib, is_seal, key, iv, trecs, src, dst, st=None, ty=None, conn=None):
+def run_tls(lib, is_seal, key, iv, trecs, src, dst, st=None, ty=None, conn=None, window=False):
+    """window: the window kernels' math (64-position segments joined with H^64) instead of the batch walk."""
     vp = C.c_void_p
-    lib.model_tls_batch.argtypes = [C.c_int, vp, C.c_size_t, vp, vp, C.c_size_t, vp, vp, vp, vp, vp]
+    fn = lib.model_tls_window if window else lib.model_tls_batch
+    fn.argtypes = [C.c_int, vp, C.c_size_t, vp, vp, C.c_size_t, vp, vp, vp, vp, vp]
     st = np.zeros(max(len(trecs), 1), np.uint32) if st is None else st
     ty = np.zeros(max(len(trecs), 1), np.uint8) if ty is None else ty
-    rc = lib.model_tls_batch(1 if is_seal else 0, key, len(key), iv, trecs.ctypes.data, len(trecs), src.ctypes.data,
-                             dst.ctypes.data, st.ctypes.data, ty.ctypes.data,
-                             None if conn is None else conn.ctypes.data)
+    rc = fn(1 if is_seal else 0, key, len(key), iv, trecs.ctypes.data, len(trecs), src.ctypes.data, dst.ctypes.data,
+            st.ctypes.data, ty.ctypes.data, None if conn is None else conn.ctypes.data)
     assert rc == 0
     return st, ty
 
 
+@pytest.mark.parametrize("window", [False, True])
 @pytest.mark.parametrize("keylen", [16, 32])
-def test_model_tls_framing(model, keylen):
+def test_model_tls_framing(model, keylen, window):
     """The FRAME walk (header AAD in registers, content-type byte spliced into the tail block) vs the oracle's
     restatement of the picotls record layer, both directions, every fragment length around the block edges."""
     import rapido_amd as ra
@@ -158,7 +160,7 @@ def test_model_tls_framing(model, keylen):
         woff += n + 22 + 1
     src = rng.integers(0, 256, off + 16, dtype=np.uint8)
     wire = np.zeros(woff + 16, np.uint8)
-    run_tls(model, True, key, iv, trecs, src, wire)
+    run_tls(model, True, key, iv, trecs, src, wire, window=window)
     for t in trecs:
         frag = bytes(src[int(t["src"]): int(t["src"]) + int(t["len"])])
         want = oracle.tls_seal_record(key, iv, int(t["seq"]), int(t["type"]), frag)
@@ -168,14 +170,15 @@ def test_model_tls_framing(model, keylen):
     orecs["src"], orecs["len"] = trecs["dst"], trecs["len"] + 17
     orecs["dst"] = np.cumsum(np.concatenate([[0], (orecs["len"] - 16)[:-1].astype(np.int64)])).astype(np.uint64)
     pt = np.zeros(int(orecs["dst"][-1]) + int(orecs["len"][-1]), np.uint8)
-    st, ty = run_tls(model, False, key, iv, orecs, wire, pt)
+    st, ty = run_tls(model, False, key, iv, orecs, wire, pt, window=window)
     assert list(st[: len(lens)]) == lens and list(ty[: len(lens)]) == list(trecs["type"])
     for t, o in zip(trecs, orecs):
         assert bytes(pt[int(o["dst"]): int(o["dst"]) + int(t["len"])]) == bytes(src[int(t["src"]): int(t["src"]) +
                                                                                     int(t["len"])])
 
 
-def test_model_tls_open_padding_and_failures(model):
+@pytest.mark.parametrize("window", [False, True])
+def test_model_tls_open_padding_and_failures(model, window):
     import rapido_amd as ra
     key, iv = bytes(range(16)), bytes(range(30, 42))
     cases = [(50, 23, 0), (50, 23, 1), (50, 23, 15), (50, 23, 16), (0, 23, 40), (300, 23, 333), (0, 0, 7)]
@@ -194,7 +197,7 @@ def test_model_tls_open_padding_and_failures(model):
         off += len(w)
         dst += max(L - 16, 0)
     pt = np.zeros(dst + 16, np.uint8)
-    st, ty = run_tls(model, False, key, iv, orecs, buf, pt)
+    st, ty = run_tls(model, False, key, iv, orecs, buf, pt, window=window)
     for i, w in enumerate(wires):
         want = oracle.tls_open_record(key, iv, seqs[i], w)
         if want == oracle.TLS_BAD_MAC:
@@ -261,7 +264,8 @@ def conn_iv(iv: bytes, conn_id: int) -> bytes:
     return head + iv[4:]
 
 
-def test_model_tls_multi_connection_window(model):
+@pytest.mark.parametrize("window", [False, True])
+def test_model_tls_multi_connection_window(model, window):
     """One batch holding the send windows of several connections of a session (same key, per-connection IV and
     seq), sealed and opened in one pass, against the oracle's record layer with each connection's derived IV."""
     import rapido_amd as ra
@@ -278,7 +282,7 @@ def test_model_tls_multi_connection_window(model):
         woff += n + 22
     src = np.frombuffer(bytes((i * 7 + 3) & 0xFF for i in range(off + 16)), np.uint8).copy()
     wire = np.zeros(woff + 16, np.uint8)
-    run_tls(model, True, key, iv, trecs, src, wire, conn=conn)
+    run_tls(model, True, key, iv, trecs, src, wire, conn=conn, window=window)
     for t, c in zip(trecs, conn):
         frag = bytes(src[int(t["src"]): int(t["src"]) + int(t["len"])])
         want = oracle.tls_seal_record(key, conn_iv(iv, int(c)), int(t["seq"]), 23, frag)
@@ -287,11 +291,31 @@ def test_model_tls_multi_connection_window(model):
     orecs["src"], orecs["len"] = trecs["dst"], trecs["len"] + 17
     orecs["dst"] = trecs["src"]
     pt = np.zeros_like(src)
-    st, ty = run_tls(model, False, key, iv, orecs, wire, pt, conn=conn)
+    st, ty = run_tls(model, False, key, iv, orecs, wire, pt, conn=conn, window=window)
     assert (st[: len(trecs)] == trecs["len"]).all() and (ty[: len(trecs)] == 23).all()
     assert bytes(pt[:off]) == bytes(src[:off])
     # a record opened under another connection's IV fails
     wrong = conn.copy()
     wrong[3] ^= 1
-    st, _ = run_tls(model, False, key, iv, orecs, wire, pt, conn=wrong)
+    st, _ = run_tls(model, False, key, iv, orecs, wire, pt, conn=wrong, window=window)
     assert st[3] == 0xFFFFFFFF and (np.delete(st[: len(trecs)], 3) == np.delete(trecs["len"], 3)).all()
+
+
+def test_model_tls_window_oversized_record(model):
+    """A record above the largest TLS record (more than 17 segments) is walked whole by the window kernels' first
+    slot: 20 000- and 70 000-byte fragments plus TLS-sized neighbours, against the oracle."""
+    import rapido_amd as ra
+    key, iv = bytes(range(16)), bytes(range(12))
+    lens = [20000, 16384, 70000, 5]
+    trecs = np.zeros(len(lens), ra.TLS_RECORD_DTYPE)
+    off = woff = 0
+    for i, n in enumerate(lens):
+        trecs[i] = (off, woff, 9 + i, n, 23)
+        off += n
+        woff += n + 22
+    src = np.frombuffer(bytes((i * 13 + 1) & 0xFF for i in range(off + 16)), np.uint8).copy()
+    wire = np.zeros(woff + 16, np.uint8)
+    run_tls(model, True, key, iv, trecs, src, wire, window=True)
+    for t in trecs:
+        want = oracle.tls_seal_record(key, iv, int(t["seq"]), 23, bytes(src[int(t["src"]): int(t["src"]) + int(t["len"])]))
+        assert bytes(wire[int(t["dst"]): int(t["dst"]) + len(want)]) == want
