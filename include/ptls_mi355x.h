@@ -250,6 +250,9 @@ int ptls_mi355x_get_lanes_per_record(void);
  * 64-block GHASH segments walked in parallel (latency of rapido-sized windows); larger batches run on the
  * batch kernels (throughput).  Default 16384; returns the previous value.  Results are identical. */
 size_t ptls_mi355x_set_tls_window_records(size_t n);
+/* the same for the AEAD batch calls (section 3) and the single-record slot calls, which are batches of
+ * one: up to n records run on the window kernels.  Default 768; returns the previous value. */
+size_t ptls_mi355x_set_aead_window_records(size_t n);
 /* name of the kernel symbol the next batch launch with these parameters uses (for profiling) */
 const char *ptls_mi355x_kernel_name(int is_seal, size_t key_size);
 /* last HIP error string seen by the engine ("" if none) */

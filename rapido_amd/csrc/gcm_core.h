@@ -870,32 +870,51 @@ enum : uint32_t {
     WIN_MAXSEG = 17, /* segments of the largest TLS record (16640-byte record: 1 + 1039 + 1 positions) */
 };
 
+/* vector v of the window image: AES image A (T0 | T1 rows) for v < 4096, then the five GHASH tables */
+GCM_HD u32x4 window_image_vec(const uint32_t *t0, const KeyImage *ki, uint32_t v)
+{
+    if (v < 0x10000u / 16u) {
+        const uint32_t off = v * 16u, x = (off >> 8) & 0xffu;
+        const uint32_t w = (off & 128u) ? rotl32(t0[x], 8) : t0[x];
+        return u32x4{w, w, w, w};
+    }
+    const uint32_t i = v - 0x10000u / 16u, slot = i / (GH_TABLE_BYTES / 16u), within = i % (GH_TABLE_BYTES / 16u);
+    const u32x4 *srcv = slot < 4u ? (const u32x4 *)ki->gh[3u - slot] : (const u32x4 *)ki->gh64;
+    return srcv[within];
+}
+
+/*
+ * Fills the window image, split over nthr threads.  Eight vectors per thread are loaded before any is
+ * stored: a fill pass is one memory latency, and with 256 threads the image takes 26 vectors per thread.
+ */
 GCM_HD void fill_lds_window(uint8_t *lds, const uint32_t *t0, const KeyImage *ki, uint32_t tid, uint32_t nthr)
 {
-    for (uint32_t i = tid; i < 0x10000u / 16u; i += nthr) { /* image A: T0 | T1 rows, 32 bank replicas each */
-        const uint32_t off = i * 16u, x = (off >> 8) & 0xffu;
-        const uint32_t v = (off & 128u) ? rotl32(t0[x], 8) : t0[x];
-        *(u32x4 *)(lds + off) = u32x4{v, v, v, v};
-    }
-    for (uint32_t i = tid; i < 5u * GH_TABLE_BYTES / 16u; i += nthr) {
-        const uint32_t slot = i / (GH_TABLE_BYTES / 16u), within = i % (GH_TABLE_BYTES / 16u);
-        const u32x4 *srcv = slot < 4u ? (const u32x4 *)ki->gh[3u - slot] : (const u32x4 *)ki->gh64;
-        *(u32x4 *)(lds + LayoutWin::gh_base + slot * GH_TABLE_BYTES + within * 16u) = srcv[within];
+    constexpr uint32_t total = 0x10000u / 16u + 5u * GH_TABLE_BYTES / 16u;
+    for (uint32_t base = tid; base < total; base += 8u * nthr) {
+        u32x4 v[8];
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k)
+            if (base + k * nthr < total)
+                v[k] = window_image_vec(t0, ki, base + k * nthr);
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k)
+            if (base + k * nthr < total)
+                *(u32x4 *)(lds + 16u * (base + k * nthr)) = v[k];
     }
 }
 
 /*
- * Segment seg of a framed record with GHASH payload plen (AAD = the 5-byte header, one block): the record's
- * g = 1 + ceil(plen/16) + 1 positions are front-padded to nseg * 64; the returned walk covers padded
- * positions [64 seg, 64 seg + 64) (its pad is negative as int32 after the first segment).
+ * Segment seg of a record of A AAD blocks and C payload blocks: its g = A + C + 1 GHASH positions are
+ * front-padded to nseg * 64; the returned walk covers padded positions [64 seg, 64 seg + 64) (its pad is
+ * negative as int32 after the first segment).  Framed records have A = 1 (the 5-byte header).
  */
-GCM_HD Walk window_segment(uint32_t plen, uint32_t seg, uint32_t *nseg)
+GCM_HD Walk window_segment(uint32_t A, uint32_t C, uint32_t seg, uint32_t *nseg)
 {
-    const uint32_t g = 1u + (plen + 15u) / 16u + 1u;
+    const uint32_t g = A + C + 1u;
     *nseg = (g + WIN_SEG - 1u) / WIN_SEG;
     Walk w;
-    w.A = 1u;
-    w.C = (plen + 15u) / 16u;
+    w.A = A;
+    w.C = C;
     w.T = WIN_SEG / 4u;
     w.pad = WIN_SEG * *nseg - g - WIN_SEG * seg;
     return w;
@@ -1013,7 +1032,8 @@ GCM_HD u32x4 shr_bytes(u32x4 v, uint32_t n)
 template <int NR, int K, bool SEAL, bool FRAME = false, class LY = Layout<K>>
 GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk, uint32_t j, const Record &rec, bool valid,
                        uint32_t Tmax, uint32_t iv0, uint32_t iv1, uint32_t iv2, const uint8_t *src, uint8_t *dst,
-                       const uint8_t *aad, const uint8_t *dummy, uint32_t ctype = 0u, const Walk *seg = nullptr)
+                       const uint8_t *aad, const uint8_t *dummy, uint32_t ctype = 0u, const Walk *seg = nullptr,
+                       uint32_t t0 = 0u)
 {
     /*
      * FRAME (TLS 1.3 record framing, lib/picotls.c:621-684 and :4779-4791): the AAD is the 5-byte
@@ -1154,6 +1174,8 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
                 const uint32_t reclen = plen + 16u;
                 X[0] = 0x00030317u | ((reclen >> 8) & 0xffu) << 24;
                 X[1] = reclen & 0xffu;
+            } else if (seg != nullptr && rec.aadlen < 16u) {
+                X = load_partial(ad, rec.aadlen); /* segment walks: the short AAD may sit in any step */
             } else {
                 X = 16u * (uint32_t)p + 16u <= rec.aadlen || rec.aadlen < 16u ? cur : shr_bytes(cur, 16u - arem);
             }
@@ -1178,12 +1200,16 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
      * An AAD shorter than 16 bytes (TLS: the 5-byte record header) is position 0, which lies in
      * step 0 (front padding < K): its lane reads it byte-exact into the first buffer.
      */
+    /*
+     * t0 (even, segment walks): the first step with a real position in any lane of the wave.  Steps before
+     * it hold only front padding, and a Horner chain stays 0 through leading zero blocks.
+     */
     u32x4 bufA;
-    if (!FRAME && valid && rec.aadlen != 0u && rec.aadlen < 16u && j == wk.pad)
+    if (!FRAME && seg == nullptr && valid && rec.aadlen != 0u && rec.aadlen < 16u && j == wk.pad)
         bufA = load_partial(ad, rec.aadlen);
     else
-        bufA = *(const u32x4_u *)fetch_ptr(0);
-    for (uint32_t t = 0; t < Tmax; t += 2u) {
+        bufA = *(const u32x4_u *)fetch_ptr(t0);
+    for (uint32_t t = t0; t < Tmax; t += 2u) {
         const u32x4 bufB = *(const u32x4_u *)fetch_ptr(t + 1u);
         step(t, bufA);
         bufA = *(const u32x4_u *)fetch_ptr(t + 2u);

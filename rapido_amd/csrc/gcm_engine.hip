@@ -238,14 +238,16 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
  * H^4..H^1 (lane scaling) and of H^64.  A record of more than WIN_MAXSEG segments (larger than a TLS
  * record) is walked whole by its first slot instead.  Results are bit-identical to the batch kernels.
  */
-template <int NR, bool SEAL, int THREADS>
-__device__ __forceinline__ void tls_window_body(const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2,
-                                                const TlsRecord *__restrict__ trecs, uint32_t nrecs, const uint8_t *src,
-                                                uint8_t *dst, uint32_t *__restrict__ status, uint8_t *__restrict__ types,
-                                                const uint32_t *__restrict__ conn)
+template <int NR, bool SEAL, bool FRAME, int THREADS>
+__device__ __forceinline__ void window_body(const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2,
+                                            const void *__restrict__ descs, uint32_t nrecs, const uint8_t *src, uint8_t *dst,
+                                            const uint8_t *__restrict__ aad, uint32_t *__restrict__ status,
+                                            uint8_t *__restrict__ types, const uint32_t *__restrict__ conn)
 {
     constexpr uint32_t SLOTS = THREADS / 4, RECS = SLOTS / WIN_MAXSEG; /* records per workgroup pass */
     __shared__ __attribute__((aligned(16))) uint8_t lds[LayoutWin::parts + RECS * WIN_MAXSEG * 16u];
+    const Record *__restrict__ recs = (const Record *)descs;
+    const TlsRecord *__restrict__ trecs = (const TlsRecord *)descs;
     fill_lds_window(lds, c_tabs.t0, ki, threadIdx.x, blockDim.x);
     uint32_t rk[4 * (NR + 1)];
 #pragma unroll
@@ -261,37 +263,48 @@ __device__ __forceinline__ void tls_window_body(const KeyImage *__restrict__ ki,
     for (uint32_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
         const uint32_t r = grp * RECS + rl;
         const bool in_batch = rl < RECS && r < nrecs;
-        Record rec = {0, 0, 0, 0, 0, 5};
+        Record rec = {0, 0, 0, 0, 0, FRAME ? 5u : 0u};
         uint32_t ctype = 0u;
         bool valid = in_batch;
-        if (in_batch) {
-            const TlsRecord t = trecs[r];
-            rec.seq = t.seq;
-            if (SEAL) {
-                rec.src = t.src;
-                rec.dst = t.dst + 5u;
-                rec.len = t.len;
-                ctype = t.type;
-            } else {
-                rec.src = t.src + 5u;
-                rec.dst = t.dst;
-                rec.len = t.len >= 16u ? t.len - 16u : 0u;
-                valid = t.len >= 16u;
+        if (FRAME) {
+            if (in_batch) {
+                const TlsRecord t = trecs[r];
+                rec.seq = t.seq;
+                if (SEAL) {
+                    rec.src = t.src;
+                    rec.dst = t.dst + 5u;
+                    rec.len = t.len;
+                    ctype = t.type;
+                } else {
+                    rec.src = t.src + 5u;
+                    rec.dst = t.dst;
+                    rec.len = t.len >= 16u ? t.len - 16u : 0u;
+                    valid = t.len >= 16u;
+                }
             }
+        } else if (in_batch) {
+            rec = recs[r];
         }
-        const uint32_t plen = SEAL ? rec.len + 1u : rec.len;
+        const uint32_t plen = FRAME && SEAL ? rec.len + 1u : rec.len;
+        const uint32_t A = FRAME ? 1u : (rec.aadlen + 15u) / 16u;
         uint32_t nseg;
-        const Walk sw = window_segment(plen, seg, &nseg);
-        const bool whole = nseg > WIN_MAXSEG; /* not a TLS-sized record: its first slot walks it all */
+        const Walk sw = window_segment(A, (plen + 15u) / 16u, seg, &nseg);
+        const bool whole = nseg > WIN_MAXSEG; /* larger than a TLS record: its first slot walks it all */
         const bool active = valid && (whole ? seg == 0u : seg < nseg);
-        uint32_t Tw = active ? (whole ? make_walk(plen, 5u, 4u, walk_out16(dst + rec.dst)).T : sw.T) : 0u;
+        uint32_t Tw = active ? (whole ? make_walk(plen, rec.aadlen, 4u, walk_out16(dst + rec.dst)).T : sw.T) : 0u;
+        /* first step holding a real position (segments that are mostly front padding start late) */
+        uint32_t tf = active && !whole && (int32_t)sw.pad > 0 ? (uint32_t)(int32_t)sw.pad / 4u : (active ? 0u : ~0u);
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1)
+        for (int o = 32; o >= 1; o >>= 1) {
             Tw = max(Tw, shfl_xor_u32(Tw, o));
+            tf = min(tf, shfl_xor_u32(tf, o));
+        }
+        const uint32_t t0 = tf == ~0u ? 0u : tf & ~1u;
         const uint32_t n1 = iv1 ^ bswap32((uint32_t)(rec.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)rec.seq);
         const uint32_t n0 = conn != nullptr && in_batch ? iv0 ^ bswap32(conn[r]) : iv0;
-        u32x4 part = lane_walk<NR, 4, SEAL, true, LayoutWin>(lds, lanesel, rk, j, rec, active, Tw, n0, n1, n2, src, dst,
-                                                             nullptr, (const uint8_t *)trecs, ctype, whole ? nullptr : &sw);
+        u32x4 part = lane_walk<NR, 4, SEAL, FRAME, LayoutWin>(lds, lanesel, rk, j, rec, active, Tw, n0, n1, n2, src, dst,
+                                                              aad, (const uint8_t *)descs, ctype, whole ? nullptr : &sw,
+                                                              t0);
         part ^= shfl_xor_u32x4(part, 1);
         part ^= shfl_xor_u32x4(part, 2);
         if (active && j == 0u)
@@ -310,9 +323,11 @@ __device__ __forceinline__ void tls_window_body(const KeyImage *__restrict__ ki,
             if (SEAL) {
                 if (j == 0u) {
                     *(u32x4_u *)(dst + rec.dst + plen) = acc;
-                    const uint32_t reclen = plen + 16u; /* 17 03 03 BE16(plen + 16) (lib/picotls.c:658-662) */
-                    store_partial(dst + rec.dst - 5u, 5u,
-                                  u32x4{0x00030317u | ((reclen >> 8) & 0xffu) << 24, reclen & 0xffu, 0u, 0u});
+                    if (FRAME) { /* 17 03 03 BE16(plen + 16) (lib/picotls.c:658-662) */
+                        const uint32_t reclen = plen + 16u;
+                        store_partial(dst + rec.dst - 5u, 5u,
+                                      u32x4{0x00030317u | ((reclen >> 8) & 0xffu) << 24, reclen & 0xffu, 0u, 0u});
+                    }
                 }
             } else if (!valid || (acc[0] | acc[1] | acc[2] | acc[3]) != 0u) {
                 /* no unverified plaintext is released (fusion leaves it, lib/fusion.c:656-679) */
@@ -325,9 +340,13 @@ __device__ __forceinline__ void tls_window_body(const KeyImage *__restrict__ ki,
                         store_partial(out + off, n, u32x4{0u, 0u, 0u, 0u});
                 }
                 if (j == 0u) {
-                    status[r] = 0xffffffffu; /* PTLS_ALERT_BAD_RECORD_MAC */
-                    types[r] = 0u;
+                    status[r] = 0xffffffffu; /* SIZE_MAX / PTLS_ALERT_BAD_RECORD_MAC */
+                    if (FRAME)
+                        types[r] = 0u;
                 }
+            } else if (!FRAME) {
+                if (j == 0u)
+                    status[r] = rec.len;
             } else if (j == 0u) {
                 /* padding strip + content-type pop (lib/picotls.c:4784-4791) over plaintext the other slots wrote */
                 __threadfence();
@@ -391,24 +410,32 @@ MI355X_GCM_KERNEL_F(mi355x_tls_seal_aes256_k4, 14, 4, true, true)
 MI355X_GCM_KERNEL_F(mi355x_tls_open_aes128_k4, 10, 4, false, true)
 MI355X_GCM_KERNEL_F(mi355x_tls_open_aes256_k4, 14, 4, false, true)
 
-#define MI355X_TLS_WIN_KERNEL(NAME, NR, SEAL, THREADS)                                                                 \
+#define MI355X_WIN_KERNEL(NAME, NR, SEAL, FRAME, THREADS)                                                              \
     extern "C" __global__ __launch_bounds__(THREADS) void NAME(                                                        \
-        const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2, const TlsRecord *__restrict__ trecs, \
-        uint32_t nrecs, const uint8_t *src, uint8_t *dst, uint32_t *__restrict__ st, uint8_t *__restrict__ types,       \
-        const uint32_t *__restrict__ conn)                                                                             \
+        const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2, const void *__restrict__ descs,     \
+        uint32_t nrecs, const uint8_t *src, uint8_t *dst, const uint8_t *__restrict__ aad, uint32_t *__restrict__ st,   \
+        uint8_t *__restrict__ types, const uint32_t *__restrict__ conn)                                                \
     {                                                                                                                  \
-        tls_window_body<NR, SEAL, THREADS>(ki, iv0, iv1, iv2, trecs, nrecs, src, dst, st, types, conn);                \
+        window_body<NR, SEAL, FRAME, THREADS>(ki, iv0, iv1, iv2, descs, nrecs, src, dst, aad, st, types, conn);        \
     }
-/* 256 threads (3 records per pass): one window spread over many CUs; 1024 threads (15 records per pass,
- * persistent): batches of hundreds of windows */
-MI355X_TLS_WIN_KERNEL(mi355x_tls_win_seal_aes128, 10, true, 256)
-MI355X_TLS_WIN_KERNEL(mi355x_tls_win_seal_aes256, 14, true, 256)
-MI355X_TLS_WIN_KERNEL(mi355x_tls_win_open_aes128, 10, false, 256)
-MI355X_TLS_WIN_KERNEL(mi355x_tls_win_open_aes256, 14, false, 256)
-MI355X_TLS_WIN_KERNEL(mi355x_tls_winw_seal_aes128, 10, true, 1024)
-MI355X_TLS_WIN_KERNEL(mi355x_tls_winw_seal_aes256, 14, true, 1024)
-MI355X_TLS_WIN_KERNEL(mi355x_tls_winw_open_aes128, 10, false, 1024)
-MI355X_TLS_WIN_KERNEL(mi355x_tls_winw_open_aes256, 14, false, 1024)
+/* 256 threads (3 records per pass): a few records spread over many CUs; 1024 threads (15 records per pass,
+ * persistent): hundreds of records */
+MI355X_WIN_KERNEL(mi355x_tls_win_seal_aes128, 10, true, true, 256)
+MI355X_WIN_KERNEL(mi355x_tls_win_seal_aes256, 14, true, true, 256)
+MI355X_WIN_KERNEL(mi355x_tls_win_open_aes128, 10, false, true, 256)
+MI355X_WIN_KERNEL(mi355x_tls_win_open_aes256, 14, false, true, 256)
+MI355X_WIN_KERNEL(mi355x_tls_winw_seal_aes128, 10, true, true, 1024)
+MI355X_WIN_KERNEL(mi355x_tls_winw_seal_aes256, 14, true, true, 1024)
+MI355X_WIN_KERNEL(mi355x_tls_winw_open_aes128, 10, false, true, 1024)
+MI355X_WIN_KERNEL(mi355x_tls_winw_open_aes256, 14, false, true, 1024)
+MI355X_WIN_KERNEL(mi355x_gcm_win_seal_aes128, 10, true, false, 256)
+MI355X_WIN_KERNEL(mi355x_gcm_win_seal_aes256, 14, true, false, 256)
+MI355X_WIN_KERNEL(mi355x_gcm_win_open_aes128, 10, false, false, 256)
+MI355X_WIN_KERNEL(mi355x_gcm_win_open_aes256, 14, false, false, 256)
+MI355X_WIN_KERNEL(mi355x_gcm_winw_seal_aes128, 10, true, false, 1024)
+MI355X_WIN_KERNEL(mi355x_gcm_winw_seal_aes256, 14, true, false, 1024)
+MI355X_WIN_KERNEL(mi355x_gcm_winw_open_aes128, 10, false, false, 1024)
+MI355X_WIN_KERNEL(mi355x_gcm_winw_open_aes256, 14, false, false, 1024)
 
 /* key image: round keys, H and the nibble tables of H^1..H^8 and H^64 (cold path, one thread) */
 extern "C" __global__ void mi355x_gcm_setup(const uint8_t *key, uint32_t keylen, KeyImage *ki, int *rc)
@@ -452,6 +479,11 @@ static thread_local char g_err[256];
 static int g_lanes = 4;
 /* framing batches of at most this many records go to the window kernels (ptls_mi355x_set_tls_window_records) */
 static size_t g_window_records = 16384;
+/* AEAD batches (section 3) of at most this many records go to the window kernels (ptls_mi355x_set_aead_window_records):
+ * the single-record slot calls and small batches, where 4 lanes per record would leave the GPU idle */
+static size_t g_aead_window_records = 768;
+/* single-record slot calls below this many bytes (payload + AAD) take the batch walk */
+constexpr size_t SLOT_WINDOW_MIN_BYTES = 2048;
 
 static int fail(const char *what, hipError_t e)
 {
@@ -530,7 +562,7 @@ static inline uint32_t le32(const uint8_t *p) { return (uint32_t)p[0] | (uint32_
 static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void *static_iv12, const void *recs,
                         const uint32_t *order, size_t n, const uint8_t *src, uint8_t *dst, const uint8_t *aad,
                         uint32_t *status, hipStream_t stream, bool frame = false, uint8_t *types = nullptr,
-                        const uint32_t *conn = nullptr)
+                        const uint32_t *conn = nullptr, bool no_window = false)
 {
     if (n == 0)
         return 0;
@@ -538,22 +570,24 @@ static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void
         snprintf(g_err, sizeof(g_err), "batch of %zu records exceeds 2^32-1", n);
         return -1;
     }
-    if (frame && n <= g_window_records) {
+    if (!no_window && n <= (frame ? g_window_records : g_aead_window_records)) {
         /*
-         * small framing batch: the window kernels (segments of 64 GHASH positions in parallel).  Up to 3 records
-         * per CU: 256-thread groups of 3 records, so a window spreads over many CUs; above that, persistent
+         * small batch: the window kernels (segments of 64 GHASH positions in parallel).  Up to 3 records per CU:
+         * 256-thread groups of 3 records, so a few records spread over many CUs; above that, persistent
          * 1024-thread groups of 15 records, one per CU.
          */
-        typedef void (*win_kernel_t)(const KeyImage *, uint32_t, uint32_t, uint32_t, const TlsRecord *, uint32_t,
-                                     const uint8_t *, uint8_t *, uint32_t *, uint8_t *, const uint32_t *);
-        const bool k256 = ctx->key_size == 32, wide = n > 3u * (uint64_t)ctx->num_cu;
-        win_kernel_t wk;
-        if (wide)
-            wk = seal ? (k256 ? mi355x_tls_winw_seal_aes256 : mi355x_tls_winw_seal_aes128)
-                      : (k256 ? mi355x_tls_winw_open_aes256 : mi355x_tls_winw_open_aes128);
-        else
-            wk = seal ? (k256 ? mi355x_tls_win_seal_aes256 : mi355x_tls_win_seal_aes128)
-                      : (k256 ? mi355x_tls_win_open_aes256 : mi355x_tls_win_open_aes128);
+        typedef void (*win_kernel_t)(const KeyImage *, uint32_t, uint32_t, uint32_t, const void *, uint32_t,
+                                     const uint8_t *, uint8_t *, const uint8_t *, uint32_t *, uint8_t *, const uint32_t *);
+        static const win_kernel_t table[2][2][2][2] = {
+            /* [frame][wide][seal][aes256] */
+            {{{mi355x_gcm_win_open_aes128, mi355x_gcm_win_open_aes256}, {mi355x_gcm_win_seal_aes128, mi355x_gcm_win_seal_aes256}},
+             {{mi355x_gcm_winw_open_aes128, mi355x_gcm_winw_open_aes256},
+              {mi355x_gcm_winw_seal_aes128, mi355x_gcm_winw_seal_aes256}}},
+            {{{mi355x_tls_win_open_aes128, mi355x_tls_win_open_aes256}, {mi355x_tls_win_seal_aes128, mi355x_tls_win_seal_aes256}},
+             {{mi355x_tls_winw_open_aes128, mi355x_tls_winw_open_aes256},
+              {mi355x_tls_winw_seal_aes128, mi355x_tls_winw_seal_aes256}}}};
+        const bool wide = n > 3u * (uint64_t)ctx->num_cu;
+        const win_kernel_t wk = table[frame][wide][seal][ctx->key_size == 32];
         const uint32_t threads = wide ? 1024u : 256u, per = (threads / 4u) / WIN_MAXSEG;
         uint64_t blocks = (n + per - 1) / per;
         if (wide && blocks > (uint64_t)ctx->num_cu)
@@ -561,7 +595,7 @@ static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void
         const uint8_t *wiv = (const uint8_t *)static_iv12;
         DeviceGuard guard(ctx->device);
         hipLaunchKernelGGL(wk, dim3((unsigned)blocks), dim3(threads), 0, stream, ctx->d_ki, le32(wiv), le32(wiv + 4),
-                           le32(wiv + 8), (const TlsRecord *)recs, (uint32_t)n, src, dst, status, types, conn);
+                           le32(wiv + 8), recs, (uint32_t)n, src, dst, aad, status, types, conn);
         HIPCHK(hipGetLastError());
         return 0;
     }
@@ -639,6 +673,13 @@ size_t ptls_mi355x_set_tls_window_records(size_t n)
 {
     const size_t prev = g_window_records;
     g_window_records = n;
+    return prev;
+}
+
+size_t ptls_mi355x_set_aead_window_records(size_t n)
+{
+    const size_t prev = g_aead_window_records;
+    g_aead_window_records = n;
     return prev;
 }
 
@@ -852,8 +893,11 @@ static int single_record(ptls_mi355x_aesgcm_context_t *ctx, bool seal, void *out
     if (!seal)
         memcpy(ctx->h_stage + off_data + inlen, tag, 16);
     HIPCHK(hipMemcpyAsync(ctx->d_stage, ctx->h_stage, off_status, hipMemcpyHostToDevice, ctx->stream));
+    /* one record: the window kernels pay off from about 2 KiB (segments in parallel), below that the batch walk
+     * is shorter than the window kernels' LDS fill (scripts/slot_latency.py, profiles/r01c_slot_latency.json) */
     if (launch_batch(ctx, seal, nonce12, (const Record *)ctx->d_stage, nullptr, 1, ctx->d_stage, ctx->d_stage, ctx->d_stage,
-                     (uint32_t *)(ctx->d_stage + off_status), ctx->stream) != 0)
+                     (uint32_t *)(ctx->d_stage + off_status), ctx->stream, false, nullptr, nullptr,
+                     inlen + aadlen < SLOT_WINDOW_MIN_BYTES) != 0)
         return -1;
     const size_t outlen = seal ? inlen + 16 : inlen;
     HIPCHK(hipMemcpyAsync(ctx->h_stage + off_data, ctx->d_stage + off_data, outlen, hipMemcpyDeviceToHost, ctx->stream));

@@ -96,9 +96,10 @@ def main():
     d_wire2 = torch.zeros(RW * (FRAG + 22), dtype=torch.uint8, device=dev)
     eng.tls_seal_records(iv, d_t2.data_ptr(), RW, d_src2.data_ptr(), d_wire2.data_ptr(), sh)
     o = t2.copy()
-    o["src"], o["len"], o["dst"] = t2["dst"], FRAG + 17, t2["src"]
+    # plaintext slots hold fragment + content type (FRAG + 1 bytes): 16-byte aligned, FRAG + 16 apart
+    o["src"], o["len"], o["dst"] = t2["dst"], FRAG + 17, np.arange(RW, dtype=np.uint64) * (FRAG + 16)
     d_o = torch.from_numpy(o.view(np.uint8)).to(dev)
-    d_pt = torch.zeros(RW * FRAG + 16, dtype=torch.uint8, device=dev)
+    d_pt = torch.zeros(RW * (FRAG + 16), dtype=torch.uint8, device=dev)
     d_st = torch.zeros(RW, dtype=torch.int32, device=dev)
     d_ty = torch.zeros(RW, dtype=torch.uint8, device=dev)
 

@@ -135,7 +135,7 @@ static void run_tls_window(const KeyImage *ki, const uint8_t *lds, const uint8_t
         const uint32_t n1 = iv1 ^ bswap32((uint32_t)(r.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)r.seq);
         const uint32_t n0 = conn ? iv0 ^ bswap32(conn[i]) : iv0;
         uint32_t nseg;
-        window_segment(plen, 0, &nseg);
+        window_segment(1, (plen + 15) / 16, 0, &nseg);
         u32x4 acc = {0, 0, 0, 0};
         if (nseg > WIN_MAXSEG) {
             const Walk wk = make_walk(plen, 5, 4, walk_out16(dst + r.dst));
@@ -144,7 +144,7 @@ static void run_tls_window(const KeyImage *ki, const uint8_t *lds, const uint8_t
                                                                src, dst, nullptr, (const uint8_t *)trecs, t.type);
         } else {
             for (uint32_t sg = 0; sg < nseg; ++sg) {
-                const Walk sw = window_segment(plen, sg, &nseg);
+                const Walk sw = window_segment(1, (plen + 15) / 16, sg, &nseg);
                 u32x4 part = {0, 0, 0, 0};
                 for (uint32_t j = 0; j < 4; ++j)
                     part ^= lane_walk<NR, 4, SEAL, true, LayoutWin>(lds, 4u * j | 0x10000u, ki->rk, j, r, true, sw.T, n0, n1,
@@ -170,6 +170,67 @@ static void run_tls_window(const KeyImage *ki, const uint8_t *lds, const uint8_t
             types[i] = m ? dst[r.dst + m - 1] : 0;
         }
     }
+}
+
+/* the window kernels' math for AEAD records (any AAD length): segments joined with H^64 */
+template <int NR, bool SEAL>
+static void run_window(const KeyImage *ki, const uint8_t *lds, const uint8_t *static_iv, const Record *recs, size_t n,
+                       const uint8_t *src, uint8_t *dst, const uint8_t *aad, uint32_t *status)
+{
+    uint32_t iv0, iv1, iv2;
+    memcpy(&iv0, static_iv, 4);
+    memcpy(&iv1, static_iv + 4, 4);
+    memcpy(&iv2, static_iv + 8, 4);
+    for (size_t i = 0; i < n; ++i) {
+        const Record &r = recs[i];
+        const uint32_t n1 = iv1 ^ bswap32((uint32_t)(r.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)r.seq);
+        const uint32_t A = (r.aadlen + 15) / 16, C = (r.len + 15) / 16;
+        uint32_t nseg;
+        window_segment(A, C, 0, &nseg);
+        u32x4 acc = {0, 0, 0, 0};
+        if (nseg > WIN_MAXSEG) {
+            const Walk wk = make_walk(r.len, r.aadlen, 4, walk_out16(dst + r.dst));
+            for (uint32_t j = 0; j < 4; ++j)
+                acc ^= lane_walk<NR, 4, SEAL, false, LayoutWin>(lds, 4u * j | 0x10000u, ki->rk, j, r, true, wk.T, iv0, n1, n2,
+                                                                src, dst, aad, (const uint8_t *)recs);
+        } else {
+            for (uint32_t sg = 0; sg < nseg; ++sg) {
+                const Walk sw = window_segment(A, C, sg, &nseg);
+                u32x4 part = {0, 0, 0, 0};
+                for (uint32_t j = 0; j < 4; ++j)
+                    part ^= lane_walk<NR, 4, SEAL, false, LayoutWin>(lds, 4u * j | 0x10000u, ki->rk, j, r, true, sw.T, iv0,
+                                                                     n1, n2, src, dst, aad, (const uint8_t *)recs, 0u, &sw);
+                acc = sg == 0 ? part : ghash_mul_lds(lds, LayoutWin::gh64, acc) ^ part;
+            }
+        }
+        if (SEAL)
+            memcpy(dst + r.dst + r.len, &acc, 16);
+        else
+            status[i] = (acc[0] | acc[1] | acc[2] | acc[3]) ? 0xffffffffu : r.len;
+    }
+}
+
+extern "C" int model_batch_window(int is_seal, const uint8_t *key, size_t keylen, const uint8_t *static_iv,
+                                  const Record *recs, size_t n, const uint8_t *src, uint8_t *dst, const uint8_t *aad,
+                                  uint32_t *status)
+{
+    KeyImage *ki = (KeyImage *)aligned_alloc(64, sizeof(KeyImage));
+    uint8_t *lds = (uint8_t *)aligned_alloc(256, 160u * 1024u);
+    if (build_key_image(kTabs.sbox, key, (uint32_t)keylen, ki) != 0) {
+        free(ki);
+        free(lds);
+        return -1;
+    }
+    fill_lds_window(lds, kTabs.t0, ki, 0, 1);
+    if (ki->rounds == 10)
+        is_seal ? run_window<10, true>(ki, lds, static_iv, recs, n, src, dst, aad, status)
+                : run_window<10, false>(ki, lds, static_iv, recs, n, src, dst, aad, status);
+    else
+        is_seal ? run_window<14, true>(ki, lds, static_iv, recs, n, src, dst, aad, status)
+                : run_window<14, false>(ki, lds, static_iv, recs, n, src, dst, aad, status);
+    free(ki);
+    free(lds);
+    return 0;
 }
 
 extern "C" int model_tls_window(int is_seal, const uint8_t *key, size_t keylen, const uint8_t *static_iv,

@@ -12,6 +12,15 @@ from rapido_amd import records
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["window", "batch"])
+def aead_kernels(request, engine_lib):
+    """Every test here runs on both kernel families: the window kernels (64-block segments in parallel; the
+    default for the slot calls and batches up to 768 records) and the batch kernels (K lanes per record)."""
+    prev = ra.set_aead_window_records(1 << 30 if request.param == "window" else 0)
+    yield request.param
+    ra.set_aead_window_records(prev)
+
+
 def to_dev(a: np.ndarray):
     import torch
     return torch.from_numpy(np.ascontiguousarray(a)).cuda()

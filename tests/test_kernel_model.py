@@ -24,8 +24,15 @@ def model():
 
 
 def run(lib, is_seal, K, key, iv, recs, src, dst, aad, st):
-    rc = lib.model_batch(1 if is_seal else 0, K, key, len(key), iv, recs.ctypes.data, len(recs), src.ctypes.data,
-                         dst.ctypes.data, aad.ctypes.data, st.ctypes.data)
+    """K = 0: the window kernels' math (64-position segments joined with H^64); else the K-lane batch walk."""
+    if K == 0:
+        lib.model_batch_window.argtypes = [C.c_int, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_size_t,
+                                           C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        rc = lib.model_batch_window(1 if is_seal else 0, key, len(key), iv, recs.ctypes.data, len(recs),
+                                    src.ctypes.data, dst.ctypes.data, aad.ctypes.data, st.ctypes.data)
+    else:
+        rc = lib.model_batch(1 if is_seal else 0, K, key, len(key), iv, recs.ctypes.data, len(recs), src.ctypes.data,
+                             dst.ctypes.data, aad.ctypes.data, st.ctypes.data)
     assert rc == 0
 
 
@@ -48,7 +55,7 @@ def spans(buf, recs, extra):
     return [bytes(buf[int(r["dst"]): int(r["dst"]) + int(r["len"]) + extra]) for r in recs]
 
 
-@pytest.mark.parametrize("K", [1, 2, 4, 8])
+@pytest.mark.parametrize("K", [1, 2, 4, 8, 0])
 @pytest.mark.parametrize("keylen", [16, 32])
 def test_model_matches_oracle(model, K, keylen):
     rng = np.random.default_rng(K * 100 + keylen)
@@ -319,3 +326,26 @@ def test_model_tls_window_oversized_record(model):
     for t in trecs:
         want = oracle.tls_seal_record(key, iv, int(t["seq"]), 23, bytes(src[int(t["src"]): int(t["src"]) + int(t["len"])]))
         assert bytes(wire[int(t["dst"]): int(t["dst"]) + len(want)]) == want
+
+
+def test_model_window_aead_edges(model):
+    """The window math for AEAD records: AAD of every length 0..40 in front of payloads around segment edges
+    (so the short AAD sits in later steps of the first segment), records above 17 segments, vs the oracle."""
+    rng = np.random.default_rng(31)
+    pairs = [(a, l) for a in range(0, 41, 3) for l in (0, 1, 15, 16, 17, 1000, 1007, 1008, 1009, 16384)]
+    pairs += [(5, 17 * 1024), (300, 16000), (13, 40000)]
+    lens = np.array([p[1] for p in pairs], np.uint64)
+    aadlens = np.array([p[0] for p in pairs], np.uint64)
+    recs, src_bytes, aad_bytes = records.layout(lens, aadlens, align=16)
+    recs["seq"] = rng.integers(0, 2 ** 63, len(recs), dtype=np.uint64)
+    src = rng.integers(0, 256, src_bytes, dtype=np.uint8)
+    aad = rng.integers(0, 256, aad_bytes, dtype=np.uint8)
+    key, iv = bytes(range(16)), bytes(range(12))
+    got, want = np.zeros_like(src), np.zeros_like(src)
+    st = np.zeros(len(recs), np.uint32)
+    run(model, True, 0, key, iv, recs, src, got, aad, st)
+    oracle.batch(True, key, iv, recs, src, want, aad)
+    assert spans(got, recs, 16) == spans(want, recs, 16)
+    pt = np.zeros_like(src)
+    run(model, False, 0, key, iv, recs, got, pt, aad, st)
+    assert (st == recs["len"]).all()
