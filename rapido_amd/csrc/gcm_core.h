@@ -669,6 +669,15 @@ struct Record {
  * 64-byte segments and measured 1.5-1.6x the algorithmic write traffic and 6-15% lower
  * throughput (scripts/pmc_lengths.py).  Alignment can cost one step; short records
  * (T < GCM_ALIGN_MIN_T) only take it when it is free.
+ *
+ * AAD hoisting (A <= K, e.g. every TLS record): the AAD blocks sit right before payload block 0, so
+ * aligning the payload used to push them into an extra step (1400-B records: 24 steps instead of 23,
+ * so alignment was skipped and the stores straddled).  Horner allows a block at lane j's position
+ * BEFORE step 0 (grid position j - K): it is simply the lane's starting accumulator, and step 0's
+ * fused multiply -- otherwise a multiply of 0 -- raises it by H^K.  So the AAD blocks may sit at
+ * negative grid positions (pad = q0 - A < 0, two's complement in the uint32) and lane_walk seeds the
+ * lanes that hold them; payload block 0 goes to its aligned grid position q0 = out16 mod K at the
+ * minimal step count ceil((q0 + C + 1) / K).
  */
 #ifndef GCM_ALIGN_MIN_T
 #define GCM_ALIGN_MIN_T 32u
@@ -676,8 +685,11 @@ struct Record {
 #ifndef GCM_ALIGN_OUTPUT
 #define GCM_ALIGN_OUTPUT 1
 #endif
+#ifndef GCM_HOIST_AAD
+#define GCM_HOIST_AAD 1
+#endif
 struct Walk {
-    uint32_t A, C, T, pad;
+    uint32_t A, C, T, pad; /* pad: int32 in two's complement (negative: hoisted AAD, or a later window segment) */
 };
 
 GCM_HD Walk make_walk(uint32_t len, uint32_t aadlen, uint32_t K, uint32_t out16 = 0xffffffffu)
@@ -685,33 +697,38 @@ GCM_HD Walk make_walk(uint32_t len, uint32_t aadlen, uint32_t K, uint32_t out16 
     Walk w;
     w.A = (aadlen + 15u) >> 4;
     w.C = (len + 15u) >> 4;
-    const uint32_t g = w.A + w.C + 1u;
-    w.pad = (K - g % K) % K; /* minimal */
-    w.T = (g + w.pad) / K;
+    /* q0: grid position of payload block 0 (pad = q0 - A); the AAD blocks precede it */
+    const uint32_t q0_min = GCM_HOIST_AAD && w.A <= K ? 0u : w.A;
+    const uint32_t n = q0_min + w.C + 1u;
+    uint32_t q0 = q0_min + (K - n % K) % K; /* minimal step count, the grid ending on a step boundary */
+    w.T = (q0 + w.C + 1u) / K;
     if (GCM_ALIGN_OUTPUT && out16 != 0xffffffffu) {
-        const uint32_t pa = (out16 - w.A) & (K - 1u); /* (A + pad) = out16 (mod K) */
-        const uint32_t Ta = (g + pa + K - 1u) / K;
+        const uint32_t qa = q0_min + ((out16 - q0_min) & (K - 1u)); /* q0 = out16 (mod K) */
+        const uint32_t Ta = (qa + w.C + 1u + K - 1u) / K;
         if (Ta == w.T || w.T >= GCM_ALIGN_MIN_T) {
-            w.pad = pa;
+            q0 = qa;
             w.T = Ta;
         }
     }
+    w.pad = q0 - w.A;
     return w;
 }
 
 /*
  * table slot (H^(K - slot)) that scales lane j's chain: exponent pad + g - q_last(j).  end_cap bounds the
- * chain to the first end_cap padded positions (a segment of the window kernels, see lane_walk).
+ * chain to the first end_cap padded positions (a segment of the window kernels, see lane_walk).  Lane j
+ * holds grid positions j + K m for m >= -1 (m = -1: a hoisted AAD block, make_walk).
  */
 GCM_HD uint32_t walk_scale_slot(const Walk &w, uint32_t j, uint32_t K, uint32_t end_cap = 0xffffffffu)
 {
-    uint32_t end = w.pad + w.A + w.C + 1u; /* one past the last real position */
-    if (end > end_cap)
-        end = end_cap;
-    if (end <= j)
+    int32_t end = (int32_t)(w.pad + w.A + w.C + 1u); /* one past the last real position (> 0) */
+    if (end_cap != 0xffffffffu && end > (int32_t)end_cap)
+        end = (int32_t)end_cap;
+    const int32_t e = end - 1 - (int32_t)j;
+    if (e < -(int32_t)K)
         return 0u; /* no real position: the chain is 0 */
-    const uint32_t q_last = j + K * ((end - 1u - j) / K);
-    return K - (end - q_last);
+    const int32_t q_last = (int32_t)j + (e >= 0 ? (int32_t)K * (e / (int32_t)K) : -(int32_t)K);
+    return K - (uint32_t)(end - q_last);
 }
 
 /* the walk's output alignment key: the payload output address in 16-byte units */
@@ -1051,6 +1068,23 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
     const uint8_t *ad = aad + rec.aad;
     const uint32_t arem = rec.aadlen & 15u;
     u32x4 acc = {0u, 0u, 0u, 0u}, ek0 = {0u, 0u, 0u, 0u};
+    if (seg == nullptr && valid) {
+        /* hoisted AAD (make_walk): an AAD block at lane j's position before step 0 seeds its chain */
+        const int32_t pv = (int32_t)j - (int32_t)K - (int32_t)wk.pad; /* record position of grid slot j - K */
+        if (pv >= 0 && (uint32_t)pv < wk.A) {
+            if (FRAME) { /* 17 03 03 BE16(plen + 16) */
+                const uint32_t reclen = plen + 16u;
+                acc[0] = 0x00030317u | ((reclen >> 8) & 0xffu) << 24;
+                acc[1] = reclen & 0xffu;
+            } else if (rec.aadlen < 16u) {
+                acc = load_partial(ad, rec.aadlen);
+            } else if (16u * (uint32_t)pv + 16u <= rec.aadlen) {
+                acc = *(const u32x4_u *)(ad + 16u * (uint32_t)pv);
+            } else { /* partial last block: its last 16 bytes, shifted */
+                acc = shr_bytes(*(const u32x4_u *)(ad + rec.aadlen - 16u), 16u - arem);
+            }
+        }
+    }
     /* hoisted round-1 (and round-2, GCM_R2CACHE) constants of the current counter window */
 #if GCM_R2CACHE
     constexpr uint32_t WIN = 0xffffff00u; /* 2^8-block windows (aes_round12_consts) */

@@ -28,6 +28,10 @@ VARIANTS = {
     "noalign": ["-DGCM_ALIGN_OUTPUT=0"],
     "freealign": ["-DGCM_ALIGN_MIN_T=100000u"],
     "align8": ["-DGCM_ALIGN_MIN_T=8u"],
+    "lanemajor": ["-DGCM_LANE_MAJOR=1"],
+    "nohoist": ["-DGCM_HOIST_AAD=0"],
+    "r01d": ["-DGCM_HOIST_AAD=0", "-DGCM_LANE_MAJOR=0"],  # the record walk before hoisting / j-major lanes
+    "hoistonly": ["-DGCM_LANE_MAJOR=0"],
     # "@src=DIR": compile gcm_engine.hip from DIR (e.g. a `git show` of an older revision) instead of csrc/
     "head": ["@src=" + os.path.join(VDIR, "src_head")],
     "no_ghash": ["-DGCM_ABLATE_GHASH=1"],
@@ -50,7 +54,8 @@ def build():
             os.makedirs(srcdir)
             for f in ("gcm_engine.hip", "gcm_core.h"):
                 with open(os.path.join(srcdir, f), "wb") as fh:
-                    fh.write(subprocess.run(["git", "-C", ROOT, "show", "HEAD:rapido_amd/csrc/" + f],
+                    rev = os.environ.get("ABLATE_REV", "HEAD")  # e.g. an older commit to A/B against
+                    fh.write(subprocess.run(["git", "-C", ROOT, "show", rev + ":rapido_amd/csrc/" + f],
                                             check=True, capture_output=True).stdout)
         flags = [f for f in flags if not f.startswith("@src=")]
         src = os.path.join(srcdir, "gcm_engine.hip")
@@ -105,14 +110,24 @@ def run(workload="1400", rounds=5, lanes=4):
             if r:  # round 0 is warmup
                 res[name]["seal"].append(ev[0].elapsed_time(ev[1]))
                 res[name]["open"].append(ev[1].elapsed_time(ev[2]))
+    # outputs vs the first variant (ablated variants differ by design)
+    ref = None
+    same = {}
+    for name, (L, ctx) in libs.items():
+        d_ct.zero_()
+        L.ptls_mi355x_seal_batch(ctx, iv, d_recs.data_ptr(), n, d_src.data_ptr(), d_ct.data_ptr(), d_aad.data_ptr(), stream)
+        torch.cuda.synchronize()
+        if ref is None:
+            ref = d_ct.clone()
+        same[name] = bool(torch.equal(d_ct, ref))
     out = {}
     for name, d in res.items():
         s, o = statistics.median(d["seal"]), statistics.median(d["open"])
         gib = n * length / 2 ** 30
         out[name] = {"seal_ms": round(s, 4), "open_ms": round(o, 4), "seal_gibps": round(gib / (s / 1e3), 1),
-                     "open_gibps": round(gib / (o / 1e3), 1)}
+                     "open_gibps": round(gib / (o / 1e3), 1), "same_output": same[name]}
         print(f"{workload:10s} K={lanes} {name:12s} seal {s:7.3f} ms {gib / (s / 1e3):8.1f} GiB/s   open {o:7.3f} ms "
-              f"{gib / (o / 1e3):8.1f} GiB/s", flush=True)
+              f"{gib / (o / 1e3):8.1f} GiB/s  same={same[name]}", flush=True)
     return out
 
 

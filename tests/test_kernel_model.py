@@ -239,6 +239,36 @@ def test_model_every_front_pad(model, K):
         assert (st == recs["len"]).all()
 
 
+@pytest.mark.parametrize("K", [1, 2, 4, 8])
+def test_model_hoisted_aad(model, K):
+    """AAD hoisting (make_walk): AADs of 0..7 blocks -- seeding the lanes' accumulators before step 0 when
+    A <= K, in the grid otherwise -- in front of payloads of every length class, at every output offset
+    modulo K blocks, sealed and opened, vs the oracle."""
+    rng = np.random.default_rng(40 + K)
+    key, iv = rng.integers(0, 256, 16, dtype=np.uint8).tobytes(), rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    aadlens = [0, 1, 5, 13, 16, 17, 31, 32, 33, 48, 63, 64, 65, 100, 112]
+    lens = [0, 1, 15, 16, 17, 100, 1392, 1400, 4096]
+    pairs = [(a, n) for a in aadlens for n in lens]
+    for shift in range(K):
+        recs, src_bytes, aad_bytes = records.layout(np.array([p[1] for p in pairs], np.uint64),
+                                                    np.array([p[0] for p in pairs], np.uint64), align=256)
+        recs["dst"] = recs["dst"] + np.uint64(16 * shift)  # slots keep >= 112 spare bytes
+        recs["seq"] = rng.integers(0, 2 ** 63, len(recs), dtype=np.uint64)
+        src = rng.integers(0, 256, src_bytes + 256, dtype=np.uint8)
+        aad = rng.integers(0, 256, aad_bytes, dtype=np.uint8)
+        got, want = np.zeros_like(src), np.zeros_like(src)
+        st = np.zeros(len(recs), np.uint32)
+        run(model, True, K, key, iv, recs, src, got, aad, st)
+        oracle.batch(True, key, iv, recs, src, want, aad)
+        assert spans(got, recs, 16) == spans(want, recs, 16), shift
+        orecs = recs.copy()
+        orecs["src"] = recs["dst"]
+        opened = np.zeros_like(got)
+        run(model, False, K, key, iv, orecs, got, opened, aad, st)
+        assert (st == recs["len"]).all()
+        assert spans(opened, orecs, 0) == [bytes(src[int(r["src"]): int(r["src"]) + int(r["len"])]) for r in recs]
+
+
 @pytest.mark.parametrize("keylen", [16, 32])
 def test_model_bitsliced_keystream(model, keylen):
     """The VALU engine of gcm_bitslice.h (quad layout: Boyar-Peralta S-box as 92 three-input LUTs, DPP
