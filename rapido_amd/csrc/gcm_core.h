@@ -74,14 +74,32 @@ enum : uint32_t {
     GH_TABLE_BYTES = 32u * 16u * 16u, /* 8 KiB */
     MAX_K = 8,                        /* tables kept in the key image: H^1..H^8 */
     MAX_KERNEL_K = 8,
+    GH5_CHUNKS = 26u,                 /* 5-bit tables: chunk c = bits [5c, 5c + 5) of the 128-bit X */
+    GH5_BYTES = GH5_CHUNKS * 512u,    /* per chunk a 256-B row of low halves, then one of high halves */
 };
 
+#ifndef GCM_GH5
+#define GCM_GH5 0
+#endif
+/*
+ * GCM_GH5 (an evaluated layout, OFF): K = 4 with the Horner factor H^4 as 5-bit tables of 8-byte halves at
+ * [0, GH5_BYTES) -- 26 chunks x 2 ds_read_b64 = 104 nominal LDS cycles per multiply instead of 32
+ * ds_read_b128 = 128, since a b64 read costs the same 2 cycles as a b32 one and 32 entries x 8 B fill one
+ * bank row -- the AES images after them, and nibble tables of H^2 | H^1 for the closing scaling (H^e, e in
+ * 1..4, as two multiplies).  Bit-exact, but measured 33% SLOWER (scripts/ablate.py nogh5 vs gh5, 1400 B):
+ * SQ_LDS_BANK_CONFLICT rose from 6 to 201 cycles per block.  Unlike ds_read_b128 on the nibble tables,
+ * ds_read_b64 does not broadcast lanes that read the same address, and random 5-bit indices put 2-4 lanes
+ * on each entry.
+ */
 template <int K>
 struct Layout {
     static constexpr bool four_tables = K <= 4;
+    static constexpr bool gh5 = GCM_GH5 && K == 4;
+    static constexpr uint32_t aes_base = gh5 ? (uint32_t)GH5_BYTES : 0u;
     static constexpr uint32_t aes_bytes = four_tables ? 0x20000u : 0x10000u;
-    static constexpr uint32_t gh_base = aes_bytes;
-    static constexpr uint32_t total = aes_bytes + (uint32_t)K * GH_TABLE_BYTES;
+    static constexpr uint32_t gh_base = aes_base + aes_bytes; /* nibble tables: slot s = H^(n_nibble - s) */
+    static constexpr uint32_t n_nibble = gh5 ? 2u : (uint32_t)K;
+    static constexpr uint32_t total = gh_base + n_nibble * GH_TABLE_BYTES;
     static_assert(total <= 160u * 1024u, "LDS budget");
 };
 
@@ -187,6 +205,18 @@ GCM_HD uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
 
 GCM_HD uint32_t lds_u32(const uint8_t *lds, uint32_t addr) { return *(const uint32_t *)(lds + addr); }
 GCM_HD u32x4 lds_u32x4(const uint8_t *lds, uint32_t addr) { return *(const u32x4 *)(lds + addr); }
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+GCM_HD u32x2 lds_u32x2(const uint8_t *lds, uint32_t addr) { return *(const u32x2 *)(lds + addr); }
+
+/* bits [s, s + 32) of the 64-bit value {hi, lo} (v_alignbit_b32), 0 <= s < 32 */
+GCM_HD uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t s)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_alignbit(hi, lo, s);
+#else
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> s);
+#endif
+}
 
 /*
  * One AES encryption of w[4] with the replicated T-table images at lds[0, 128K).
@@ -292,6 +322,69 @@ GCM_HD void ghash_quarter_acc(const u32x4 g[4], u32x4 &P)
     }
 }
 
+/*
+ * 5-bit GHASH tables (Layout<4>::gh5, built by fill_lds from the key image's nibble tables): chunk c of X
+ * is bits [5c, 5c + 5) (bit 32d + i = bit i of dword d; chunk 25 has 3 bits).  Row c*512 holds the low
+ * 8 bytes of (chunk value v placed at bit 5c) * H^4 for v = 0..31, row c*512 + 256 the high 8 bytes.
+ * The row offset of v, 8v, comes from one shift (or v_alignbit across dwords) and one AND: the tables
+ * sit at LDS address 0, so the chunk's row is the read's immediate offset.
+ */
+GCM_HD uint32_t gh5_off(const u32x4 &X, int c)
+{
+    const int b = 5 * c, d = b >> 5, o = b & 31;
+    uint32_t t;
+    if (o + 5 <= 32 || d == 3)
+        t = o >= 3 ? X[d] >> (o - 3) : X[d] << (3 - o);
+    else
+        t = alignbit(X[d + 1], X[d], (uint32_t)(o - 3));
+    return t & 0xf8u;
+}
+
+/* the 2n reads of chunks c0 .. c0+n-1 (n <= 4) */
+GCM_HD void gh5_issue(const uint8_t *lds, const u32x4 &X, int c0, int n, u32x2 g[8])
+{
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+        const uint32_t a = gh5_off(X, c0 + i) + (uint32_t)(c0 + i) * 512u;
+        g[2 * i] = lds_u32x2(lds, a);
+        g[2 * i + 1] = lds_u32x2(lds, a + 256u);
+    }
+}
+
+GCM_HD void gh5_acc(const u32x2 g[8], int n, u32x4 &P)
+{
+#pragma unroll
+    for (int i = 0; i + 1 < n; i += 2) {
+        P[0] = xor3_pinned(P[0], g[2 * i][0], g[2 * i + 2][0]);
+        P[1] = xor3_pinned(P[1], g[2 * i][1], g[2 * i + 2][1]);
+        P[2] = xor3_pinned(P[2], g[2 * i + 1][0], g[2 * i + 3][0]);
+        P[3] = xor3_pinned(P[3], g[2 * i + 1][1], g[2 * i + 3][1]);
+    }
+    if (n & 1) {
+        P[0] ^= g[2 * (n - 1)][0];
+        P[1] ^= g[2 * (n - 1)][1];
+        P[2] ^= g[2 * (n - 1) + 1][0];
+        P[3] ^= g[2 * (n - 1) + 1][1];
+    }
+}
+
+/* chunks of GHASH slot s (0..7) of a fused multiply: 3,3,3,3,3,3,4,4 */
+GCM_HDC int gh5_slot_first(int s) { return s < 6 ? 3 * s : 18 + 4 * (s - 6); }
+GCM_HDC int gh5_slot_count(int s) { return s < 6 ? 3 : 4; }
+
+/* X * H^4 from the 5-bit tables, not fused */
+GCM_HD u32x4 ghash5_mul_lds(const uint8_t *lds, u32x4 X)
+{
+    u32x4 P = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+        u32x2 g[8];
+        gh5_issue(lds, X, gh5_slot_first(s), gh5_slot_count(s), g);
+        gh5_acc(g, gh5_slot_count(s), P);
+    }
+    return P;
+}
+
 #ifndef GCM_ROUND_ASM
 #define GCM_ROUND_ASM 1
 #endif
@@ -307,6 +400,8 @@ GCM_HD void ghash_quarter_acc(const u32x4 g[4], u32x4 &P)
  * lgkmcnt(0): no read of it is outstanding afterwards, so the compiler's own counted waits
  * stay exact (DS reads complete in order).  Bit-identical to the aes_col sequence.
  */
+/* BASE: LDS address of the AES images (Layout::aes_base), folded into the reads' immediate offsets */
+template <uint32_t BASE = 0u>
 __device__ __forceinline__ void aes_round_tt4_asm(uint32_t ls, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3,
                                                   const uint32_t *k, uint32_t &n0, uint32_t &n1, uint32_t &n2,
                                                   uint32_t &n3)
@@ -318,34 +413,34 @@ __device__ __forceinline__ void aes_round_tt4_asm(uint32_t ls, uint32_t s0, uint
         "v_perm_b32 %[t1], %[s1], %[ls], %[a1]\n\t"
         "v_perm_b32 %[t2], %[s2], %[ls], %[b2]\n\t"
         "v_perm_b32 %[t3], %[s3], %[ls], %[b3]\n\t"
-        "ds_read_b32 %[n0], %[n0]\n\t"
-        "ds_read_b32 %[t1], %[t1] offset:128\n\t"
-        "ds_read_b32 %[t2], %[t2]\n\t"
-        "ds_read_b32 %[t3], %[t3] offset:128\n\t"
+        "ds_read_b32 %[n0], %[n0] offset:%[o0]\n\t"
+        "ds_read_b32 %[t1], %[t1] offset:%[o1]\n\t"
+        "ds_read_b32 %[t2], %[t2] offset:%[o0]\n\t"
+        "ds_read_b32 %[t3], %[t3] offset:%[o1]\n\t"
         "v_perm_b32 %[n1], %[s1], %[ls], %[a0]\n\t"
         "v_perm_b32 %[t5], %[s2], %[ls], %[a1]\n\t"
         "v_perm_b32 %[t6], %[s3], %[ls], %[b2]\n\t"
         "v_perm_b32 %[t7], %[s0], %[ls], %[b3]\n\t"
-        "ds_read_b32 %[n1], %[n1]\n\t"
-        "ds_read_b32 %[t5], %[t5] offset:128\n\t"
-        "ds_read_b32 %[t6], %[t6]\n\t"
-        "ds_read_b32 %[t7], %[t7] offset:128\n\t"
+        "ds_read_b32 %[n1], %[n1] offset:%[o0]\n\t"
+        "ds_read_b32 %[t5], %[t5] offset:%[o1]\n\t"
+        "ds_read_b32 %[t6], %[t6] offset:%[o0]\n\t"
+        "ds_read_b32 %[t7], %[t7] offset:%[o1]\n\t"
         "v_perm_b32 %[n2], %[s2], %[ls], %[a0]\n\t"
         "v_perm_b32 %[t9], %[s3], %[ls], %[a1]\n\t"
         "v_perm_b32 %[t10], %[s0], %[ls], %[b2]\n\t"
         "v_perm_b32 %[t11], %[s1], %[ls], %[b3]\n\t"
-        "ds_read_b32 %[n2], %[n2]\n\t"
-        "ds_read_b32 %[t9], %[t9] offset:128\n\t"
-        "ds_read_b32 %[t10], %[t10]\n\t"
-        "ds_read_b32 %[t11], %[t11] offset:128\n\t"
+        "ds_read_b32 %[n2], %[n2] offset:%[o0]\n\t"
+        "ds_read_b32 %[t9], %[t9] offset:%[o1]\n\t"
+        "ds_read_b32 %[t10], %[t10] offset:%[o0]\n\t"
+        "ds_read_b32 %[t11], %[t11] offset:%[o1]\n\t"
         "v_perm_b32 %[n3], %[s3], %[ls], %[a0]\n\t"
         "v_perm_b32 %[t13], %[s0], %[ls], %[a1]\n\t"
         "v_perm_b32 %[t14], %[s1], %[ls], %[b2]\n\t"
         "v_perm_b32 %[t15], %[s2], %[ls], %[b3]\n\t"
-        "ds_read_b32 %[n3], %[n3]\n\t"
-        "ds_read_b32 %[t13], %[t13] offset:128\n\t"
-        "ds_read_b32 %[t14], %[t14]\n\t"
-        "ds_read_b32 %[t15], %[t15] offset:128\n\t"
+        "ds_read_b32 %[n3], %[n3] offset:%[o0]\n\t"
+        "ds_read_b32 %[t13], %[t13] offset:%[o1]\n\t"
+        "ds_read_b32 %[t14], %[t14] offset:%[o0]\n\t"
+        "ds_read_b32 %[t15], %[t15] offset:%[o1]\n\t"
         "s_waitcnt lgkmcnt(12)\n\t"
         "v_bitop3_b32 %[n0], %[n0], %[t1], %[k0] bitop3:0x96\n\t"
         "v_bitop3_b32 %[n0], %[n0], %[t2], %[t3] bitop3:0x96\n\t"
@@ -363,7 +458,7 @@ __device__ __forceinline__ void aes_round_tt4_asm(uint32_t ls, uint32_t s0, uint
           [t11] "=&v"(t11), [t13] "=&v"(t13), [t14] "=&v"(t14), [t15] "=&v"(t15)
         : [s0] "v"(s0), [s1] "v"(s1), [s2] "v"(s2), [s3] "v"(s3), [ls] "v"(ls), [k0] "s"(k[0]), [k1] "s"(k[1]),
           [k2] "s"(k[2]), [k3] "s"(k[3]), [a0] "s"(0x0c0c0400u), [a1] "s"(0x0c0c0500u), [b2] "s"(0x0c020600u),
-          [b3] "s"(0x0c020700u)
+          [b3] "s"(0x0c020700u), [o0] "i"(BASE), [o1] "i"(BASE + 128u)
         : "memory");
 }
 #endif
@@ -493,24 +588,33 @@ GCM_HD void aes_round12_consts(const uint8_t *lds, uint32_t lanesel, const uint3
 /*
  * aes_ghash_fused for a block whose round 1 is hoisted (c from the block's 2^16 window): 2 table reads in round 1
  * instead of 16; the GHASH reads go to rounds 2..9.  Writes the keystream to w[4].
+ * GH5: P = A * H^4 from the 5-bit tables at LDS 0 (eight slots of 3-4 chunks); otherwise from the nibble
+ * tables at basereg (eight quarters).  AES_BASE: LDS address of the AES images.
  */
-template <int NR, bool FOUR = true>
+template <int NR, bool FOUR = true, bool GH5 = false, uint32_t AES_BASE = 0u>
 GCM_HD u32x4 aes_ghash_fused_h(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk, const uint32_t *c,
                                uint32_t ctr, uint32_t w[4], uint32_t basereg, u32x4 A)
 {
 #define GCM_TA(x, k) perm((x), lanesel, 0x0c0c0400u | ((4u + (k)) << 8))
+    const uint8_t *la = lds + AES_BASE;
     u32x4 P = {0u, 0u, 0u, 0u};
     const uint32_t s3 = bswap32(ctr) ^ rk[3];
 #if GCM_R2CACHE
     /* rounds 1 and 2 from the window constants c[0..7] (aes_round12_consts): 5 reads */
-    const uint32_t n0 = c[0] ^ tlook<FOUR>(lds, lanesel, s3, 3, 3);
-    uint32_t s0 = c[4] ^ tlook<FOUR>(lds, lanesel, n0, 0, 0), s1 = c[5] ^ tlook<FOUR>(lds, lanesel, n0, 3, 3);
-    uint32_t s2 = c[6] ^ tlook<FOUR>(lds, lanesel, n0, 2, 2), s3r = c[7] ^ tlook<FOUR>(lds, lanesel, n0, 1, 1);
-    ghash_quarter(lds, basereg, A[0], 0, 0, P);
+    const uint32_t n0 = c[0] ^ tlook<FOUR>(la, lanesel, s3, 3, 3);
+    uint32_t s0 = c[4] ^ tlook<FOUR>(la, lanesel, n0, 0, 0), s1 = c[5] ^ tlook<FOUR>(la, lanesel, n0, 3, 3);
+    uint32_t s2 = c[6] ^ tlook<FOUR>(la, lanesel, n0, 2, 2), s3r = c[7] ^ tlook<FOUR>(la, lanesel, n0, 1, 1);
+    if (GH5) {
+        u32x2 g5[8];
+        gh5_issue(lds, A, gh5_slot_first(0), gh5_slot_count(0), g5);
+        gh5_acc(g5, gh5_slot_count(0), P);
+    } else {
+        ghash_quarter(lds, basereg, A[0], 0, 0, P);
+    }
     GCM_SCHED_FENCE();
     constexpr int R0 = 3;
 #else
-    uint32_t s0 = c[0] ^ tlook<FOUR>(lds, lanesel, s3, 3, 3), s1 = c[1] ^ tlook<FOUR>(lds, lanesel, s3, 2, 2);
+    uint32_t s0 = c[0] ^ tlook<FOUR>(la, lanesel, s3, 3, 3), s1 = c[1] ^ tlook<FOUR>(la, lanesel, s3, 2, 2);
     uint32_t s2 = c[2], s3r = c[3];
     constexpr int R0 = 2;
 #endif
@@ -520,22 +624,38 @@ GCM_HD u32x4 aes_ghash_fused_h(const uint8_t *lds, uint32_t lanesel, const uint3
         uint32_t n0, n1, n2, n3;
 #if defined(__HIP_DEVICE_COMPILE__) && GCM_ROUND_ASM
         if (FOUR) {
-            /* GHASH quarter: reads issued ahead of the round, accumulated after it */
-            u32x4 g[4];
-            if (r <= 9)
-                ghash_quarter_issue(lds, basereg, A[(r - 2) >> 1], (r - 2) >> 1, ((r - 2) & 1) * 2, g);
-            aes_round_tt4_asm(lanesel, s0, s1, s2, s3r, k, n0, n1, n2, n3);
-            if (r <= 9)
-                ghash_quarter_acc(g, P);
+            /* GHASH slot: reads issued ahead of the round, accumulated after it */
+            if (GH5) {
+                u32x2 g5[8];
+                if (r <= 9)
+                    gh5_issue(lds, A, gh5_slot_first(r - 2), gh5_slot_count(r - 2), g5);
+                aes_round_tt4_asm<AES_BASE>(lanesel, s0, s1, s2, s3r, k, n0, n1, n2, n3);
+                if (r <= 9)
+                    gh5_acc(g5, gh5_slot_count(r - 2), P);
+            } else {
+                u32x4 g[4];
+                if (r <= 9)
+                    ghash_quarter_issue(lds, basereg, A[(r - 2) >> 1], (r - 2) >> 1, ((r - 2) & 1) * 2, g);
+                aes_round_tt4_asm<AES_BASE>(lanesel, s0, s1, s2, s3r, k, n0, n1, n2, n3);
+                if (r <= 9)
+                    ghash_quarter_acc(g, P);
+            }
         } else
 #endif
         {
-            n0 = aes_col<FOUR>(lds, lanesel, s0, s1, s2, s3r, k[0]);
-            n1 = aes_col<FOUR>(lds, lanesel, s1, s2, s3r, s0, k[1]);
-            n2 = aes_col<FOUR>(lds, lanesel, s2, s3r, s0, s1, k[2]);
-            n3 = aes_col<FOUR>(lds, lanesel, s3r, s0, s1, s2, k[3]);
-            if (r <= 9)
-                ghash_quarter(lds, basereg, A[(r - 2) >> 1], (r - 2) >> 1, ((r - 2) & 1) * 2, P);
+            n0 = aes_col<FOUR>(la, lanesel, s0, s1, s2, s3r, k[0]);
+            n1 = aes_col<FOUR>(la, lanesel, s1, s2, s3r, s0, k[1]);
+            n2 = aes_col<FOUR>(la, lanesel, s2, s3r, s0, s1, k[2]);
+            n3 = aes_col<FOUR>(la, lanesel, s3r, s0, s1, s2, k[3]);
+            if (r <= 9) {
+                if (GH5) {
+                    u32x2 g5[8];
+                    gh5_issue(lds, A, gh5_slot_first(r - 2), gh5_slot_count(r - 2), g5);
+                    gh5_acc(g5, gh5_slot_count(r - 2), P);
+                } else {
+                    ghash_quarter(lds, basereg, A[(r - 2) >> 1], (r - 2) >> 1, ((r - 2) & 1) * 2, P);
+                }
+            }
         }
         GCM_SCHED_FENCE();
         s0 = n0;
@@ -548,10 +668,10 @@ GCM_HD u32x4 aes_ghash_fused_h(const uint8_t *lds, uint32_t lanesel, const uint3
         uint32_t x[4] = {s0, s1, s2, s3r};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            uint32_t ra = lds_u32(lds, GCM_TA(x[j], 0));
-            uint32_t rb = lds_u32(lds, GCM_TA(x[(j + 1) & 3], 1));
-            uint32_t rc = lds_u32(lds, GCM_TA(x[(j + 2) & 3], 2));
-            uint32_t rd = lds_u32(lds, GCM_TA(x[(j + 3) & 3], 3));
+            uint32_t ra = lds_u32(la, GCM_TA(x[j], 0));
+            uint32_t rb = lds_u32(la, GCM_TA(x[(j + 1) & 3], 1));
+            uint32_t rc = lds_u32(la, GCM_TA(x[(j + 2) & 3], 2));
+            uint32_t rd = lds_u32(la, GCM_TA(x[(j + 3) & 3], 3));
             w[j] = xor3(perm(rb, ra, 0x0c0c0501u), perm(rd, rc, 0x06020c0cu), k[j]);
         }
     }
@@ -848,9 +968,33 @@ GCM_HD int build_key_image(const uint8_t *sbox, const uint8_t *key, uint32_t key
  * LDS image fill, split over nthr threads: AES T-table replicas and the K GHASH tables
  * (slot j = tables of H^(K-j)).  Called by every thread of a workgroup before the barrier.
  */
+/*
+ * 8-byte half `half` of entry v of chunk c of the 5-bit tables of H^4: XOR of the single-bit products
+ * (bit 5c + q set) * H^4, q in v, read from the nibble tables of H^4 (bit i of dword d is bit k = i % 8 of
+ * byte m = i / 8: nibble table 8d + 2m + k / 4, entry 1 << (k % 4)).
+ */
+GCM_HD u32x2 gh5_entry(const KeyImage *ki, uint32_t c, uint32_t half, uint32_t v)
+{
+    u32x2 r = {0u, 0u};
+    for (uint32_t q = 0; q < 5u; ++q) {
+        const uint32_t b = 5u * c + q;
+        if (((v >> q) & 1u) == 0u || b >= 128u)
+            continue;
+        const uint32_t d = b >> 5, i = b & 31u, m = i >> 3, k = i & 7u;
+        const uint32_t *e = (const uint32_t *)ki->gh[3][8u * d + 2u * m + (k >> 2)][1u << (k & 3u)];
+        r[0] ^= e[2u * half];
+        r[1] ^= e[2u * half + 1u];
+    }
+    return r;
+}
+
 GCM_HD void fill_lds(uint8_t *lds, const uint32_t *t0, const KeyImage *ki, uint32_t K, uint32_t tid, uint32_t nthr)
 {
-    const uint32_t aes_bytes = K <= 4 ? 0x20000u : 0x10000u, gh_base = aes_bytes;
+    /* mirrors struct Layout<K> */
+    const bool gh5 = GCM_GH5 && K == 4u;
+    const uint32_t aes_base = gh5 ? (uint32_t)GH5_BYTES : 0u;
+    const uint32_t aes_bytes = K <= 4 ? 0x20000u : 0x10000u, gh_base = aes_base + aes_bytes;
+    const uint32_t n_nibble = gh5 ? 2u : K;
     for (uint32_t i = tid; i < aes_bytes / 16; i += nthr) {
         uint32_t off = i * 16, x = (off >> 8) & 0xffu;
         uint32_t v = t0[x];
@@ -859,13 +1003,18 @@ GCM_HD void fill_lds(uint8_t *lds, const uint32_t *t0, const KeyImage *ki, uint3
         if (rot)
             v = rotl32(v, (int)rot);
         u32x4 q = {v, v, v, v};
-        *(u32x4 *)(lds + LDS_AES_BASE + off) = q;
+        *(u32x4 *)(lds + aes_base + off) = q;
     }
-    const uint32_t nvec = K * (GH_TABLE_BYTES / 16);
+    const uint32_t nvec = n_nibble * (GH_TABLE_BYTES / 16);
     for (uint32_t i = tid; i < nvec; i += nthr) {
         uint32_t slot = i / (GH_TABLE_BYTES / 16), within = i % (GH_TABLE_BYTES / 16);
-        const u32x4 *srcv = (const u32x4 *)ki->gh[K - slot - 1];
+        const u32x4 *srcv = (const u32x4 *)ki->gh[n_nibble - slot - 1];
         *(u32x4 *)(lds + gh_base + slot * GH_TABLE_BYTES + within * 16) = srcv[within];
+    }
+    if (gh5) {
+        /* entry e: chunk e / 64, half (e / 32) & 1, value e & 31 -> byte 8e */
+        for (uint32_t e = tid; e < GH5_BYTES / 8u; e += nthr)
+            *(u32x2 *)(lds + 8u * e) = gh5_entry(ki, e >> 6, (e >> 5) & 1u, e & 31u);
     }
 }
 
@@ -878,6 +1027,8 @@ GCM_HD void fill_lds(uint8_t *lds, const uint32_t *t0, const KeyImage *ki, uint3
  */
 struct LayoutWin {
     static constexpr bool four_tables = false;
+    static constexpr bool gh5 = false;
+    static constexpr uint32_t aes_base = 0u;
     static constexpr uint32_t gh_base = 0x10000u;
     static constexpr uint32_t gh64 = gh_base + 4u * GH_TABLE_BYTES;
     static constexpr uint32_t parts = gh64 + GH_TABLE_BYTES;
@@ -1089,11 +1240,11 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
 #if GCM_R2CACHE
     constexpr uint32_t WIN = 0xffffff00u; /* 2^8-block windows (aes_round12_consts) */
     uint32_t c1[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, c1_hi = 0u;
-    aes_round12_consts<LY::four_tables>(lds, lanesel, rk, iv0, iv1, iv2, 0u, c1);
+    aes_round12_consts<LY::four_tables>(lds + LY::aes_base, lanesel, rk, iv0, iv1, iv2, 0u, c1);
 #else
     constexpr uint32_t WIN = 0xffff0000u; /* 2^16-block windows (aes_round1_consts) */
     uint32_t c1[4] = {0u, 0u, 0u, 0u}, c1_hi = 0u;
-    aes_round1_consts<LY::four_tables>(lds, lanesel, rk, iv0, iv1, iv2, 0u, c1);
+    aes_round1_consts<LY::four_tables>(lds + LY::aes_base, lanesel, rk, iv0, iv1, iv2, 0u, c1);
 #endif
 
     /*
@@ -1146,9 +1297,9 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
 #if GCM_ABLATE_AES && GCM_ABLATE_GHASH
         const u32x4 P = acc;
 #elif GCM_ABLATE_AES
-        const u32x4 P = ghash_mul_lds(lds, LY::gh_base, acc);
+        const u32x4 P = LY::gh5 ? ghash5_mul_lds(lds, acc) : ghash_mul_lds(lds, LY::gh_base, acc);
 #elif GCM_ABLATE_GHASH
-        aes_encrypt_tt<NR, LY::four_tables>(lds, lanesel, rk, w);
+        aes_encrypt_tt<NR, LY::four_tables>(lds + LY::aes_base, lanesel, rk, w);
         const u32x4 P = acc;
 #else
         if ((ctr & WIN) != c1_hi) { /* a record crossing a counter window (>= 2^8 blocks with GCM_R2CACHE) */
@@ -1160,13 +1311,13 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
             GCM_OPAQUE(o2);
             GCM_OPAQUE(ol);
 #if GCM_R2CACHE
-            aes_round12_consts<LY::four_tables>(lds, ol, rk, o0, o1, o2, c1_hi, c1);
+            aes_round12_consts<LY::four_tables>(lds + LY::aes_base, ol, rk, o0, o1, o2, c1_hi, c1);
 #else
-            aes_round1_consts<LY::four_tables>(lds, ol, rk, o0, o1, o2, c1_hi, c1);
+            aes_round1_consts<LY::four_tables>(lds + LY::aes_base, ol, rk, o0, o1, o2, c1_hi, c1);
 #endif
         }
         const u32x4 P =
-            aes_ghash_fused_h<NR, LY::four_tables>(lds, lanesel, rk, c1, ctr, w, LY::gh_base, acc);
+            aes_ghash_fused_h<NR, LY::four_tables, LY::gh5, LY::aes_base>(lds, lanesel, rk, c1, ctr, w, LY::gh_base, acc);
 #endif
         const u32x4 ks = {w[0], w[1], w[2], w[3]};
 
@@ -1251,7 +1402,16 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
             step(t + 1u, bufB);
     }
     /* scale the chain by H^(pad + g - q_last(j)) (make_walk) */
-    acc = ghash_mul_lds(lds, LY::gh_base + walk_scale_slot(wk, j, K, end_cap) * GH_TABLE_BYTES, acc);
+    if (LY::gh5) {
+        /* H^e, e = 4 - slot in 1..4, from the nibble tables of H^2 (slot 0) and H^1 (slot 1) */
+        const uint32_t e = (uint32_t)K - walk_scale_slot(wk, j, K, end_cap);
+        acc = ghash_mul_lds(lds, LY::gh_base + (e >= 2u ? 0u : GH_TABLE_BYTES), acc);
+        const u32x4 y = ghash_mul_lds(lds, LY::gh_base + (e == 4u ? 0u : GH_TABLE_BYTES), acc);
+        if (e >= 3u)
+            acc = y;
+    } else {
+        acc = ghash_mul_lds(lds, LY::gh_base + walk_scale_slot(wk, j, K, end_cap) * GH_TABLE_BYTES, acc);
+    }
     return acc ^ ek0;
 }
 

@@ -32,6 +32,7 @@ VARIANTS = {
     "nohoist": ["-DGCM_HOIST_AAD=0"],
     "r01d": ["-DGCM_HOIST_AAD=0", "-DGCM_LANE_MAJOR=0"],  # the record walk before hoisting / j-major lanes
     "hoistonly": ["-DGCM_LANE_MAJOR=0"],
+    "gh5": ["-DGCM_GH5=1"],  # 5-bit ds_read_b64 GHASH tables for K = 4 (evaluated: 33% slower, bank conflicts)
     # "@src=DIR": compile gcm_engine.hip from DIR (e.g. a `git show` of an older revision) instead of csrc/
     "head": ["@src=" + os.path.join(VDIR, "src_head")],
     "no_ghash": ["-DGCM_ABLATE_GHASH=1"],
