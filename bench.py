@@ -131,10 +131,17 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal only (a 1-GPU box): RAPIDO_BENCH_SAME_DEVICE=1 puts every rank on cuda:0 and
+    # RAPIDO_BENCH_BACKEND=gloo replaces RCCL, which refuses two ranks on one GPU
+    dev_index = 0 if os.environ.get("RAPIDO_BENCH_SAME_DEVICE") == "1" else local_rank
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank if world > 1 else 0)
+        torch.cuda.set_device(dev_index)
+        backend = os.environ.get("RAPIDO_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", dev_index if world > 1 else 0)
     torch.cuda.set_device(dev)
     ra.require_gpu()
     if args.lanes:
