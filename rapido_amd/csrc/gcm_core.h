@@ -461,6 +461,80 @@ __device__ __forceinline__ void aes_round_tt4_asm(uint32_t ls, uint32_t s0, uint
           [b3] "s"(0x0c020700u), [o0] "i"(BASE), [o1] "i"(BASE + 128u)
         : "memory");
 }
+
+/*
+ * The same for the two-table image (T0 | T1 rows only: K = 8 batch kernels, window kernels): column c is
+ * T0[a] ^ T1[b] ^ k ^ rotl16(T0[c'] ^ T1[d']) (T2 = rotl16(T0), T3 = rotl16(T1)).  All 16 reads are issued
+ * before the first wait; at one wave per SIMD (window kernels) the compiler's grouped waits otherwise
+ * expose an LDS latency per group.
+ */
+template <uint32_t BASE = 0u>
+__device__ __forceinline__ void aes_round_tt2_asm(uint32_t ls, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3,
+                                                  const uint32_t *k, uint32_t &n0, uint32_t &n1, uint32_t &n2,
+                                                  uint32_t &n3)
+{
+    uint32_t t1, t2, t3, t5, t6, t7, t9, t10, t11, t13, t14, t15;
+    asm volatile(
+        "v_perm_b32 %[n0], %[s0], %[ls], %[a0]\n\t"
+        "v_perm_b32 %[t1], %[s1], %[ls], %[a1]\n\t"
+        "v_perm_b32 %[t2], %[s2], %[ls], %[a2]\n\t"
+        "v_perm_b32 %[t3], %[s3], %[ls], %[a3]\n\t"
+        "ds_read_b32 %[n0], %[n0] offset:%[o0]\n\t"
+        "ds_read_b32 %[t1], %[t1] offset:%[o1]\n\t"
+        "ds_read_b32 %[t2], %[t2] offset:%[o0]\n\t"
+        "ds_read_b32 %[t3], %[t3] offset:%[o1]\n\t"
+        "v_perm_b32 %[n1], %[s1], %[ls], %[a0]\n\t"
+        "v_perm_b32 %[t5], %[s2], %[ls], %[a1]\n\t"
+        "v_perm_b32 %[t6], %[s3], %[ls], %[a2]\n\t"
+        "v_perm_b32 %[t7], %[s0], %[ls], %[a3]\n\t"
+        "ds_read_b32 %[n1], %[n1] offset:%[o0]\n\t"
+        "ds_read_b32 %[t5], %[t5] offset:%[o1]\n\t"
+        "ds_read_b32 %[t6], %[t6] offset:%[o0]\n\t"
+        "ds_read_b32 %[t7], %[t7] offset:%[o1]\n\t"
+        "v_perm_b32 %[n2], %[s2], %[ls], %[a0]\n\t"
+        "v_perm_b32 %[t9], %[s3], %[ls], %[a1]\n\t"
+        "v_perm_b32 %[t10], %[s0], %[ls], %[a2]\n\t"
+        "v_perm_b32 %[t11], %[s1], %[ls], %[a3]\n\t"
+        "ds_read_b32 %[n2], %[n2] offset:%[o0]\n\t"
+        "ds_read_b32 %[t9], %[t9] offset:%[o1]\n\t"
+        "ds_read_b32 %[t10], %[t10] offset:%[o0]\n\t"
+        "ds_read_b32 %[t11], %[t11] offset:%[o1]\n\t"
+        "v_perm_b32 %[n3], %[s3], %[ls], %[a0]\n\t"
+        "v_perm_b32 %[t13], %[s0], %[ls], %[a1]\n\t"
+        "v_perm_b32 %[t14], %[s1], %[ls], %[a2]\n\t"
+        "v_perm_b32 %[t15], %[s2], %[ls], %[a3]\n\t"
+        "ds_read_b32 %[n3], %[n3] offset:%[o0]\n\t"
+        "ds_read_b32 %[t13], %[t13] offset:%[o1]\n\t"
+        "ds_read_b32 %[t14], %[t14] offset:%[o0]\n\t"
+        "ds_read_b32 %[t15], %[t15] offset:%[o1]\n\t"
+        "s_waitcnt lgkmcnt(12)\n\t"
+        "v_xor_b32 %[t2], %[t2], %[t3]\n\t"
+        "v_bitop3_b32 %[n0], %[n0], %[t1], %[k0] bitop3:0x96\n\t"
+        "v_alignbit_b32 %[t2], %[t2], %[t2], 16\n\t"
+        "v_xor_b32 %[n0], %[n0], %[t2]\n\t"
+        "s_waitcnt lgkmcnt(8)\n\t"
+        "v_xor_b32 %[t6], %[t6], %[t7]\n\t"
+        "v_bitop3_b32 %[n1], %[n1], %[t5], %[k1] bitop3:0x96\n\t"
+        "v_alignbit_b32 %[t6], %[t6], %[t6], 16\n\t"
+        "v_xor_b32 %[n1], %[n1], %[t6]\n\t"
+        "s_waitcnt lgkmcnt(4)\n\t"
+        "v_xor_b32 %[t10], %[t10], %[t11]\n\t"
+        "v_bitop3_b32 %[n2], %[n2], %[t9], %[k2] bitop3:0x96\n\t"
+        "v_alignbit_b32 %[t10], %[t10], %[t10], 16\n\t"
+        "v_xor_b32 %[n2], %[n2], %[t10]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_xor_b32 %[t14], %[t14], %[t15]\n\t"
+        "v_bitop3_b32 %[n3], %[n3], %[t13], %[k3] bitop3:0x96\n\t"
+        "v_alignbit_b32 %[t14], %[t14], %[t14], 16\n\t"
+        "v_xor_b32 %[n3], %[n3], %[t14]"
+        : [n0] "=&v"(n0), [n1] "=&v"(n1), [n2] "=&v"(n2), [n3] "=&v"(n3), [t1] "=&v"(t1), [t2] "=&v"(t2),
+          [t3] "=&v"(t3), [t5] "=&v"(t5), [t6] "=&v"(t6), [t7] "=&v"(t7), [t9] "=&v"(t9), [t10] "=&v"(t10),
+          [t11] "=&v"(t11), [t13] "=&v"(t13), [t14] "=&v"(t14), [t15] "=&v"(t15)
+        : [s0] "v"(s0), [s1] "v"(s1), [s2] "v"(s2), [s3] "v"(s3), [ls] "v"(ls), [k0] "s"(k[0]), [k1] "s"(k[1]),
+          [k2] "s"(k[2]), [k3] "s"(k[3]), [a0] "s"(0x0c0c0400u), [a1] "s"(0x0c0c0500u), [a2] "s"(0x0c0c0600u),
+          [a3] "s"(0x0c0c0700u), [o0] "i"(BASE), [o1] "i"(BASE + 128u)
+        : "memory");
+}
 #endif
 
 /*
@@ -623,9 +697,9 @@ GCM_HD u32x4 aes_ghash_fused_h(const uint8_t *lds, uint32_t lanesel, const uint3
         const uint32_t *k = rk + 4 * r;
         uint32_t n0, n1, n2, n3;
 #if defined(__HIP_DEVICE_COMPILE__) && GCM_ROUND_ASM
-        if (FOUR) {
+        if (true) {
             /* GHASH slot: reads issued ahead of the round, accumulated after it */
-            if (GH5) {
+            if (GH5 && FOUR) {
                 u32x2 g5[8];
                 if (r <= 9)
                     gh5_issue(lds, A, gh5_slot_first(r - 2), gh5_slot_count(r - 2), g5);
@@ -636,7 +710,10 @@ GCM_HD u32x4 aes_ghash_fused_h(const uint8_t *lds, uint32_t lanesel, const uint3
                 u32x4 g[4];
                 if (r <= 9)
                     ghash_quarter_issue(lds, basereg, A[(r - 2) >> 1], (r - 2) >> 1, ((r - 2) & 1) * 2, g);
-                aes_round_tt4_asm<AES_BASE>(lanesel, s0, s1, s2, s3r, k, n0, n1, n2, n3);
+                if (FOUR)
+                    aes_round_tt4_asm<AES_BASE>(lanesel, s0, s1, s2, s3r, k, n0, n1, n2, n3);
+                else
+                    aes_round_tt2_asm<AES_BASE>(lanesel, s0, s1, s2, s3r, k, n0, n1, n2, n3);
                 if (r <= 9)
                     ghash_quarter_acc(g, P);
             }
@@ -702,6 +779,36 @@ GCM_HD u32x4 ghash_mul_lds(const uint8_t *lds, uint32_t basereg, u32x4 x)
             r[2] = xor3(r[2], e[2], f[2]);
             r[3] = xor3(r[3], e[3], f[3]);
         }
+    }
+    return r;
+}
+
+/*
+ * ghash_mul_lds with all 32 table reads issued before the first XOR: for latency-bound chains (the window
+ * kernels' segment join), where the compiler otherwise waits on the reads in small groups.  128 VGPRs of
+ * reads in flight, so only for kernels with registers to spare (one wave per SIMD).
+ */
+GCM_HD u32x4 ghash_mul_lds_wide(const uint8_t *lds, uint32_t basereg, u32x4 x)
+{
+    u32x4 e[32];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const uint32_t lo = (x[d] << 4) & 0xf0f0f0f0u, hi = x[d] & 0xf0f0f0f0u;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const uint32_t sel = 0x0c020100u | (4u + (uint32_t)m);
+            e[8 * d + 2 * m] = lds_u32x4(lds, perm(lo, basereg, sel) + (uint32_t)(8 * d + 2 * m) * 256u);
+            e[8 * d + 2 * m + 1] = lds_u32x4(lds, perm(hi, basereg, sel) + (uint32_t)(8 * d + 2 * m + 1) * 256u);
+        }
+    }
+    GCM_SCHED_FENCE();
+    u32x4 r = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < 32; i += 2) {
+        r[0] = xor3(r[0], e[i][0], e[i + 1][0]);
+        r[1] = xor3(r[1], e[i][1], e[i + 1][1]);
+        r[2] = xor3(r[2], e[i][2], e[i + 1][2]);
+        r[3] = xor3(r[3], e[i][3], e[i + 1][3]);
     }
     return r;
 }
@@ -1021,16 +1128,17 @@ GCM_HD void fill_lds(uint8_t *lds, const uint32_t *t0, const KeyImage *ki, uint3
 /* ------------------------------------------------------------------ window kernels --------- */
 
 /*
- * LDS map of the window kernels (small framing batches, gcm_engine.hip tls_window_body): the two-table
- * AES image, the tables of H^4..H^1 (slot j = H^(4-j), the lane scaling of a K = 4 walk), the tables of
- * H^64 (joining 64-position segments), then the segment sums.
+ * LDS map of the window kernels (small framing / AEAD batches, gcm_engine.hip window_body), KW lanes per
+ * segment: the two-table AES image, the tables of H^KW..H^1 (slot j = H^(KW-j), the lane scaling of a
+ * KW-lane walk), the tables of H^64 (joining 64-position segments), then the segment sums.
  */
+template <int KW = 4>
 struct LayoutWin {
     static constexpr bool four_tables = false;
     static constexpr bool gh5 = false;
     static constexpr uint32_t aes_base = 0u;
     static constexpr uint32_t gh_base = 0x10000u;
-    static constexpr uint32_t gh64 = gh_base + 4u * GH_TABLE_BYTES;
+    static constexpr uint32_t gh64 = gh_base + (uint32_t)KW * GH_TABLE_BYTES;
     static constexpr uint32_t parts = gh64 + GH_TABLE_BYTES;
 };
 enum : uint32_t {
@@ -1038,8 +1146,8 @@ enum : uint32_t {
     WIN_MAXSEG = 17, /* segments of the largest TLS record (16640-byte record: 1 + 1039 + 1 positions) */
 };
 
-/* vector v of the window image: AES image A (T0 | T1 rows) for v < 4096, then the five GHASH tables */
-GCM_HD u32x4 window_image_vec(const uint32_t *t0, const KeyImage *ki, uint32_t v)
+/* vector v of the window image: AES image A (T0 | T1 rows) for v < 4096, then the kw + 1 GHASH tables */
+GCM_HD u32x4 window_image_vec(const uint32_t *t0, const KeyImage *ki, uint32_t v, uint32_t kw)
 {
     if (v < 0x10000u / 16u) {
         const uint32_t off = v * 16u, x = (off >> 8) & 0xffu;
@@ -1047,7 +1155,7 @@ GCM_HD u32x4 window_image_vec(const uint32_t *t0, const KeyImage *ki, uint32_t v
         return u32x4{w, w, w, w};
     }
     const uint32_t i = v - 0x10000u / 16u, slot = i / (GH_TABLE_BYTES / 16u), within = i % (GH_TABLE_BYTES / 16u);
-    const u32x4 *srcv = slot < 4u ? (const u32x4 *)ki->gh[3u - slot] : (const u32x4 *)ki->gh64;
+    const u32x4 *srcv = slot < kw ? (const u32x4 *)ki->gh[kw - 1u - slot] : (const u32x4 *)ki->gh64;
     return srcv[within];
 }
 
@@ -1055,15 +1163,16 @@ GCM_HD u32x4 window_image_vec(const uint32_t *t0, const KeyImage *ki, uint32_t v
  * Fills the window image, split over nthr threads.  Eight vectors per thread are loaded before any is
  * stored: a fill pass is one memory latency, and with 256 threads the image takes 26 vectors per thread.
  */
-GCM_HD void fill_lds_window(uint8_t *lds, const uint32_t *t0, const KeyImage *ki, uint32_t tid, uint32_t nthr)
+GCM_HD void fill_lds_window(uint8_t *lds, const uint32_t *t0, const KeyImage *ki, uint32_t tid, uint32_t nthr,
+                            uint32_t kw = 4u)
 {
-    constexpr uint32_t total = 0x10000u / 16u + 5u * GH_TABLE_BYTES / 16u;
+    const uint32_t total = 0x10000u / 16u + (kw + 1u) * GH_TABLE_BYTES / 16u;
     for (uint32_t base = tid; base < total; base += 8u * nthr) {
         u32x4 v[8];
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k)
             if (base + k * nthr < total)
-                v[k] = window_image_vec(t0, ki, base + k * nthr);
+                v[k] = window_image_vec(t0, ki, base + k * nthr, kw);
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k)
             if (base + k * nthr < total)
@@ -1076,14 +1185,14 @@ GCM_HD void fill_lds_window(uint8_t *lds, const uint32_t *t0, const KeyImage *ki
  * front-padded to nseg * 64; the returned walk covers padded positions [64 seg, 64 seg + 64) (its pad is
  * negative as int32 after the first segment).  Framed records have A = 1 (the 5-byte header).
  */
-GCM_HD Walk window_segment(uint32_t A, uint32_t C, uint32_t seg, uint32_t *nseg)
+GCM_HD Walk window_segment(uint32_t A, uint32_t C, uint32_t seg, uint32_t *nseg, uint32_t kw = 4u)
 {
     const uint32_t g = A + C + 1u;
     *nseg = (g + WIN_SEG - 1u) / WIN_SEG;
     Walk w;
     w.A = A;
     w.C = C;
-    w.T = WIN_SEG / 4u;
+    w.T = WIN_SEG / kw; /* kw lanes per segment */
     w.pad = WIN_SEG * *nseg - g - WIN_SEG * seg;
     return w;
 }
@@ -1197,7 +1306,7 @@ GCM_HD u32x4 shr_bytes(u32x4 v, uint32_t n)
  * padded position (negative as int32 for later segments); the lane's chain is scaled to the segment's end.
  * LY: the LDS layout (T-table image count and GHASH table base).
  */
-template <int NR, int K, bool SEAL, bool FRAME = false, class LY = Layout<K>>
+template <int NR, int K, bool SEAL, bool FRAME = false, class LY = Layout<K>, int PF = 1>
 GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk, uint32_t j, const Record &rec, bool valid,
                        uint32_t Tmax, uint32_t iv0, uint32_t iv1, uint32_t iv2, const uint8_t *src, uint8_t *dst,
                        const uint8_t *aad, const uint8_t *dummy, uint32_t ctype = 0u, const Walk *seg = nullptr,
@@ -1394,12 +1503,33 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
         bufA = load_partial(ad, rec.aadlen);
     else
         bufA = *(const u32x4_u *)fetch_ptr(t0);
-    for (uint32_t t = t0; t < Tmax; t += 2u) {
-        const u32x4 bufB = *(const u32x4_u *)fetch_ptr(t + 1u);
-        step(t, bufA);
-        bufA = *(const u32x4_u *)fetch_ptr(t + 2u);
-        if (t + 1u < Tmax)
-            step(t + 1u, bufB);
+    if (PF >= 3) {
+        /*
+         * Prefetch three steps ahead (window kernels at one wave per SIMD, where nothing else hides a load's
+         * latency behind a step): four buffers, four steps per trip.
+         */
+        u32x4 b1 = *(const u32x4_u *)fetch_ptr(t0 + 1u), b2 = *(const u32x4_u *)fetch_ptr(t0 + 2u);
+        for (uint32_t t = t0; t < Tmax; t += 4u) {
+            const u32x4 b3 = *(const u32x4_u *)fetch_ptr(t + 3u);
+            step(t, bufA);
+            bufA = *(const u32x4_u *)fetch_ptr(t + 4u);
+            if (t + 1u < Tmax)
+                step(t + 1u, b1);
+            b1 = *(const u32x4_u *)fetch_ptr(t + 5u);
+            if (t + 2u < Tmax)
+                step(t + 2u, b2);
+            b2 = *(const u32x4_u *)fetch_ptr(t + 6u);
+            if (t + 3u < Tmax)
+                step(t + 3u, b3);
+        }
+    } else {
+        for (uint32_t t = t0; t < Tmax; t += 2u) {
+            const u32x4 bufB = *(const u32x4_u *)fetch_ptr(t + 1u);
+            step(t, bufA);
+            bufA = *(const u32x4_u *)fetch_ptr(t + 2u);
+            if (t + 1u < Tmax)
+                step(t + 1u, bufB);
+        }
     }
     /* scale the chain by H^(pad + g - q_last(j)) (make_walk) */
     if (LY::gh5) {

@@ -41,6 +41,24 @@ constexpr int WG_THREADS = MI355X_WG_THREADS; /* 16 waves: 4 per SIMD */
 #ifndef GCM_LANE_MAJOR
 #define GCM_LANE_MAJOR 1
 #endif
+/*
+ * Phase timestamps of the window kernels' first workgroup (measurement builds only, scripts/window_phases.py):
+ * s_memrealtime (100 MHz) at entry, after the LDS fill, after the first pass's walk, after its barrier,
+ * after its join and at the end of the pass.
+ */
+#ifndef GCM_WIN_TIMING
+#define GCM_WIN_TIMING 0
+#endif
+#if GCM_WIN_TIMING
+__device__ uint64_t g_win_times[8];
+#define WIN_STAMP(i)                                                                                                   \
+    do {                                                                                                               \
+        if (blockIdx.x == 0 && threadIdx.x == 0 && grp == blockIdx.x)                                                  \
+            g_win_times[i] = __builtin_amdgcn_s_memrealtime();                                                         \
+    } while (0)
+#else
+#define WIN_STAMP(i) ((void)0)
+#endif
 
 __device__ __forceinline__ uint32_t shfl_xor_u32(uint32_t v, int mask) { return (uint32_t)__shfl_xor((int)v, mask, 64); }
 
@@ -251,24 +269,37 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
  * H^4..H^1 (lane scaling) and of H^64.  A record of more than WIN_MAXSEG segments (larger than a TLS
  * record) is walked whole by its first slot instead.  Results are bit-identical to the batch kernels.
  */
-template <int NR, bool SEAL, bool FRAME, int THREADS>
+template <int NR, bool SEAL, bool FRAME, int THREADS, int KW>
 __device__ __forceinline__ void window_body(const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2,
                                             const void *__restrict__ descs, uint32_t nrecs, const uint8_t *src, uint8_t *dst,
                                             const uint8_t *__restrict__ aad, uint32_t *__restrict__ status,
                                             uint8_t *__restrict__ types, const uint32_t *__restrict__ conn)
 {
-    constexpr uint32_t SLOTS = THREADS / 4, RECS = SLOTS / WIN_MAXSEG; /* records per workgroup pass */
-    __shared__ __attribute__((aligned(16))) uint8_t lds[LayoutWin::parts + RECS * WIN_MAXSEG * 16u];
+    typedef LayoutWin<KW> LW;
+    constexpr uint32_t SLOTS = THREADS / KW, RECS = SLOTS / WIN_MAXSEG; /* records per workgroup pass */
+    constexpr bool LATENCY = THREADS <= 512;   /* few records: up to 2 waves per SIMD */
+    constexpr int WIN_PF = LATENCY ? 3 : 1;    /* prefetch 3 steps ahead when little else hides a load (lane_walk) */
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LW::parts + RECS * WIN_MAXSEG * 16u];
     const Record *__restrict__ recs = (const Record *)descs;
     const TlsRecord *__restrict__ trecs = (const TlsRecord *)descs;
-    fill_lds_window(lds, c_tabs.t0, ki, threadIdx.x, blockDim.x);
+    {
+        const uint32_t grp = blockIdx.x;
+        (void)grp;
+        WIN_STAMP(0);
+    }
+    fill_lds_window(lds, c_tabs.t0, ki, threadIdx.x, blockDim.x, (uint32_t)KW);
     uint32_t rk[4 * (NR + 1)];
 #pragma unroll
     for (int i = 0; i < 4 * (NR + 1); ++i)
         rk[i] = ki->rk[i];
     __syncthreads();
+    {
+        const uint32_t grp = blockIdx.x;
+        (void)grp;
+        WIN_STAMP(1);
+    }
 
-    const uint32_t lane = threadIdx.x & 63u, slot = threadIdx.x >> 2, j = lane & 3u;
+    const uint32_t lane = threadIdx.x & 63u, slot = threadIdx.x / KW, j = lane % KW;
     const uint32_t lanesel = (lane & 31u) * 4u | 0x10000u;
     const uint32_t rl = slot / WIN_MAXSEG, seg = slot % WIN_MAXSEG;
     const uint32_t ngroups = (nrecs + RECS - 1u) / RECS;
@@ -301,12 +332,12 @@ __device__ __forceinline__ void window_body(const KeyImage *__restrict__ ki, uin
         const uint32_t plen = FRAME && SEAL ? rec.len + 1u : rec.len;
         const uint32_t A = FRAME ? 1u : (rec.aadlen + 15u) / 16u;
         uint32_t nseg;
-        const Walk sw = window_segment(A, (plen + 15u) / 16u, seg, &nseg);
+        const Walk sw = window_segment(A, (plen + 15u) / 16u, seg, &nseg, (uint32_t)KW);
         const bool whole = nseg > WIN_MAXSEG; /* larger than a TLS record: its first slot walks it all */
         const bool active = valid && (whole ? seg == 0u : seg < nseg);
-        uint32_t Tw = active ? (whole ? make_walk(plen, rec.aadlen, 4u, walk_out16(dst + rec.dst)).T : sw.T) : 0u;
+        uint32_t Tw = active ? (whole ? make_walk(plen, rec.aadlen, (uint32_t)KW, walk_out16(dst + rec.dst)).T : sw.T) : 0u;
         /* first step holding a real position (segments that are mostly front padding start late) */
-        uint32_t tf = active && !whole && (int32_t)sw.pad > 0 ? (uint32_t)(int32_t)sw.pad / 4u : (active ? 0u : ~0u);
+        uint32_t tf = active && !whole && (int32_t)sw.pad > 0 ? (uint32_t)(int32_t)sw.pad / (uint32_t)KW : (active ? 0u : ~0u);
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) {
             Tw = max(Tw, shfl_xor_u32(Tw, o));
@@ -315,24 +346,28 @@ __device__ __forceinline__ void window_body(const KeyImage *__restrict__ ki, uin
         const uint32_t t0 = tf == ~0u ? 0u : tf & ~1u;
         const uint32_t n1 = iv1 ^ bswap32((uint32_t)(rec.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)rec.seq);
         const uint32_t n0 = conn != nullptr && in_batch ? iv0 ^ bswap32(conn[r]) : iv0;
-        u32x4 part = lane_walk<NR, 4, SEAL, FRAME, LayoutWin>(lds, lanesel, rk, j, rec, active, Tw, n0, n1, n2, src, dst,
+        u32x4 part = lane_walk<NR, KW, SEAL, FRAME, LW, WIN_PF>(lds, lanesel, rk, j, rec, active, Tw, n0, n1, n2, src, dst,
                                                               aad, (const uint8_t *)descs, ctype, whole ? nullptr : &sw,
                                                               t0);
-        part ^= shfl_xor_u32x4(part, 1);
-        part ^= shfl_xor_u32x4(part, 2);
+#pragma unroll
+        for (int o = 1; o < KW; o <<= 1)
+            part ^= shfl_xor_u32x4(part, o);
+        WIN_STAMP(2);
         if (active && j == 0u)
-            *(u32x4 *)(lds + LayoutWin::parts + (rl * WIN_MAXSEG + seg) * 16u) = part;
+            *(u32x4 *)(lds + LW::parts + (rl * WIN_MAXSEG + seg) * 16u) = part;
         __syncthreads();
+        WIN_STAMP(3);
         if (in_batch && seg == 0u) {
             /* the record's first slot joins the segment sums: tag (seal) or tag ^ received tag (open) */
             u32x4 acc = {0u, 0u, 0u, 0u};
             if (valid) {
                 const uint32_t ns = whole ? 1u : nseg;
-                acc = *(const u32x4 *)(lds + LayoutWin::parts + rl * WIN_MAXSEG * 16u);
+                acc = *(const u32x4 *)(lds + LW::parts + rl * WIN_MAXSEG * 16u);
                 for (uint32_t k = 1; k < ns; ++k)
-                    acc = ghash_mul_lds(lds, LayoutWin::gh64, acc) ^
-                          *(const u32x4 *)(lds + LayoutWin::parts + (rl * WIN_MAXSEG + k) * 16u);
+                    acc = (LATENCY ? ghash_mul_lds_wide(lds, LW::gh64, acc) : ghash_mul_lds(lds, LW::gh64, acc)) ^
+                          *(const u32x4 *)(lds + LW::parts + (rl * WIN_MAXSEG + k) * 16u);
             }
+            WIN_STAMP(4);
             if (SEAL) {
                 if (j == 0u) {
                     *(u32x4_u *)(dst + rec.dst + plen) = acc;
@@ -345,7 +380,7 @@ __device__ __forceinline__ void window_body(const KeyImage *__restrict__ ki, uin
             } else if (!valid || (acc[0] | acc[1] | acc[2] | acc[3]) != 0u) {
                 /* no unverified plaintext is released (fusion leaves it, lib/fusion.c:656-679) */
                 uint8_t *out = dst + rec.dst;
-                for (uint32_t off = 16u * j; off < rec.len; off += 64u) {
+                for (uint32_t off = 16u * j; off < rec.len; off += 16u * KW) {
                     const uint32_t n = rec.len - off;
                     if (n >= 16u)
                         *(u32x4_u *)(out + off) = u32x4{0u, 0u, 0u, 0u};
@@ -383,6 +418,7 @@ __device__ __forceinline__ void window_body(const KeyImage *__restrict__ ki, uin
             }
         }
         __syncthreads(); /* the segment sums of this pass are consumed before the next pass writes them */
+        WIN_STAMP(5);
     }
 }
 
@@ -423,32 +459,32 @@ MI355X_GCM_KERNEL_F(mi355x_tls_seal_aes256_k4, 14, 4, true, true)
 MI355X_GCM_KERNEL_F(mi355x_tls_open_aes128_k4, 10, 4, false, true)
 MI355X_GCM_KERNEL_F(mi355x_tls_open_aes256_k4, 14, 4, false, true)
 
-#define MI355X_WIN_KERNEL(NAME, NR, SEAL, FRAME, THREADS)                                                              \
+#define MI355X_WIN_KERNEL(NAME, NR, SEAL, FRAME, THREADS, KW)                                                              \
     extern "C" __global__ __launch_bounds__(THREADS) void NAME(                                                        \
         const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2, const void *__restrict__ descs,     \
         uint32_t nrecs, const uint8_t *src, uint8_t *dst, const uint8_t *__restrict__ aad, uint32_t *__restrict__ st,   \
         uint8_t *__restrict__ types, const uint32_t *__restrict__ conn)                                                \
     {                                                                                                                  \
-        window_body<NR, SEAL, FRAME, THREADS>(ki, iv0, iv1, iv2, descs, nrecs, src, dst, aad, st, types, conn);        \
+        window_body<NR, SEAL, FRAME, THREADS, KW>(ki, iv0, iv1, iv2, descs, nrecs, src, dst, aad, st, types, conn);        \
     }
 /* 256 threads (3 records per pass): a few records spread over many CUs; 1024 threads (15 records per pass,
  * persistent): hundreds of records */
-MI355X_WIN_KERNEL(mi355x_tls_win_seal_aes128, 10, true, true, 256)
-MI355X_WIN_KERNEL(mi355x_tls_win_seal_aes256, 14, true, true, 256)
-MI355X_WIN_KERNEL(mi355x_tls_win_open_aes128, 10, false, true, 256)
-MI355X_WIN_KERNEL(mi355x_tls_win_open_aes256, 14, false, true, 256)
-MI355X_WIN_KERNEL(mi355x_tls_winw_seal_aes128, 10, true, true, 1024)
-MI355X_WIN_KERNEL(mi355x_tls_winw_seal_aes256, 14, true, true, 1024)
-MI355X_WIN_KERNEL(mi355x_tls_winw_open_aes128, 10, false, true, 1024)
-MI355X_WIN_KERNEL(mi355x_tls_winw_open_aes256, 14, false, true, 1024)
-MI355X_WIN_KERNEL(mi355x_gcm_win_seal_aes128, 10, true, false, 256)
-MI355X_WIN_KERNEL(mi355x_gcm_win_seal_aes256, 14, true, false, 256)
-MI355X_WIN_KERNEL(mi355x_gcm_win_open_aes128, 10, false, false, 256)
-MI355X_WIN_KERNEL(mi355x_gcm_win_open_aes256, 14, false, false, 256)
-MI355X_WIN_KERNEL(mi355x_gcm_winw_seal_aes128, 10, true, false, 1024)
-MI355X_WIN_KERNEL(mi355x_gcm_winw_seal_aes256, 14, true, false, 1024)
-MI355X_WIN_KERNEL(mi355x_gcm_winw_open_aes128, 10, false, false, 1024)
-MI355X_WIN_KERNEL(mi355x_gcm_winw_open_aes256, 14, false, false, 1024)
+MI355X_WIN_KERNEL(mi355x_tls_win_seal_aes128, 10, true, true, 512, 8)
+MI355X_WIN_KERNEL(mi355x_tls_win_seal_aes256, 14, true, true, 512, 8)
+MI355X_WIN_KERNEL(mi355x_tls_win_open_aes128, 10, false, true, 512, 8)
+MI355X_WIN_KERNEL(mi355x_tls_win_open_aes256, 14, false, true, 512, 8)
+MI355X_WIN_KERNEL(mi355x_tls_winw_seal_aes128, 10, true, true, 1024, 4)
+MI355X_WIN_KERNEL(mi355x_tls_winw_seal_aes256, 14, true, true, 1024, 4)
+MI355X_WIN_KERNEL(mi355x_tls_winw_open_aes128, 10, false, true, 1024, 4)
+MI355X_WIN_KERNEL(mi355x_tls_winw_open_aes256, 14, false, true, 1024, 4)
+MI355X_WIN_KERNEL(mi355x_gcm_win_seal_aes128, 10, true, false, 512, 8)
+MI355X_WIN_KERNEL(mi355x_gcm_win_seal_aes256, 14, true, false, 512, 8)
+MI355X_WIN_KERNEL(mi355x_gcm_win_open_aes128, 10, false, false, 512, 8)
+MI355X_WIN_KERNEL(mi355x_gcm_win_open_aes256, 14, false, false, 512, 8)
+MI355X_WIN_KERNEL(mi355x_gcm_winw_seal_aes128, 10, true, false, 1024, 4)
+MI355X_WIN_KERNEL(mi355x_gcm_winw_seal_aes256, 14, true, false, 1024, 4)
+MI355X_WIN_KERNEL(mi355x_gcm_winw_open_aes128, 10, false, false, 1024, 4)
+MI355X_WIN_KERNEL(mi355x_gcm_winw_open_aes256, 14, false, false, 1024, 4)
 
 /* key image: round keys, H and the nibble tables of H^1..H^8 and H^64 (cold path, one thread) */
 extern "C" __global__ void mi355x_gcm_setup(const uint8_t *key, uint32_t keylen, KeyImage *ki, int *rc)
@@ -495,8 +531,6 @@ static size_t g_window_records = 16384;
 /* AEAD batches (section 3) of at most this many records go to the window kernels (ptls_mi355x_set_aead_window_records):
  * the single-record slot calls and small batches, where 4 lanes per record would leave the GPU idle */
 static size_t g_aead_window_records = 768;
-/* single-record slot calls below this many bytes (payload + AAD) take the batch walk */
-constexpr size_t SLOT_WINDOW_MIN_BYTES = 2048;
 
 static int fail(const char *what, hipError_t e)
 {
@@ -575,7 +609,7 @@ static inline uint32_t le32(const uint8_t *p) { return (uint32_t)p[0] | (uint32_
 static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void *static_iv12, const void *recs,
                         const uint32_t *order, size_t n, const uint8_t *src, uint8_t *dst, const uint8_t *aad,
                         uint32_t *status, hipStream_t stream, bool frame = false, uint8_t *types = nullptr,
-                        const uint32_t *conn = nullptr, bool no_window = false)
+                        const uint32_t *conn = nullptr)
 {
     if (n == 0)
         return 0;
@@ -583,11 +617,12 @@ static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void
         snprintf(g_err, sizeof(g_err), "batch of %zu records exceeds 2^32-1", n);
         return -1;
     }
-    if (!no_window && n <= (frame ? g_window_records : g_aead_window_records)) {
+    if (n <= (frame ? g_window_records : g_aead_window_records)) {
         /*
          * small batch: the window kernels (segments of 64 GHASH positions in parallel).  Up to 3 records per CU:
-         * 256-thread groups of 3 records, so a few records spread over many CUs; above that, persistent
-         * 1024-thread groups of 15 records, one per CU.
+         * 512-thread groups of 3 records, 8 lanes (8 steps) per segment, so a few records spread over many CUs
+         * with short chains; above that, persistent 1024-thread groups of 15 records, 4 lanes per segment, one
+         * per CU.
          */
         typedef void (*win_kernel_t)(const KeyImage *, uint32_t, uint32_t, uint32_t, const void *, uint32_t,
                                      const uint8_t *, uint8_t *, const uint8_t *, uint32_t *, uint8_t *, const uint32_t *);
@@ -601,7 +636,8 @@ static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void
               {mi355x_tls_winw_seal_aes128, mi355x_tls_winw_seal_aes256}}}};
         const bool wide = n > 3u * (uint64_t)ctx->num_cu;
         const win_kernel_t wk = table[frame][wide][seal][ctx->key_size == 32];
-        const uint32_t threads = wide ? 1024u : 256u, per = (threads / 4u) / WIN_MAXSEG;
+        /* latency kernels: 512 threads, 8 lanes per segment; wide: 1024 threads, 4 lanes (MI355X_WIN_KERNEL list) */
+        const uint32_t threads = wide ? 1024u : 512u, per = (threads / (wide ? 4u : 8u)) / WIN_MAXSEG;
         uint64_t blocks = (n + per - 1) / per;
         if (wide && blocks > (uint64_t)ctx->num_cu)
             blocks = (uint64_t)ctx->num_cu;
@@ -906,11 +942,10 @@ static int single_record(ptls_mi355x_aesgcm_context_t *ctx, bool seal, void *out
     if (!seal)
         memcpy(ctx->h_stage + off_data + inlen, tag, 16);
     HIPCHK(hipMemcpyAsync(ctx->d_stage, ctx->h_stage, off_status, hipMemcpyHostToDevice, ctx->stream));
-    /* one record: the window kernels pay off from about 2 KiB (segments in parallel), below that the batch walk
-     * is shorter than the window kernels' LDS fill (scripts/slot_latency.py, profiles/r01c_slot_latency.json) */
+    /* one record: the window kernels (8-lane segments in parallel, leading pad steps skipped) are as fast as the
+     * batch walk at 64 B and faster above it (scripts/slot_latency.py, profiles/r01f_slot_latency.txt) */
     if (launch_batch(ctx, seal, nonce12, (const Record *)ctx->d_stage, nullptr, 1, ctx->d_stage, ctx->d_stage, ctx->d_stage,
-                     (uint32_t *)(ctx->d_stage + off_status), ctx->stream, false, nullptr, nullptr,
-                     inlen + aadlen < SLOT_WINDOW_MIN_BYTES) != 0)
+                     (uint32_t *)(ctx->d_stage + off_status), ctx->stream, false, nullptr, nullptr) != 0)
         return -1;
     const size_t outlen = seal ? inlen + 16 : inlen;
     HIPCHK(hipMemcpyAsync(ctx->h_stage + off_data, ctx->d_stage + off_data, outlen, hipMemcpyDeviceToHost, ctx->stream));
@@ -964,3 +999,11 @@ int ptls_mi355x_aesecb_encrypt(ptls_mi355x_aesgcm_context_t *ctx, void *output, 
 }
 
 } /* extern "C" */
+
+#if GCM_WIN_TIMING
+/* measurement builds: the phase stamps of the last window launch (s_memrealtime ticks, 100 MHz) */
+extern "C" int ptls_mi355x_debug_window_times(uint64_t *out)
+{
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_win_times), sizeof(uint64_t) * 8) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -18,6 +18,17 @@ using namespace mi355x;
 
 static constexpr AesTables kTabs{};
 
+/* lanes per 64-position segment of the window math: 8 (latency kernels) or 4 (wide kernels) */
+static int g_window_lanes = 8;
+extern "C" int model_set_window_lanes(int kw)
+{
+    if (kw != 4 && kw != 8)
+        return -1;
+    const int prev = g_window_lanes;
+    g_window_lanes = kw;
+    return prev;
+}
+
 template <int NR, int K, bool SEAL>
 static void run(const KeyImage *ki, const uint8_t *lds, const uint8_t *static_iv, const Record *recs, size_t n,
                 const uint8_t *src, uint8_t *dst, const uint8_t *aad, uint32_t *status)
@@ -105,7 +116,7 @@ static void run_tls(const KeyImage *ki, const uint8_t *lds, const uint8_t *stati
 
 /* the window kernels' math (tls_window_body): per record, every 64-position segment walked by 4 lanes, sums
  * joined by Horner with H^64 (records above WIN_MAXSEG segments walked whole, as the kernel does) */
-template <int NR, bool SEAL>
+template <int NR, bool SEAL, int KW>
 static void run_tls_window(const KeyImage *ki, const uint8_t *lds, const uint8_t *static_iv, const TlsRecord *trecs,
                            size_t n, const uint8_t *src, uint8_t *dst, uint32_t *status, uint8_t *types,
                            const uint32_t *conn)
@@ -135,22 +146,22 @@ static void run_tls_window(const KeyImage *ki, const uint8_t *lds, const uint8_t
         const uint32_t n1 = iv1 ^ bswap32((uint32_t)(r.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)r.seq);
         const uint32_t n0 = conn ? iv0 ^ bswap32(conn[i]) : iv0;
         uint32_t nseg;
-        window_segment(1, (plen + 15) / 16, 0, &nseg);
+        window_segment(1, (plen + 15) / 16, 0, &nseg, KW);
         u32x4 acc = {0, 0, 0, 0};
         if (nseg > WIN_MAXSEG) {
-            const Walk wk = make_walk(plen, 5, 4, walk_out16(dst + r.dst));
-            for (uint32_t j = 0; j < 4; ++j)
-                acc ^= lane_walk<NR, 4, SEAL, true, LayoutWin>(lds, 4u * j | 0x10000u, ki->rk, j, r, true, wk.T, n0, n1, n2,
+            const Walk wk = make_walk(plen, 5, KW, walk_out16(dst + r.dst));
+            for (uint32_t j = 0; j < (uint32_t)KW; ++j)
+                acc ^= lane_walk<NR, KW, SEAL, true, LayoutWin<KW>, 3>(lds, 4u * j | 0x10000u, ki->rk, j, r, true, wk.T, n0, n1, n2,
                                                                src, dst, nullptr, (const uint8_t *)trecs, t.type);
         } else {
             for (uint32_t sg = 0; sg < nseg; ++sg) {
-                const Walk sw = window_segment(1, (plen + 15) / 16, sg, &nseg);
+                const Walk sw = window_segment(1, (plen + 15) / 16, sg, &nseg, KW);
                 u32x4 part = {0, 0, 0, 0};
-                for (uint32_t j = 0; j < 4; ++j)
-                    part ^= lane_walk<NR, 4, SEAL, true, LayoutWin>(lds, 4u * j | 0x10000u, ki->rk, j, r, true, sw.T, n0, n1,
+                for (uint32_t j = 0; j < (uint32_t)KW; ++j)
+                    part ^= lane_walk<NR, KW, SEAL, true, LayoutWin<KW>, 3>(lds, 4u * j | 0x10000u, ki->rk, j, r, true, sw.T, n0, n1,
                                                                     n2, src, dst, nullptr, (const uint8_t *)trecs, t.type,
                                                                     &sw);
-                acc = sg == 0 ? part : ghash_mul_lds(lds, LayoutWin::gh64, acc) ^ part;
+                acc = sg == 0 ? part : ghash_mul_lds_wide(lds, LayoutWin<KW>::gh64, acc) ^ part;
             }
         }
         if (SEAL) {
@@ -172,8 +183,8 @@ static void run_tls_window(const KeyImage *ki, const uint8_t *lds, const uint8_t
     }
 }
 
-/* the window kernels' math for AEAD records (any AAD length): segments joined with H^64 */
-template <int NR, bool SEAL>
+/* the window kernels' math for AEAD records (any AAD length): segments joined with H^64, KW lanes per segment */
+template <int NR, bool SEAL, int KW>
 static void run_window(const KeyImage *ki, const uint8_t *lds, const uint8_t *static_iv, const Record *recs, size_t n,
                        const uint8_t *src, uint8_t *dst, const uint8_t *aad, uint32_t *status)
 {
@@ -186,21 +197,21 @@ static void run_window(const KeyImage *ki, const uint8_t *lds, const uint8_t *st
         const uint32_t n1 = iv1 ^ bswap32((uint32_t)(r.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)r.seq);
         const uint32_t A = (r.aadlen + 15) / 16, C = (r.len + 15) / 16;
         uint32_t nseg;
-        window_segment(A, C, 0, &nseg);
+        window_segment(A, C, 0, &nseg, KW);
         u32x4 acc = {0, 0, 0, 0};
         if (nseg > WIN_MAXSEG) {
-            const Walk wk = make_walk(r.len, r.aadlen, 4, walk_out16(dst + r.dst));
-            for (uint32_t j = 0; j < 4; ++j)
-                acc ^= lane_walk<NR, 4, SEAL, false, LayoutWin>(lds, 4u * j | 0x10000u, ki->rk, j, r, true, wk.T, iv0, n1, n2,
+            const Walk wk = make_walk(r.len, r.aadlen, KW, walk_out16(dst + r.dst));
+            for (uint32_t j = 0; j < (uint32_t)KW; ++j)
+                acc ^= lane_walk<NR, KW, SEAL, false, LayoutWin<KW>, 3>(lds, 4u * j | 0x10000u, ki->rk, j, r, true, wk.T, iv0, n1, n2,
                                                                 src, dst, aad, (const uint8_t *)recs);
         } else {
             for (uint32_t sg = 0; sg < nseg; ++sg) {
-                const Walk sw = window_segment(A, C, sg, &nseg);
+                const Walk sw = window_segment(A, C, sg, &nseg, KW);
                 u32x4 part = {0, 0, 0, 0};
-                for (uint32_t j = 0; j < 4; ++j)
-                    part ^= lane_walk<NR, 4, SEAL, false, LayoutWin>(lds, 4u * j | 0x10000u, ki->rk, j, r, true, sw.T, iv0,
+                for (uint32_t j = 0; j < (uint32_t)KW; ++j)
+                    part ^= lane_walk<NR, KW, SEAL, false, LayoutWin<KW>, 3>(lds, 4u * j | 0x10000u, ki->rk, j, r, true, sw.T, iv0,
                                                                      n1, n2, src, dst, aad, (const uint8_t *)recs, 0u, &sw);
-                acc = sg == 0 ? part : ghash_mul_lds(lds, LayoutWin::gh64, acc) ^ part;
+                acc = sg == 0 ? part : ghash_mul_lds_wide(lds, LayoutWin<KW>::gh64, acc) ^ part;
             }
         }
         if (SEAL)
@@ -221,13 +232,18 @@ extern "C" int model_batch_window(int is_seal, const uint8_t *key, size_t keylen
         free(lds);
         return -1;
     }
-    fill_lds_window(lds, kTabs.t0, ki, 0, 1);
-    if (ki->rounds == 10)
-        is_seal ? run_window<10, true>(ki, lds, static_iv, recs, n, src, dst, aad, status)
-                : run_window<10, false>(ki, lds, static_iv, recs, n, src, dst, aad, status);
-    else
-        is_seal ? run_window<14, true>(ki, lds, static_iv, recs, n, src, dst, aad, status)
-                : run_window<14, false>(ki, lds, static_iv, recs, n, src, dst, aad, status);
+    fill_lds_window(lds, kTabs.t0, ki, 0, 1, (uint32_t)g_window_lanes);
+#define WIN_CASE(KWV)                                                                                                  \
+    if (g_window_lanes == KWV) {                                                                                       \
+        if (ki->rounds == 10)                                                                                          \
+            is_seal ? run_window<10, true, KWV>(ki, lds, static_iv, recs, n, src, dst, aad, status)                    \
+                    : run_window<10, false, KWV>(ki, lds, static_iv, recs, n, src, dst, aad, status);                  \
+        else                                                                                                           \
+            is_seal ? run_window<14, true, KWV>(ki, lds, static_iv, recs, n, src, dst, aad, status)                    \
+                    : run_window<14, false, KWV>(ki, lds, static_iv, recs, n, src, dst, aad, status);                  \
+    }
+    WIN_CASE(4) WIN_CASE(8)
+#undef WIN_CASE
     free(ki);
     free(lds);
     return 0;
@@ -244,13 +260,18 @@ extern "C" int model_tls_window(int is_seal, const uint8_t *key, size_t keylen, 
         free(lds);
         return -1;
     }
-    fill_lds_window(lds, kTabs.t0, ki, 0, 1);
-    if (ki->rounds == 10)
-        is_seal ? run_tls_window<10, true>(ki, lds, static_iv, trecs, n, src, dst, status, types, conn)
-                : run_tls_window<10, false>(ki, lds, static_iv, trecs, n, src, dst, status, types, conn);
-    else
-        is_seal ? run_tls_window<14, true>(ki, lds, static_iv, trecs, n, src, dst, status, types, conn)
-                : run_tls_window<14, false>(ki, lds, static_iv, trecs, n, src, dst, status, types, conn);
+    fill_lds_window(lds, kTabs.t0, ki, 0, 1, (uint32_t)g_window_lanes);
+#define WIN_CASE(KWV)                                                                                                  \
+    if (g_window_lanes == KWV) {                                                                                       \
+        if (ki->rounds == 10)                                                                                          \
+            is_seal ? run_tls_window<10, true, KWV>(ki, lds, static_iv, trecs, n, src, dst, status, types, conn)       \
+                    : run_tls_window<10, false, KWV>(ki, lds, static_iv, trecs, n, src, dst, status, types, conn);     \
+        else                                                                                                           \
+            is_seal ? run_tls_window<14, true, KWV>(ki, lds, static_iv, trecs, n, src, dst, status, types, conn)       \
+                    : run_tls_window<14, false, KWV>(ki, lds, static_iv, trecs, n, src, dst, status, types, conn);     \
+    }
+    WIN_CASE(4) WIN_CASE(8)
+#undef WIN_CASE
     free(ki);
     free(lds);
     return 0;
