@@ -870,6 +870,7 @@ struct KeyImage {
     uint8_t H[16];      /* E_K(0^128) */
     uint8_t gh[MAX_K][32][16][16]; /* gh[p-1] = nibble tables of H^p, p = 1..MAX_K */
     uint8_t gh64[32][16][16];      /* nibble tables of H^64: joins the 64-position segments of the window kernels */
+    uint8_t gh256[32][16][16];     /* nibble tables of H^256: joins groups of 4 segments (window_join) */
 };
 
 /* ------------------------------------------------------------------ record walk ----------- */
@@ -1068,6 +1069,10 @@ GCM_HD int build_key_image(const uint8_t *sbox, const uint8_t *key, uint32_t key
     for (int sq = 0; sq < 3; ++sq)
         gf128_mul_bytes(hp, hp, hp);
     nibble_tables(hp, ki->gh64);
+    /* H^256 = (H^64)^4 */
+    for (int sq = 0; sq < 2; ++sq)
+        gf128_mul_bytes(hp, hp, hp);
+    nibble_tables(hp, ki->gh256);
     return 0;
 }
 
@@ -1139,14 +1144,15 @@ struct LayoutWin {
     static constexpr uint32_t aes_base = 0u;
     static constexpr uint32_t gh_base = 0x10000u;
     static constexpr uint32_t gh64 = gh_base + (uint32_t)KW * GH_TABLE_BYTES;
-    static constexpr uint32_t parts = gh64 + GH_TABLE_BYTES;
+    static constexpr uint32_t gh256 = gh64 + GH_TABLE_BYTES;
+    static constexpr uint32_t parts = gh256 + GH_TABLE_BYTES;
 };
 enum : uint32_t {
     WIN_SEG = 64,    /* GHASH positions per segment: 4 lanes x 16 steps */
     WIN_MAXSEG = 17, /* segments of the largest TLS record (16640-byte record: 1 + 1039 + 1 positions) */
 };
 
-/* vector v of the window image: AES image A (T0 | T1 rows) for v < 4096, then the kw + 1 GHASH tables */
+/* vector v of the window image: AES image A (T0 | T1 rows) for v < 4096, then the kw + 2 GHASH tables */
 GCM_HD u32x4 window_image_vec(const uint32_t *t0, const KeyImage *ki, uint32_t v, uint32_t kw)
 {
     if (v < 0x10000u / 16u) {
@@ -1155,7 +1161,8 @@ GCM_HD u32x4 window_image_vec(const uint32_t *t0, const KeyImage *ki, uint32_t v
         return u32x4{w, w, w, w};
     }
     const uint32_t i = v - 0x10000u / 16u, slot = i / (GH_TABLE_BYTES / 16u), within = i % (GH_TABLE_BYTES / 16u);
-    const u32x4 *srcv = slot < kw ? (const u32x4 *)ki->gh[kw - 1u - slot] : (const u32x4 *)ki->gh64;
+    const u32x4 *srcv = slot < kw ? (const u32x4 *)ki->gh[kw - 1u - slot]
+                                  : slot == kw ? (const u32x4 *)ki->gh64 : (const u32x4 *)ki->gh256;
     return srcv[within];
 }
 
@@ -1166,7 +1173,7 @@ GCM_HD u32x4 window_image_vec(const uint32_t *t0, const KeyImage *ki, uint32_t v
 GCM_HD void fill_lds_window(uint8_t *lds, const uint32_t *t0, const KeyImage *ki, uint32_t tid, uint32_t nthr,
                             uint32_t kw = 4u)
 {
-    const uint32_t total = 0x10000u / 16u + (kw + 1u) * GH_TABLE_BYTES / 16u;
+    const uint32_t total = 0x10000u / 16u + (kw + 2u) * GH_TABLE_BYTES / 16u;
     for (uint32_t base = tid; base < total; base += 8u * nthr) {
         u32x4 v[8];
 #pragma unroll
@@ -1195,6 +1202,21 @@ GCM_HD Walk window_segment(uint32_t A, uint32_t C, uint32_t seg, uint32_t *nseg,
     w.T = WIN_SEG / kw; /* kw lanes per segment */
     w.pad = WIN_SEG * *nseg - g - WIN_SEG * seg;
     return w;
+}
+
+/*
+ * Joining a record's segment sums P_0..P_{ns-1}: GHASH = sum_s P_s * H^(64 (ns-1-s)).  The segments are
+ * grouped in fours aligned to the record's END (the first group holds the ns mod 4 leftovers), so every group
+ * after the first spans exactly 4 segments: phase A folds each group with H^64 (<= 3 multiplies, all groups
+ * in parallel), phase B chains the groups with H^256 (<= 4 multiplies for 17 segments) -- 7 dependent
+ * multiplies instead of 16.  window_group_end(s) is one past the last segment of the group led by s.
+ */
+GCM_HD uint32_t window_group_offset(uint32_t ns) { return (4u - ns % 4u) % 4u; }
+GCM_HD bool window_group_leader(uint32_t s, uint32_t ns) { return s < ns && (s == 0u || (s + window_group_offset(ns)) % 4u == 0u); }
+GCM_HD uint32_t window_group_end(uint32_t s, uint32_t ns)
+{
+    const uint32_t o = window_group_offset(ns), e = ((s + o) & ~3u) + 4u - o;
+    return e < ns ? e : ns;
 }
 
 /* ------------------------------------------------------------------ per-lane record walk -- */

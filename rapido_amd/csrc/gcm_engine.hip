@@ -357,14 +357,24 @@ __device__ __forceinline__ void window_body(const KeyImage *__restrict__ ki, uin
             *(u32x4 *)(lds + LW::parts + (rl * WIN_MAXSEG + seg) * 16u) = part;
         __syncthreads();
         WIN_STAMP(3);
+        /* join, phase A: each group leader folds its (up to 4) segments with H^64, in place (window_group_end) */
+        const uint32_t ns = whole ? 1u : nseg;
+        if (in_batch && valid && window_group_leader(seg, ns)) {
+            u32x4 g = *(const u32x4 *)(lds + LW::parts + (rl * WIN_MAXSEG + seg) * 16u);
+            const uint32_t gend = window_group_end(seg, ns);
+            for (uint32_t k = seg + 1u; k < gend; ++k)
+                g = (LATENCY ? ghash_mul_lds_wide(lds, LW::gh64, g) : ghash_mul_lds(lds, LW::gh64, g)) ^
+                    *(const u32x4 *)(lds + LW::parts + (rl * WIN_MAXSEG + k) * 16u);
+            *(u32x4 *)(lds + LW::parts + (rl * WIN_MAXSEG + seg) * 16u) = g;
+        }
+        __syncthreads();
         if (in_batch && seg == 0u) {
-            /* the record's first slot joins the segment sums: tag (seal) or tag ^ received tag (open) */
+            /* phase B: the record's first slot chains the groups with H^256: tag (seal) or tag ^ received tag (open) */
             u32x4 acc = {0u, 0u, 0u, 0u};
             if (valid) {
-                const uint32_t ns = whole ? 1u : nseg;
                 acc = *(const u32x4 *)(lds + LW::parts + rl * WIN_MAXSEG * 16u);
-                for (uint32_t k = 1; k < ns; ++k)
-                    acc = (LATENCY ? ghash_mul_lds_wide(lds, LW::gh64, acc) : ghash_mul_lds(lds, LW::gh64, acc)) ^
+                for (uint32_t k = window_group_end(0u, ns); k < ns; k += 4u)
+                    acc = (LATENCY ? ghash_mul_lds_wide(lds, LW::gh256, acc) : ghash_mul_lds(lds, LW::gh256, acc)) ^
                           *(const u32x4 *)(lds + LW::parts + (rl * WIN_MAXSEG + k) * 16u);
             }
             WIN_STAMP(4);

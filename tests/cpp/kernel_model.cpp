@@ -60,6 +60,24 @@ struct TlsRecord {
     uint32_t len, type;
 };
 
+/* the window kernels' two-phase join (window_group_*): groups of 4 folded with H^64, chained with H^256 */
+template <int KW>
+static u32x4 model_window_join(const uint8_t *lds, u32x4 *parts, uint32_t ns)
+{
+    for (uint32_t s = 0; s < ns; ++s) {
+        if (!window_group_leader(s, ns))
+            continue;
+        u32x4 g = parts[s];
+        for (uint32_t k = s + 1; k < window_group_end(s, ns); ++k)
+            g = ghash_mul_lds_wide(lds, LayoutWin<KW>::gh64, g) ^ parts[k];
+        parts[s] = g;
+    }
+    u32x4 acc = parts[0];
+    for (uint32_t k = window_group_end(0, ns); k < ns; k += 4)
+        acc = ghash_mul_lds_wide(lds, LayoutWin<KW>::gh256, acc) ^ parts[k];
+    return acc;
+}
+
 /* the FRAME walk (TLS 1.3 record framing) with the framing kernels' prologue/epilogue, K = 4 */
 template <int NR, bool SEAL>
 static void run_tls(const KeyImage *ki, const uint8_t *lds, const uint8_t *static_iv, const TlsRecord *trecs, size_t n,
@@ -154,6 +172,7 @@ static void run_tls_window(const KeyImage *ki, const uint8_t *lds, const uint8_t
                 acc ^= lane_walk<NR, KW, SEAL, true, LayoutWin<KW>, 3>(lds, 4u * j | 0x10000u, ki->rk, j, r, true, wk.T, n0, n1, n2,
                                                                src, dst, nullptr, (const uint8_t *)trecs, t.type);
         } else {
+            u32x4 parts[WIN_MAXSEG];
             for (uint32_t sg = 0; sg < nseg; ++sg) {
                 const Walk sw = window_segment(1, (plen + 15) / 16, sg, &nseg, KW);
                 u32x4 part = {0, 0, 0, 0};
@@ -161,8 +180,9 @@ static void run_tls_window(const KeyImage *ki, const uint8_t *lds, const uint8_t
                     part ^= lane_walk<NR, KW, SEAL, true, LayoutWin<KW>, 3>(lds, 4u * j | 0x10000u, ki->rk, j, r, true, sw.T, n0, n1,
                                                                     n2, src, dst, nullptr, (const uint8_t *)trecs, t.type,
                                                                     &sw);
-                acc = sg == 0 ? part : ghash_mul_lds_wide(lds, LayoutWin<KW>::gh64, acc) ^ part;
+                parts[sg] = part;
             }
+            acc = model_window_join<KW>(lds, parts, nseg);
         }
         if (SEAL) {
             memcpy(dst + r.dst + plen, &acc, 16);
@@ -205,14 +225,16 @@ static void run_window(const KeyImage *ki, const uint8_t *lds, const uint8_t *st
                 acc ^= lane_walk<NR, KW, SEAL, false, LayoutWin<KW>, 3>(lds, 4u * j | 0x10000u, ki->rk, j, r, true, wk.T, iv0, n1, n2,
                                                                 src, dst, aad, (const uint8_t *)recs);
         } else {
+            u32x4 parts[WIN_MAXSEG];
             for (uint32_t sg = 0; sg < nseg; ++sg) {
                 const Walk sw = window_segment(A, C, sg, &nseg, KW);
                 u32x4 part = {0, 0, 0, 0};
                 for (uint32_t j = 0; j < (uint32_t)KW; ++j)
                     part ^= lane_walk<NR, KW, SEAL, false, LayoutWin<KW>, 3>(lds, 4u * j | 0x10000u, ki->rk, j, r, true, sw.T, iv0,
                                                                      n1, n2, src, dst, aad, (const uint8_t *)recs, 0u, &sw);
-                acc = sg == 0 ? part : ghash_mul_lds_wide(lds, LayoutWin<KW>::gh64, acc) ^ part;
+                parts[sg] = part;
             }
+            acc = model_window_join<KW>(lds, parts, nseg);
         }
         if (SEAL)
             memcpy(dst + r.dst + r.len, &acc, 16);
