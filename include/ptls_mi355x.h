@@ -253,6 +253,13 @@ size_t ptls_mi355x_set_tls_window_records(size_t n);
 /* the same for the AEAD batch calls (section 3) and the single-record slot calls, which are batches of
  * one: up to n records run on the window kernels.  Default 768; returns the previous value. */
 size_t ptls_mi355x_set_aead_window_records(size_t n);
+/*
+ * Single-record slot calls (ptls_mi355x_aesgcm_encrypt/decrypt, the ptls_aead slot) whose staged bytes
+ * (64 + AAD + record + tag, 16-byte rounded) are at most n run zero-copy: the kernel reads the record from
+ * the context's pinned staging buffer and writes the result back into it over PCIe, with no DMA copies.
+ * Larger ones are copied in and out.  Returns the previous value (default 1 MiB).  Process-wide.
+ */
+size_t ptls_mi355x_set_slot_zero_copy_bytes(size_t n);
 /* name of the kernel symbol the next batch launch with these parameters uses (for profiling) */
 const char *ptls_mi355x_kernel_name(int is_seal, size_t key_size);
 /* last HIP error string seen by the engine ("" if none) */

@@ -526,7 +526,8 @@ struct st_ptls_mi355x_aesgcm_context {
     KeyImage *d_ki;
     hipStream_t stream;  /* private stream for the synchronous single-record calls */
     uint8_t *d_stage;    /* device staging for single-record calls */
-    uint8_t *h_stage;    /* pinned host staging */
+    uint8_t *h_stage;    /* pinned host staging (mapped, coherent) */
+    uint8_t *h_stage_dev; /* h_stage as the GPU addresses it: zero-copy slot calls read and write it directly */
     size_t stage_cap;
     uint32_t *d_work;    /* WORK_SLOTS dynamic-scheduling counters, zeroed per launch */
     uint32_t work_next;
@@ -541,6 +542,8 @@ static size_t g_window_records = 16384;
 /* AEAD batches (section 3) of at most this many records go to the window kernels (ptls_mi355x_set_aead_window_records):
  * the single-record slot calls and small batches, where 4 lanes per record would leave the GPU idle */
 static size_t g_aead_window_records = 768;
+/* single-record slot calls staging at most this many bytes run zero-copy (ptls_mi355x_set_slot_zero_copy_bytes) */
+static size_t g_slot_zero_copy_bytes = 1u << 20;
 
 static int fail(const char *what, hipError_t e)
 {
@@ -693,9 +696,12 @@ static int ensure_stage(ptls_mi355x_aesgcm_context_t *ctx, size_t need)
         (void)hipHostFree(ctx->h_stage);
     ctx->d_stage = nullptr;
     ctx->h_stage = nullptr;
+    ctx->h_stage_dev = nullptr;
     ctx->stage_cap = 0;
     HIPCHK(hipMalloc(&ctx->d_stage, cap));
-    HIPCHK(hipHostMalloc(&ctx->h_stage, cap, hipHostMallocDefault));
+    /* coherent: the GPU's zero-copy reads never see stale cache lines of a previous call */
+    HIPCHK(hipHostMalloc(&ctx->h_stage, cap, hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostGetDevicePointer((void **)&ctx->h_stage_dev, ctx->h_stage, 0));
     ctx->stage_cap = cap;
     return 0;
 }
@@ -739,6 +745,13 @@ size_t ptls_mi355x_set_aead_window_records(size_t n)
 {
     const size_t prev = g_aead_window_records;
     g_aead_window_records = n;
+    return prev;
+}
+
+size_t ptls_mi355x_set_slot_zero_copy_bytes(size_t n)
+{
+    const size_t prev = g_slot_zero_copy_bytes;
+    g_slot_zero_copy_bytes = n;
     return prev;
 }
 
@@ -951,16 +964,27 @@ static int single_record(ptls_mi355x_aesgcm_context_t *ctx, bool seal, void *out
         memcpy(ctx->h_stage + off_data, input, inlen);
     if (!seal)
         memcpy(ctx->h_stage + off_data + inlen, tag, 16);
-    HIPCHK(hipMemcpyAsync(ctx->d_stage, ctx->h_stage, off_status, hipMemcpyHostToDevice, ctx->stream));
+    /*
+     * Zero-copy up to g_slot_zero_copy_bytes staged bytes: the kernel reads the record from the pinned staging
+     * buffer over PCIe and writes the result back into it, so a call is one launch and one synchronisation
+     * instead of an H2D copy, the launch, a D2H copy and the synchronisation.  Larger records are copied.
+     */
+    const bool zc = total <= g_slot_zero_copy_bytes;
+    uint8_t *base = zc ? ctx->h_stage_dev : ctx->d_stage;
+    if (!zc)
+        HIPCHK(hipMemcpyAsync(ctx->d_stage, ctx->h_stage, off_status, hipMemcpyHostToDevice, ctx->stream));
     /* one record: the window kernels (8-lane segments in parallel, leading pad steps skipped) are as fast as the
      * batch walk at 64 B and faster above it (scripts/slot_latency.py, profiles/r01f_slot_latency.txt) */
-    if (launch_batch(ctx, seal, nonce12, (const Record *)ctx->d_stage, nullptr, 1, ctx->d_stage, ctx->d_stage, ctx->d_stage,
-                     (uint32_t *)(ctx->d_stage + off_status), ctx->stream, false, nullptr, nullptr) != 0)
+    if (launch_batch(ctx, seal, nonce12, (const Record *)base, nullptr, 1, base, base, base,
+                     (uint32_t *)(base + off_status), ctx->stream, false, nullptr, nullptr) != 0)
         return -1;
     const size_t outlen = seal ? inlen + 16 : inlen;
-    HIPCHK(hipMemcpyAsync(ctx->h_stage + off_data, ctx->d_stage + off_data, outlen, hipMemcpyDeviceToHost, ctx->stream));
-    if (!seal)
-        HIPCHK(hipMemcpyAsync(ctx->h_stage + off_status, ctx->d_stage + off_status, 4, hipMemcpyDeviceToHost, ctx->stream));
+    if (!zc) {
+        HIPCHK(hipMemcpyAsync(ctx->h_stage + off_data, ctx->d_stage + off_data, outlen, hipMemcpyDeviceToHost, ctx->stream));
+        if (!seal)
+            HIPCHK(hipMemcpyAsync(ctx->h_stage + off_status, ctx->d_stage + off_status, 4, hipMemcpyDeviceToHost,
+                                  ctx->stream));
+    }
     HIPCHK(hipStreamSynchronize(ctx->stream));
     if (outlen)
         memcpy(output, ctx->h_stage + off_data, outlen);

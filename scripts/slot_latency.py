@@ -1,6 +1,7 @@
 """Latency of the synchronous AEAD slot (ptls_aead_encrypt / ptls_aead_decrypt through the exported
 ptls_aead_algorithm_t, as picotls' record layer calls it) and of the streaming record-layer sequence,
-per record size.  Host buffers in, host buffers out (one GPU round trip per call)."""
+per record size.  Host buffers in, host buffers out (one GPU round trip per call): zero-copy (the kernel
+reads and writes the pinned staging buffer over PCIe) or DMA copies in and out."""
 import json
 import os
 import sys
@@ -19,8 +20,10 @@ def main():
     enc = ra.aead_new_direct("aes128gcm", True, key, iv)
     dec = ra.aead_new_direct("aes128gcm", False, key, iv)
     res = {}
-    for mode, limit in (("window", 1 << 30), ("batch", 0)):
+    # window kernels zero-copy (the default), window kernels with DMA copies, batch kernels with DMA copies
+    for mode, limit, zc in (("window-zerocopy", 1 << 30, 1 << 30), ("window-copy", 1 << 30, 0), ("batch-copy", 0, 0)):
         ra.set_aead_window_records(limit)
+        ra.set_slot_zero_copy_bytes(zc)
         for L in (64, 1400, 4096, 16384):
             pt = bytes(i & 0xFF for i in range(L))
             aad = bytes([0x17, 3, 3, (L + 16) >> 8, (L + 16) & 0xFF])
@@ -38,6 +41,8 @@ def main():
             res[f"{mode}/{L}"] = {"encrypt_us": round((t1 - t0) / reps * 1e6, 1),
                                   "decrypt_us": round((t2 - t1) / reps * 1e6, 1)}
             print(mode, L, res[f"{mode}/{L}"], flush=True)
+    ra.set_aead_window_records(768)
+    ra.set_slot_zero_copy_bytes(1 << 20)
     print(json.dumps(res))
 
 
