@@ -187,6 +187,32 @@ def test_slot_gcm_basic_and_iv96(gpu):
     a.free()
 
 
+@pytest.mark.parametrize("zero_copy", [True, False])
+def test_slot_zero_copy_and_copied(gpu, zero_copy):
+    """The slot's two staging paths (the kernel reading/writing pinned host memory, or DMA copies in and out) give
+    the oracle's bytes for every size class, and a tampered tag fails without releasing plaintext."""
+    prev = ra.set_slot_zero_copy_bytes(1 << 30 if zero_copy else 0)
+    try:
+        rng = np.random.default_rng(5 if zero_copy else 6)
+        key, iv = rng.integers(0, 256, 16, dtype=np.uint8).tobytes(), rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+        a = ra.aead_new_direct("aes128gcm", True, key, iv)
+        d = ra.aead_new_direct("aes128gcm", False, key, iv)
+        for n, alen in [(0, 0), (1, 5), (15, 13), (16, 0), (1400, 5), (4097, 33), (16384, 5), (20000, 100)]:
+            pt = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+            aad = rng.integers(0, 256, alen, dtype=np.uint8).tobytes()
+            seq = int(rng.integers(0, 2 ** 48))
+            ct = a.encrypt(pt, seq, aad)
+            assert ct == oracle.seal(key, oracle.build_iv(iv, seq), aad, pt), n
+            assert d.decrypt(ct, seq, aad) == pt
+            bad = bytearray(ct)
+            bad[-1] ^= 1
+            assert d.decrypt(bytes(bad), seq, aad) is None
+        a.free()
+        d.free()
+    finally:
+        ra.set_slot_zero_copy_bytes(prev)
+
+
 @pytest.mark.parametrize("algo,keylen", [("aes128gcm", 16), ("aes256gcm", 32)])
 def test_slot_streaming_and_record_layer(gpu, algo, keylen):
     """The TLS record-layer call sequence (lib/picotls.c:630-643) and t/picotls.c:161-198."""
