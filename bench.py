@@ -79,7 +79,7 @@ def cpu_baseline(wl: dict, threads: int) -> dict:
         ref = oracle.Reference()
         if not ref.supported():
             raise RuntimeError("CPU lacks AES-NI/PCLMUL/AVX2")
-        per_thread = max(2000, int(1.5e9 / length))  # ~1.5 GB sealed (+ opened) per thread
+        per_thread = max(2000, int(3e9 / length))  # ~3 GB sealed (+ opened) per thread: ~10-20 s of CPU work
         s1, o1, _, f1 = ref.bench(wl["key"], length, 5, per_thread, 1)
         sN, oN, wall, fN = ref.bench(wl["key"], length, 5, per_thread, threads)
         if f1 or fN:
@@ -117,7 +117,8 @@ def main() -> None:
     ap.add_argument("--lanes", type=int, default=0, help="lanes per record (1/2/4/8); 0 = engine default")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--e2e", action="store_true", help="also time the PCIe-inclusive path (pinned host in/out)")
+    ap.add_argument("--e2e", action="store_true", help="time the PCIe-inclusive path (pinned host in/out); default at N=1")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive path")
     ap.add_argument("--check", type=int, default=64, help="records re-checked against the CPU oracle after timing")
     args = ap.parse_args()
 
@@ -294,7 +295,7 @@ def main() -> None:
                                     f"{lds_cycles_per_block:.2f} LDS clk/block/CU, {ncu} CU x {LDS_CLOCK_GHZ} GHz",
                            "note": "this read mix alone sustains 0.78 of the nominal rate (profiles/r01c_lds_ceiling.json)"}
 
-    if args.e2e:
+    if (args.e2e or world == 1) and not args.no_e2e:
         # PCIe-inclusive: records start and end in pinned host memory
         h_src = torch.empty(src_bytes, dtype=torch.uint8, pin_memory=True)
         h_dst = torch.empty(src_bytes, dtype=torch.uint8, pin_memory=True)
