@@ -541,7 +541,7 @@ static int g_lanes = 4;
 static size_t g_window_records = 16384;
 /* AEAD batches (section 3) of at most this many records go to the window kernels (ptls_mi355x_set_aead_window_records):
  * the single-record slot calls and small batches, where 4 lanes per record would leave the GPU idle */
-static size_t g_aead_window_records = 768;
+static size_t g_aead_window_records = 2048; /* break-even of 1400-B records (scripts/window_bench.py aead_batches) */
 /* single-record slot calls staging at most this many bytes run zero-copy (ptls_mi355x_set_slot_zero_copy_bytes) */
 static size_t g_slot_zero_copy_bytes = 1u << 20;
 
@@ -632,10 +632,10 @@ static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void
     }
     if (n <= (frame ? g_window_records : g_aead_window_records)) {
         /*
-         * small batch: the window kernels (segments of 64 GHASH positions in parallel).  Up to 3 records per CU:
+         * small batch: the window kernels (segments of 64 GHASH positions in parallel).  Up to 15 records per CU:
          * 512-thread groups of 3 records, 8 lanes (8 steps) per segment, so a few records spread over many CUs
-         * with short chains; above that, persistent 1024-thread groups of 15 records, 4 lanes per segment, one
-         * per CU.
+         * with short chains; above that, when they fill every CU, persistent 1024-thread groups of 15 records,
+         * 4 lanes per segment, one per CU.
          */
         typedef void (*win_kernel_t)(const KeyImage *, uint32_t, uint32_t, uint32_t, const void *, uint32_t,
                                      const uint8_t *, uint8_t *, const uint8_t *, uint32_t *, uint8_t *, const uint32_t *);
@@ -647,7 +647,7 @@ static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void
             {{{mi355x_tls_win_open_aes128, mi355x_tls_win_open_aes256}, {mi355x_tls_win_seal_aes128, mi355x_tls_win_seal_aes256}},
              {{mi355x_tls_winw_open_aes128, mi355x_tls_winw_open_aes256},
               {mi355x_tls_winw_seal_aes128, mi355x_tls_winw_seal_aes256}}}};
-        const bool wide = n > 3u * (uint64_t)ctx->num_cu;
+        const bool wide = n > 15u * (uint64_t)ctx->num_cu; /* the wide groups (15 records) fill every CU */
         const win_kernel_t wk = table[frame][wide][seal][ctx->key_size == 32];
         /* latency kernels: 512 threads, 8 lanes per segment; wide: 1024 threads, 4 lanes (MI355X_WIN_KERNEL list) */
         const uint32_t threads = wide ? 1024u : 512u, per = (threads / (wide ? 4u : 8u)) / WIN_MAXSEG;

@@ -41,7 +41,7 @@ def main():
             res[f"{mode}/{L}"] = {"encrypt_us": round((t1 - t0) / reps * 1e6, 1),
                                   "decrypt_us": round((t2 - t1) / reps * 1e6, 1)}
             print(mode, L, res[f"{mode}/{L}"], flush=True)
-    ra.set_aead_window_records(768)
+    ra.set_aead_window_records(2048)
     ra.set_slot_zero_copy_bytes(1 << 20)
     print(json.dumps(res))
 

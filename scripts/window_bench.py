@@ -132,6 +132,26 @@ def main():
                                         "us_per_launch": round(ms * 1e3, 1), "gibps": round(n * FRAG / (ms * 1e-3) / 2 ** 30, 1)})
         del d_t, d_c, d_src, d_wire
     ra.set_tls_window_records(16384)
+
+    # AEAD batches (ptls_mi355x_seal_batch, 5-byte AAD): where the window kernels stop paying off
+    from rapido_amd import records
+    res["aead_batches"] = []
+    for length in (1400, 16384):
+        for n in (16, 256, 768, 1024, 4096, 16384):
+            recs, src_bytes, aad_bytes = records.layout(np.full(n, length, np.uint64), np.full(n, 5, np.uint64), align=256)
+            d_r = torch.from_numpy(recs.view(np.uint8)).to(dev)
+            d_s = torch.randint(0, 256, (src_bytes,), dtype=torch.uint8, device=dev)
+            d_o = torch.zeros_like(d_s)
+            d_a = torch.zeros(aad_bytes, dtype=torch.uint8, device=dev)
+            for mode in ("window", "batch"):
+                ra.set_aead_window_records(1 << 30 if mode == "window" else 0)
+                ms = timed(lambda: eng.seal_batch(iv, d_r.data_ptr(), n, d_s.data_ptr(), d_o.data_ptr(), d_a.data_ptr(), sh),
+                           max(5, args.reps // max(1, n // 64)))
+                res["aead_batches"].append({"record_bytes": length, "records": n, "kernels": mode,
+                                            "us_per_launch": round(ms * 1e3, 1),
+                                            "gibps": round(n * length / (ms * 1e-3) / 2 ** 30, 1)})
+            del d_r, d_s, d_o, d_a
+    ra.set_aead_window_records(2048)
     eng.close()
     line = json.dumps(res)
     print(line)

@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(autouse=True, params=["window", "batch"])
 def aead_kernels(request, engine_lib):
     """Every test here runs on both kernel families: the window kernels (64-block segments in parallel; the
-    default for the slot calls and batches up to 768 records) and the batch kernels (K lanes per record)."""
+    default for the slot calls and batches up to 2048 records) and the batch kernels (K lanes per record)."""
     prev = ra.set_aead_window_records(1 << 30 if request.param == "window" else 0)
     yield request.param
     ra.set_aead_window_records(prev)
