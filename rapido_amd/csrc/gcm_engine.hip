@@ -91,7 +91,7 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
                                                uint32_t nrecs, const uint8_t *src, uint8_t *dst,
                                                const uint8_t *__restrict__ aad, uint32_t *__restrict__ status,
                                                uint8_t *__restrict__ types, uint32_t *__restrict__ work,
-                                               const uint32_t *__restrict__ conn)
+                                               uint32_t work_base, const uint32_t *__restrict__ conn)
 {
     static_assert(K <= MAX_KERNEL_K, "LDS holds at most MAX_KERNEL_K GHASH tables");
     __shared__ __attribute__((aligned(16))) uint8_t lds[Layout<K>::total];
@@ -131,7 +131,7 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
     for (;;) {
         uint32_t g = 0;
         if (lane == 0)
-            g = atomicAdd(work, 1u);
+            g = atomicAdd(work, 1u) - work_base; /* tickets of this launch start at work_base (mod 2^32) */
         g = (uint32_t)__shfl((int)g, 0, 64);
         if (g >= ngroups)
             break;
@@ -440,10 +440,10 @@ __device__ __forceinline__ void window_body(const KeyImage *__restrict__ ki, uin
         const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2, const void *__restrict__ descs,     \
         const uint32_t *__restrict__ order, uint32_t nrecs, const uint8_t *src, uint8_t *dst,                          \
         const uint8_t *__restrict__ aad, uint32_t *__restrict__ st, uint8_t *__restrict__ types,                       \
-        uint32_t *__restrict__ work, const uint32_t *__restrict__ conn)                                                \
+        uint32_t *__restrict__ work, uint32_t work_base, const uint32_t *__restrict__ conn)                            \
     {                                                                                                                  \
         gcm_batch_body<NR, K, SEAL, FRAME>(ki, iv0, iv1, iv2, descs, order, nrecs, src, dst, aad, st, types, work,     \
-                                           conn);                                                                      \
+                                           work_base, conn);                                                           \
     }
 #define MI355X_GCM_KERNEL(NAME, NR, K, SEAL) MI355X_GCM_KERNEL_F(NAME, NR, K, SEAL, false)
 
@@ -515,7 +515,7 @@ extern "C" __global__ void mi355x_aes_ecb(const KeyImage *__restrict__ ki, const
 
 typedef void (*batch_kernel_t)(const KeyImage *, uint32_t, uint32_t, uint32_t, const void *, const uint32_t *, uint32_t,
                                const uint8_t *, uint8_t *, const uint8_t *, uint32_t *, uint8_t *, uint32_t *,
-                               const uint32_t *);
+                               uint32_t, const uint32_t *);
 
 constexpr uint32_t WORK_SLOTS = 256; /* per-context ring of work counters: one per launch in flight */
 
@@ -529,7 +529,8 @@ struct st_ptls_mi355x_aesgcm_context {
     uint8_t *h_stage;    /* pinned host staging (mapped, coherent) */
     uint8_t *h_stage_dev; /* h_stage as the GPU addresses it: zero-copy slot calls read and write it directly */
     size_t stage_cap;
-    uint32_t *d_work;    /* WORK_SLOTS dynamic-scheduling counters, zeroed per launch */
+    uint32_t *d_work;    /* WORK_SLOTS dynamic-scheduling ticket counters, zeroed once at setup */
+    uint32_t work_base[WORK_SLOTS]; /* each counter's value at the start of its next launch */
     uint32_t work_next;
     void *d_sort;        /* ptls_mi355x_order_by_length workspace */
     size_t sort_cap;
@@ -675,10 +676,17 @@ static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void
     if (blocks > (uint64_t)ctx->num_cu)
         blocks = (uint64_t)ctx->num_cu;
     DeviceGuard guard(ctx->device);
-    uint32_t *work = ctx->d_work + (ctx->work_next++ % WORK_SLOTS);
-    HIPCHK(hipMemsetAsync(work, 0, sizeof(uint32_t), stream));
+    /*
+     * Work counters are never reset: every wave takes tickets until one is out of range, so a launch
+     * consumes exactly ngroups + (its waves) tickets, and the next launch on the slot starts there.
+     */
+    const uint32_t wslot = ctx->work_next++ % WORK_SLOTS;
+    uint32_t *work = ctx->d_work + wslot;
+    const uint32_t work_base = ctx->work_base[wslot];
+    ctx->work_base[wslot] = work_base + (uint32_t)ngroups + (uint32_t)(blocks * waves);
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(WG_THREADS), 0, stream, ctx->d_ki, le32(iv), le32(iv + 4),
-                       le32(iv + 8), recs, order, (uint32_t)n, src, dst, aad, status, types, work, conn);
+                       le32(iv + 8), recs, order, (uint32_t)n, src, dst, aad, status, types, work, work_base,
+                       conn);
     HIPCHK(hipGetLastError());
     return 0;
 }
@@ -781,7 +789,8 @@ ptls_mi355x_aesgcm_context_t *ptls_mi355x_aesgcm_new(const void *key, size_t key
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess)
         goto Fail;
     if (hipMalloc(&ctx->d_ki, sizeof(KeyImage)) != hipSuccess || ensure_stage(ctx, 4096) != 0 ||
-        hipMalloc(&ctx->d_work, WORK_SLOTS * sizeof(uint32_t)) != hipSuccess)
+        hipMalloc(&ctx->d_work, WORK_SLOTS * sizeof(uint32_t)) != hipSuccess ||
+        hipMemsetAsync(ctx->d_work, 0, WORK_SLOTS * sizeof(uint32_t), ctx->stream) != hipSuccess)
         goto Fail;
     memcpy(ctx->h_stage, key, key_size);
     d_rc = (int *)(ctx->d_stage + 64);
