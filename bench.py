@@ -39,6 +39,10 @@ WORKLOADS = {
     "1400": dict(name="AES-128-GCM seal+open, 1M x 1400 B TLS records", key=16, n=1 << 20, length=1400),
     "16k": dict(name="AES-256-GCM seal+open, 256K x 16 KiB TLS records", key=32, n=1 << 18, length=16384),
     "16k-aes128": dict(name="AES-128-GCM seal+open, 256K x 16 KiB TLS records", key=16, n=1 << 18, length=16384),
+    # TLS-max inner plaintext: 16384 data bytes + the content-type byte (lib/picotls.c:636-639), SURVEY.md 8(d)
+    "16k-max": dict(name="AES-256-GCM seal+open, 256K x 16385 B TLS-max records", key=32, n=1 << 18, length=16385),
+    "16k-max-aes128": dict(name="AES-128-GCM seal+open, 256K x 16385 B TLS-max records", key=16, n=1 << 18,
+                           length=16385),
     "ragged": dict(name="AES-128-GCM seal+open, 1M records U{64..16384} B", key=16, n=1 << 20, length=None),
 }
 

@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-round}
 mkdir -p $OUT
 timeout -k 10 400 python bench.py --steps 20 --warmup 3 --e2e > $OUT/bench_1400.json 2> $OUT/bench.err
-for w in 16k 16k-aes128 ragged; do
+for w in 16k 16k-aes128 16k-max 16k-max-aes128 ragged; do
   timeout -k 10 300 python bench.py --workload $w --steps 8 --warmup 2 --no-cpu-baseline --no-e2e >> $OUT/bench_other.jsonl 2>> $OUT/bench.err
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e > $OUT/trace.log 2>&1

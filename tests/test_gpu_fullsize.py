@@ -23,6 +23,7 @@ pytestmark = pytest.mark.gpu
 CASES = [
     ("1400", 16, 1 << 20, 1400),
     ("16k-aes256", 32, 1 << 18, 16384),
+    ("16k-max-aes128", 16, 1 << 18, 16385),  # TLS-max inner plaintext: a 1-byte tail block per record
     ("ragged", 16, 1 << 20, None),
 ]
 
