@@ -77,3 +77,28 @@ def tls_batch(lengths, seed: int, align: int = 256):
     aad = np.zeros(aad_bytes, dtype=np.uint8)
     aad[: 5 * n] = tls_aad(lengths)
     return recs, src, aad
+
+
+def shard_by_bytes(lengths, aadlens, world: int):
+    """Contiguous shards of a global ragged batch, one per rank, balanced by GHASH work.
+
+    A record's cost is its GHASH step count, ceil(aad/16) + ceil(len/16) + 1 (the length block),
+    which is also what its AES-CTR work and HBM bytes scale with.  Rank r gets the records whose
+    cumulative cost midpoint falls in [r/world, (r+1)/world) of the total, so shard boundaries sit at
+    the prefix-sum quantiles.  Returns a list of (first, count) per rank; the shards are disjoint,
+    cover the batch in order, and need no exchange (records are independent).
+    """
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    lengths = np.asarray(lengths, dtype=np.uint64)
+    aadlens = np.asarray(aadlens, dtype=np.uint64)
+    if lengths.shape != aadlens.shape:
+        raise ValueError("lengths and aadlens differ in shape")
+    n = len(lengths)
+    cost = (aadlens + 15) // 16 + (lengths + 15) // 16 + 1
+    csum = np.cumsum(cost, dtype=np.uint64)
+    total = int(csum[-1]) if n else 0
+    mid = csum.astype(np.float64) - cost.astype(np.float64) / 2.0
+    owner = np.minimum((mid * world / max(total, 1)).astype(np.int64), world - 1) if n else np.zeros(0, np.int64)
+    bounds = np.searchsorted(owner, np.arange(world + 1), side="left")
+    return [(int(bounds[r]), int(bounds[r + 1] - bounds[r])) for r in range(world)]

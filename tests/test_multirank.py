@@ -49,3 +49,59 @@ def test_rank_shard_validates():
     import bench
     with pytest.raises(ValueError):
         bench.rank_shard(2, 2, 10)
+
+
+def _ragged_worker(rank, world, port, q):
+    """Rank `rank` seals its byte-balanced shard of one global ragged batch with the oracle (the CPU
+    checker; the GPU ranks run the engine on the same shards) and reports its tags and work."""
+    import hashlib
+
+    import numpy as np
+    import torch.distributed as dist
+    import oracle
+    from rapido_amd import records
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(11)
+    lengths = rng.integers(0, 3000, 64).astype(np.uint64)
+    key, iv = bytes(range(16)), bytes(range(0xA0, 0xAC))
+    first, n = records.shard_by_bytes(lengths, np.full(64, 5, np.uint64), world)[rank]
+    out = {}
+    for i in range(first, first + n):
+        pt = hashlib.sha256(b"rec%d" % i).digest() * (int(lengths[i]) // 32 + 1)
+        pt = pt[: int(lengths[i])]
+        out[i] = oracle.seal(key, oracle.build_iv(iv, i), bytes(records.tls_aad(lengths[i:i + 1])), pt)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, out)
+    q.put((rank, gathered))
+    dist.destroy_process_group()
+
+
+def test_ragged_byte_shards_cover_the_batch():
+    import hashlib
+
+    import numpy as np
+    import oracle
+    from rapido_amd import records
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_ragged_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rng = np.random.default_rng(11)
+    lengths = rng.integers(0, 3000, 64).astype(np.uint64)
+    key, iv = bytes(range(16)), bytes(range(0xA0, 0xAC))
+    for _, gathered in res:
+        merged = {}
+        for part in gathered:
+            assert not set(part) & set(merged)  # shards are disjoint
+            merged.update(part)
+        assert sorted(merged) == list(range(64))
+        for i, sealed in merged.items():
+            pt = (hashlib.sha256(b"rec%d" % i).digest() * (int(lengths[i]) // 32 + 1))[: int(lengths[i])]
+            assert sealed == oracle.seal(key, oracle.build_iv(iv, i), bytes(records.tls_aad(lengths[i:i + 1])), pt)

@@ -1,5 +1,6 @@
 """Host-side batch layout helpers (rapido_amd/records.py)."""
 import numpy as np
+import pytest
 
 from rapido_amd import RECORD_DTYPE, records
 
@@ -27,3 +28,32 @@ def test_xorshift_deterministic():
     assert (a == records.xorshift64star(5, 1000)).all()
     assert not (a == records.xorshift64star(6, 1000)).all()
     assert (records.xorshift64star(5, 100) == a[:100]).all()
+
+
+def test_shard_by_bytes_balances_ragged_work():
+    rng = np.random.default_rng(3)
+    n = 100000
+    lengths = rng.integers(64, 16385, n).astype(np.uint64)
+    aadlens = np.full(n, 5, dtype=np.uint64)
+    cost = (aadlens + 15) // 16 + (lengths + 15) // 16 + 1
+    for world in (1, 2, 3, 8):
+        shards = records.shard_by_bytes(lengths, aadlens, world)
+        assert len(shards) == world
+        # disjoint, in order, covering every record
+        assert shards[0][0] == 0 and sum(c for _, c in shards) == n
+        for (f0, c0), (f1, _) in zip(shards, shards[1:]):
+            assert f0 + c0 == f1
+        work = [int(cost[f:f + c].sum()) for f, c in shards]
+        # balanced to within one record's cost (at most 1026 steps) of the ideal share
+        ideal = int(cost.sum()) / world
+        assert max(abs(w - ideal) for w in work) <= 1026
+
+
+def test_shard_by_bytes_edges():
+    assert records.shard_by_bytes([], [], 4) == [(0, 0)] * 4
+    assert records.shard_by_bytes([100], [5], 3) in ([(0, 1), (1, 0), (1, 0)], [(0, 0), (0, 1), (1, 0)],
+                                                      [(0, 0), (0, 0), (0, 1)])
+    # one TLS-max record (1026 steps) then 1024 x 64 B (6 steps each): rank 0 takes it plus 426 small ones
+    assert records.shard_by_bytes([16384] + [64] * 1024, [5] * 1025, 2) == [(0, 427), (427, 598)]
+    with pytest.raises(ValueError):
+        records.shard_by_bytes([1], [1], 0)
