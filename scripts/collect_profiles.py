@@ -55,12 +55,29 @@ def main(tag, label):
         pmc[k] = {"FETCH_SIZE_kB": fetch[k]["FETCH_SIZE"], "WRITE_SIZE_kB": write.get(k, {}).get("WRITE_SIZE"),
                   "hbm_bytes_per_launch": int(fb + wb), "sq": sq.get(k, {})}
         traffic[k] = {"hbm_bytes_per_launch": int(fb + wb), "source": f"profiles/{label}_pmc.json"}
-    with open(os.path.join(dst, f"{label}_pmc.json"), "w") as f:
-        json.dump({"workload": "1400 (bench.py default)", "correction": "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024",
-                   "kernels": pmc}, f, indent=1)
     tpath = os.path.join(dst, "pmc_traffic.json")
     allt = json.load(open(tpath)) if os.path.exists(tpath) else {}
     allt["1400"] = traffic
+    # other workloads: FETCH / WRITE passes only (scripts/gpu_round_bench.sh)
+    others = {}
+    for w in ("16k", "16k-aes128", "16k-max", "16k-max-aes128", "ragged"):
+        fp = os.path.join(src, f"pmc_fetch_{w}", "run_counter_collection.csv")
+        wp = os.path.join(src, f"pmc_write_{w}", "run_counter_collection.csv")
+        if not (os.path.exists(fp) and os.path.exists(wp)):
+            continue
+        fw, ww = counters(fp), counters(wp)
+        t = {}
+        for k in fw:
+            if "setup" in k or "mi355x_gcm_" not in k:
+                continue
+            b = int(fw[k]["FETCH_SIZE"] * 1024 * 2 + ww.get(k, {}).get("WRITE_SIZE", 0.0) * 1024)
+            t[k] = {"hbm_bytes_per_launch": b, "source": f"profiles/{label}_pmc.json"}
+            others.setdefault(w, {})[k] = {"FETCH_SIZE_kB": fw[k]["FETCH_SIZE"],
+                                           "WRITE_SIZE_kB": ww.get(k, {}).get("WRITE_SIZE"), "hbm_bytes_per_launch": b}
+        allt[w] = t
+    with open(os.path.join(dst, f"{label}_pmc.json"), "w") as f:
+        json.dump({"workload": "1400 (bench.py default)", "correction": "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024",
+                   "kernels": pmc, "other_workloads": others}, f, indent=1)
     with open(tpath, "w") as f:
         json.dump(allt, f, indent=1)
     print(json.dumps(pmc, indent=1))

@@ -13,3 +13,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_fetch -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-e2e --check 0 > $OUT/pmc_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/pmc_write -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-e2e --check 0 > $OUT/pmc_write.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --kernel-trace -d $OUT/pmc_sq -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-e2e --check 0 > $OUT/pmc_sq.log 2>&1
+# HBM traffic of the other workloads (roofline.traffic of their bench lines): FETCH / WRITE in separate passes
+for w in 16k 16k-aes128 16k-max 16k-max-aes128 ragged; do
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_fetch_$w -o run --output-format csv -- python bench.py --workload $w --steps 2 --warmup 1 --no-cpu-baseline --no-e2e --check 0 > $OUT/pmc_fetch_$w.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/pmc_write_$w -o run --output-format csv -- python bench.py --workload $w --steps 2 --warmup 1 --no-cpu-baseline --no-e2e --check 0 > $OUT/pmc_write_$w.log 2>&1
+done
