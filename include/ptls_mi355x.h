@@ -261,6 +261,12 @@ size_t ptls_mi355x_set_aead_window_records(size_t n);
  * Larger ones are copied in and out.  Returns the previous value (default 1 MiB).  Process-wide.
  */
 size_t ptls_mi355x_set_slot_zero_copy_bytes(size_t n);
+/*
+ * Diagnostics: the batch kernels' work counters are never reset (each launch starts where the previous one
+ * on its slot ended, modulo 2^32).  Contexts created after this call start their counters at `origin`
+ * instead of 0, so a test can place the 2^32 wrap inside its first launches.  Returns the previous value.
+ */
+uint32_t ptls_mi355x_set_work_ticket_origin(uint32_t origin);
 /* name of the kernel symbol the next batch launch with these parameters uses (for profiling) */
 const char *ptls_mi355x_kernel_name(int is_seal, size_t key_size);
 /* last HIP error string seen by the engine ("" if none) */

@@ -56,7 +56,8 @@ EXPORTED_FUNCTIONS = (
     "ptls_mi355x_get_lanes_per_record", "ptls_mi355x_kernel_name", "ptls_mi355x_last_error",
     "ptls_mi355x_tls_seal_records", "ptls_mi355x_tls_open_records", "ptls_mi355x_tls_seal_records_multi",
     "ptls_mi355x_tls_open_records_multi", "ptls_mi355x_set_tls_window_records",
-    "ptls_mi355x_set_aead_window_records", "ptls_mi355x_set_slot_zero_copy_bytes", "ptls_mi355x_tls_plan_send",
+    "ptls_mi355x_set_aead_window_records", "ptls_mi355x_set_slot_zero_copy_bytes",
+    "ptls_mi355x_set_work_ticket_origin", "ptls_mi355x_tls_plan_send",
     "ptls_mi355x_tls_parse_records",
 )
 EXPORTED_OBJECTS = ("ptls_mi355x_aes128gcm", "ptls_mi355x_aes256gcm", "ptls_mi355x_aes128ctr",
@@ -141,6 +142,8 @@ def lib() -> C.CDLL:
         L.ptls_mi355x_set_aead_window_records.restype = sz
         L.ptls_mi355x_set_slot_zero_copy_bytes.argtypes = [sz]
         L.ptls_mi355x_set_slot_zero_copy_bytes.restype = sz
+        L.ptls_mi355x_set_work_ticket_origin.argtypes = [C.c_uint32]
+        L.ptls_mi355x_set_work_ticket_origin.restype = C.c_uint32
         L.ptls_mi355x_tls_open_records_multi.argtypes = [vp, vp, vp, vp, sz, vp, vp, vp, vp, vp]
         L.ptls_mi355x_tls_plan_send.argtypes = [sz, C.c_uint32, C.POINTER(u64), u64, u64, vp, sz, C.POINTER(sz)]
         L.ptls_mi355x_tls_plan_send.restype = sz
@@ -423,6 +426,11 @@ def set_slot_zero_copy_bytes(n: int) -> int:
     """Slot calls staging at most n bytes run zero-copy (the kernel reads/writes pinned host memory); returns the
     previous limit."""
     return lib().ptls_mi355x_set_slot_zero_copy_bytes(n)
+
+
+def set_work_ticket_origin(origin: int) -> int:
+    """Contexts created afterwards start their batch work counters at `origin` (diagnostics: the 2^32 wrap)."""
+    return lib().ptls_mi355x_set_work_ticket_origin(origin & 0xFFFFFFFF)
 
 
 def kernel_name(is_seal: bool, key_size: int) -> str:

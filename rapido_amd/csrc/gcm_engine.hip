@@ -545,6 +545,8 @@ static size_t g_window_records = 16384;
 static size_t g_aead_window_records = 2048; /* break-even of 1400-B records (scripts/window_bench.py aead_batches) */
 /* single-record slot calls staging at most this many bytes run zero-copy (ptls_mi355x_set_slot_zero_copy_bytes) */
 static size_t g_slot_zero_copy_bytes = 1u << 20;
+/* starting value of new contexts' work counters (ptls_mi355x_set_work_ticket_origin; tests the 2^32 wrap) */
+static uint32_t g_ticket_origin = 0u;
 
 static int fail(const char *what, hipError_t e)
 {
@@ -756,6 +758,13 @@ size_t ptls_mi355x_set_aead_window_records(size_t n)
     return prev;
 }
 
+uint32_t ptls_mi355x_set_work_ticket_origin(uint32_t origin)
+{
+    const uint32_t prev = g_ticket_origin;
+    g_ticket_origin = origin;
+    return prev;
+}
+
 size_t ptls_mi355x_set_slot_zero_copy_bytes(size_t n)
 {
     const size_t prev = g_slot_zero_copy_bytes;
@@ -790,8 +799,10 @@ ptls_mi355x_aesgcm_context_t *ptls_mi355x_aesgcm_new(const void *key, size_t key
         goto Fail;
     if (hipMalloc(&ctx->d_ki, sizeof(KeyImage)) != hipSuccess || ensure_stage(ctx, 4096) != 0 ||
         hipMalloc(&ctx->d_work, WORK_SLOTS * sizeof(uint32_t)) != hipSuccess ||
-        hipMemsetAsync(ctx->d_work, 0, WORK_SLOTS * sizeof(uint32_t), ctx->stream) != hipSuccess)
+        hipMemsetD32Async((hipDeviceptr_t)ctx->d_work, (int)g_ticket_origin, WORK_SLOTS, ctx->stream) != hipSuccess)
         goto Fail;
+    for (uint32_t i = 0; i < WORK_SLOTS; ++i)
+        ctx->work_base[i] = g_ticket_origin;
     memcpy(ctx->h_stage, key, key_size);
     d_rc = (int *)(ctx->d_stage + 64);
     if (hipMemcpyAsync(ctx->d_stage, ctx->h_stage, key_size, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)

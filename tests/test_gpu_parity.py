@@ -326,3 +326,29 @@ def test_record_beyond_2p16_blocks(gpu, lanes):
         assert (st == recs["len"]).all()
     finally:
         ra.set_lanes_per_record(prev)
+
+
+def test_work_counter_wrap(gpu, aead_kernels):
+    """The batch kernels' work counters are never reset (a launch starts at the ticket where the previous one
+    on its ring slot ended, mod 2^32).  Start them 25 tickets below 2^32 so every launch's range (groups plus
+    one exit ticket per wave) crosses the wrap, and check seal/open stay bit-exact."""
+    if aead_kernels == "window":
+        pytest.skip("the window kernels use no work counter")
+    rng = np.random.default_rng(77)
+    recs, src, aad = random_batch(rng, 300)
+    key = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+    iv = rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    prev = ra.set_work_ticket_origin(2 ** 32 - 25)
+    try:
+        eng = ra.Engine(key)
+    finally:
+        ra.set_work_ticket_origin(prev)
+    want = np.zeros_like(src)
+    oracle.batch(True, key, iv, recs, src, want, aad)
+    for _ in range(3):  # later launches reuse nothing; each slot's first range crosses 2^32
+        got, _ = run_batch(eng, True, iv, recs, src, len(src), aad)
+        assert slices(got, recs, 16) == slices(want, recs, 16)
+        pt, st = run_batch(eng, False, iv, recs, got, len(src), aad)
+        assert (st == recs["len"]).all()
+        assert slices(pt, recs, 0) == [bytes(src[int(r["src"]): int(r["src"]) + int(r["len"])]) for r in recs]
+    eng.close()
