@@ -262,6 +262,13 @@ size_t ptls_mi355x_set_aead_window_records(size_t n);
  */
 size_t ptls_mi355x_set_slot_zero_copy_bytes(size_t n);
 /*
+ * Window batches (see above) of at most n records -- the slot calls and a few connections' windows -- cut
+ * records into 32-position GHASH segments (4 steps of 8 lanes, one record per workgroup) instead of 64:
+ * half the walk latency, for a slightly longer join.  SIZE_MAX (the default) means the device's CU count,
+ * 0 disables.  Returns the previous value.  Results are identical.
+ */
+size_t ptls_mi355x_set_seg32_records(size_t n);
+/*
  * Diagnostics: the batch kernels' work counters are never reset (each launch starts where the previous one
  * on its slot ended, modulo 2^32).  Contexts created after this call start their counters at `origin`
  * instead of 0, so a test can place the 2^32 wrap inside its first launches.  Returns the previous value.

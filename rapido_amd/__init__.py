@@ -57,7 +57,7 @@ EXPORTED_FUNCTIONS = (
     "ptls_mi355x_tls_seal_records", "ptls_mi355x_tls_open_records", "ptls_mi355x_tls_seal_records_multi",
     "ptls_mi355x_tls_open_records_multi", "ptls_mi355x_set_tls_window_records",
     "ptls_mi355x_set_aead_window_records", "ptls_mi355x_set_slot_zero_copy_bytes",
-    "ptls_mi355x_set_work_ticket_origin", "ptls_mi355x_tls_plan_send",
+    "ptls_mi355x_set_work_ticket_origin", "ptls_mi355x_set_seg32_records", "ptls_mi355x_tls_plan_send",
     "ptls_mi355x_tls_parse_records",
 )
 EXPORTED_OBJECTS = ("ptls_mi355x_aes128gcm", "ptls_mi355x_aes256gcm", "ptls_mi355x_aes128ctr",
@@ -143,6 +143,8 @@ def lib() -> C.CDLL:
         L.ptls_mi355x_set_slot_zero_copy_bytes.argtypes = [sz]
         L.ptls_mi355x_set_slot_zero_copy_bytes.restype = sz
         L.ptls_mi355x_set_work_ticket_origin.argtypes = [C.c_uint32]
+        L.ptls_mi355x_set_seg32_records.argtypes = [sz]
+        L.ptls_mi355x_set_seg32_records.restype = sz
         L.ptls_mi355x_set_work_ticket_origin.restype = C.c_uint32
         L.ptls_mi355x_tls_open_records_multi.argtypes = [vp, vp, vp, vp, sz, vp, vp, vp, vp, vp]
         L.ptls_mi355x_tls_plan_send.argtypes = [sz, C.c_uint32, C.POINTER(u64), u64, u64, vp, sz, C.POINTER(sz)]
@@ -426,6 +428,14 @@ def set_slot_zero_copy_bytes(n: int) -> int:
     """Slot calls staging at most n bytes run zero-copy (the kernel reads/writes pinned host memory); returns the
     previous limit."""
     return lib().ptls_mi355x_set_slot_zero_copy_bytes(n)
+
+
+SEG32_AUTO = (1 << 64) - 1  # SIZE_MAX: the device's CU count
+
+
+def set_seg32_records(n: int) -> int:
+    """Window batches of at most n records use 32-position segments (0: never; SEG32_AUTO: one per CU)."""
+    return lib().ptls_mi355x_set_seg32_records(n)
 
 
 def set_work_ticket_origin(origin: int) -> int:

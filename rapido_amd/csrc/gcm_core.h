@@ -871,6 +871,8 @@ struct KeyImage {
     uint8_t gh[MAX_K][32][16][16]; /* gh[p-1] = nibble tables of H^p, p = 1..MAX_K */
     uint8_t gh64[32][16][16];      /* nibble tables of H^64: joins the 64-position segments of the window kernels */
     uint8_t gh256[32][16][16];     /* nibble tables of H^256: joins groups of 4 segments (window_join) */
+    uint8_t gh32[32][16][16];      /* H^32 and H^128: the same joins for the 32-position segments of the */
+    uint8_t gh128[32][16][16];     /* single-record latency kernels (window_body SEG = 32) */
 };
 
 /* ------------------------------------------------------------------ record walk ----------- */
@@ -1065,13 +1067,15 @@ GCM_HD int build_key_image(const uint8_t *sbox, const uint8_t *key, uint32_t key
             gf128_mul_bytes(hp, ki->H, hp);
         nibble_tables(hp, ki->gh[p - 1]);
     }
-    /* H^64 = ((H^8)^2)^2)^2 */
-    for (int sq = 0; sq < 3; ++sq)
-        gf128_mul_bytes(hp, hp, hp);
-    nibble_tables(hp, ki->gh64);
-    /* H^256 = (H^64)^4 */
+    /* H^32 = ((H^8)^2)^2, H^64 = (H^32)^2, H^128 = (H^64)^2, H^256 = (H^128)^2 */
     for (int sq = 0; sq < 2; ++sq)
         gf128_mul_bytes(hp, hp, hp);
+    nibble_tables(hp, ki->gh32);
+    gf128_mul_bytes(hp, hp, hp);
+    nibble_tables(hp, ki->gh64);
+    gf128_mul_bytes(hp, hp, hp);
+    nibble_tables(hp, ki->gh128);
+    gf128_mul_bytes(hp, hp, hp);
     nibble_tables(hp, ki->gh256);
     return 0;
 }
@@ -1150,10 +1154,11 @@ struct LayoutWin {
 enum : uint32_t {
     WIN_SEG = 64,    /* GHASH positions per segment: 4 lanes x 16 steps */
     WIN_MAXSEG = 17, /* segments of the largest TLS record (16640-byte record: 1 + 1039 + 1 positions) */
+    WIN_SEG32_MAXSEG = 33, /* the same in 32-position segments (single-record latency kernels) */
 };
 
 /* vector v of the window image: AES image A (T0 | T1 rows) for v < 4096, then the kw + 2 GHASH tables */
-GCM_HD u32x4 window_image_vec(const uint32_t *t0, const KeyImage *ki, uint32_t v, uint32_t kw)
+GCM_HD u32x4 window_image_vec(const uint32_t *t0, const KeyImage *ki, uint32_t v, uint32_t kw, uint32_t seglen = 64u)
 {
     if (v < 0x10000u / 16u) {
         const uint32_t off = v * 16u, x = (off >> 8) & 0xffu;
@@ -1161,8 +1166,10 @@ GCM_HD u32x4 window_image_vec(const uint32_t *t0, const KeyImage *ki, uint32_t v
         return u32x4{w, w, w, w};
     }
     const uint32_t i = v - 0x10000u / 16u, slot = i / (GH_TABLE_BYTES / 16u), within = i % (GH_TABLE_BYTES / 16u);
-    const u32x4 *srcv = slot < kw ? (const u32x4 *)ki->gh[kw - 1u - slot]
-                                  : slot == kw ? (const u32x4 *)ki->gh64 : (const u32x4 *)ki->gh256;
+    /* the two join tables: H^seglen (groups of 4 segments) and H^(4 seglen) (chaining the groups) */
+    const u32x4 *srcv = slot < kw    ? (const u32x4 *)ki->gh[kw - 1u - slot]
+                        : slot == kw ? (const u32x4 *)(seglen == 32u ? ki->gh32 : ki->gh64)
+                                     : (const u32x4 *)(seglen == 32u ? ki->gh128 : ki->gh256);
     return srcv[within];
 }
 
@@ -1171,7 +1178,7 @@ GCM_HD u32x4 window_image_vec(const uint32_t *t0, const KeyImage *ki, uint32_t v
  * stored: a fill pass is one memory latency, and with 256 threads the image takes 26 vectors per thread.
  */
 GCM_HD void fill_lds_window(uint8_t *lds, const uint32_t *t0, const KeyImage *ki, uint32_t tid, uint32_t nthr,
-                            uint32_t kw = 4u)
+                            uint32_t kw = 4u, uint32_t seglen = 64u)
 {
     const uint32_t total = 0x10000u / 16u + (kw + 2u) * GH_TABLE_BYTES / 16u;
     for (uint32_t base = tid; base < total; base += 8u * nthr) {
@@ -1179,7 +1186,7 @@ GCM_HD void fill_lds_window(uint8_t *lds, const uint32_t *t0, const KeyImage *ki
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k)
             if (base + k * nthr < total)
-                v[k] = window_image_vec(t0, ki, base + k * nthr, kw);
+                v[k] = window_image_vec(t0, ki, base + k * nthr, kw, seglen);
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k)
             if (base + k * nthr < total)
@@ -1189,18 +1196,19 @@ GCM_HD void fill_lds_window(uint8_t *lds, const uint32_t *t0, const KeyImage *ki
 
 /*
  * Segment seg of a record of A AAD blocks and C payload blocks: its g = A + C + 1 GHASH positions are
- * front-padded to nseg * 64; the returned walk covers padded positions [64 seg, 64 seg + 64) (its pad is
+ * front-padded to nseg * seglen; the returned walk covers padded positions [seglen seg, seglen (seg + 1)) (its pad is
  * negative as int32 after the first segment).  Framed records have A = 1 (the 5-byte header).
  */
-GCM_HD Walk window_segment(uint32_t A, uint32_t C, uint32_t seg, uint32_t *nseg, uint32_t kw = 4u)
+GCM_HD Walk window_segment(uint32_t A, uint32_t C, uint32_t seg, uint32_t *nseg, uint32_t kw = 4u,
+                           uint32_t seglen = WIN_SEG)
 {
     const uint32_t g = A + C + 1u;
-    *nseg = (g + WIN_SEG - 1u) / WIN_SEG;
+    *nseg = (g + seglen - 1u) / seglen;
     Walk w;
     w.A = A;
     w.C = C;
-    w.T = WIN_SEG / kw; /* kw lanes per segment */
-    w.pad = WIN_SEG * *nseg - g - WIN_SEG * seg;
+    w.T = seglen / kw; /* kw lanes per segment */
+    w.pad = seglen * *nseg - g - seglen * seg;
     return w;
 }
 

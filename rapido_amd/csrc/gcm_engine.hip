@@ -269,17 +269,21 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
  * H^4..H^1 (lane scaling) and of H^64.  A record of more than WIN_MAXSEG segments (larger than a TLS
  * record) is walked whole by its first slot instead.  Results are bit-identical to the batch kernels.
  */
-template <int NR, bool SEAL, bool FRAME, int THREADS, int KW>
+template <int NR, bool SEAL, bool FRAME, int THREADS, int KW, int SEG = 64>
 __device__ __forceinline__ void window_body(const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2,
                                             const void *__restrict__ descs, uint32_t nrecs, const uint8_t *src, uint8_t *dst,
                                             const uint8_t *__restrict__ aad, uint32_t *__restrict__ status,
                                             uint8_t *__restrict__ types, const uint32_t *__restrict__ conn)
 {
     typedef LayoutWin<KW> LW;
-    constexpr uint32_t SLOTS = THREADS / KW, RECS = SLOTS / WIN_MAXSEG; /* records per workgroup pass */
+    /* SEG = 32: half-length segments, twice as many, half the steps (single-record latency kernels) */
+    static_assert(SEG == 64 || SEG == 32, "segment length");
+    constexpr uint32_t MAXSEG = SEG == 64 ? WIN_MAXSEG : WIN_SEG32_MAXSEG;
+    constexpr uint32_t SLOTS = THREADS / KW, RECS = SLOTS / MAXSEG; /* records per workgroup pass */
+    static_assert(RECS >= 1, "a workgroup holds at least one record");
     constexpr bool LATENCY = THREADS <= 512;   /* few records: up to 2 waves per SIMD */
     constexpr int WIN_PF = LATENCY ? 3 : 1;    /* prefetch 3 steps ahead when little else hides a load (lane_walk) */
-    __shared__ __attribute__((aligned(16))) uint8_t lds[LW::parts + RECS * WIN_MAXSEG * 16u];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LW::parts + RECS * MAXSEG * 16u];
     const Record *__restrict__ recs = (const Record *)descs;
     const TlsRecord *__restrict__ trecs = (const TlsRecord *)descs;
     {
@@ -287,7 +291,7 @@ __device__ __forceinline__ void window_body(const KeyImage *__restrict__ ki, uin
         (void)grp;
         WIN_STAMP(0);
     }
-    fill_lds_window(lds, c_tabs.t0, ki, threadIdx.x, blockDim.x, (uint32_t)KW);
+    fill_lds_window(lds, c_tabs.t0, ki, threadIdx.x, blockDim.x, (uint32_t)KW, (uint32_t)SEG);
     uint32_t rk[4 * (NR + 1)];
 #pragma unroll
     for (int i = 0; i < 4 * (NR + 1); ++i)
@@ -301,7 +305,7 @@ __device__ __forceinline__ void window_body(const KeyImage *__restrict__ ki, uin
 
     const uint32_t lane = threadIdx.x & 63u, slot = threadIdx.x / KW, j = lane % KW;
     const uint32_t lanesel = (lane & 31u) * 4u | 0x10000u;
-    const uint32_t rl = slot / WIN_MAXSEG, seg = slot % WIN_MAXSEG;
+    const uint32_t rl = slot / MAXSEG, seg = slot % MAXSEG;
     const uint32_t ngroups = (nrecs + RECS - 1u) / RECS;
     /* persistent: the workgroup fills its LDS once and takes record groups with a grid stride */
     for (uint32_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
@@ -332,8 +336,8 @@ __device__ __forceinline__ void window_body(const KeyImage *__restrict__ ki, uin
         const uint32_t plen = FRAME && SEAL ? rec.len + 1u : rec.len;
         const uint32_t A = FRAME ? 1u : (rec.aadlen + 15u) / 16u;
         uint32_t nseg;
-        const Walk sw = window_segment(A, (plen + 15u) / 16u, seg, &nseg, (uint32_t)KW);
-        const bool whole = nseg > WIN_MAXSEG; /* larger than a TLS record: its first slot walks it all */
+        const Walk sw = window_segment(A, (plen + 15u) / 16u, seg, &nseg, (uint32_t)KW, (uint32_t)SEG);
+        const bool whole = nseg > MAXSEG; /* larger than a TLS record: its first slot walks it all */
         const bool active = valid && (whole ? seg == 0u : seg < nseg);
         uint32_t Tw = active ? (whole ? make_walk(plen, rec.aadlen, (uint32_t)KW, walk_out16(dst + rec.dst)).T : sw.T) : 0u;
         /* first step holding a real position (segments that are mostly front padding start late) */
@@ -354,28 +358,28 @@ __device__ __forceinline__ void window_body(const KeyImage *__restrict__ ki, uin
             part ^= shfl_xor_u32x4(part, o);
         WIN_STAMP(2);
         if (active && j == 0u)
-            *(u32x4 *)(lds + LW::parts + (rl * WIN_MAXSEG + seg) * 16u) = part;
+            *(u32x4 *)(lds + LW::parts + (rl * MAXSEG + seg) * 16u) = part;
         __syncthreads();
         WIN_STAMP(3);
         /* join, phase A: each group leader folds its (up to 4) segments with H^64, in place (window_group_end) */
         const uint32_t ns = whole ? 1u : nseg;
         if (in_batch && valid && window_group_leader(seg, ns)) {
-            u32x4 g = *(const u32x4 *)(lds + LW::parts + (rl * WIN_MAXSEG + seg) * 16u);
+            u32x4 g = *(const u32x4 *)(lds + LW::parts + (rl * MAXSEG + seg) * 16u);
             const uint32_t gend = window_group_end(seg, ns);
             for (uint32_t k = seg + 1u; k < gend; ++k)
                 g = (LATENCY ? ghash_mul_lds_wide(lds, LW::gh64, g) : ghash_mul_lds(lds, LW::gh64, g)) ^
-                    *(const u32x4 *)(lds + LW::parts + (rl * WIN_MAXSEG + k) * 16u);
-            *(u32x4 *)(lds + LW::parts + (rl * WIN_MAXSEG + seg) * 16u) = g;
+                    *(const u32x4 *)(lds + LW::parts + (rl * MAXSEG + k) * 16u);
+            *(u32x4 *)(lds + LW::parts + (rl * MAXSEG + seg) * 16u) = g;
         }
         __syncthreads();
         if (in_batch && seg == 0u) {
             /* phase B: the record's first slot chains the groups with H^256: tag (seal) or tag ^ received tag (open) */
             u32x4 acc = {0u, 0u, 0u, 0u};
             if (valid) {
-                acc = *(const u32x4 *)(lds + LW::parts + rl * WIN_MAXSEG * 16u);
+                acc = *(const u32x4 *)(lds + LW::parts + rl * MAXSEG * 16u);
                 for (uint32_t k = window_group_end(0u, ns); k < ns; k += 4u)
                     acc = (LATENCY ? ghash_mul_lds_wide(lds, LW::gh256, acc) : ghash_mul_lds(lds, LW::gh256, acc)) ^
-                          *(const u32x4 *)(lds + LW::parts + (rl * WIN_MAXSEG + k) * 16u);
+                          *(const u32x4 *)(lds + LW::parts + (rl * MAXSEG + k) * 16u);
             }
             WIN_STAMP(4);
             if (SEAL) {
@@ -477,6 +481,23 @@ MI355X_GCM_KERNEL_F(mi355x_tls_open_aes256_k4, 14, 4, false, true)
     {                                                                                                                  \
         window_body<NR, SEAL, FRAME, THREADS, KW>(ki, iv0, iv1, iv2, descs, nrecs, src, dst, aad, st, types, conn);        \
     }
+/* single-record latency kernels: 32-position segments (4 steps of 8 lanes), one record per 512-thread group */
+#define MI355X_WIN32_KERNEL(NAME, NR, SEAL, FRAME)                                                                     \
+    extern "C" __global__ __launch_bounds__(512) void NAME(                                                            \
+        const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2, const void *__restrict__ descs,     \
+        uint32_t nrecs, const uint8_t *src, uint8_t *dst, const uint8_t *__restrict__ aad, uint32_t *__restrict__ st,   \
+        uint8_t *__restrict__ types, const uint32_t *__restrict__ conn)                                                \
+    {                                                                                                                  \
+        window_body<NR, SEAL, FRAME, 512, 8, 32>(ki, iv0, iv1, iv2, descs, nrecs, src, dst, aad, st, types, conn);     \
+    }
+MI355X_WIN32_KERNEL(mi355x_tls_win32_seal_aes128, 10, true, true)
+MI355X_WIN32_KERNEL(mi355x_tls_win32_seal_aes256, 14, true, true)
+MI355X_WIN32_KERNEL(mi355x_tls_win32_open_aes128, 10, false, true)
+MI355X_WIN32_KERNEL(mi355x_tls_win32_open_aes256, 14, false, true)
+MI355X_WIN32_KERNEL(mi355x_gcm_win32_seal_aes128, 10, true, false)
+MI355X_WIN32_KERNEL(mi355x_gcm_win32_seal_aes256, 14, true, false)
+MI355X_WIN32_KERNEL(mi355x_gcm_win32_open_aes128, 10, false, false)
+MI355X_WIN32_KERNEL(mi355x_gcm_win32_open_aes256, 14, false, false)
 /* 256 threads (3 records per pass): a few records spread over many CUs; 1024 threads (15 records per pass,
  * persistent): hundreds of records */
 MI355X_WIN_KERNEL(mi355x_tls_win_seal_aes128, 10, true, true, 512, 8)
@@ -547,6 +568,9 @@ static size_t g_aead_window_records = 2048; /* break-even of 1400-B records (scr
 static size_t g_slot_zero_copy_bytes = 1u << 20;
 /* starting value of new contexts' work counters (ptls_mi355x_set_work_ticket_origin; tests the 2^32 wrap) */
 static uint32_t g_ticket_origin = 0u;
+/* window batches of at most this many records use 32-position segments (ptls_mi355x_set_seg32_records;
+ * SIZE_MAX = the device's CU count) */
+static size_t g_seg32_records = SIZE_MAX;
 
 static int fail(const char *what, hipError_t e)
 {
@@ -650,10 +674,20 @@ static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void
             {{{mi355x_tls_win_open_aes128, mi355x_tls_win_open_aes256}, {mi355x_tls_win_seal_aes128, mi355x_tls_win_seal_aes256}},
              {{mi355x_tls_winw_open_aes128, mi355x_tls_winw_open_aes256},
               {mi355x_tls_winw_seal_aes128, mi355x_tls_winw_seal_aes256}}}};
+        static const win_kernel_t table32[2][2][2] = {
+            /* [frame][seal][aes256]: 32-position segments, one record per group */
+            {{mi355x_gcm_win32_open_aes128, mi355x_gcm_win32_open_aes256},
+             {mi355x_gcm_win32_seal_aes128, mi355x_gcm_win32_seal_aes256}},
+            {{mi355x_tls_win32_open_aes128, mi355x_tls_win32_open_aes256},
+             {mi355x_tls_win32_seal_aes128, mi355x_tls_win32_seal_aes256}}};
         const bool wide = n > 15u * (uint64_t)ctx->num_cu; /* the wide groups (15 records) fill every CU */
-        const win_kernel_t wk = table[frame][wide][seal][ctx->key_size == 32];
+        /* at most g_seg32_records (default: one per CU): half-length segments, half the walk (4 steps) */
+        const bool seg32 = !wide && n <= (g_seg32_records == SIZE_MAX ? (size_t)ctx->num_cu : g_seg32_records);
+        const win_kernel_t wk = seg32 ? table32[frame][seal][ctx->key_size == 32]
+                                      : table[frame][wide][seal][ctx->key_size == 32];
         /* latency kernels: 512 threads, 8 lanes per segment; wide: 1024 threads, 4 lanes (MI355X_WIN_KERNEL list) */
-        const uint32_t threads = wide ? 1024u : 512u, per = (threads / (wide ? 4u : 8u)) / WIN_MAXSEG;
+        const uint32_t threads = wide ? 1024u : 512u,
+                       per = seg32 ? 1u : (threads / (wide ? 4u : 8u)) / WIN_MAXSEG;
         uint64_t blocks = (n + per - 1) / per;
         if (wide && blocks > (uint64_t)ctx->num_cu)
             blocks = (uint64_t)ctx->num_cu;
@@ -755,6 +789,13 @@ size_t ptls_mi355x_set_aead_window_records(size_t n)
 {
     const size_t prev = g_aead_window_records;
     g_aead_window_records = n;
+    return prev;
+}
+
+size_t ptls_mi355x_set_seg32_records(size_t n)
+{
+    const size_t prev = g_seg32_records;
+    g_seg32_records = n;
     return prev;
 }
 

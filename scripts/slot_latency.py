@@ -21,9 +21,13 @@ def main():
     dec = ra.aead_new_direct("aes128gcm", False, key, iv)
     res = {}
     # window kernels zero-copy (the default), window kernels with DMA copies, batch kernels with DMA copies
-    for mode, limit, zc in (("window-zerocopy", 1 << 30, 1 << 30), ("window-copy", 1 << 30, 0), ("batch-copy", 0, 0)):
+    # window-zerocopy-seg64: the same with the 64-position segments (32-position ones are the default for a
+    # single record, ptls_mi355x_set_seg32_records)
+    for mode, limit, zc in (("window-zerocopy", 1 << 30, 1 << 30), ("window-zerocopy-seg64", 1 << 30, 1 << 30),
+                            ("window-copy", 1 << 30, 0), ("batch-copy", 0, 0)):
         ra.set_aead_window_records(limit)
         ra.set_slot_zero_copy_bytes(zc)
+        ra.set_seg32_records(0 if mode.endswith("seg64") else ra.SEG32_AUTO)
         for L in (64, 1400, 4096, 16384):
             pt = bytes(i & 0xFF for i in range(L))
             aad = bytes([0x17, 3, 3, (L + 16) >> 8, (L + 16) & 0xFF])
@@ -43,6 +47,7 @@ def main():
             print(mode, L, res[f"{mode}/{L}"], flush=True)
     ra.set_aead_window_records(2048)
     ra.set_slot_zero_copy_bytes(1 << 20)
+    ra.set_seg32_records(ra.SEG32_AUTO)
     print(json.dumps(res))
 
 

@@ -24,11 +24,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default="")
     ap.add_argument("--reps", type=int, default=200)
+    ap.add_argument("--seg32", type=int, default=-1,
+                    help="window batches of at most this many records use 32-position segments (-1: default, 1 per CU)")
     args = ap.parse_args()
     import torch
 
     import rapido_amd as ra
     ra.require_gpu()
+    if args.seg32 >= 0:
+        ra.set_seg32_records(args.seg32)
     dev = torch.device("cuda:0")
     key, iv = bytes(range(16)), bytes(range(40, 52))
     eng = ra.Engine(key)

@@ -20,6 +20,15 @@ static constexpr AesTables kTabs{};
 
 /* lanes per 64-position segment of the window math: 8 (latency kernels) or 4 (wide kernels) */
 static int g_window_lanes = 8;
+static uint32_t g_window_seglen = 64; /* 64, or 32 (the single-record latency kernels) */
+extern "C" int model_set_window_seglen(int seglen)
+{
+    if (seglen != 64 && seglen != 32)
+        return -1;
+    const int prev = (int)g_window_seglen;
+    g_window_seglen = (uint32_t)seglen;
+    return prev;
+}
 extern "C" int model_set_window_lanes(int kw)
 {
     if (kw != 4 && kw != 8)
@@ -60,7 +69,8 @@ struct TlsRecord {
     uint32_t len, type;
 };
 
-/* the window kernels' two-phase join (window_group_*): groups of 4 folded with H^64, chained with H^256 */
+/* the window kernels' two-phase join (window_group_*): groups of 4 folded with H^seglen, chained with H^(4 seglen)
+ * (the LDS slots named gh64 / gh256 hold H^32 / H^128 when seglen is 32) */
 template <int KW>
 static u32x4 model_window_join(const uint8_t *lds, u32x4 *parts, uint32_t ns)
 {
@@ -164,17 +174,17 @@ static void run_tls_window(const KeyImage *ki, const uint8_t *lds, const uint8_t
         const uint32_t n1 = iv1 ^ bswap32((uint32_t)(r.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)r.seq);
         const uint32_t n0 = conn ? iv0 ^ bswap32(conn[i]) : iv0;
         uint32_t nseg;
-        window_segment(1, (plen + 15) / 16, 0, &nseg, KW);
+        window_segment(1, (plen + 15) / 16, 0, &nseg, KW, g_window_seglen);
         u32x4 acc = {0, 0, 0, 0};
-        if (nseg > WIN_MAXSEG) {
+        if (nseg > (g_window_seglen == 32u ? (uint32_t)WIN_SEG32_MAXSEG : (uint32_t)WIN_MAXSEG)) {
             const Walk wk = make_walk(plen, 5, KW, walk_out16(dst + r.dst));
             for (uint32_t j = 0; j < (uint32_t)KW; ++j)
                 acc ^= lane_walk<NR, KW, SEAL, true, LayoutWin<KW>, 3>(lds, 4u * j | 0x10000u, ki->rk, j, r, true, wk.T, n0, n1, n2,
                                                                src, dst, nullptr, (const uint8_t *)trecs, t.type);
         } else {
-            u32x4 parts[WIN_MAXSEG];
+            u32x4 parts[WIN_SEG32_MAXSEG];
             for (uint32_t sg = 0; sg < nseg; ++sg) {
-                const Walk sw = window_segment(1, (plen + 15) / 16, sg, &nseg, KW);
+                const Walk sw = window_segment(1, (plen + 15) / 16, sg, &nseg, KW, g_window_seglen);
                 u32x4 part = {0, 0, 0, 0};
                 for (uint32_t j = 0; j < (uint32_t)KW; ++j)
                     part ^= lane_walk<NR, KW, SEAL, true, LayoutWin<KW>, 3>(lds, 4u * j | 0x10000u, ki->rk, j, r, true, sw.T, n0, n1,
@@ -217,17 +227,17 @@ static void run_window(const KeyImage *ki, const uint8_t *lds, const uint8_t *st
         const uint32_t n1 = iv1 ^ bswap32((uint32_t)(r.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)r.seq);
         const uint32_t A = (r.aadlen + 15) / 16, C = (r.len + 15) / 16;
         uint32_t nseg;
-        window_segment(A, C, 0, &nseg, KW);
+        window_segment(A, C, 0, &nseg, KW, g_window_seglen);
         u32x4 acc = {0, 0, 0, 0};
-        if (nseg > WIN_MAXSEG) {
+        if (nseg > (g_window_seglen == 32u ? (uint32_t)WIN_SEG32_MAXSEG : (uint32_t)WIN_MAXSEG)) {
             const Walk wk = make_walk(r.len, r.aadlen, KW, walk_out16(dst + r.dst));
             for (uint32_t j = 0; j < (uint32_t)KW; ++j)
                 acc ^= lane_walk<NR, KW, SEAL, false, LayoutWin<KW>, 3>(lds, 4u * j | 0x10000u, ki->rk, j, r, true, wk.T, iv0, n1, n2,
                                                                 src, dst, aad, (const uint8_t *)recs);
         } else {
-            u32x4 parts[WIN_MAXSEG];
+            u32x4 parts[WIN_SEG32_MAXSEG];
             for (uint32_t sg = 0; sg < nseg; ++sg) {
-                const Walk sw = window_segment(A, C, sg, &nseg, KW);
+                const Walk sw = window_segment(A, C, sg, &nseg, KW, g_window_seglen);
                 u32x4 part = {0, 0, 0, 0};
                 for (uint32_t j = 0; j < (uint32_t)KW; ++j)
                     part ^= lane_walk<NR, KW, SEAL, false, LayoutWin<KW>, 3>(lds, 4u * j | 0x10000u, ki->rk, j, r, true, sw.T, iv0,
@@ -254,7 +264,7 @@ extern "C" int model_batch_window(int is_seal, const uint8_t *key, size_t keylen
         free(lds);
         return -1;
     }
-    fill_lds_window(lds, kTabs.t0, ki, 0, 1, (uint32_t)g_window_lanes);
+    fill_lds_window(lds, kTabs.t0, ki, 0, 1, (uint32_t)g_window_lanes, g_window_seglen);
 #define WIN_CASE(KWV)                                                                                                  \
     if (g_window_lanes == KWV) {                                                                                       \
         if (ki->rounds == 10)                                                                                          \
@@ -282,7 +292,7 @@ extern "C" int model_tls_window(int is_seal, const uint8_t *key, size_t keylen, 
         free(lds);
         return -1;
     }
-    fill_lds_window(lds, kTabs.t0, ki, 0, 1, (uint32_t)g_window_lanes);
+    fill_lds_window(lds, kTabs.t0, ki, 0, 1, (uint32_t)g_window_lanes, g_window_seglen);
 #define WIN_CASE(KWV)                                                                                                  \
     if (g_window_lanes == KWV) {                                                                                       \
         if (ki->rounds == 10)                                                                                          \

@@ -33,16 +33,17 @@ def make_batch(rng, n):
     return recs, src, aad
 
 
-@pytest.mark.parametrize("family", ["window", "batch"])
+@pytest.mark.parametrize("family", ["window", "window32", "batch"])
 @pytest.mark.parametrize("lanes", [1, 2, 4, 8])
 @pytest.mark.parametrize("keylen", [16, 32])
 def test_fuzz_seal_open(gpu, family, lanes, keylen):
     import torch
-    rng = np.random.default_rng(7000 + 10 * lanes + keylen + (1 if family == "window" else 0))
+    rng = np.random.default_rng(7000 + 10 * lanes + keylen + {"batch": 0, "window": 1, "window32": 2}[family])
     recs, src, aad = make_batch(rng, 120)
     key = rng.integers(0, 256, keylen, dtype=np.uint8).tobytes()
     iv = rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
-    prev_w = ra.set_aead_window_records(1 << 30 if family == "window" else 0)
+    prev_w = ra.set_aead_window_records(0 if family == "batch" else 1 << 30)
+    prev_32 = ra.set_seg32_records(1 << 30 if family == "window32" else 0)
     prev_k = ra.set_lanes_per_record(lanes)
     try:
         eng = ra.Engine(key)
@@ -67,4 +68,5 @@ def test_fuzz_seal_open(gpu, family, lanes, keylen):
         eng.close()
     finally:
         ra.set_aead_window_records(prev_w)
+        ra.set_seg32_records(prev_32)
         ra.set_lanes_per_record(prev_k)

@@ -12,13 +12,16 @@ from rapido_amd import records
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["window", "batch"])
+@pytest.fixture(autouse=True, params=["window", "window32", "batch"])
 def aead_kernels(request, engine_lib):
-    """Every test here runs on both kernel families: the window kernels (64-block segments in parallel; the
-    default for the slot calls and batches up to 2048 records) and the batch kernels (K lanes per record)."""
-    prev = ra.set_aead_window_records(1 << 30 if request.param == "window" else 0)
+    """Every test here runs on each kernel family: the window kernels with 64-block segments walked in parallel
+    (the default for batches up to 2048 records), the same with 32-block segments (the default up to one record
+    per CU, so the slot calls), and the batch kernels (K lanes per record)."""
+    prev = ra.set_aead_window_records(0 if request.param == "batch" else 1 << 30)
+    prev32 = ra.set_seg32_records(1 << 30 if request.param == "window32" else 0)
     yield request.param
     ra.set_aead_window_records(prev)
+    ra.set_seg32_records(prev32)
 
 
 def to_dev(a: np.ndarray):
@@ -332,7 +335,7 @@ def test_work_counter_wrap(gpu, aead_kernels):
     """The batch kernels' work counters are never reset (a launch starts at the ticket where the previous one
     on its ring slot ended, mod 2^32).  Start them 25 tickets below 2^32 so every launch's range (groups plus
     one exit ticket per wave) crosses the wrap, and check seal/open stay bit-exact."""
-    if aead_kernels == "window":
+    if aead_kernels != "batch":
         pytest.skip("the window kernels use no work counter")
     rng = np.random.default_rng(77)
     recs, src, aad = random_batch(rng, 300)

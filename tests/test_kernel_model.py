@@ -26,8 +26,10 @@ def model():
 def run(lib, is_seal, K, key, iv, recs, src, dst, aad, st):
     """K = "w4" / "w8": the window kernels' math (64-position segments of 4 / 8 lanes joined with H^64);
     else the K-lane batch walk."""
-    if isinstance(K, str):
-        assert lib.model_set_window_lanes(int(K[1:])) > 0
+    if isinstance(K, str):  # "w4", "w8", or "w8s32" (32-position segments: the single-record latency kernels)
+        lanes, _, seglen = K[1:].partition("s")
+        assert lib.model_set_window_lanes(int(lanes)) > 0
+        assert lib.model_set_window_seglen(int(seglen or 64)) > 0
         lib.model_batch_window.argtypes = [C.c_int, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_size_t,
                                            C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         rc = lib.model_batch_window(1 if is_seal else 0, key, len(key), iv, recs.ctypes.data, len(recs),
@@ -57,10 +59,10 @@ def spans(buf, recs, extra):
     return [bytes(buf[int(r["dst"]): int(r["dst"]) + int(r["len"]) + extra]) for r in recs]
 
 
-@pytest.mark.parametrize("K", [1, 2, 4, 8, "w4", "w8"])
+@pytest.mark.parametrize("K", [1, 2, 4, 8, "w4", "w8", "w8s32"])
 @pytest.mark.parametrize("keylen", [16, 32])
 def test_model_matches_oracle(model, K, keylen):
-    rng = np.random.default_rng((K if isinstance(K, int) else 900 + int(K[1:])) * 100 + keylen)
+    rng = np.random.default_rng((K if isinstance(K, int) else 900 + int(K[1:].replace("s", ""))) * 100 + keylen)
     recs, src, aad = batch(rng, 150, 700, 48)
     key = rng.integers(0, 256, keylen, dtype=np.uint8).tobytes()
     iv = rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
@@ -143,8 +145,10 @@ def run_tls(lib, is_seal, key, iv, trecs, src, dst, st=None, ty=None, conn=None,
     """window = 4 / 8: the window kernels' math (64-position segments of that many lanes, joined with H^64)
     instead of the batch walk."""
     vp = C.c_void_p
-    if window:  # 4 or 8 lanes per segment (the wide and the latency window kernels)
-        assert lib.model_set_window_lanes(int(window)) > 0
+    if window:  # 4 or 8 lanes per segment (the wide and the latency window kernels); "8s32": 32-position segments
+        lanes, _, seglen = str(window).partition("s")
+        assert lib.model_set_window_lanes(int(lanes)) > 0
+        assert lib.model_set_window_seglen(int(seglen or 64)) > 0
     fn = lib.model_tls_window if window else lib.model_tls_batch
     fn.argtypes = [C.c_int, vp, C.c_size_t, vp, vp, C.c_size_t, vp, vp, vp, vp, vp]
     st = np.zeros(max(len(trecs), 1), np.uint32) if st is None else st
@@ -155,7 +159,7 @@ def run_tls(lib, is_seal, key, iv, trecs, src, dst, st=None, ty=None, conn=None,
     return st, ty
 
 
-@pytest.mark.parametrize("window", [False, 4, 8])
+@pytest.mark.parametrize("window", [False, 4, 8, "8s32"])
 @pytest.mark.parametrize("keylen", [16, 32])
 def test_model_tls_framing(model, keylen, window):
     """The FRAME walk (header AAD in registers, content-type byte spliced into the tail block) vs the oracle's
@@ -189,7 +193,7 @@ def test_model_tls_framing(model, keylen, window):
                                                                                     int(t["len"])])
 
 
-@pytest.mark.parametrize("window", [False, 4, 8])
+@pytest.mark.parametrize("window", [False, 4, 8, "8s32"])
 def test_model_tls_open_padding_and_failures(model, window):
     import rapido_amd as ra
     key, iv = bytes(range(16)), bytes(range(30, 42))
@@ -306,7 +310,7 @@ def conn_iv(iv: bytes, conn_id: int) -> bytes:
     return head + iv[4:]
 
 
-@pytest.mark.parametrize("window", [False, 4, 8])
+@pytest.mark.parametrize("window", [False, 4, 8, "8s32"])
 def test_model_tls_multi_connection_window(model, window):
     """One batch holding the send windows of several connections of a session (same key, per-connection IV and
     seq), sealed and opened in one pass, against the oracle's record layer with each connection's derived IV."""
@@ -343,7 +347,7 @@ def test_model_tls_multi_connection_window(model, window):
     assert st[3] == 0xFFFFFFFF and (np.delete(st[: len(trecs)], 3) == np.delete(trecs["len"], 3)).all()
 
 
-@pytest.mark.parametrize("kw", [4, 8])
+@pytest.mark.parametrize("kw", [4, 8, "8s32"])
 def test_model_tls_window_oversized_record(model, kw):
     """A record above the largest TLS record (more than 17 segments) is walked whole by the window kernels' first
     slot: 20 000- and 70 000-byte fragments plus TLS-sized neighbours, against the oracle."""
@@ -364,7 +368,7 @@ def test_model_tls_window_oversized_record(model, kw):
         assert bytes(wire[int(t["dst"]): int(t["dst"]) + len(want)]) == want
 
 
-@pytest.mark.parametrize("kw", ["w4", "w8"])
+@pytest.mark.parametrize("kw", ["w4", "w8", "w8s32"])
 def test_model_window_aead_edges(model, kw):
     """The window math for AEAD records: AAD of every length 0..40 in front of payloads around segment edges
     (so the short AAD sits in later steps of the first segment), records above 17 segments, vs the oracle."""
