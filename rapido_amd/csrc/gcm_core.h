@@ -1141,15 +1141,18 @@ GCM_HD void fill_lds(uint8_t *lds, const uint32_t *t0, const KeyImage *ki, uint3
  * segment: the two-table AES image, the tables of H^KW..H^1 (slot j = H^(KW-j), the lane scaling of a
  * KW-lane walk), the tables of H^64 (joining 64-position segments), then the segment sums.
  */
-template <int KW = 4>
+template <int KW = 4, int SEG = 64>
 struct LayoutWin {
     static constexpr bool four_tables = false;
     static constexpr bool gh5 = false;
     static constexpr uint32_t aes_base = 0u;
     static constexpr uint32_t gh_base = 0x10000u;
+    /* join tables: H^SEG (within groups of 4 segments), H^(4 SEG) (across groups); SEG = 32 adds H^256
+     * (across pairs of groups, window_pair_*) */
     static constexpr uint32_t gh64 = gh_base + (uint32_t)KW * GH_TABLE_BYTES;
     static constexpr uint32_t gh256 = gh64 + GH_TABLE_BYTES;
-    static constexpr uint32_t parts = gh256 + GH_TABLE_BYTES;
+    static constexpr uint32_t ghpair = gh256 + GH_TABLE_BYTES;
+    static constexpr uint32_t parts = ghpair + (SEG == 32 ? GH_TABLE_BYTES : 0u);
 };
 enum : uint32_t {
     WIN_SEG = 64,    /* GHASH positions per segment: 4 lanes x 16 steps */
@@ -1167,9 +1170,10 @@ GCM_HD u32x4 window_image_vec(const uint32_t *t0, const KeyImage *ki, uint32_t v
     }
     const uint32_t i = v - 0x10000u / 16u, slot = i / (GH_TABLE_BYTES / 16u), within = i % (GH_TABLE_BYTES / 16u);
     /* the two join tables: H^seglen (groups of 4 segments) and H^(4 seglen) (chaining the groups) */
-    const u32x4 *srcv = slot < kw    ? (const u32x4 *)ki->gh[kw - 1u - slot]
-                        : slot == kw ? (const u32x4 *)(seglen == 32u ? ki->gh32 : ki->gh64)
-                                     : (const u32x4 *)(seglen == 32u ? ki->gh128 : ki->gh256);
+    const u32x4 *srcv = slot < kw           ? (const u32x4 *)ki->gh[kw - 1u - slot]
+                        : slot == kw        ? (const u32x4 *)(seglen == 32u ? ki->gh32 : ki->gh64)
+                        : slot == kw + 1u   ? (const u32x4 *)(seglen == 32u ? ki->gh128 : ki->gh256)
+                                            : (const u32x4 *)ki->gh256; /* seglen 32: H^256 joins pairs of groups */
     return srcv[within];
 }
 
@@ -1177,18 +1181,21 @@ GCM_HD u32x4 window_image_vec(const uint32_t *t0, const KeyImage *ki, uint32_t v
  * Fills the window image, split over nthr threads.  Eight vectors per thread are loaded before any is
  * stored: a fill pass is one memory latency, and with 256 threads the image takes 26 vectors per thread.
  */
+#ifndef GCM_WIN_FILL
+#define GCM_WIN_FILL 8u /* vectors loaded per thread before any is stored (one memory latency per pass) */
+#endif
 GCM_HD void fill_lds_window(uint8_t *lds, const uint32_t *t0, const KeyImage *ki, uint32_t tid, uint32_t nthr,
                             uint32_t kw = 4u, uint32_t seglen = 64u)
 {
-    const uint32_t total = 0x10000u / 16u + (kw + 2u) * GH_TABLE_BYTES / 16u;
-    for (uint32_t base = tid; base < total; base += 8u * nthr) {
-        u32x4 v[8];
+    const uint32_t total = 0x10000u / 16u + (kw + (seglen == 32u ? 3u : 2u)) * GH_TABLE_BYTES / 16u;
+    for (uint32_t base = tid; base < total; base += GCM_WIN_FILL * nthr) {
+        u32x4 v[GCM_WIN_FILL];
 #pragma unroll
-        for (uint32_t k = 0; k < 8; ++k)
+        for (uint32_t k = 0; k < GCM_WIN_FILL; ++k)
             if (base + k * nthr < total)
                 v[k] = window_image_vec(t0, ki, base + k * nthr, kw, seglen);
 #pragma unroll
-        for (uint32_t k = 0; k < 8; ++k)
+        for (uint32_t k = 0; k < GCM_WIN_FILL; ++k)
             if (base + k * nthr < total)
                 *(u32x4 *)(lds + 16u * (base + k * nthr)) = v[k];
     }
@@ -1226,6 +1233,15 @@ GCM_HD uint32_t window_group_end(uint32_t s, uint32_t ns)
     const uint32_t o = window_group_offset(ns), e = ((s + o) & ~3u) + 4u - o;
     return e < ns ? e : ns;
 }
+/*
+ * 32-position segments (up to 33 per record, 9 groups): a middle level joins the groups in pairs, also
+ * aligned to the record's end, before the chain -- G_a H^128 + G_b per pair in parallel, then the pairs
+ * (8 segments = 256 positions apart) chained with H^256: 3 + 1 + 4 dependent multiplies instead of 3 + 8.
+ * Group g (0-based) leads a pair when ng - g is even; the first group stands alone when ng is odd.
+ * window_group_start(g, ns) is the leading segment of group g.
+ */
+GCM_HD uint32_t window_group_count(uint32_t ns) { return (ns + window_group_offset(ns) + 3u) / 4u; }
+GCM_HD uint32_t window_group_start(uint32_t g, uint32_t ns) { return g == 0u ? 0u : 4u * g - window_group_offset(ns); }
 
 /* ------------------------------------------------------------------ per-lane record walk -- */
 

@@ -275,7 +275,7 @@ __device__ __forceinline__ void window_body(const KeyImage *__restrict__ ki, uin
                                             const uint8_t *__restrict__ aad, uint32_t *__restrict__ status,
                                             uint8_t *__restrict__ types, const uint32_t *__restrict__ conn)
 {
-    typedef LayoutWin<KW> LW;
+    typedef LayoutWin<KW, SEG> LW;
     /* SEG = 32: half-length segments, twice as many, half the steps (single-record latency kernels) */
     static_assert(SEG == 64 || SEG == 32, "segment length");
     constexpr uint32_t MAXSEG = SEG == 64 ? WIN_MAXSEG : WIN_SEG32_MAXSEG;
@@ -372,14 +372,36 @@ __device__ __forceinline__ void window_body(const KeyImage *__restrict__ ki, uin
             *(u32x4 *)(lds + LW::parts + (rl * MAXSEG + seg) * 16u) = g;
         }
         __syncthreads();
+        const uint32_t ng = window_group_count(ns);
+        if constexpr (SEG == 32) {
+            /* phase P (window_group_count): pair leaders fold the next group in with H^128 = H^(4 SEG), in place */
+            if (in_batch && valid && window_group_leader(seg, ns)) {
+                const uint32_t g = seg == 0u ? 0u : (seg + window_group_offset(ns)) / 4u;
+                if ((ng - g) % 2u == 0u) {
+                    const u32x4 a = *(const u32x4 *)(lds + LW::parts + (rl * MAXSEG + seg) * 16u);
+                    const u32x4 b = *(const u32x4 *)(lds + LW::parts + (rl * MAXSEG + window_group_start(g + 1u, ns)) * 16u);
+                    *(u32x4 *)(lds + LW::parts + (rl * MAXSEG + seg) * 16u) = ghash_mul_lds_wide(lds, LW::gh256, a) ^ b;
+                }
+            }
+            __syncthreads();
+        }
         if (in_batch && seg == 0u) {
-            /* phase B: the record's first slot chains the groups with H^256: tag (seal) or tag ^ received tag (open) */
+            /*
+             * phase B: the record's first slot chains the groups with H^(4 SEG) (SEG = 64), or the pairs of groups
+             * with H^256 (SEG = 32): tag (seal) or tag ^ received tag (open)
+             */
             u32x4 acc = {0u, 0u, 0u, 0u};
             if (valid) {
                 acc = *(const u32x4 *)(lds + LW::parts + rl * MAXSEG * 16u);
-                for (uint32_t k = window_group_end(0u, ns); k < ns; k += 4u)
-                    acc = (LATENCY ? ghash_mul_lds_wide(lds, LW::gh256, acc) : ghash_mul_lds(lds, LW::gh256, acc)) ^
-                          *(const u32x4 *)(lds + LW::parts + (rl * MAXSEG + k) * 16u);
+                if constexpr (SEG == 32) {
+                    for (uint32_t g = 2u - ng % 2u; g < ng; g += 2u)
+                        acc = ghash_mul_lds_wide(lds, LW::ghpair, acc) ^
+                              *(const u32x4 *)(lds + LW::parts + (rl * MAXSEG + window_group_start(g, ns)) * 16u);
+                } else {
+                    for (uint32_t k = window_group_end(0u, ns); k < ns; k += 4u)
+                        acc = (LATENCY ? ghash_mul_lds_wide(lds, LW::gh256, acc) : ghash_mul_lds(lds, LW::gh256, acc)) ^
+                              *(const u32x4 *)(lds + LW::parts + (rl * MAXSEG + k) * 16u);
+                }
             }
             WIN_STAMP(4);
             if (SEAL) {

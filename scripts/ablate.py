@@ -38,6 +38,7 @@ VARIANTS = {
     "no_ghash": ["-DGCM_ABLATE_GHASH=1"],
     "no_aes": ["-DGCM_ABLATE_AES=1"],
     "no_both": ["-DGCM_ABLATE_AES=1", "-DGCM_ABLATE_GHASH=1"],
+    "fill16": ["-DGCM_WIN_FILL=16u"],  # window kernels: 16 vectors in flight per thread during the LDS fill
 }
 if os.environ.get("ABLATE_VARIANTS"):
     VARIANTS = {k: v for k, v in VARIANTS.items() if k in os.environ["ABLATE_VARIANTS"].split(",")}

@@ -82,7 +82,19 @@ static u32x4 model_window_join(const uint8_t *lds, u32x4 *parts, uint32_t ns)
             g = ghash_mul_lds_wide(lds, LayoutWin<KW>::gh64, g) ^ parts[k];
         parts[s] = g;
     }
+    const uint32_t ng = window_group_count(ns);
     u32x4 acc = parts[0];
+    if (g_window_seglen == 32u) { /* pairs of groups (H^128), then the pairs chained with H^256 */
+        for (uint32_t g = 0; g + 1 < ng; ++g)
+            if ((ng - g) % 2u == 0u)
+                parts[window_group_start(g, ns)] = ghash_mul_lds_wide(lds, LayoutWin<KW, 32>::gh256,
+                                                                      parts[window_group_start(g, ns)]) ^
+                                                   parts[window_group_start(g + 1, ns)];
+        acc = parts[0];
+        for (uint32_t g = 2 - ng % 2; g < ng; g += 2)
+            acc = ghash_mul_lds_wide(lds, LayoutWin<KW, 32>::ghpair, acc) ^ parts[window_group_start(g, ns)];
+        return acc;
+    }
     for (uint32_t k = window_group_end(0, ns); k < ns; k += 4)
         acc = ghash_mul_lds_wide(lds, LayoutWin<KW>::gh256, acc) ^ parts[k];
     return acc;
