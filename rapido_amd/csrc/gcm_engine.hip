@@ -504,13 +504,17 @@ MI355X_GCM_KERNEL_F(mi355x_tls_open_aes256_k4, 14, 4, false, true)
         window_body<NR, SEAL, FRAME, THREADS, KW>(ki, iv0, iv1, iv2, descs, nrecs, src, dst, aad, st, types, conn);        \
     }
 /* single-record latency kernels: 32-position segments (4 steps of 8 lanes), one record per 512-thread group */
+#ifndef MI355X_WIN32_THREADS
+#define MI355X_WIN32_THREADS 512
+#endif
 #define MI355X_WIN32_KERNEL(NAME, NR, SEAL, FRAME)                                                                     \
-    extern "C" __global__ __launch_bounds__(512) void NAME(                                                            \
+    extern "C" __global__ __launch_bounds__(MI355X_WIN32_THREADS) void NAME(                                           \
         const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2, const void *__restrict__ descs,     \
         uint32_t nrecs, const uint8_t *src, uint8_t *dst, const uint8_t *__restrict__ aad, uint32_t *__restrict__ st,   \
         uint8_t *__restrict__ types, const uint32_t *__restrict__ conn)                                                \
     {                                                                                                                  \
-        window_body<NR, SEAL, FRAME, 512, 8, 32>(ki, iv0, iv1, iv2, descs, nrecs, src, dst, aad, st, types, conn);     \
+        window_body<NR, SEAL, FRAME, MI355X_WIN32_THREADS, 8, 32>(ki, iv0, iv1, iv2, descs, nrecs, src, dst, aad, st,  \
+                                                                  types, conn);                                      \
     }
 MI355X_WIN32_KERNEL(mi355x_tls_win32_seal_aes128, 10, true, true)
 MI355X_WIN32_KERNEL(mi355x_tls_win32_seal_aes256, 14, true, true)
@@ -704,12 +708,13 @@ static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void
              {mi355x_tls_win32_seal_aes128, mi355x_tls_win32_seal_aes256}}};
         const bool wide = n > 15u * (uint64_t)ctx->num_cu; /* the wide groups (15 records) fill every CU */
         /* at most g_seg32_records (default: one per CU): half-length segments, half the walk (4 steps) */
-        const bool seg32 = !wide && n <= (g_seg32_records == SIZE_MAX ? (size_t)ctx->num_cu : g_seg32_records);
+        constexpr uint32_t per32 = (MI355X_WIN32_THREADS / 8u) / WIN_SEG32_MAXSEG; /* records per 32-position group */
+        const bool seg32 = !wide && n <= (g_seg32_records == SIZE_MAX ? (size_t)per32 * ctx->num_cu : g_seg32_records);
         const win_kernel_t wk = seg32 ? table32[frame][seal][ctx->key_size == 32]
                                       : table[frame][wide][seal][ctx->key_size == 32];
         /* latency kernels: 512 threads, 8 lanes per segment; wide: 1024 threads, 4 lanes (MI355X_WIN_KERNEL list) */
-        const uint32_t threads = wide ? 1024u : 512u,
-                       per = seg32 ? 1u : (threads / (wide ? 4u : 8u)) / WIN_MAXSEG;
+        const uint32_t threads = seg32 ? (uint32_t)MI355X_WIN32_THREADS : wide ? 1024u : 512u,
+                       per = seg32 ? per32 : (threads / (wide ? 4u : 8u)) / WIN_MAXSEG;
         uint64_t blocks = (n + per - 1) / per;
         if (wide && blocks > (uint64_t)ctx->num_cu)
             blocks = (uint64_t)ctx->num_cu;

@@ -38,7 +38,8 @@ VARIANTS = {
     "no_ghash": ["-DGCM_ABLATE_GHASH=1"],
     "no_aes": ["-DGCM_ABLATE_AES=1"],
     "no_both": ["-DGCM_ABLATE_AES=1", "-DGCM_ABLATE_GHASH=1"],
-    "fill16": ["-DGCM_WIN_FILL=16u"],  # window kernels: 16 vectors in flight per thread during the LDS fill
+    "fill16": ["-DGCM_WIN_FILL=16u"],
+    "w32t1024": ["-DMI355X_WIN32_THREADS=1024"],  # 32-position window kernels: 3 records per 1024-thread group  # window kernels: 16 vectors in flight per thread during the LDS fill
 }
 if os.environ.get("ABLATE_VARIANTS"):
     VARIANTS = {k: v for k, v in VARIANTS.items() if k in os.environ["ABLATE_VARIANTS"].split(",")}
