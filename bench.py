@@ -299,6 +299,33 @@ def main() -> None:
                                     f"{lds_cycles_per_block:.2f} LDS clk/block/CU, {ncu} CU x {LDS_CLOCK_GHZ} GHz",
                            "note": "this read mix alone sustains 0.78 of the nominal rate (profiles/r01c_lds_ceiling.json)"}
 
+    if world == 1 and not args.no_e2e:
+        # latency side (not `value`): one rapido send window, 16 x 16 KiB records framed in one launch on the
+        # window kernels, device-resident, back-to-back launches timed with HIP events
+        WIN, FRAG = 16, 16384
+        t = np.zeros(WIN, ra.TLS_RECORD_DTYPE)
+        t["src"] = np.arange(WIN, dtype=np.uint64) * FRAG
+        t["dst"] = np.arange(WIN, dtype=np.uint64) * (FRAG + 22)
+        t["seq"] = np.arange(WIN, dtype=np.uint64)
+        t["len"], t["type"] = FRAG, 23
+        d_t = torch.from_numpy(t.view(np.uint8)).to(dev)
+        d_wire = torch.zeros(WIN * (FRAG + 22), dtype=torch.uint8, device=dev)
+
+        def window():
+            eng.tls_seal_records(iv, d_t.data_ptr(), WIN, d_src.data_ptr(), d_wire.data_ptr(), sh)
+
+        for _ in range(5):
+            window()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record(stream)
+        for _ in range(100):
+            window()
+        ev[1].record(stream)
+        torch.cuda.synchronize(dev)
+        out["window_latency"] = {"us_per_window": round(ev[0].elapsed_time(ev[1]) * 10.0, 2),
+                                 "window": f"{WIN} x {FRAG} B TLS records sealed in one launch (rapido send window), "
+                                           f"AES-{8 * wl['key']}, device-resident, 100 back-to-back launches"}
+
     if (args.e2e or world == 1) and not args.no_e2e:
         # PCIe-inclusive: records start and end in pinned host memory
         h_src = torch.empty(src_bytes, dtype=torch.uint8, pin_memory=True)
