@@ -35,6 +35,10 @@ def main(tag, label):
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, f"{label}_kernel_stats.csv"))
+    for w in ("16k", "16k-aes128", "ragged"):
+        p = os.path.join(src, f"trace_{w}", "run_kernel_stats.csv")
+        if os.path.exists(p):
+            shutil.copy(p, os.path.join(dst, f"{label}_kernel_stats_{w}.csv"))
     with open(os.path.join(dst, f"{label}_bench.jsonl"), "w") as f:
         for name in ("bench_1400.json", "bench_other.jsonl"):
             p = os.path.join(src, name)
