@@ -99,9 +99,17 @@ typedef const struct st_ptls_aead_algorithm_t {
  * ====================================================================================== */
 extern ptls_cipher_algorithm_t ptls_mi355x_aes128ctr, ptls_mi355x_aes256ctr;
 extern ptls_aead_algorithm_t ptls_mi355x_aes128gcm, ptls_mi355x_aes256gcm;
+/*
+ * AES-ECB cipher objects, the aead->ecb_cipher of both AEAD objects (fusion leaves ecb_cipher NULL,
+ * lib/fusion.c:990,1000; the generic suite t/picotls.c:266-307 needs it).  Like ptls_openssl_aes{128,256}ecb
+ * (lib/openssl.c:1580-1597): block_size 16, iv_size 0, no do_init; setup_crypto(ctx, is_enc, key) picks the
+ * AES cipher (is_enc != 0) or the inverse cipher (is_enc == 0); do_transform processes len / 16 whole blocks
+ * (len must be a multiple of 16).
+ */
+extern ptls_cipher_algorithm_t ptls_mi355x_aes128ecb, ptls_mi355x_aes256ecb;
 
 /* Capability probe -- replaces ptls_fusion_is_supported_by_cpu (lib/fusion.c:1041-1065):
- * 1 when a gfx950 device is visible to the HIP runtime, else 0. */
+ * 1 when the calling thread's current HIP device is a gfx950, else 0 (contexts bind to that device). */
 int ptls_mi355x_is_supported(void);
 
 /* ======================================================================================
@@ -125,8 +133,24 @@ int ptls_mi355x_aesgcm_encrypt(ptls_mi355x_aesgcm_context_t *ctx, void *output, 
 int ptls_mi355x_aesgcm_decrypt(ptls_mi355x_aesgcm_context_t *ctx, void *output, const void *input, size_t inlen,
                                const void *nonce12, const void *aad, size_t aadlen, const void *tag);
 
-/* AES-ECB encryption of nblocks 16-byte blocks in host memory (header protection, H, ...). */
+/* AES-ECB encryption of nblocks 16-byte blocks in host memory with the context's key
+ * (ptls_fusion_aesecb_encrypt, lib/fusion.c:747-752). */
 int ptls_mi355x_aesecb_encrypt(ptls_mi355x_aesgcm_context_t *ctx, void *output, const void *input, size_t nblocks);
+
+/*
+ * Round-keys-only AES context: the ECB and CTR cipher objects and header protection (the analogue of
+ * ptls_fusion_aesecb_context_t, include/picotls/fusion.h:36-39 / ptls_fusion_aesecb_init, lib/fusion.c:692-740).
+ * Holds the encryption schedule and the equivalent-inverse-cipher schedule (FIPS-197 5.3.5) on the device
+ * that is current at creation -- 480 bytes, no GHASH tables.
+ *   ptls_mi355x_aes_ecb:       host buffers, synchronous (is_enc 0 = decrypt)
+ *   ptls_mi355x_aes_ecb_batch: device buffers, asynchronous on `stream`
+ */
+typedef struct st_ptls_mi355x_aes_context ptls_mi355x_aes_context_t;
+ptls_mi355x_aes_context_t *ptls_mi355x_aes_new(const void *key, size_t key_size);
+void ptls_mi355x_aes_free(ptls_mi355x_aes_context_t *ctx);
+int ptls_mi355x_aes_ecb(ptls_mi355x_aes_context_t *ctx, int is_enc, void *output, const void *input, size_t nblocks);
+int ptls_mi355x_aes_ecb_batch(ptls_mi355x_aes_context_t *ctx, int is_enc, uint8_t *dst, const uint8_t *src,
+                              size_t nblocks, void *stream);
 
 /* ======================================================================================
  * 3. Batch extension (the hot path).  Seals or opens n independent records in ONE launch.
@@ -188,6 +212,8 @@ int ptls_mi355x_open_batch_ordered(ptls_mi355x_aesgcm_context_t *ctx, const void
  *               status[i] = inner plaintext length and types[i] = content type, or
  *               status[i] = PTLS_MI355X_TLS_BAD_RECORD_MAC (tag, or len < 16; plaintext zeroed)
  *                           PTLS_MI355X_TLS_UNEXPECTED_MESSAGE (no non-zero byte)
+ *    A context is used by one host thread at a time (as picotls contexts are); launches may go to any
+ *    streams.
  *    Device pointers, asynchronous on `stream`, like section 3.  Headers are parsed and
  *    descriptors planned on the host (ptls_mi355x_tls_plan_send / _parse_records below).
  * ====================================================================================== */
@@ -195,7 +221,7 @@ typedef struct st_ptls_mi355x_tls_record_t {
     uint64_t src;  /* seal: fragment offset in src;     open: record (header) offset in src */
     uint64_t dst;  /* seal: record (header) offset in dst; open: plaintext offset in dst */
     uint64_t seq;  /* record sequence number */
-    uint32_t len;  /* seal: fragment bytes (<= 16384); open: the header's length field */
+    uint32_t len;  /* seal: fragment bytes (<= 16384; a longer one is skipped, nothing written); open: the header's length field */
     uint32_t type; /* seal: inner content type (23 = application_data); open: unused */
 } ptls_mi355x_tls_record_t;
 
@@ -205,6 +231,7 @@ typedef struct st_ptls_mi355x_tls_record_t {
 #define PTLS_MI355X_TLS_OVERHEAD (5 + 1 + 16)           /* header + content type + tag */
 #define PTLS_MI355X_TLS_BAD_RECORD_MAC 0xffffffffu      /* -> PTLS_ALERT_BAD_RECORD_MAC (20) */
 #define PTLS_MI355X_TLS_UNEXPECTED_MESSAGE 0xfffffffeu  /* -> PTLS_ALERT_UNEXPECTED_MESSAGE (10) */
+#define PTLS_MI355X_TLS_NOT_PROCESSED 0xfffffffdu       /* behind a failed record (PTLS_MI355X_OPEN_STOP_AT_FAILURE) */
 
 int ptls_mi355x_tls_seal_records(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12,
                                  const ptls_mi355x_tls_record_t *recs, size_t n, const uint8_t *src, uint8_t *dst,
@@ -224,6 +251,22 @@ int ptls_mi355x_tls_open_records_multi(ptls_mi355x_aesgcm_context_t *ctx, const 
                                        const ptls_mi355x_tls_record_t *recs, const uint32_t *conn_ids, size_t n,
                                        const uint8_t *src, uint8_t *dst, uint32_t *status, uint8_t *types,
                                        void *stream);
+
+/*
+ * picotls stops at the first record that fails and never advances seq past it (aead_decrypt returns
+ * PTLS_ALERT_BAD_RECORD_MAC, lib/picotls.c:650-652; an all-zero inner plaintext PTLS_ALERT_UNEXPECTED_MESSAGE,
+ * :4790).  The batch open above verifies every record independently.  With PTLS_MI355X_OPEN_STOP_AT_FAILURE,
+ * every record behind a failed record OF THE SAME CONNECTION gets status PTLS_MI355X_TLS_NOT_PROCESSED, type 0
+ * and a zeroed plaintext slot, so the accepted records are exactly the ones ptls_receive would have delivered
+ * before raising the alert.  Connections are runs of equal conn_ids (conn_ids == NULL: one connection); a
+ * connection's records must be contiguous and in seq order, as tls_parse_records lays out a recv window.
+ * Without the flag the caller must discard the statuses after a connection's first failure itself.
+ */
+#define PTLS_MI355X_OPEN_STOP_AT_FAILURE 1
+int ptls_mi355x_tls_open_records_ex(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12,
+                                    const ptls_mi355x_tls_record_t *recs, const uint32_t *conn_ids, size_t n,
+                                    const uint8_t *src, uint8_t *dst, uint32_t *status, uint8_t *types, int flags,
+                                    void *stream);
 
 /* Host-side planning (no device access), the loops of the reference record layer:
  *  plan_send: splits len bytes at src_off into <= 16384-byte fragments with consecutive seq
@@ -274,8 +317,9 @@ size_t ptls_mi355x_set_seg32_records(size_t n);
  * instead of 0, so a test can place the 2^32 wrap inside its first launches.  Returns the previous value.
  */
 uint32_t ptls_mi355x_set_work_ticket_origin(uint32_t origin);
-/* name of the kernel symbol the next batch launch with these parameters uses (for profiling) */
-const char *ptls_mi355x_kernel_name(int is_seal, size_t key_size);
+/* name of the kernel symbol a launch of n records with these parameters uses on the current device (framing:
+ * the section-4 entry points) -- the same selection launch_batch makes (for profiling and reports) */
+const char *ptls_mi355x_kernel_name(int is_seal, size_t key_size, size_t n, int framing);
 /* last HIP error string seen by the engine ("" if none) */
 const char *ptls_mi355x_last_error(void);
 

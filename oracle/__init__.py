@@ -46,6 +46,10 @@ def _load():
         lib.oracle_gcm_open.restype = C.c_size_t
         lib.oracle_aes_ecb_encrypt.argtypes = [vp, sz, vp, vp]
         lib.oracle_aes_ecb_encrypt.restype = C.c_int
+        lib.oracle_aes_ecb_encrypt_n.argtypes = [vp, sz, vp, vp, sz]
+        lib.oracle_aes_ecb_encrypt_n.restype = C.c_int
+        lib.oracle_aes_ecb_decrypt.argtypes = [vp, sz, vp, vp, sz]
+        lib.oracle_aes_ecb_decrypt.restype = C.c_int
         lib.oracle_build_iv.argtypes = [vp, C.c_uint64, vp]
         lib.oracle_gf128_mul.argtypes = [vp, vp, vp]
         lib.oracle_gcm_batch.argtypes = [C.c_int, vp, sz, vp, vp, sz, vp, vp, vp, vp, C.c_int]
@@ -92,6 +96,16 @@ def ecb(key: bytes, block: bytes) -> bytes:
     if _load().oracle_aes_ecb_encrypt(_buf(key), len(key), _buf(block), out) != 0:
         raise ValueError("bad key size")
     return out.raw
+
+
+def ecb_blocks(key: bytes, data: bytes, encrypt: bool = True) -> bytes:
+    """AES-ECB over len(data) // 16 blocks: FIPS-197 Cipher (encrypt) or InvCipher (decrypt)."""
+    assert len(data) % 16 == 0
+    out = C.create_string_buffer(max(len(data), 1))
+    f = _load().oracle_aes_ecb_encrypt_n if encrypt else _load().oracle_aes_ecb_decrypt
+    if f(_buf(key), len(key), _buf(data), out, len(data) // 16) != 0:
+        raise ValueError("bad key size")
+    return out.raw[:len(data)]
 
 
 def gf128_mul(x: bytes, y: bytes) -> bytes:
@@ -159,6 +173,7 @@ class Reference:
         lib.ref_slot_open.argtypes = [vp, sz, vp, vp, sz, C.c_uint64, vp, sz, vp, sz, vp]
         lib.ref_slot_open.restype = C.c_size_t
         lib.ref_ecb.argtypes = [vp, sz, vp, vp]
+        lib.ref_ecb_decrypt.argtypes = [vp, sz, vp, vp]
         lib.ref_bench.argtypes = [sz, sz, sz, sz, C.c_int, C.POINTER(C.c_double)]
         lib.ref_bench.restype = C.c_int
         lib.ref_tls_send.argtypes = [vp, sz, vp, C.c_uint64, vp, sz, vp, sz, C.POINTER(C.c_size_t),
@@ -206,6 +221,12 @@ class Reference:
     def ecb(self, key, block) -> bytes:
         out = C.create_string_buffer(16)
         self.lib.ref_ecb(_buf(key), len(key), _buf(block), out)
+        return out.raw
+
+    def ecb_decrypt(self, key, block) -> bytes:
+        """cifra's cf_aes_decrypt (the reference minicrypto ECB decrypt, lib/cifra/aes-common.h:48-53)."""
+        out = C.create_string_buffer(16)
+        self.lib.ref_ecb_decrypt(_buf(key), len(key), _buf(block), out)
         return out.raw
 
     def tls_send(self, key, static_iv, seq0, data):

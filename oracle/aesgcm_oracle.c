@@ -11,6 +11,8 @@
  *     lib/fusion.c:681-740 (ptls_fusion_aesecb_init / expand_key).  Written here
  *     from FIPS-197 sec. 5.1-5.2 (byte oriented, no tables except the S-box,
  *     which is itself derived from the GF(2^8) inverse + affine map).
+ *   - AES-128/256 block decryption (FIPS-197 sec. 5.3 InvCipher), the inverse of the
+ *     ECB cipher the generic suite needs (t/picotls.c:266-307: encrypt, then decrypt back).
  *   - GHASH and GCM with a 96-bit IV; reference: ptls_fusion_aesgcm_encrypt /
  *     _decrypt (lib/fusion.c:239-679), structured as in NIST SP 800-38D
  *     (Algorithm 1 for the multiply, Algorithm 4/5 for seal/open) -- the same
@@ -143,6 +145,42 @@ static void aes_encrypt(const oracle_aes_t *a, const uint8_t in[16], uint8_t out
     memcpy(out, s, 16);
 }
 
+/*
+ * FIPS-197 sec. 5.3 InvCipher() (the straightforward inverse, not the equivalent inverse cipher the
+ * engine uses): AddRoundKey with the last round key, then per round InvShiftRows, InvSubBytes,
+ * AddRoundKey, InvMixColumns.  Reference counterpart: AES-ECB decryption of the generic suite's
+ * ecb_cipher (t/picotls.c:266-307; OpenSSL EVP_aes_*_ecb, lib/openssl.c:831-838).
+ */
+static void aes_decrypt(const oracle_aes_t *a, const uint8_t in[16], uint8_t out[16])
+{
+    uint8_t inv[256], s[16], t[16];
+    for (int x = 0; x < 256; ++x)
+        inv[sbox[x]] = (uint8_t)x;
+    for (int i = 0; i < 16; ++i)
+        s[i] = in[i] ^ a->rk[a->rounds][i];
+    for (int r = a->rounds - 1; r >= 0; --r) {
+        /* InvShiftRows + InvSubBytes: row r of column c comes from column (c - r) mod 4 */
+        for (int c = 0; c < 4; ++c)
+            for (int row = 0; row < 4; ++row)
+                t[row + 4 * c] = inv[s[row + 4 * ((c - row + 4) & 3)]];
+        for (int i = 0; i < 16; ++i)
+            t[i] ^= a->rk[r][i];
+        if (r != 0) {
+            /* InvMixColumns */
+            for (int c = 0; c < 4; ++c) {
+                uint8_t *col = t + 4 * c, a0 = col[0], a1 = col[1], a2 = col[2], a3 = col[3];
+                s[4 * c + 0] = (uint8_t)(gf8_mul(a0, 14) ^ gf8_mul(a1, 11) ^ gf8_mul(a2, 13) ^ gf8_mul(a3, 9));
+                s[4 * c + 1] = (uint8_t)(gf8_mul(a0, 9) ^ gf8_mul(a1, 14) ^ gf8_mul(a2, 11) ^ gf8_mul(a3, 13));
+                s[4 * c + 2] = (uint8_t)(gf8_mul(a0, 13) ^ gf8_mul(a1, 9) ^ gf8_mul(a2, 14) ^ gf8_mul(a3, 11));
+                s[4 * c + 3] = (uint8_t)(gf8_mul(a0, 11) ^ gf8_mul(a1, 13) ^ gf8_mul(a2, 9) ^ gf8_mul(a3, 14));
+            }
+        } else {
+            memcpy(s, t, 16);
+        }
+    }
+    memcpy(out, s, 16);
+}
+
 /* -------------------------------------------------------------- GHASH ----- */
 
 /* SP 800-38D Algorithm 1: Z = X * Y in GF(2^128), bit 0 = MSB of byte 0. */
@@ -250,6 +288,28 @@ int oracle_aes_ecb_encrypt(const uint8_t *key, size_t keylen, const uint8_t in[1
     if (aes_expand(&a, key, keylen) != 0)
         return -1;
     aes_encrypt(&a, in, out);
+    return 0;
+}
+
+/* nblocks of AES-ECB decryption (FIPS-197 InvCipher) */
+int oracle_aes_ecb_decrypt(const uint8_t *key, size_t keylen, const uint8_t *in, uint8_t *out, size_t nblocks)
+{
+    oracle_aes_t a;
+    if (aes_expand(&a, key, keylen) != 0)
+        return -1;
+    for (size_t b = 0; b < nblocks; ++b)
+        aes_decrypt(&a, in + 16 * b, out + 16 * b);
+    return 0;
+}
+
+/* nblocks of AES-ECB encryption */
+int oracle_aes_ecb_encrypt_n(const uint8_t *key, size_t keylen, const uint8_t *in, uint8_t *out, size_t nblocks)
+{
+    oracle_aes_t a;
+    if (aes_expand(&a, key, keylen) != 0)
+        return -1;
+    for (size_t b = 0; b < nblocks; ++b)
+        aes_encrypt(&a, in + 16 * b, out + 16 * b);
     return 0;
 }
 

@@ -25,6 +25,7 @@
 #include <immintrin.h>
 #include "picotls.h"
 #include "picotls/fusion.h"
+#include "aes.h" /* deps/cifra/src/aes.h: the reference's minicrypto AES (ECB decrypt, lib/cifra/aes-common.h:48-53) */
 
 static __m128i nonce_to_ctr(const uint8_t iv[12])
 {
@@ -108,6 +109,20 @@ int ref_ecb(const uint8_t *key, size_t keylen, const uint8_t in[16], uint8_t out
     ptls_fusion_aesecb_init(&ecb, 1, key, keylen);
     ptls_fusion_aesecb_encrypt(&ecb, out, in);
     ptls_fusion_aesecb_dispose(&ecb);
+    return 0;
+}
+
+/*
+ * AES-ECB decryption of the reference's minicrypto binding (aesecb_decrypt, lib/cifra/aes-common.h:48-53:
+ * cf_aes_init + cf_aes_decrypt of the vendored deps/cifra/src/aes.c, compiled from where it lies) -- fusion
+ * has no decryption; this pins the oracle's InvCipher to reference code.
+ */
+int ref_ecb_decrypt(const uint8_t *key, size_t keylen, const uint8_t in[16], uint8_t out[16])
+{
+    cf_aes_context aes;
+    cf_aes_init(&aes, key, keylen);
+    cf_aes_decrypt(&aes, in, out);
+    cf_aes_finish(&aes);
     return 0;
 }
 

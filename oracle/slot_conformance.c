@@ -15,6 +15,8 @@
  *   4. lib/picotls.c:630-654 record-layer sequence (build_aad, init, update(data), update(type),
  *      final) on the engine, equal to fusion's one-shot encryption of data||type, for TLS lengths
  *   5. t/picotls.c:161-198 test_ciphersuite streaming + tamper detection
+ *   6. t/picotls.c:266-321 test_ecb (encrypt, then decrypt with an is_enc = 0 context) for aead->ecb_cipher of
+ *      both AEADs, and test_ctr for aead->ctr_cipher
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -187,6 +189,71 @@ static void test_ciphersuite_streaming(ptls_aead_algorithm_t *algo)
     ptls_aead_free(c);
 }
 
+/*
+ * t/picotls.c:266-307 test_ecb through aead->ecb_cipher, with the reference's ptls_cipher_new / ptls_cipher_free
+ * (lib/picotls.c) and ptls_cipher_encrypt dispatcher: FIPS-197 C.1 / C.3 encryption, then decryption in place with
+ * a context made with is_enc = 0.  Plus a 64-block buffer against fusion's ECB encryption, and back.
+ */
+static void test_ecb_cipher(ptls_aead_algorithm_t *aead, const char *expected_hex)
+{
+    static const uint8_t fips_pt[16] = {0x00, 0x11, 0x22, 0x33, 0x44, 0x55, 0x66, 0x77,
+                                        0x88, 0x99, 0xaa, 0xbb, 0xcc, 0xdd, 0xee, 0xff};
+    uint8_t key[32], expected[16], actual[16];
+    for (int i = 0; i < 32; ++i)
+        key[i] = (uint8_t)i;
+    for (int i = 0; i < 16; ++i)
+        sscanf(expected_hex + 2 * i, "%2hhx", &expected[i]);
+    ptls_cipher_algorithm_t *algo = aead->ecb_cipher;
+    CHECK(algo != NULL, "%s has an ecb_cipher", aead->name);
+    if (algo == NULL)
+        return;
+    ptls_cipher_context_t *c = ptls_cipher_new(algo, 1, key);
+    CHECK(c != NULL, "ptls_cipher_new(ecb, enc)");
+    memset(actual, 0, sizeof(actual));
+    ptls_cipher_encrypt(c, actual, fips_pt, sizeof(actual));
+    ptls_cipher_free(c);
+    CHECK(memcmp(actual, expected, 16) == 0, "%s ecb encrypt (FIPS-197)", algo->name);
+    c = ptls_cipher_new(algo, 0, key);
+    ptls_cipher_encrypt(c, actual, actual, sizeof(actual));
+    ptls_cipher_free(c);
+    CHECK(memcmp(actual, fips_pt, 16) == 0, "%s ecb decrypt back to the plaintext", algo->name);
+
+    uint8_t buf[64 * 16], enc[64 * 16], want[64 * 16];
+    rnd_bytes(key, sizeof(key));
+    rnd_bytes(buf, sizeof(buf));
+    ptls_fusion_aesecb_context_t f;
+    ptls_fusion_aesecb_init(&f, 1, key, algo->key_size);
+    for (int b = 0; b < 64; ++b)
+        ptls_fusion_aesecb_encrypt(&f, want + 16 * b, buf + 16 * b);
+    ptls_fusion_aesecb_dispose(&f);
+    c = ptls_cipher_new(algo, 1, key);
+    ptls_cipher_encrypt(c, enc, buf, sizeof(buf));
+    ptls_cipher_free(c);
+    CHECK(memcmp(enc, want, sizeof(enc)) == 0, "%s ecb 64 blocks vs fusion", algo->name);
+    c = ptls_cipher_new(algo, 0, key);
+    ptls_cipher_encrypt(c, enc, enc, sizeof(enc));
+    ptls_cipher_free(c);
+    CHECK(memcmp(enc, buf, sizeof(enc)) == 0, "%s ecb 64 blocks decrypt", algo->name);
+}
+
+/* t/picotls.c:309-321 test_ctr through aead->ctr_cipher: AES128-CTR keystream of 16 zero bytes */
+static void test_ctr_cipher(void)
+{
+    static const uint8_t key[16] = {0x2b, 0x7e, 0x15, 0x16, 0x28, 0xae, 0xd2, 0xa6, 0xab, 0xf7, 0x15, 0x88, 0x09, 0xcf, 0x4f, 0x3c},
+                         iv[16] = {0x6b, 0xc1, 0xbe, 0xe2, 0x2e, 0x40, 0x9f, 0x96, 0xe9, 0x3d, 0x7e, 0x11, 0x73, 0x93, 0x17, 0x2a},
+                         expected[16] = {0x3a, 0xd7, 0x7b, 0xb4, 0x0d, 0x7a, 0x36, 0x60,
+                                         0xa8, 0x9e, 0xca, 0xf3, 0x24, 0x66, 0xef, 0x97};
+    static const uint8_t zeroes[16] = {0};
+    uint8_t buf[16];
+    ptls_cipher_algorithm_t *algo = ptls_mi355x_aes128gcm.ctr_cipher;
+    CHECK(algo->key_size == 16 && algo->iv_size == 16, "ctr cipher sizes");
+    ptls_cipher_context_t *c = ptls_cipher_new(algo, 1, key);
+    ptls_cipher_init(c, iv);
+    ptls_cipher_encrypt(c, buf, zeroes, sizeof(buf));
+    ptls_cipher_free(c);
+    CHECK(memcmp(buf, expected, 16) == 0, "aes128ctr KAT");
+}
+
 int main(int argc, char **argv)
 {
     int runs = argc > 1 ? atoi(argv[1]) : 1000;
@@ -206,6 +273,9 @@ int main(int argc, char **argv)
     test_record_layer_sequence(1);
     test_ciphersuite_streaming(&ptls_mi355x_aes128gcm);
     test_ciphersuite_streaming(&ptls_mi355x_aes256gcm);
+    test_ecb_cipher(&ptls_mi355x_aes128gcm, "69c4e0d86a7b0430d8cdb78070b4c55a");
+    test_ecb_cipher(&ptls_mi355x_aes256gcm, "8ea2b7ca516745bfeafc49904b496089");
+    test_ctr_cipher();
     printf("%d ok, %d failed\n", n_ok, n_fail);
     return n_fail ? 1 : 0;
 }

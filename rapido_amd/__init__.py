@@ -46,6 +46,8 @@ TLS_MAX_RECORD = 16384 + 256
 TLS_OVERHEAD = 5 + 1 + 16
 TLS_BAD_RECORD_MAC = 0xFFFFFFFF  # -> PTLS_ALERT_BAD_RECORD_MAC (20)
 TLS_UNEXPECTED_MESSAGE = 0xFFFFFFFE  # -> PTLS_ALERT_UNEXPECTED_MESSAGE (10)
+TLS_NOT_PROCESSED = 0xFFFFFFFD  # behind a failed record of its connection (OPEN_STOP_AT_FAILURE)
+OPEN_STOP_AT_FAILURE = 1
 
 #: every symbol include/ptls_mi355x.h declares
 EXPORTED_FUNCTIONS = (
@@ -58,10 +60,11 @@ EXPORTED_FUNCTIONS = (
     "ptls_mi355x_tls_open_records_multi", "ptls_mi355x_set_tls_window_records",
     "ptls_mi355x_set_aead_window_records", "ptls_mi355x_set_slot_zero_copy_bytes",
     "ptls_mi355x_set_work_ticket_origin", "ptls_mi355x_set_seg32_records", "ptls_mi355x_tls_plan_send",
-    "ptls_mi355x_tls_parse_records",
+    "ptls_mi355x_tls_parse_records", "ptls_mi355x_tls_open_records_ex", "ptls_mi355x_aes_new", "ptls_mi355x_aes_free",
+    "ptls_mi355x_aes_ecb", "ptls_mi355x_aes_ecb_batch",
 )
 EXPORTED_OBJECTS = ("ptls_mi355x_aes128gcm", "ptls_mi355x_aes256gcm", "ptls_mi355x_aes128ctr",
-                    "ptls_mi355x_aes256ctr")
+                    "ptls_mi355x_aes256ctr", "ptls_mi355x_aes128ecb", "ptls_mi355x_aes256ecb")
 
 # ----------------------------------------------------------------- picotls ABI (ctypes) ---
 vp, sz, u64 = C.c_void_p, C.c_size_t, C.c_uint64
@@ -130,7 +133,7 @@ def lib() -> C.CDLL:
         L.ptls_mi355x_seal_batch_ordered.argtypes = [vp, vp, vp, vp, sz, vp, vp, vp, vp]
         L.ptls_mi355x_open_batch_ordered.argtypes = [vp, vp, vp, vp, sz, vp, vp, vp, vp, vp]
         L.ptls_mi355x_set_lanes_per_record.argtypes = [C.c_int]
-        L.ptls_mi355x_kernel_name.argtypes = [C.c_int, sz]
+        L.ptls_mi355x_kernel_name.argtypes = [C.c_int, sz, sz, C.c_int]
         L.ptls_mi355x_kernel_name.restype = C.c_char_p
         L.ptls_mi355x_last_error.restype = C.c_char_p
         L.ptls_mi355x_tls_seal_records.argtypes = [vp, vp, vp, sz, vp, vp, vp]
@@ -147,6 +150,12 @@ def lib() -> C.CDLL:
         L.ptls_mi355x_set_seg32_records.restype = sz
         L.ptls_mi355x_set_work_ticket_origin.restype = C.c_uint32
         L.ptls_mi355x_tls_open_records_multi.argtypes = [vp, vp, vp, vp, sz, vp, vp, vp, vp, vp]
+        L.ptls_mi355x_tls_open_records_ex.argtypes = [vp, vp, vp, vp, sz, vp, vp, vp, vp, C.c_int, vp]
+        L.ptls_mi355x_aes_new.argtypes = [vp, sz]
+        L.ptls_mi355x_aes_new.restype = vp
+        L.ptls_mi355x_aes_free.argtypes = [vp]
+        L.ptls_mi355x_aes_ecb.argtypes = [vp, C.c_int, vp, vp, sz]
+        L.ptls_mi355x_aes_ecb_batch.argtypes = [vp, C.c_int, vp, vp, sz, vp]
         L.ptls_mi355x_tls_plan_send.argtypes = [sz, C.c_uint32, C.POINTER(u64), u64, u64, vp, sz, C.POINTER(sz)]
         L.ptls_mi355x_tls_plan_send.restype = sz
         L.ptls_mi355x_tls_parse_records.argtypes = [vp, sz, u64, C.POINTER(u64), u64, vp, sz, C.POINTER(sz),
@@ -374,10 +383,44 @@ class Engine:
             raise RuntimeError("tls_seal_records failed: " + last_error())
 
     def tls_open_records(self, static_iv: bytes, recs_ptr: int, n: int, src_ptr: int, dst_ptr: int, status_ptr: int,
-                         types_ptr: int, stream: int = 0, conn_ptr: int = 0) -> None:
-        if lib().ptls_mi355x_tls_open_records_multi(self.handle, _cbuf(static_iv), recs_ptr, conn_ptr or None, n,
-                                                    src_ptr, dst_ptr, status_ptr, types_ptr, stream or None):
+                         types_ptr: int, stream: int = 0, conn_ptr: int = 0, flags: int = 0) -> None:
+        """flags: OPEN_STOP_AT_FAILURE -- records behind a connection's first failure become TLS_NOT_PROCESSED."""
+        if lib().ptls_mi355x_tls_open_records_ex(self.handle, _cbuf(static_iv), recs_ptr, conn_ptr or None, n,
+                                                 src_ptr, dst_ptr, status_ptr, types_ptr, flags, stream or None):
             raise RuntimeError("tls_open_records failed: " + last_error())
+
+
+class AesKeys:
+    """ptls_mi355x_aes_context_t: round keys only (the ECB/CTR ciphers), on the current device."""
+
+    def __init__(self, key: bytes):
+        if len(key) not in (16, 32):
+            raise ValueError("key must be 16 or 32 bytes")
+        self.handle = lib().ptls_mi355x_aes_new(_cbuf(key), len(key))
+        if not self.handle:
+            raise RuntimeError("ptls_mi355x_aes_new failed: " + last_error())
+
+    def ecb(self, data: bytes, encrypt: bool = True) -> bytes:
+        assert len(data) % 16 == 0
+        out = C.create_string_buffer(max(len(data), 1))
+        if lib().ptls_mi355x_aes_ecb(self.handle, 1 if encrypt else 0, out, _cbuf(data), len(data) // 16):
+            raise RuntimeError("aes_ecb failed: " + last_error())
+        return out.raw[:len(data)]
+
+    def ecb_batch(self, dst_ptr: int, src_ptr: int, nblocks: int, encrypt: bool = True, stream: int = 0) -> None:
+        if lib().ptls_mi355x_aes_ecb_batch(self.handle, 1 if encrypt else 0, dst_ptr, src_ptr, nblocks, stream or None):
+            raise RuntimeError("aes_ecb_batch failed: " + last_error())
+
+    def close(self) -> None:
+        if self.handle:
+            lib().ptls_mi355x_aes_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def tls_plan_send(length: int, seq: int, content_type: int = 23, src_off: int = 0, dst_off: int = 0):
@@ -443,5 +486,6 @@ def set_work_ticket_origin(origin: int) -> int:
     return lib().ptls_mi355x_set_work_ticket_origin(origin & 0xFFFFFFFF)
 
 
-def kernel_name(is_seal: bool, key_size: int) -> str:
-    return lib().ptls_mi355x_kernel_name(1 if is_seal else 0, key_size).decode()
+def kernel_name(is_seal: bool, key_size: int, n: int, framing: bool = False) -> str:
+    """The kernel a launch of n records runs on (the selection launch_batch makes on the current device)."""
+    return lib().ptls_mi355x_kernel_name(1 if is_seal else 0, key_size, n, 1 if framing else 0).decode()

@@ -8,6 +8,7 @@
  *   aesgcm_xor_iv         (lib/fusion.c:934-940)  -> aesgcm_xor_iv
  *   streaming stubs       (lib/fusion.c:881-896)  -> implemented (buffering)
  *   ctr cipher            (lib/fusion.c:822-872)  -> struct mi355x_ctr
+ *   ecb cipher            (NULL in fusion, lib/fusion.c:990) -> struct mi355x_ecb (t/picotls.c:266-307)
  * Every AES/GHASH computation is done by the HIP engine (gcm_engine.hip); this file only
  * keeps per-context state (static IV, streaming buffer) and maps picotls' arguments onto
  * the engine's record descriptor.  A GPU failure inside a void slot entry point aborts with
@@ -43,9 +44,10 @@ static void engine_abort(const char *what)
 
 /* ------------------------------------------------------------------------ AES-CTR ------ */
 
+/* both ciphers hold a round-keys-only device context (ptls_mi355x_aes_new), no GHASH tables */
 struct mi355x_ctr {
     ptls_cipher_context_t super;
-    ptls_mi355x_aesgcm_context_t *engine;
+    ptls_mi355x_aes_context_t *aes;
     uint8_t bits[16];
     int is_ready;
 };
@@ -53,8 +55,8 @@ struct mi355x_ctr {
 static void ctr_dispose(ptls_cipher_context_t *_ctx)
 {
     struct mi355x_ctr *ctx = (struct mi355x_ctr *)_ctx;
-    ptls_mi355x_aesgcm_free(ctx->engine);
-    ctx->engine = NULL;
+    ptls_mi355x_aes_free(ctx->aes);
+    ctx->aes = NULL;
     memset(ctx->bits, 0, sizeof(ctx->bits));
 }
 
@@ -62,7 +64,7 @@ static void ctr_dispose(ptls_cipher_context_t *_ctx)
 static void ctr_init(ptls_cipher_context_t *_ctx, const void *iv)
 {
     struct mi355x_ctr *ctx = (struct mi355x_ctr *)_ctx;
-    if (ptls_mi355x_aesecb_encrypt(ctx->engine, ctx->bits, iv, 1) != 0)
+    if (ptls_mi355x_aes_ecb(ctx->aes, 1, ctx->bits, iv, 1) != 0)
         engine_abort("aes-ecb");
     ctx->is_ready = 1;
 }
@@ -87,7 +89,7 @@ static int aesctr_setup(ptls_cipher_context_t *_ctx, const void *key, size_t key
     ctx->super.do_init = ctr_init;
     ctx->super.do_transform = ctr_transform;
     ctx->is_ready = 0;
-    if ((ctx->engine = ptls_mi355x_aesgcm_new(key, key_size, 16)) == NULL)
+    if ((ctx->aes = ptls_mi355x_aes_new(key, key_size)) == NULL)
         return PTLS_ERROR_LIBRARY;
     return 0;
 }
@@ -102,6 +104,59 @@ static int aes256ctr_setup(ptls_cipher_context_t *ctx, int is_enc, const void *k
 {
     (void)is_enc;
     return aesctr_setup(ctx, key, 32);
+}
+
+/* ------------------------------------------------------------------------ AES-ECB ------ */
+
+/*
+ * The ECB cipher of the generic suite (t/picotls.c:266-307; ptls_openssl_aes{128,256}ecb, lib/openssl.c:831-838,
+ * 1580-1597; cifra's aesecb_setup_crypto, lib/cifra/aes-common.h:55-63): is_enc selects the AES cipher or the
+ * inverse cipher, there is no IV, and every transform is len / 16 independent blocks.
+ */
+struct mi355x_ecb {
+    ptls_cipher_context_t super;
+    ptls_mi355x_aes_context_t *aes;
+    int is_enc;
+};
+
+static void ecb_dispose(ptls_cipher_context_t *_ctx)
+{
+    struct mi355x_ecb *ctx = (struct mi355x_ecb *)_ctx;
+    ptls_mi355x_aes_free(ctx->aes);
+    ctx->aes = NULL;
+}
+
+static void ecb_transform(ptls_cipher_context_t *_ctx, void *output, const void *input, size_t len)
+{
+    struct mi355x_ecb *ctx = (struct mi355x_ecb *)_ctx;
+    if (len % 16 != 0) {
+        fprintf(stderr, "ptls_mi355x: ECB transform of %zu bytes (not a multiple of the block size)\n", len);
+        abort();
+    }
+    if (ptls_mi355x_aes_ecb(ctx->aes, ctx->is_enc, output, input, len / 16) != 0)
+        engine_abort(ctx->is_enc ? "aes-ecb encrypt" : "aes-ecb decrypt");
+}
+
+static int aesecb_setup(ptls_cipher_context_t *_ctx, int is_enc, const void *key, size_t key_size)
+{
+    struct mi355x_ecb *ctx = (struct mi355x_ecb *)_ctx;
+    ctx->super.do_dispose = ecb_dispose;
+    ctx->super.do_init = NULL;
+    ctx->super.do_transform = ecb_transform;
+    ctx->is_enc = is_enc != 0;
+    if ((ctx->aes = ptls_mi355x_aes_new(key, key_size)) == NULL)
+        return PTLS_ERROR_LIBRARY;
+    return 0;
+}
+
+static int aes128ecb_setup(ptls_cipher_context_t *ctx, int is_enc, const void *key)
+{
+    return aesecb_setup(ctx, is_enc, key, 16);
+}
+
+static int aes256ecb_setup(ptls_cipher_context_t *ctx, int is_enc, const void *key)
+{
+    return aesecb_setup(ctx, is_enc, key, 32);
 }
 
 /* ------------------------------------------------------------------------ AES-GCM ------ */
@@ -272,12 +327,14 @@ static int aes256gcm_setup(ptls_aead_context_t *ctx, int is_enc, const void *key
 
 ptls_cipher_algorithm_t ptls_mi355x_aes128ctr = {"AES128-CTR", 16, 1, 16, sizeof(struct mi355x_ctr), aes128ctr_setup};
 ptls_cipher_algorithm_t ptls_mi355x_aes256ctr = {"AES256-CTR", 32, 1, 16, sizeof(struct mi355x_ctr), aes256ctr_setup};
+ptls_cipher_algorithm_t ptls_mi355x_aes128ecb = {"AES128-ECB", 16, 16, 0, sizeof(struct mi355x_ecb), aes128ecb_setup};
+ptls_cipher_algorithm_t ptls_mi355x_aes256ecb = {"AES256-ECB", 32, 16, 0, sizeof(struct mi355x_ecb), aes256ecb_setup};
 
 ptls_aead_algorithm_t ptls_mi355x_aes128gcm = {"AES128-GCM",
                                                PTLS_AESGCM_CONFIDENTIALITY_LIMIT,
                                                PTLS_AESGCM_INTEGRITY_LIMIT,
                                                &ptls_mi355x_aes128ctr,
-                                               NULL, /* ecb: not provided, as in fusion (lib/fusion.c:990) */
+                                               &ptls_mi355x_aes128ecb, /* fusion: NULL (lib/fusion.c:990) */
                                                16,
                                                MI355X_IV_SIZE,
                                                MI355X_TAG_SIZE,
@@ -288,7 +345,7 @@ ptls_aead_algorithm_t ptls_mi355x_aes256gcm = {"AES256-GCM",
                                                PTLS_AESGCM_CONFIDENTIALITY_LIMIT,
                                                PTLS_AESGCM_INTEGRITY_LIMIT,
                                                &ptls_mi355x_aes256ctr,
-                                               NULL,
+                                               &ptls_mi355x_aes256ecb,
                                                32,
                                                MI355X_IV_SIZE,
                                                MI355X_TAG_SIZE,

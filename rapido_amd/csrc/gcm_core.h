@@ -107,10 +107,24 @@ struct Layout {
 
 GCM_HDC uint8_t gf8_xtime(uint8_t a) { return (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0)); }
 
+GCM_HDC uint8_t gf8_mul(uint8_t a, uint8_t b)
+{
+    uint8_t r = 0;
+    for (int i = 0; i < 8; ++i) {
+        if (b & 1)
+            r = (uint8_t)(r ^ a);
+        a = gf8_xtime(a);
+        b = (uint8_t)(b >> 1);
+    }
+    return r;
+}
+
 struct AesTables {
     uint8_t sbox[256];
     uint32_t t0[256];
-    constexpr AesTables() : sbox{}, t0{}
+    uint8_t inv_sbox[256]; /* FIPS-197 5.3.2 */
+    uint32_t td0[256];     /* InvMixColumns column 0 times InvS[x]: (e, 9, d, b) * InvS[x], packed LE */
+    constexpr AesTables() : sbox{}, t0{}, inv_sbox{}, td0{}
     {
         /* S-box from log/antilog tables of generator 3 (FIPS-197 sec. 5.1.1) */
         uint8_t exp_[256] = {}, log_[256] = {};
@@ -130,6 +144,13 @@ struct AesTables {
         for (int v = 0; v < 256; ++v) {
             uint8_t s = sbox[v], s2 = gf8_xtime(s), s3 = (uint8_t)(s2 ^ s);
             t0[v] = (uint32_t)s2 | ((uint32_t)s << 8) | ((uint32_t)s << 16) | ((uint32_t)s3 << 24);
+        }
+        for (int v = 0; v < 256; ++v)
+            inv_sbox[sbox[v]] = (uint8_t)v;
+        for (int v = 0; v < 256; ++v) {
+            uint8_t s = inv_sbox[v];
+            td0[v] = (uint32_t)gf8_mul(s, 0x0e) | ((uint32_t)gf8_mul(s, 0x09) << 8) | ((uint32_t)gf8_mul(s, 0x0d) << 16) |
+                     ((uint32_t)gf8_mul(s, 0x0b) << 24);
         }
     }
 };
@@ -1020,6 +1041,194 @@ GCM_HD void aes_encrypt_bytes(const uint8_t *sbox, const uint32_t *rk, uint32_t 
     }
     for (int i = 0; i < 16; ++i)
         out[i] = s[i];
+}
+
+/* ------------------------------------------------------------------ AES-ECB cipher (cold) -- */
+
+/* InvMixColumns of one column (FIPS-197 5.3.3), LE dword: byte r = row r */
+GCM_HD uint32_t aes_inv_mix_column(uint32_t c)
+{
+    const uint8_t a0 = (uint8_t)c, a1 = (uint8_t)(c >> 8), a2 = (uint8_t)(c >> 16), a3 = (uint8_t)(c >> 24);
+    const uint8_t b0 = (uint8_t)(gf8_mul(a0, 14) ^ gf8_mul(a1, 11) ^ gf8_mul(a2, 13) ^ gf8_mul(a3, 9));
+    const uint8_t b1 = (uint8_t)(gf8_mul(a0, 9) ^ gf8_mul(a1, 14) ^ gf8_mul(a2, 11) ^ gf8_mul(a3, 13));
+    const uint8_t b2 = (uint8_t)(gf8_mul(a0, 13) ^ gf8_mul(a1, 9) ^ gf8_mul(a2, 14) ^ gf8_mul(a3, 11));
+    const uint8_t b3 = (uint8_t)(gf8_mul(a0, 11) ^ gf8_mul(a1, 13) ^ gf8_mul(a2, 9) ^ gf8_mul(a3, 14));
+    return (uint32_t)b0 | ((uint32_t)b1 << 8) | ((uint32_t)b2 << 16) | ((uint32_t)b3 << 24);
+}
+
+/*
+ * Round keys of the equivalent inverse cipher (FIPS-197 5.3.5): dk_0 = rk_nr, dk_r = InvMixColumns(rk_(nr-r))
+ * for 0 < r < nr, dk_nr = rk_0, so decryption runs the same table-round shape as encryption.
+ */
+GCM_HD void aes_decrypt_key_schedule(const uint32_t *rk, uint32_t nr, uint32_t *dk)
+{
+    for (uint32_t c = 0; c < 4; ++c) {
+        dk[c] = rk[4 * nr + c];
+        dk[4 * nr + c] = rk[c];
+    }
+    for (uint32_t r = 1; r < nr; ++r)
+        for (uint32_t c = 0; c < 4; ++c)
+            dk[4 * r + c] = aes_inv_mix_column(rk[4 * (nr - r) + c]);
+}
+
+/*
+ * One AES block, encryption (T = T0, S = S-box, k = the FIPS-197 schedule) or decryption (T = Td0,
+ * S = InvS-box, k = aes_decrypt_key_schedule), from a single 1 KiB table and its byte rotations
+ * (T_i = rotl(T, 8 i)).  Encryption: column c of a round takes row r from column c + r (ShiftRows);
+ * decryption from column c - r (InvShiftRows).  T and S may live in LDS (the ECB kernels) or host
+ * memory (the kernel model).
+ */
+template <bool DEC>
+GCM_HD void aes_ecb_block(const uint32_t *T, const uint8_t *S, const uint32_t *k, uint32_t nr, uint32_t w[4])
+{
+    uint32_t s[4] = {w[0] ^ k[0], w[1] ^ k[1], w[2] ^ k[2], w[3] ^ k[3]};
+    for (uint32_t r = 1; r < nr; ++r) {
+        uint32_t n[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int c1 = DEC ? (c + 3) & 3 : (c + 1) & 3, c2 = (c + 2) & 3, c3 = DEC ? (c + 1) & 3 : (c + 3) & 3;
+            n[c] = T[s[c] & 0xffu] ^ rotl32(T[(s[c1] >> 8) & 0xffu], 8) ^ rotl32(T[(s[c2] >> 16) & 0xffu], 16) ^
+                   rotl32(T[s[c3] >> 24], 24) ^ k[4 * r + (uint32_t)c];
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            s[c] = n[c];
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int c1 = DEC ? (c + 3) & 3 : (c + 1) & 3, c2 = (c + 2) & 3, c3 = DEC ? (c + 1) & 3 : (c + 3) & 3;
+        w[c] = ((uint32_t)S[s[c] & 0xffu] | ((uint32_t)S[(s[c1] >> 8) & 0xffu] << 8) |
+                ((uint32_t)S[(s[c2] >> 16) & 0xffu] << 16) | ((uint32_t)S[s[c3] >> 24] << 24)) ^
+               k[4 * nr + (uint32_t)c];
+    }
+}
+
+/* Round keys only: the context of the ECB/CTR ciphers (no GHASH tables) */
+struct AesKeys {
+    uint32_t rk[60]; /* encryption schedule */
+    uint32_t dk[60]; /* equivalent-inverse-cipher schedule */
+    uint32_t rounds;
+    uint32_t key_size;
+    uint32_t pad_[2];
+};
+
+GCM_HD int build_aes_keys(const uint8_t *sbox, const uint8_t *key, uint32_t keylen, AesKeys *k)
+{
+    if (keylen != 16 && keylen != 32)
+        return -1;
+    for (int i = 0; i < 60; ++i)
+        k->rk[i] = k->dk[i] = 0;
+    k->rounds = aes_expand_key(sbox, key, keylen, k->rk);
+    aes_decrypt_key_schedule(k->rk, k->rounds, k->dk);
+    k->key_size = keylen;
+    k->pad_[0] = k->pad_[1] = 0;
+    return 0;
+}
+
+/* ------------------------------------------------------------------ parallel key image -- */
+
+/*
+ * GF(2^128) elements as a big-endian 128-bit integer {hi, lo}: GCM bit k (x^k, bit 7 - k % 8 of
+ * stream byte k / 8) is bit 127 - k.  Multiplying by x is a right shift, and x^128 = 1 + x + x^2 + x^7.
+ */
+struct Gf128 {
+    uint64_t hi, lo;
+};
+
+GCM_HD Gf128 gf_from_bytes(const uint8_t b[16])
+{
+    Gf128 r = {0u, 0u};
+    for (int i = 0; i < 8; ++i) {
+        r.hi = (r.hi << 8) | b[i];
+        r.lo = (r.lo << 8) | b[8 + i];
+    }
+    return r;
+}
+
+GCM_HD void gf_to_bytes(Gf128 v, uint8_t b[16])
+{
+    for (int i = 0; i < 8; ++i) {
+        b[i] = (uint8_t)(v.hi >> (56 - 8 * i));
+        b[8 + i] = (uint8_t)(v.lo >> (56 - 8 * i));
+    }
+}
+
+GCM_HD Gf128 gf_shr(Gf128 v, uint32_t n) /* n < 128 */
+{
+    if (n == 0)
+        return v;
+    if (n >= 64)
+        return Gf128{0u, v.hi >> (n - 64)};
+    return Gf128{v.hi >> n, (v.lo >> n) | (v.hi << (64 - n))};
+}
+
+GCM_HD Gf128 gf_shl(Gf128 v, uint32_t n) /* n < 128 */
+{
+    if (n == 0)
+        return v;
+    if (n >= 64)
+        return Gf128{v.lo << (n - 64), 0u};
+    return Gf128{(v.hi << n) | (v.lo >> (64 - n)), v.lo << n};
+}
+
+GCM_HD Gf128 gf_xor(Gf128 a, Gf128 b) { return Gf128{a.hi ^ b.hi, a.lo ^ b.lo}; }
+
+/*
+ * v * x^i for i <= 64, branch-light: the i bits shifted out below x^127 come back as
+ * T * (1 + x + x^2 + x^7), T = those bits placed at x^0 .. x^(i-1) (bit positions >= 64 of {hi, lo}),
+ * so one reduction pass suffices (T x^7 stays below x^71).
+ */
+GCM_HD Gf128 gf_mul_xpow64(Gf128 v, uint32_t i)
+{
+    if (i == 0)
+        return v;
+    const Gf128 t = gf_shl(v, 128u - i);
+    return gf_xor(gf_xor(gf_shr(v, i), t), gf_xor(gf_xor(gf_shr(t, 1), gf_shr(t, 2)), gf_shr(t, 7)));
+}
+
+/* v * x^i, 0 <= i < 128 */
+GCM_HD Gf128 gf_mul_xpow(Gf128 v, uint32_t i) { return i > 64u ? gf_mul_xpow64(gf_mul_xpow64(v, 64u), i - 64u) : gf_mul_xpow64(v, i); }
+
+/* the element's GCM bit k (coefficient of x^k) */
+GCM_HD uint32_t gf_bit(Gf128 v, uint32_t k) { return (uint32_t)((k < 64 ? v.hi >> (63 - k) : v.lo >> (127 - k)) & 1u); }
+
+/*
+ * Lane `lane` (0..63)'s share of X * Y in the wave-parallel multiply of the key setup: Y x^lane and
+ * Y x^(lane + 64), masked by X's bits lane and lane + 64.  X * Y is the XOR of the 64 shares.
+ */
+GCM_HD Gf128 gf_mul_lane_share(Gf128 X, Gf128 Y, uint32_t lane)
+{
+    const Gf128 a = gf_mul_xpow64(Y, lane), b = gf_mul_xpow64(gf_mul_xpow64(Y, 64u), lane);
+    Gf128 acc = {0u, 0u};
+    if (gf_bit(X, lane))
+        acc = a;
+    if (gf_bit(X, lane + 64u))
+        acc = gf_xor(acc, b);
+    return acc;
+}
+
+/* The 13 multipliers of the key image, in KeyImage table order: H^1..H^8, H^64, H^256, H^32, H^128. */
+enum : uint32_t { KEY_IMAGE_TABLES = MAX_K + 4 };
+
+GCM_HD uint8_t (*key_image_table(KeyImage *ki, uint32_t s))[16][16]
+{
+    return s < (uint32_t)MAX_K ? ki->gh[s] : s == (uint32_t)MAX_K ? ki->gh64 : s == MAX_K + 1u ? ki->gh256 : s == MAX_K + 2u ? ki->gh32 : ki->gh128;
+}
+
+/*
+ * Entry i of the 13 x 32 x 16 nibble-table entries: table s = i / 512, nibble t, value v; the XOR of the
+ * single-bit products bits[s][k] = P_s x^k of v's set bits (bit b of nibble t is GCM bit nibble_bit_index(t, b)),
+ * stored as its 16 stream bytes in LE dwords.
+ */
+GCM_HD void key_image_store_entry(KeyImage *ki, const Gf128 (*bits)[128], uint32_t i)
+{
+    const uint32_t s = i >> 9, t = (i >> 4) & 31u, v = i & 15u;
+    Gf128 e = {0u, 0u};
+    for (int b = 0; b < 4; ++b)
+        if ((v >> b) & 1u)
+            e = gf_xor(e, bits[s][nibble_bit_index((int)t, b)]);
+    *(u32x4 *)key_image_table(ki, s)[t][v] = u32x4{bswap32((uint32_t)(e.hi >> 32)), bswap32((uint32_t)e.hi),
+                                                    bswap32((uint32_t)(e.lo >> 32)), bswap32((uint32_t)e.lo)};
 }
 
 /* the 32 nibble tables of multiplication by c: tab[t][v] = (nibble t of the element = v) * c */

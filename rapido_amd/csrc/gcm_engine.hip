@@ -22,6 +22,9 @@
 #include <stdlib.h>
 #include <string.h>
 #include <hipcub/hipcub.hpp>
+#include <rocprim/iterator/constant_iterator.hpp>
+#include <mutex>
+#include <new>
 #include "gcm_core.h"
 #include "../../include/ptls_mi355x.h"
 
@@ -151,6 +154,7 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
                     rec.dst = t.dst + 5u;
                     rec.len = t.len;
                     ctype = t.type;
+                    valid = t.len <= PTLS_MI355X_TLS_MAX_FRAGMENT; /* larger: not a TLS record, nothing written */
                 } else { /* header at t.src; length field = ciphertext + tag */
                     rec.src = t.src + 5u;
                     rec.dst = t.dst;
@@ -323,6 +327,7 @@ __device__ __forceinline__ void window_body(const KeyImage *__restrict__ ki, uin
                     rec.dst = t.dst + 5u;
                     rec.len = t.len;
                     ctype = t.type;
+                    valid = t.len <= PTLS_MI355X_TLS_MAX_FRAGMENT; /* larger: not a TLS record, nothing written */
                 } else {
                     rec.src = t.src + 5u;
                     rec.dst = t.dst;
@@ -405,7 +410,7 @@ __device__ __forceinline__ void window_body(const KeyImage *__restrict__ ki, uin
             }
             WIN_STAMP(4);
             if (SEAL) {
-                if (j == 0u) {
+                if (j == 0u && valid) {
                     *(u32x4_u *)(dst + rec.dst + plen) = acc;
                     if (FRAME) { /* 17 03 03 BE16(plen + 16) (lib/picotls.c:658-662) */
                         const uint32_t reclen = plen + 16u;
@@ -543,19 +548,196 @@ MI355X_WIN_KERNEL(mi355x_gcm_winw_seal_aes256, 14, true, false, 1024, 4)
 MI355X_WIN_KERNEL(mi355x_gcm_winw_open_aes128, 10, false, false, 1024, 4)
 MI355X_WIN_KERNEL(mi355x_gcm_winw_open_aes256, 14, false, false, 1024, 4)
 
-/* key image: round keys, H and the nibble tables of H^1..H^8 and H^64 (cold path, one thread) */
-extern "C" __global__ void mi355x_gcm_setup(const uint8_t *key, uint32_t keylen, KeyImage *ki, int *rc)
+/* ================================================================== cold kernels ========= */
+
+/*
+ * Key image setup (ptls_fusion_aesgcm_new, lib/fusion.c:775-795): one 1024-thread workgroup.
+ *   1. thread 0: key expansion and H = E_K(0^128);
+ *   2. wave 0: the 12 powers H^2..H^8, H^32, H^64, H^128, H^256 by wave-parallel multiplies
+ *      (lane l forms Y x^l and Y x^(l+64), masks them by bits l, l+64 of X, the wave XOR-reduces);
+ *   3. all threads: the 13 x 128 single-bit products P x^k (gf_mul_xpow), into LDS;
+ *   4. all threads: the 13 x 32 x 16 nibble-table entries, each the XOR of <= 4 single-bit products.
+ * Bit-identical to build_key_image (tests/test_kernel_model.py checks the same steps on the host).
+ */
+__device__ __forceinline__ Gf128 gf_wave_reduce(Gf128 v)
 {
-    if (threadIdx.x == 0 && blockIdx.x == 0)
-        *rc = build_key_image(c_tabs.sbox, key, keylen, ki);
+    uint32_t w[4] = {(uint32_t)(v.hi >> 32), (uint32_t)v.hi, (uint32_t)(v.lo >> 32), (uint32_t)v.lo};
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+            w[d] ^= shfl_xor_u32(w[d], o);
+    return Gf128{((uint64_t)w[0] << 32) | w[1], ((uint64_t)w[2] << 32) | w[3]};
 }
 
-/* AES-ECB, one thread per block (cold path: header protection, ctr cipher) */
-extern "C" __global__ void mi355x_aes_ecb(const KeyImage *__restrict__ ki, const uint8_t *in, uint8_t *out, uint32_t nblocks)
+/* X * Y, every lane of the wave taking part (all lanes return the product) */
+__device__ __forceinline__ Gf128 gf_mul_wave(Gf128 X, Gf128 Y, uint32_t lane) { return gf_wave_reduce(gf_mul_lane_share(X, Y, lane)); }
+
+extern "C" __global__ __launch_bounds__(1024) void mi355x_gcm_setup(const uint8_t *key, uint32_t keylen, KeyImage *ki,
+                                                                    int *rc)
+{
+    __shared__ Gf128 s_pow[KEY_IMAGE_TABLES];
+    __shared__ Gf128 s_bit[KEY_IMAGE_TABLES][128];
+    __shared__ uint32_t s_ok;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    if (tid == 0) {
+        s_ok = 0u;
+        if (keylen == 16u || keylen == 32u) {
+            uint8_t k[32], h[16];
+            for (uint32_t i = 0; i < keylen; ++i)
+                k[i] = key[i];
+            uint32_t rk[60];
+            for (int i = 0; i < 60; ++i)
+                rk[i] = 0u;
+            const uint32_t nr = aes_expand_key(c_tabs.sbox, k, keylen, rk);
+            const uint8_t zero[16] = {0};
+            aes_encrypt_bytes(c_tabs.sbox, rk, nr, zero, h);
+            for (int i = 0; i < 60; ++i)
+                ki->rk[i] = rk[i];
+            ki->rounds = nr;
+            ki->key_size = keylen;
+            ki->pad_[0] = ki->pad_[1] = 0u;
+            for (int i = 0; i < 16; ++i)
+                ki->H[i] = h[i];
+            for (int i = 0; i < 32; ++i)
+                k[i] = 0u;
+            s_pow[0] = gf_from_bytes(h);
+            s_ok = 1u;
+        }
+        *rc = s_ok ? 0 : -1;
+    }
+    __syncthreads();
+    if (!s_ok)
+        return;
+    if (tid < 64u) {
+        const Gf128 h = s_pow[0];
+        Gf128 p = h;
+        for (uint32_t e = 2; e <= (uint32_t)MAX_K; ++e) { /* H^2 .. H^8 */
+            p = gf_mul_wave(p, h, lane);
+            if (lane == 0)
+                s_pow[e - 1] = p;
+        }
+        p = gf_mul_wave(p, p, lane); /* H^16 */
+        p = gf_mul_wave(p, p, lane); /* H^32 */
+        if (lane == 0)
+            s_pow[MAX_K + 2] = p;
+        p = gf_mul_wave(p, p, lane); /* H^64 */
+        if (lane == 0)
+            s_pow[MAX_K] = p;
+        p = gf_mul_wave(p, p, lane); /* H^128 */
+        if (lane == 0)
+            s_pow[MAX_K + 3] = p;
+        p = gf_mul_wave(p, p, lane); /* H^256 */
+        if (lane == 0)
+            s_pow[MAX_K + 1] = p;
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < KEY_IMAGE_TABLES * 128u; i += blockDim.x)
+        s_bit[i >> 7][i & 127u] = gf_mul_xpow(s_pow[i >> 7], i & 127u);
+    __syncthreads();
+    for (uint32_t i = tid; i < KEY_IMAGE_TABLES * 32u * 16u; i += blockDim.x)
+        key_image_store_entry(ki, s_bit, i);
+}
+
+/* round keys of the ECB/CTR ciphers (one thread: a key schedule is 60 words) */
+extern "C" __global__ void mi355x_aes_setup(const uint8_t *key, uint32_t keylen, AesKeys *out, int *rc)
+{
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        uint8_t k[32];
+        for (uint32_t i = 0; i < keylen && i < 32u; ++i)
+            k[i] = key[i];
+        AesKeys ks;
+        *rc = build_aes_keys(c_tabs.sbox, k, keylen, &ks);
+        *out = ks;
+        for (int i = 0; i < 32; ++i)
+            k[i] = 0u;
+    }
+}
+
+/*
+ * AES-ECB over nblocks 16-byte blocks, grid-stride, one block per thread: encryption (FIPS-197 Cipher,
+ * lib/fusion.c:187-197 aesecb_encrypt) or decryption (InvCipher, the equivalent inverse cipher of
+ * FIPS-197 5.3.5).  The 1 KiB table and the (inverse) S-box sit in LDS.  Cold path: header protection
+ * masks, the ECB/CTR cipher objects.
+ */
+template <bool DEC>
+__device__ __forceinline__ void aes_ecb_body(const uint32_t *__restrict__ k, uint32_t nr, const uint8_t *in, uint8_t *out,
+                                             uint32_t nblocks)
+{
+    __shared__ uint32_t s_t[256];
+    __shared__ uint8_t s_s[256];
+    for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) {
+        s_t[i] = DEC ? c_tabs.td0[i] : c_tabs.t0[i];
+        s_s[i] = DEC ? c_tabs.inv_sbox[i] : c_tabs.sbox[i];
+    }
+    uint32_t rk[60];
+    for (uint32_t i = 0; i < 4u * (nr + 1u); ++i)
+        rk[i] = k[i];
+    __syncthreads();
+    for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < nblocks; b += gridDim.x * blockDim.x) {
+        const u32x4 v = *(const u32x4_u *)(in + 16u * b);
+        uint32_t w[4] = {v[0], v[1], v[2], v[3]};
+        aes_ecb_block<DEC>(s_t, s_s, rk, nr, w);
+        *(u32x4_u *)(out + 16u * b) = u32x4{w[0], w[1], w[2], w[3]};
+    }
+}
+
+extern "C" __global__ __launch_bounds__(256) void mi355x_aes_ecb_enc(const uint32_t *k, uint32_t nr, const uint8_t *in,
+                                                                     uint8_t *out, uint32_t nblocks)
+{
+    aes_ecb_body<false>(k, nr, in, out, nblocks);
+}
+
+extern "C" __global__ __launch_bounds__(256) void mi355x_aes_ecb_dec(const uint32_t *k, uint32_t nr, const uint8_t *in,
+                                                                     uint8_t *out, uint32_t nblocks)
+{
+    aes_ecb_body<true>(k, nr, in, out, nblocks);
+}
+
+/*
+ * Stop at the first failure (PTLS_MI355X_OPEN_STOP_AT_FAILURE): picotls stops reading at a record that
+ * fails (aead_decrypt's SIZE_MAX -> PTLS_ALERT_BAD_RECORD_MAC, lib/picotls.c:650-652, or an all-zero
+ * inner plaintext -> PTLS_ALERT_UNEXPECTED_MESSAGE, :4790) and never advances seq past it.  Record i is
+ * "behind a failure" when a record j < i of the same connection (equal conn_ids over a contiguous run)
+ * failed: fail_pos[i] = i for a failed record, else ~0; an inclusive min-scan by connection gives the
+ * first failure at or before i; records strictly behind it are reset to NOT_PROCESSED and zeroed.
+ */
+extern "C" __global__ void mi355x_tls_fail_pos(const uint32_t *__restrict__ status, uint32_t n, uint32_t *fail_pos)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n)
+        fail_pos[i] = status[i] >= PTLS_MI355X_TLS_UNEXPECTED_MESSAGE ? i : 0xffffffffu;
+}
+
+extern "C" __global__ void mi355x_tls_truncate(const TlsRecord *__restrict__ recs, uint32_t n, const uint32_t *first_fail,
+                                               uint8_t *dst, uint32_t *status, uint8_t *types)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || first_fail[i] >= i)
+        return;
+    status[i] = PTLS_MI355X_TLS_NOT_PROCESSED;
+    types[i] = 0u;
+    const TlsRecord t = recs[i];
+    const uint32_t plen = t.len >= 16u ? t.len - 16u : 0u;
+    uint8_t *p = dst + t.dst;
+    for (uint32_t off = 0; off < plen; off += 16u) {
+        if (plen - off >= 16u)
+            *(u32x4_u *)(p + off) = u32x4{0u, 0u, 0u, 0u};
+        else
+            store_partial(p + off, plen - off, u32x4{0u, 0u, 0u, 0u});
+    }
+}
+
+/* keys = GHASH steps of each record (its work), values = record index */
+extern "C" __global__ void mi355x_sort_keys(const Record *__restrict__ recs, uint32_t n, uint32_t *keys, uint32_t *vals)
 {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < nblocks)
-        aes_encrypt_bytes(c_tabs.sbox, ki->rk, ki->rounds, in + 16u * i, out + 16u * i);
+    if (i < n) {
+        Record r = recs[i];
+        uint64_t blocks = ((uint64_t)r.len + 15) / 16 + ((uint64_t)r.aadlen + 15) / 16 + 1;
+        keys[i] = blocks > 0xffffffu ? 0xffffffu : (uint32_t)blocks;
+        vals[i] = i;
+    }
 }
 
 /* ================================================================== host side ============ */
@@ -563,24 +745,47 @@ extern "C" __global__ void mi355x_aes_ecb(const KeyImage *__restrict__ ki, const
 typedef void (*batch_kernel_t)(const KeyImage *, uint32_t, uint32_t, uint32_t, const void *, const uint32_t *, uint32_t,
                                const uint8_t *, uint8_t *, const uint8_t *, uint32_t *, uint8_t *, uint32_t *,
                                uint32_t, const uint32_t *);
+typedef void (*win_kernel_t)(const KeyImage *, uint32_t, uint32_t, uint32_t, const void *, uint32_t, const uint8_t *,
+                             uint8_t *, const uint8_t *, uint32_t *, uint8_t *, const uint32_t *);
 
 constexpr uint32_t WORK_SLOTS = 256; /* per-context ring of work counters: one per launch in flight */
+
+/*
+ * Per-device resources shared by every context on the device (created on first use, kept for the
+ * process): the stream and the pinned, mapped staging buffer of the synchronous calls (slot calls, ECB
+ * cipher, key setup).  The mutex serialises those calls per device; the buffer never holds key material
+ * or records after a call returns.
+ */
+struct DeviceShared {
+    std::mutex mu;
+    hipStream_t stream = nullptr;
+    uint8_t *d_stage = nullptr;     /* device staging (records above the zero-copy limit) */
+    uint8_t *h_stage = nullptr;     /* pinned host staging (mapped, coherent) */
+    uint8_t *h_stage_dev = nullptr; /* h_stage as the GPU addresses it */
+    size_t cap = 0;
+};
 
 struct st_ptls_mi355x_aesgcm_context {
     int device;
     int num_cu;
     uint32_t key_size;
     KeyImage *d_ki;
-    hipStream_t stream;  /* private stream for the synchronous single-record calls */
-    uint8_t *d_stage;    /* device staging for single-record calls */
-    uint8_t *h_stage;    /* pinned host staging (mapped, coherent) */
-    uint8_t *h_stage_dev; /* h_stage as the GPU addresses it: zero-copy slot calls read and write it directly */
-    size_t stage_cap;
-    uint32_t *d_work;    /* WORK_SLOTS dynamic-scheduling ticket counters, zeroed once at setup */
+    DeviceShared *shared;
+    uint32_t *d_work;               /* WORK_SLOTS dynamic-scheduling ticket counters, set once at setup */
     uint32_t work_base[WORK_SLOTS]; /* each counter's value at the start of its next launch */
+    hipStream_t work_stream[WORK_SLOTS]; /* stream of the slot's last launch */
     uint32_t work_next;
-    void *d_sort;        /* ptls_mi355x_order_by_length workspace */
-    size_t sort_cap;
+    hipEvent_t reuse_event;         /* orders a slot's reuse on another stream after its last launch */
+    void *d_scratch;                /* order_by_length / stop-at-failure workspace */
+    size_t scratch_cap;
+};
+
+struct st_ptls_mi355x_aes_context {
+    int device;
+    int num_cu;
+    uint32_t key_size, rounds;
+    AesKeys *d_keys;
+    DeviceShared *shared;
 };
 
 static thread_local char g_err[256];
@@ -628,47 +833,144 @@ struct DeviceGuard {
     }
 };
 
-static batch_kernel_t pick_kernel(bool seal, uint32_t rounds, int k, const char **name)
+static std::mutex g_shared_mu;
+static DeviceShared *g_shared[64];
+
+/* the device's shared resources (the device must be current) */
+static DeviceShared *device_shared(int dev)
 {
-#define PICK(NAME)                                                                                                     \
-    do {                                                                                                               \
-        if (name)                                                                                                      \
-            *name = #NAME;                                                                                             \
-        return NAME;                                                                                                   \
-    } while (0)
-    if (seal && rounds == 10) {
-        if (k == 1) PICK(mi355x_gcm_seal_aes128_k1);
-        if (k == 2) PICK(mi355x_gcm_seal_aes128_k2);
-        if (k == 4) PICK(mi355x_gcm_seal_aes128_k4);
-        if (k == 8) PICK(mi355x_gcm_seal_aes128_k8);
-    } else if (seal && rounds == 14) {
-        if (k == 1) PICK(mi355x_gcm_seal_aes256_k1);
-        if (k == 2) PICK(mi355x_gcm_seal_aes256_k2);
-        if (k == 4) PICK(mi355x_gcm_seal_aes256_k4);
-        if (k == 8) PICK(mi355x_gcm_seal_aes256_k8);
-    } else if (!seal && rounds == 10) {
-        if (k == 1) PICK(mi355x_gcm_open_aes128_k1);
-        if (k == 2) PICK(mi355x_gcm_open_aes128_k2);
-        if (k == 4) PICK(mi355x_gcm_open_aes128_k4);
-        if (k == 8) PICK(mi355x_gcm_open_aes128_k8);
-    } else if (!seal && rounds == 14) {
-        if (k == 1) PICK(mi355x_gcm_open_aes256_k1);
-        if (k == 2) PICK(mi355x_gcm_open_aes256_k2);
-        if (k == 4) PICK(mi355x_gcm_open_aes256_k4);
-        if (k == 8) PICK(mi355x_gcm_open_aes256_k8);
+    if (dev < 0 || dev >= 64) {
+        snprintf(g_err, sizeof(g_err), "device ordinal %d out of range", dev);
+        return nullptr;
     }
-#undef PICK
-    if (name)
-        *name = "";
-    return nullptr;
+    std::lock_guard<std::mutex> lk(g_shared_mu);
+    if (g_shared[dev] == nullptr) {
+        DeviceShared *d = new (std::nothrow) DeviceShared();
+        if (d == nullptr)
+            return nullptr;
+        hipError_t e = hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            fail("hipStreamCreateWithFlags", e);
+            delete d;
+            return nullptr;
+        }
+        g_shared[dev] = d;
+    }
+    return g_shared[dev];
 }
 
-static batch_kernel_t pick_tls_kernel(bool seal, uint32_t rounds)
+/* grows the shared staging to `need` bytes (caller holds d->mu) */
+static int ensure_stage(DeviceShared *d, size_t need)
 {
-    if (rounds == 10)
-        return seal ? mi355x_tls_seal_aes128_k4 : mi355x_tls_open_aes128_k4;
-    return seal ? mi355x_tls_seal_aes256_k4 : mi355x_tls_open_aes256_k4;
+    if (need <= d->cap)
+        return 0;
+    size_t cap = d->cap ? d->cap : 4096;
+    while (cap < need)
+        cap *= 2;
+    if (d->d_stage)
+        (void)hipFree(d->d_stage);
+    if (d->h_stage)
+        (void)hipHostFree(d->h_stage);
+    d->d_stage = nullptr;
+    d->h_stage = nullptr;
+    d->h_stage_dev = nullptr;
+    d->cap = 0;
+    HIPCHK(hipMalloc(&d->d_stage, cap));
+    /* coherent: the GPU's zero-copy reads never see stale cache lines of a previous call */
+    HIPCHK(hipHostMalloc(&d->h_stage, cap, hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostGetDevicePointer((void **)&d->h_stage_dev, d->h_stage, 0));
+    d->cap = cap;
+    return 0;
 }
+
+/* ------------------------------------------------------------------ kernel selection ----- */
+
+struct LaunchPlan {
+    const char *name = "";
+    batch_kernel_t batch = nullptr;
+    win_kernel_t win = nullptr;
+    uint32_t blocks = 0, threads = 0;
+};
+
+#define KN(f) {#f, f}
+struct BatchEntry {
+    const char *name;
+    batch_kernel_t f;
+};
+struct WinEntry {
+    const char *name;
+    win_kernel_t f;
+};
+
+/*
+ * The kernel a batch of n records runs on (launch_batch, ptls_mi355x_kernel_name):
+ *  - framing (section 4) batches of at most g_window_records and AEAD batches of at most g_aead_window_records
+ *    go to the window kernels: up to one record per CU the 32-position single-record kernels (win32), up to
+ *    15 records per CU the 3-record latency groups (win), above that the persistent 15-record groups (winw);
+ *  - larger batches go to the batch kernels (K lanes per record; framing always K = 4).
+ */
+static LaunchPlan plan_launch(bool seal, bool frame, uint32_t key_size, size_t n, int num_cu)
+{
+    LaunchPlan p;
+    const int a256 = key_size == 32 ? 1 : 0, s = seal ? 1 : 0, f = frame ? 1 : 0;
+    if (n <= (frame ? g_window_records : g_aead_window_records)) {
+        static const WinEntry table[2][2][2][2] = {
+            /* [frame][wide][seal][aes256] */
+            {{{KN(mi355x_gcm_win_open_aes128), KN(mi355x_gcm_win_open_aes256)},
+              {KN(mi355x_gcm_win_seal_aes128), KN(mi355x_gcm_win_seal_aes256)}},
+             {{KN(mi355x_gcm_winw_open_aes128), KN(mi355x_gcm_winw_open_aes256)},
+              {KN(mi355x_gcm_winw_seal_aes128), KN(mi355x_gcm_winw_seal_aes256)}}},
+            {{{KN(mi355x_tls_win_open_aes128), KN(mi355x_tls_win_open_aes256)},
+              {KN(mi355x_tls_win_seal_aes128), KN(mi355x_tls_win_seal_aes256)}},
+             {{KN(mi355x_tls_winw_open_aes128), KN(mi355x_tls_winw_open_aes256)},
+              {KN(mi355x_tls_winw_seal_aes128), KN(mi355x_tls_winw_seal_aes256)}}}};
+        static const WinEntry table32[2][2][2] = {
+            /* [frame][seal][aes256]: 32-position segments, one record per group */
+            {{KN(mi355x_gcm_win32_open_aes128), KN(mi355x_gcm_win32_open_aes256)},
+             {KN(mi355x_gcm_win32_seal_aes128), KN(mi355x_gcm_win32_seal_aes256)}},
+            {{KN(mi355x_tls_win32_open_aes128), KN(mi355x_tls_win32_open_aes256)},
+             {KN(mi355x_tls_win32_seal_aes128), KN(mi355x_tls_win32_seal_aes256)}}};
+        const bool wide = n > 15u * (uint64_t)num_cu; /* the wide groups (15 records) fill every CU */
+        constexpr uint32_t per32 = (MI355X_WIN32_THREADS / 8u) / WIN_SEG32_MAXSEG; /* records per 32-position group */
+        const bool seg32 = !wide && n <= (g_seg32_records == SIZE_MAX ? (size_t)per32 * num_cu : g_seg32_records);
+        const WinEntry &e = seg32 ? table32[f][s][a256] : table[f][wide][s][a256];
+        p.name = e.name;
+        p.win = e.f;
+        p.threads = seg32 ? (uint32_t)MI355X_WIN32_THREADS : wide ? 1024u : 512u;
+        const uint32_t per = seg32 ? per32 : (p.threads / (wide ? 4u : 8u)) / WIN_MAXSEG;
+        uint64_t blocks = (n + per - 1) / per;
+        if (wide && blocks > (uint64_t)num_cu)
+            blocks = (uint64_t)num_cu;
+        p.blocks = (uint32_t)blocks;
+        return p;
+    }
+    static const BatchEntry gcm[2][2][4] = {
+        /* [seal][aes256][log2 K] */
+        {{KN(mi355x_gcm_open_aes128_k1), KN(mi355x_gcm_open_aes128_k2), KN(mi355x_gcm_open_aes128_k4),
+          KN(mi355x_gcm_open_aes128_k8)},
+         {KN(mi355x_gcm_open_aes256_k1), KN(mi355x_gcm_open_aes256_k2), KN(mi355x_gcm_open_aes256_k4),
+          KN(mi355x_gcm_open_aes256_k8)}},
+        {{KN(mi355x_gcm_seal_aes128_k1), KN(mi355x_gcm_seal_aes128_k2), KN(mi355x_gcm_seal_aes128_k4),
+          KN(mi355x_gcm_seal_aes128_k8)},
+         {KN(mi355x_gcm_seal_aes256_k1), KN(mi355x_gcm_seal_aes256_k2), KN(mi355x_gcm_seal_aes256_k4),
+          KN(mi355x_gcm_seal_aes256_k8)}}};
+    static const BatchEntry tls[2][2] = {/* [seal][aes256] */
+                                         {KN(mi355x_tls_open_aes128_k4), KN(mi355x_tls_open_aes256_k4)},
+                                         {KN(mi355x_tls_seal_aes128_k4), KN(mi355x_tls_seal_aes256_k4)}};
+    const int k = frame ? 4 : g_lanes;
+    const int lk = k == 1 ? 0 : k == 2 ? 1 : k == 4 ? 2 : 3;
+    const BatchEntry &e = frame ? tls[s][a256] : gcm[s][a256][lk];
+    p.name = e.name;
+    p.batch = e.f;
+    p.threads = WG_THREADS;
+    const uint64_t ngroups = (n + (64 / k) - 1) / (64 / k), waves = WG_THREADS / 64;
+    uint64_t blocks = (ngroups + waves - 1) / waves;
+    if (blocks > (uint64_t)num_cu)
+        blocks = (uint64_t)num_cu;
+    p.blocks = (uint32_t)blocks;
+    return p;
+}
+#undef KN
 
 static inline uint32_t le32(const uint8_t *p) { return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24; }
 
@@ -683,101 +985,58 @@ static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void
         snprintf(g_err, sizeof(g_err), "batch of %zu records exceeds 2^32-1", n);
         return -1;
     }
-    if (n <= (frame ? g_window_records : g_aead_window_records)) {
-        /*
-         * small batch: the window kernels (segments of 64 GHASH positions in parallel).  Up to 15 records per CU:
-         * 512-thread groups of 3 records, 8 lanes (8 steps) per segment, so a few records spread over many CUs
-         * with short chains; above that, when they fill every CU, persistent 1024-thread groups of 15 records,
-         * 4 lanes per segment, one per CU.
-         */
-        typedef void (*win_kernel_t)(const KeyImage *, uint32_t, uint32_t, uint32_t, const void *, uint32_t,
-                                     const uint8_t *, uint8_t *, const uint8_t *, uint32_t *, uint8_t *, const uint32_t *);
-        static const win_kernel_t table[2][2][2][2] = {
-            /* [frame][wide][seal][aes256] */
-            {{{mi355x_gcm_win_open_aes128, mi355x_gcm_win_open_aes256}, {mi355x_gcm_win_seal_aes128, mi355x_gcm_win_seal_aes256}},
-             {{mi355x_gcm_winw_open_aes128, mi355x_gcm_winw_open_aes256},
-              {mi355x_gcm_winw_seal_aes128, mi355x_gcm_winw_seal_aes256}}},
-            {{{mi355x_tls_win_open_aes128, mi355x_tls_win_open_aes256}, {mi355x_tls_win_seal_aes128, mi355x_tls_win_seal_aes256}},
-             {{mi355x_tls_winw_open_aes128, mi355x_tls_winw_open_aes256},
-              {mi355x_tls_winw_seal_aes128, mi355x_tls_winw_seal_aes256}}}};
-        static const win_kernel_t table32[2][2][2] = {
-            /* [frame][seal][aes256]: 32-position segments, one record per group */
-            {{mi355x_gcm_win32_open_aes128, mi355x_gcm_win32_open_aes256},
-             {mi355x_gcm_win32_seal_aes128, mi355x_gcm_win32_seal_aes256}},
-            {{mi355x_tls_win32_open_aes128, mi355x_tls_win32_open_aes256},
-             {mi355x_tls_win32_seal_aes128, mi355x_tls_win32_seal_aes256}}};
-        const bool wide = n > 15u * (uint64_t)ctx->num_cu; /* the wide groups (15 records) fill every CU */
-        /* at most g_seg32_records (default: one per CU): half-length segments, half the walk (4 steps) */
-        constexpr uint32_t per32 = (MI355X_WIN32_THREADS / 8u) / WIN_SEG32_MAXSEG; /* records per 32-position group */
-        const bool seg32 = !wide && n <= (g_seg32_records == SIZE_MAX ? (size_t)per32 * ctx->num_cu : g_seg32_records);
-        const win_kernel_t wk = seg32 ? table32[frame][seal][ctx->key_size == 32]
-                                      : table[frame][wide][seal][ctx->key_size == 32];
-        /* latency kernels: 512 threads, 8 lanes per segment; wide: 1024 threads, 4 lanes (MI355X_WIN_KERNEL list) */
-        const uint32_t threads = seg32 ? (uint32_t)MI355X_WIN32_THREADS : wide ? 1024u : 512u,
-                       per = seg32 ? per32 : (threads / (wide ? 4u : 8u)) / WIN_MAXSEG;
-        uint64_t blocks = (n + per - 1) / per;
-        if (wide && blocks > (uint64_t)ctx->num_cu)
-            blocks = (uint64_t)ctx->num_cu;
-        const uint8_t *wiv = (const uint8_t *)static_iv12;
-        DeviceGuard guard(ctx->device);
-        hipLaunchKernelGGL(wk, dim3((unsigned)blocks), dim3(threads), 0, stream, ctx->d_ki, le32(wiv), le32(wiv + 4),
-                           le32(wiv + 8), recs, (uint32_t)n, src, dst, aad, status, types, conn);
+    const LaunchPlan p = plan_launch(seal, frame, ctx->key_size, n, ctx->num_cu);
+    const uint8_t *iv = (const uint8_t *)static_iv12;
+    DeviceGuard guard(ctx->device);
+    if (p.win != nullptr) {
+        hipLaunchKernelGGL(p.win, dim3(p.blocks), dim3(p.threads), 0, stream, ctx->d_ki, le32(iv), le32(iv + 4),
+                           le32(iv + 8), recs, (uint32_t)n, src, dst, aad, status, types, conn);
         HIPCHK(hipGetLastError());
         return 0;
     }
-    const int k = frame ? 4 : g_lanes;
-    batch_kernel_t kern = frame ? pick_tls_kernel(seal, ctx->key_size == 32 ? 14u : 10u)
-                                : pick_kernel(seal, ctx->key_size == 32 ? 14u : 10u, k, nullptr);
-    if (kern == nullptr) {
-        snprintf(g_err, sizeof(g_err), "no kernel for lanes-per-record %d", k);
-        return -1;
-    }
-    const uint8_t *iv = (const uint8_t *)static_iv12;
-    const uint64_t ngroups = (n + (64 / k) - 1) / (64 / k);
-    const uint64_t waves = WG_THREADS / 64;
-    uint64_t blocks = (ngroups + waves - 1) / waves;
-    if (blocks > (uint64_t)ctx->num_cu)
-        blocks = (uint64_t)ctx->num_cu;
-    DeviceGuard guard(ctx->device);
     /*
-     * Work counters are never reset: every wave takes tickets until one is out of range, so a launch
-     * consumes exactly ngroups + (its waves) tickets, and the next launch on the slot starts there.
+     * Work counters are never reset: every wave takes tickets until one is out of range, so a launch consumes
+     * exactly ngroups + (its waves) tickets, and the next launch on the slot starts there.  A slot is reused
+     * every WORK_SLOTS launches; when its previous launch went to another stream, the new stream first waits
+     * for everything queued on that one (reuse_event), so two launches never share a counter at once.  The
+     * slot's base is committed only once the launch has been accepted.
      */
-    const uint32_t wslot = ctx->work_next++ % WORK_SLOTS;
+    const uint32_t k = frame ? 4u : (uint32_t)g_lanes;
+    const uint32_t ngroups = (uint32_t)((n + (64 / k) - 1) / (64 / k));
+    const uint32_t wslot = ctx->work_next % WORK_SLOTS;
     uint32_t *work = ctx->d_work + wslot;
     const uint32_t work_base = ctx->work_base[wslot];
-    ctx->work_base[wslot] = work_base + (uint32_t)ngroups + (uint32_t)(blocks * waves);
-    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(WG_THREADS), 0, stream, ctx->d_ki, le32(iv), le32(iv + 4),
-                       le32(iv + 8), recs, order, (uint32_t)n, src, dst, aad, status, types, work, work_base,
-                       conn);
+    if (ctx->work_stream[wslot] != stream && ctx->work_next >= WORK_SLOTS) {
+        if (hipEventRecord(ctx->reuse_event, ctx->work_stream[wslot]) == hipSuccess) {
+            HIPCHK(hipStreamWaitEvent(stream, ctx->reuse_event, 0));
+        } else { /* that stream is gone (its work with it) or unusable: wait for the device instead */
+            (void)hipGetLastError();
+            HIPCHK(hipDeviceSynchronize());
+        }
+    }
+    hipLaunchKernelGGL(p.batch, dim3(p.blocks), dim3(p.threads), 0, stream, ctx->d_ki, le32(iv), le32(iv + 4),
+                       le32(iv + 8), recs, order, (uint32_t)n, src, dst, aad, status, types, work, work_base, conn);
     HIPCHK(hipGetLastError());
-    return 0;
-}
-
-static int ensure_stage(ptls_mi355x_aesgcm_context_t *ctx, size_t need)
-{
-    if (need <= ctx->stage_cap)
-        return 0;
-    size_t cap = ctx->stage_cap ? ctx->stage_cap : 4096;
-    while (cap < need)
-        cap *= 2;
-    if (ctx->d_stage)
-        (void)hipFree(ctx->d_stage);
-    if (ctx->h_stage)
-        (void)hipHostFree(ctx->h_stage);
-    ctx->d_stage = nullptr;
-    ctx->h_stage = nullptr;
-    ctx->h_stage_dev = nullptr;
-    ctx->stage_cap = 0;
-    HIPCHK(hipMalloc(&ctx->d_stage, cap));
-    /* coherent: the GPU's zero-copy reads never see stale cache lines of a previous call */
-    HIPCHK(hipHostMalloc(&ctx->h_stage, cap, hipHostMallocMapped | hipHostMallocCoherent));
-    HIPCHK(hipHostGetDevicePointer((void **)&ctx->h_stage_dev, ctx->h_stage, 0));
-    ctx->stage_cap = cap;
+    ctx->work_base[wslot] = work_base + ngroups + p.blocks * (uint32_t)(WG_THREADS / 64);
+    ctx->work_stream[wslot] = stream;
+    ++ctx->work_next;
     return 0;
 }
 
 static inline size_t up16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+static int ensure_scratch(ptls_mi355x_aesgcm_context_t *ctx, size_t need)
+{
+    if (need <= ctx->scratch_cap)
+        return 0;
+    if (ctx->d_scratch)
+        (void)hipFree(ctx->d_scratch);
+    ctx->d_scratch = nullptr;
+    ctx->scratch_cap = 0;
+    HIPCHK(hipMalloc(&ctx->d_scratch, need));
+    ctx->scratch_cap = need;
+    return 0;
+}
 
 extern "C" {
 
@@ -785,11 +1044,11 @@ const char *ptls_mi355x_last_error(void) { return g_err; }
 
 int ptls_mi355x_is_supported(void)
 {
-    int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+    int n = 0, dev = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || hipGetDevice(&dev) != hipSuccess)
         return 0;
     hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, 0) != hipSuccess)
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess)
         return 0;
     return strncmp(prop.gcnArchName, "gfx950", 6) == 0;
 }
@@ -840,11 +1099,12 @@ size_t ptls_mi355x_set_slot_zero_copy_bytes(size_t n)
     return prev;
 }
 
-const char *ptls_mi355x_kernel_name(int is_seal, size_t key_size)
+const char *ptls_mi355x_kernel_name(int is_seal, size_t key_size, size_t n, int framing)
 {
-    const char *name = "";
-    pick_kernel(is_seal != 0, key_size == 32 ? 14u : 10u, g_lanes, &name);
-    return name;
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        ncu = 256;
+    return plan_launch(is_seal != 0, framing != 0, key_size == 32 ? 32u : 16u, n, ncu).name;
 }
 
 ptls_mi355x_aesgcm_context_t *ptls_mi355x_aesgcm_new(const void *key, size_t key_size, size_t capacity)
@@ -858,30 +1118,39 @@ ptls_mi355x_aesgcm_context_t *ptls_mi355x_aesgcm_new(const void *key, size_t key
     if (ctx == nullptr)
         return nullptr;
     ctx->key_size = (uint32_t)key_size;
+    int rc = -1;
     hipDeviceProp_t prop;
-    int *d_rc = nullptr, rc = -1;
-    if (hipGetDevice(&ctx->device) != hipSuccess || hipGetDeviceProperties(&prop, ctx->device) != hipSuccess)
+    DeviceShared *d = nullptr;
+    if (hipGetDevice(&ctx->device) != hipSuccess || hipGetDeviceProperties(&prop, ctx->device) != hipSuccess ||
+        (d = device_shared(ctx->device)) == nullptr)
         goto Fail;
+    ctx->shared = d;
     ctx->num_cu = prop.multiProcessorCount;
-    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess)
-        goto Fail;
-    if (hipMalloc(&ctx->d_ki, sizeof(KeyImage)) != hipSuccess || ensure_stage(ctx, 4096) != 0 ||
+    if (hipMalloc(&ctx->d_ki, sizeof(KeyImage)) != hipSuccess ||
         hipMalloc(&ctx->d_work, WORK_SLOTS * sizeof(uint32_t)) != hipSuccess ||
-        hipMemsetD32Async((hipDeviceptr_t)ctx->d_work, (int)g_ticket_origin, WORK_SLOTS, ctx->stream) != hipSuccess)
+        hipEventCreateWithFlags(&ctx->reuse_event, hipEventDisableTiming) != hipSuccess)
         goto Fail;
-    for (uint32_t i = 0; i < WORK_SLOTS; ++i)
+    for (uint32_t i = 0; i < WORK_SLOTS; ++i) {
         ctx->work_base[i] = g_ticket_origin;
-    memcpy(ctx->h_stage, key, key_size);
-    d_rc = (int *)(ctx->d_stage + 64);
-    if (hipMemcpyAsync(ctx->d_stage, ctx->h_stage, key_size, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
-        goto Fail;
-    hipLaunchKernelGGL(mi355x_gcm_setup, dim3(1), dim3(64), 0, ctx->stream, ctx->d_stage, (uint32_t)key_size, ctx->d_ki, d_rc);
-    if (hipGetLastError() != hipSuccess)
-        goto Fail;
-    if (hipMemcpyAsync(&rc, d_rc, sizeof(int), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
-        hipStreamSynchronize(ctx->stream) != hipSuccess || rc != 0)
-        goto Fail;
-    memset(ctx->h_stage, 0, key_size);
+        ctx->work_stream[i] = nullptr;
+    }
+    {
+        /* the key goes through the shared pinned staging (zero-copy read by the setup kernel), cleared after */
+        std::lock_guard<std::mutex> lk(d->mu);
+        if (ensure_stage(d, 64 + 16) != 0)
+            goto Fail;
+        memcpy(d->h_stage, key, key_size);
+        *(volatile int *)(d->h_stage + 64) = -2;
+        if (hipMemsetD32Async((hipDeviceptr_t)ctx->d_work, (int)g_ticket_origin, WORK_SLOTS, d->stream) != hipSuccess)
+            goto Fail;
+        hipLaunchKernelGGL(mi355x_gcm_setup, dim3(1), dim3(1024), 0, d->stream, d->h_stage_dev, (uint32_t)key_size,
+                           ctx->d_ki, (int *)(d->h_stage_dev + 64));
+        const hipError_t e1 = hipGetLastError(), e2 = hipStreamSynchronize(d->stream);
+        memset(d->h_stage, 0, key_size);
+        rc = *(volatile int *)(d->h_stage + 64);
+        if (e1 != hipSuccess || e2 != hipSuccess || rc != 0)
+            goto Fail;
+    }
     return ctx;
 Fail:
     if (g_err[0] == 0)
@@ -895,24 +1164,17 @@ void ptls_mi355x_aesgcm_free(ptls_mi355x_aesgcm_context_t *ctx)
     if (ctx == nullptr)
         return;
     DeviceGuard guard(ctx->device);
-    if (ctx->stream)
-        (void)hipStreamSynchronize(ctx->stream);
+    (void)hipDeviceSynchronize(); /* launches on caller streams may still read the key image */
     if (ctx->d_ki) {
         (void)hipMemset(ctx->d_ki, 0, sizeof(KeyImage)); /* clear key material, as ptls_fusion_aesgcm_free does */
         (void)hipFree(ctx->d_ki);
     }
-    if (ctx->d_stage)
-        (void)hipFree(ctx->d_stage);
     if (ctx->d_work)
         (void)hipFree(ctx->d_work);
-    if (ctx->d_sort)
-        (void)hipFree(ctx->d_sort);
-    if (ctx->h_stage) {
-        memset(ctx->h_stage, 0, ctx->stage_cap);
-        (void)hipHostFree(ctx->h_stage);
-    }
-    if (ctx->stream)
-        (void)hipStreamDestroy(ctx->stream);
+    if (ctx->d_scratch)
+        (void)hipFree(ctx->d_scratch);
+    if (ctx->reuse_event)
+        (void)hipEventDestroy(ctx->reuse_event);
     free(ctx);
 }
 
@@ -959,7 +1221,7 @@ int ptls_mi355x_tls_open_records(ptls_mi355x_aesgcm_context_t *ctx, const void *
                                  const ptls_mi355x_tls_record_t *recs, size_t n, const uint8_t *src, uint8_t *dst,
                                  uint32_t *status, uint8_t *types, void *stream)
 {
-    return ptls_mi355x_tls_open_records_multi(ctx, static_iv12, recs, nullptr, n, src, dst, status, types, stream);
+    return ptls_mi355x_tls_open_records_ex(ctx, static_iv12, recs, nullptr, n, src, dst, status, types, 0, stream);
 }
 
 int ptls_mi355x_tls_seal_records_multi(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12,
@@ -974,24 +1236,55 @@ int ptls_mi355x_tls_open_records_multi(ptls_mi355x_aesgcm_context_t *ctx, const 
                                        const ptls_mi355x_tls_record_t *recs, const uint32_t *conn_ids, size_t n,
                                        const uint8_t *src, uint8_t *dst, uint32_t *status, uint8_t *types, void *stream)
 {
+    return ptls_mi355x_tls_open_records_ex(ctx, static_iv12, recs, conn_ids, n, src, dst, status, types, 0, stream);
+}
+
+int ptls_mi355x_tls_open_records_ex(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12,
+                                    const ptls_mi355x_tls_record_t *recs, const uint32_t *conn_ids, size_t n,
+                                    const uint8_t *src, uint8_t *dst, uint32_t *status, uint8_t *types, int flags,
+                                    void *stream_)
+{
     if (n != 0 && (status == nullptr || types == nullptr)) {
         snprintf(g_err, sizeof(g_err), "tls_open_records needs status and types");
         return -1;
     }
-    return launch_batch(ctx, false, static_iv12, recs, nullptr, n, src, dst, nullptr, status, (hipStream_t)stream,
-                        true, types, conn_ids);
-}
-
-/* keys = GHASH steps of each record (its work), values = record index */
-extern "C" __global__ void mi355x_sort_keys(const Record *__restrict__ recs, uint32_t n, uint32_t *keys, uint32_t *vals)
-{
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) {
-        Record r = recs[i];
-        uint64_t blocks = ((uint64_t)r.len + 15) / 16 + ((uint64_t)r.aadlen + 15) / 16 + 1;
-        keys[i] = blocks > 0xffffffu ? 0xffffffu : (uint32_t)blocks;
-        vals[i] = i;
+    if ((flags & ~PTLS_MI355X_OPEN_STOP_AT_FAILURE) != 0) {
+        snprintf(g_err, sizeof(g_err), "unknown flags %#x", flags);
+        return -1;
     }
+    hipStream_t stream = (hipStream_t)stream_;
+    if (launch_batch(ctx, false, static_iv12, recs, nullptr, n, src, dst, nullptr, status, stream, true, types,
+                     conn_ids) != 0)
+        return -1;
+    if (n == 0 || !(flags & PTLS_MI355X_OPEN_STOP_AT_FAILURE))
+        return 0;
+    DeviceGuard guard(ctx->device);
+    size_t temp = 0;
+    rocprim::constant_iterator<uint32_t> one_conn(0u);
+    if (conn_ids != nullptr)
+        HIPCHK(hipcub::DeviceScan::InclusiveScanByKey(nullptr, temp, conn_ids, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                                      hipcub::Min(), (uint32_t)n, hipcub::Equality(), stream));
+    else
+        HIPCHK(hipcub::DeviceScan::InclusiveScanByKey(nullptr, temp, one_conn, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                                      hipcub::Min(), (uint32_t)n, hipcub::Equality(), stream));
+    const size_t arr = ((n * sizeof(uint32_t)) + 255) & ~(size_t)255;
+    if (ensure_scratch(ctx, 2 * arr + temp) != 0)
+        return -1;
+    uint8_t *base = (uint8_t *)ctx->d_scratch;
+    uint32_t *pos = (uint32_t *)base, *first = (uint32_t *)(base + arr);
+    const unsigned g = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(mi355x_tls_fail_pos, dim3(g), dim3(256), 0, stream, status, (uint32_t)n, pos);
+    HIPCHK(hipGetLastError());
+    if (conn_ids != nullptr)
+        HIPCHK(hipcub::DeviceScan::InclusiveScanByKey(base + 2 * arr, temp, conn_ids, pos, first, hipcub::Min(), (uint32_t)n,
+                                                      hipcub::Equality(), stream));
+    else
+        HIPCHK(hipcub::DeviceScan::InclusiveScanByKey(base + 2 * arr, temp, one_conn, pos, first, hipcub::Min(), (uint32_t)n,
+                                                      hipcub::Equality(), stream));
+    hipLaunchKernelGGL(mi355x_tls_truncate, dim3(g), dim3(256), 0, stream, (const TlsRecord *)recs, (uint32_t)n, first,
+                       dst, status, types);
+    HIPCHK(hipGetLastError());
+    return 0;
 }
 
 int ptls_mi355x_order_by_length(ptls_mi355x_aesgcm_context_t *ctx, const ptls_mi355x_record_t *recs, size_t n,
@@ -1009,16 +1302,9 @@ int ptls_mi355x_order_by_length(ptls_mi355x_aesgcm_context_t *ctx, const ptls_mi
     HIPCHK(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, temp, (uint32_t *)nullptr, (uint32_t *)nullptr,
                                                         (uint32_t *)nullptr, (uint32_t *)nullptr, (int)n, 0, 24, stream));
     const size_t arr = ((n * sizeof(uint32_t)) + 255) & ~(size_t)255;
-    const size_t need = 3 * arr + temp;
-    if (need > ctx->sort_cap) {
-        if (ctx->d_sort)
-            (void)hipFree(ctx->d_sort);
-        ctx->d_sort = nullptr;
-        ctx->sort_cap = 0;
-        HIPCHK(hipMalloc(&ctx->d_sort, need));
-        ctx->sort_cap = need;
-    }
-    uint8_t *base = (uint8_t *)ctx->d_sort;
+    if (ensure_scratch(ctx, 3 * arr + temp) != 0)
+        return -1;
+    uint8_t *base = (uint8_t *)ctx->d_scratch;
     uint32_t *keys_in = (uint32_t *)base, *keys_out = (uint32_t *)(base + arr), *vals_in = (uint32_t *)(base + 2 * arr);
     hipLaunchKernelGGL(mi355x_sort_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, (const Record *)recs,
                        (uint32_t)n, keys_in, vals_in);
@@ -1029,7 +1315,8 @@ int ptls_mi355x_order_by_length(ptls_mi355x_aesgcm_context_t *ctx, const ptls_mi
 }
 
 /*
- * Single record in host memory.  Stage layout (device and pinned host alike):
+ * Single record in host memory (the slot calls), on the device's shared stream and staging.  Stage layout
+ * (device and pinned host alike):
  *   [0, 64) descriptor | [64, 64 + A) aad | [D, D + inlen + 16) data (in place) | status
  */
 static int single_record(ptls_mi355x_aesgcm_context_t *ctx, bool seal, void *output, const void *input, size_t inlen,
@@ -1040,47 +1327,51 @@ static int single_record(ptls_mi355x_aesgcm_context_t *ctx, bool seal, void *out
         return -1;
     }
     DeviceGuard guard(ctx->device);
+    DeviceShared *d = ctx->shared;
+    std::lock_guard<std::mutex> lk(d->mu);
     const size_t off_aad = 64, off_data = off_aad + up16(aadlen), off_status = off_data + up16(inlen + 16);
     const size_t total = off_status + 16;
-    if (ensure_stage(ctx, total) != 0)
+    if (ensure_stage(d, total) != 0)
         return -1;
     Record rec = {off_data, off_data, off_aad, 0, (uint32_t)inlen, (uint32_t)aadlen};
-    memcpy(ctx->h_stage, &rec, sizeof(rec));
+    memcpy(d->h_stage, &rec, sizeof(rec));
     if (aadlen)
-        memcpy(ctx->h_stage + off_aad, aad, aadlen);
+        memcpy(d->h_stage + off_aad, aad, aadlen);
     if (inlen)
-        memcpy(ctx->h_stage + off_data, input, inlen);
+        memcpy(d->h_stage + off_data, input, inlen);
     if (!seal)
-        memcpy(ctx->h_stage + off_data + inlen, tag, 16);
+        memcpy(d->h_stage + off_data + inlen, tag, 16);
     /*
      * Zero-copy up to g_slot_zero_copy_bytes staged bytes: the kernel reads the record from the pinned staging
      * buffer over PCIe and writes the result back into it, so a call is one launch and one synchronisation
      * instead of an H2D copy, the launch, a D2H copy and the synchronisation.  Larger records are copied.
      */
     const bool zc = total <= g_slot_zero_copy_bytes;
-    uint8_t *base = zc ? ctx->h_stage_dev : ctx->d_stage;
+    uint8_t *base = zc ? d->h_stage_dev : d->d_stage;
     if (!zc)
-        HIPCHK(hipMemcpyAsync(ctx->d_stage, ctx->h_stage, off_status, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(hipMemcpyAsync(d->d_stage, d->h_stage, off_status, hipMemcpyHostToDevice, d->stream));
     /* one record: the window kernels (8-lane segments in parallel, leading pad steps skipped) are as fast as the
      * batch walk at 64 B and faster above it (scripts/slot_latency.py, profiles/r01f_slot_latency.txt) */
     if (launch_batch(ctx, seal, nonce12, (const Record *)base, nullptr, 1, base, base, base,
-                     (uint32_t *)(base + off_status), ctx->stream, false, nullptr, nullptr) != 0)
+                     (uint32_t *)(base + off_status), d->stream, false, nullptr, nullptr) != 0)
         return -1;
     const size_t outlen = seal ? inlen + 16 : inlen;
     if (!zc) {
-        HIPCHK(hipMemcpyAsync(ctx->h_stage + off_data, ctx->d_stage + off_data, outlen, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipMemcpyAsync(d->h_stage + off_data, d->d_stage + off_data, outlen, hipMemcpyDeviceToHost, d->stream));
         if (!seal)
-            HIPCHK(hipMemcpyAsync(ctx->h_stage + off_status, ctx->d_stage + off_status, 4, hipMemcpyDeviceToHost,
-                                  ctx->stream));
+            HIPCHK(hipMemcpyAsync(d->h_stage + off_status, d->d_stage + off_status, 4, hipMemcpyDeviceToHost,
+                                  d->stream));
     }
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipStreamSynchronize(d->stream));
     if (outlen)
-        memcpy(output, ctx->h_stage + off_data, outlen);
-    memset(ctx->h_stage + off_aad, 0, off_status - off_aad);
+        memcpy(output, d->h_stage + off_data, outlen);
+    uint32_t st;
+    memcpy(&st, d->h_stage + off_status, 4);
+    memset(d->h_stage, 0, total);
+    if (!zc)
+        HIPCHK(hipMemsetAsync(d->d_stage, 0, total, d->stream)); /* nothing of the record stays on the device */
     if (seal)
         return 0;
-    uint32_t st;
-    memcpy(&st, ctx->h_stage + off_status, 4);
     return st == (uint32_t)inlen ? 1 : 0;
 }
 
@@ -1096,7 +1387,9 @@ int ptls_mi355x_aesgcm_decrypt(ptls_mi355x_aesgcm_context_t *ctx, void *output, 
     return single_record(ctx, false, output, input, inlen, nonce12, aad, aadlen, tag);
 }
 
-int ptls_mi355x_aesecb_encrypt(ptls_mi355x_aesgcm_context_t *ctx, void *output, const void *input, size_t nblocks)
+/* nblocks of AES-ECB on host buffers through the shared staging: zero-copy up to the slot limit */
+static int ecb_host(int device, int num_cu, DeviceShared *d, const uint32_t *d_keys, uint32_t nr, bool dec, void *output,
+                    const void *input, size_t nblocks)
 {
     if (nblocks == 0)
         return 0;
@@ -1104,19 +1397,115 @@ int ptls_mi355x_aesecb_encrypt(ptls_mi355x_aesgcm_context_t *ctx, void *output, 
         snprintf(g_err, sizeof(g_err), "too many blocks");
         return -1;
     }
-    DeviceGuard guard(ctx->device);
+    DeviceGuard guard(device);
+    std::lock_guard<std::mutex> lk(d->mu);
     const size_t bytes = 16 * nblocks;
-    if (ensure_stage(ctx, 2 * bytes) != 0)
+    if (ensure_stage(d, bytes) != 0)
         return -1;
-    memcpy(ctx->h_stage, input, bytes);
-    HIPCHK(hipMemcpyAsync(ctx->d_stage, ctx->h_stage, bytes, hipMemcpyHostToDevice, ctx->stream));
-    hipLaunchKernelGGL(mi355x_aes_ecb, dim3((unsigned)((nblocks + 255) / 256)), dim3(256), 0, ctx->stream, ctx->d_ki,
-                       ctx->d_stage, ctx->d_stage + bytes, (uint32_t)nblocks);
+    memcpy(d->h_stage, input, bytes);
+    const bool zc = bytes <= g_slot_zero_copy_bytes;
+    uint8_t *base = zc ? d->h_stage_dev : d->d_stage;
+    if (!zc)
+        HIPCHK(hipMemcpyAsync(d->d_stage, d->h_stage, bytes, hipMemcpyHostToDevice, d->stream));
+    uint64_t blocks = (nblocks + 255) / 256;
+    if (blocks > 8ull * (uint64_t)num_cu)
+        blocks = 8ull * (uint64_t)num_cu;
+    hipLaunchKernelGGL(dec ? mi355x_aes_ecb_dec : mi355x_aes_ecb_enc, dim3((unsigned)blocks), dim3(256), 0, d->stream,
+                       d_keys, nr, base, base, (uint32_t)nblocks);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(ctx->h_stage + bytes, ctx->d_stage + bytes, bytes, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-    memcpy(output, ctx->h_stage + bytes, bytes);
-    memset(ctx->h_stage, 0, 2 * bytes);
+    if (!zc)
+        HIPCHK(hipMemcpyAsync(d->h_stage, d->d_stage, bytes, hipMemcpyDeviceToHost, d->stream));
+    HIPCHK(hipStreamSynchronize(d->stream));
+    memcpy(output, d->h_stage, bytes);
+    memset(d->h_stage, 0, bytes);
+    if (!zc)
+        HIPCHK(hipMemsetAsync(d->d_stage, 0, bytes, d->stream));
+    return 0;
+}
+
+int ptls_mi355x_aesecb_encrypt(ptls_mi355x_aesgcm_context_t *ctx, void *output, const void *input, size_t nblocks)
+{
+    /* the key image starts with the FIPS-197 schedule (KeyImage::rk) */
+    return ecb_host(ctx->device, ctx->num_cu, ctx->shared, ctx->d_ki->rk, ctx->key_size == 32 ? 14u : 10u, false, output,
+                    input, nblocks);
+}
+
+ptls_mi355x_aes_context_t *ptls_mi355x_aes_new(const void *key, size_t key_size)
+{
+    if (key_size != 16 && key_size != 32) {
+        snprintf(g_err, sizeof(g_err), "unsupported key size %zu", key_size);
+        return nullptr;
+    }
+    ptls_mi355x_aes_context_t *ctx = (ptls_mi355x_aes_context_t *)calloc(1, sizeof(*ctx));
+    if (ctx == nullptr)
+        return nullptr;
+    ctx->key_size = (uint32_t)key_size;
+    ctx->rounds = key_size == 32 ? 14u : 10u;
+    int rc = -1;
+    DeviceShared *d = nullptr;
+    if (hipGetDevice(&ctx->device) != hipSuccess ||
+        hipDeviceGetAttribute(&ctx->num_cu, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess ||
+        (d = device_shared(ctx->device)) == nullptr || hipMalloc(&ctx->d_keys, sizeof(AesKeys)) != hipSuccess)
+        goto Fail;
+    ctx->shared = d;
+    {
+        std::lock_guard<std::mutex> lk(d->mu);
+        if (ensure_stage(d, 64 + 16) != 0)
+            goto Fail;
+        memcpy(d->h_stage, key, key_size);
+        *(volatile int *)(d->h_stage + 64) = -2;
+        hipLaunchKernelGGL(mi355x_aes_setup, dim3(1), dim3(64), 0, d->stream, d->h_stage_dev, (uint32_t)key_size,
+                           ctx->d_keys, (int *)(d->h_stage_dev + 64));
+        const hipError_t e1 = hipGetLastError(), e2 = hipStreamSynchronize(d->stream);
+        memset(d->h_stage, 0, key_size);
+        rc = *(volatile int *)(d->h_stage + 64);
+        if (e1 != hipSuccess || e2 != hipSuccess || rc != 0)
+            goto Fail;
+    }
+    return ctx;
+Fail:
+    if (g_err[0] == 0)
+        snprintf(g_err, sizeof(g_err), "cipher setup failed: %s", hipGetErrorString(hipGetLastError()));
+    ptls_mi355x_aes_free(ctx);
+    return nullptr;
+}
+
+void ptls_mi355x_aes_free(ptls_mi355x_aes_context_t *ctx)
+{
+    if (ctx == nullptr)
+        return;
+    DeviceGuard guard(ctx->device);
+    if (ctx->d_keys) {
+        (void)hipDeviceSynchronize();
+        (void)hipMemset(ctx->d_keys, 0, sizeof(AesKeys));
+        (void)hipFree(ctx->d_keys);
+    }
+    free(ctx);
+}
+
+int ptls_mi355x_aes_ecb(ptls_mi355x_aes_context_t *ctx, int is_enc, void *output, const void *input, size_t nblocks)
+{
+    return ecb_host(ctx->device, ctx->num_cu, ctx->shared, is_enc ? ctx->d_keys->rk : ctx->d_keys->dk, ctx->rounds, !is_enc,
+                    output, input, nblocks);
+}
+
+int ptls_mi355x_aes_ecb_batch(ptls_mi355x_aes_context_t *ctx, int is_enc, uint8_t *dst, const uint8_t *src, size_t nblocks,
+                              void *stream)
+{
+    if (nblocks == 0)
+        return 0;
+    if (nblocks > 0xffffffffull) {
+        snprintf(g_err, sizeof(g_err), "too many blocks");
+        return -1;
+    }
+    DeviceGuard guard(ctx->device);
+    uint64_t blocks = (nblocks + 255) / 256;
+    if (blocks > 8ull * (uint64_t)ctx->num_cu)
+        blocks = 8ull * (uint64_t)ctx->num_cu;
+    hipLaunchKernelGGL(is_enc ? mi355x_aes_ecb_enc : mi355x_aes_ecb_dec, dim3((unsigned)blocks), dim3(256), 0,
+                       (hipStream_t)stream, is_enc ? ctx->d_keys->rk : ctx->d_keys->dk, ctx->rounds, src, dst,
+                       (uint32_t)nblocks);
+    HIPCHK(hipGetLastError());
     return 0;
 }
 

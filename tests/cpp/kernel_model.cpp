@@ -413,3 +413,64 @@ extern "C" int model_bs_keystream(const uint8_t *key, size_t keylen, const uint8
     free(kp);
     return 0;
 }
+
+/*
+ * The parallel key setup of mi355x_gcm_setup, step by step on the host: the wave multiplies as the XOR of
+ * the 64 lane shares (gf_mul_lane_share), the 13 x 128 single-bit products, then every table entry
+ * (key_image_store_entry).  Must equal build_key_image byte for byte.
+ */
+extern "C" int model_key_image_parallel(const uint8_t *key, size_t keylen, void *out, size_t outlen)
+{
+    if (outlen < sizeof(KeyImage) || (keylen != 16 && keylen != 32))
+        return -1;
+    KeyImage *ki = (KeyImage *)out;
+    memset(ki, 0, sizeof(KeyImage));
+    ki->rounds = aes_expand_key(kTabs.sbox, key, (uint32_t)keylen, ki->rk);
+    ki->key_size = (uint32_t)keylen;
+    const uint8_t zero[16] = {0};
+    aes_encrypt_bytes(kTabs.sbox, ki->rk, ki->rounds, zero, ki->H);
+    auto wave_mul = [](Gf128 x, Gf128 y) {
+        Gf128 acc = {0u, 0u};
+        for (uint32_t lane = 0; lane < 64; ++lane)
+            acc = gf_xor(acc, gf_mul_lane_share(x, y, lane));
+        return acc;
+    };
+    Gf128 pw[KEY_IMAGE_TABLES];
+    const Gf128 h = gf_from_bytes(ki->H);
+    pw[0] = h;
+    Gf128 p = h;
+    for (int e = 2; e <= MAX_K; ++e)
+        pw[e - 1] = p = wave_mul(p, h);
+    p = wave_mul(p, p);                    /* H^16 */
+    pw[MAX_K + 2] = p = wave_mul(p, p);    /* H^32 */
+    pw[MAX_K] = p = wave_mul(p, p);        /* H^64 */
+    pw[MAX_K + 3] = p = wave_mul(p, p);    /* H^128 */
+    pw[MAX_K + 1] = p = wave_mul(p, p);    /* H^256 */
+    static Gf128 bits[KEY_IMAGE_TABLES][128];
+    for (uint32_t i = 0; i < KEY_IMAGE_TABLES * 128u; ++i)
+        bits[i >> 7][i & 127u] = gf_mul_xpow(pw[i >> 7], i & 127u);
+    for (uint32_t i = 0; i < KEY_IMAGE_TABLES * 32u * 16u; ++i)
+        key_image_store_entry(ki, bits, i);
+    return 0;
+}
+
+/* gf_mul_xpow (the monomial multiply of the key setup) on stream-order bytes */
+extern "C" void model_gf_mul_xpow(const uint8_t *v, uint32_t i, uint8_t *out) { gf_to_bytes(gf_mul_xpow(gf_from_bytes(v), i), out); }
+
+/* the ECB kernels' block function (aes_ecb_block) on the host: nblocks in place, encrypt or decrypt */
+extern "C" int model_aes_ecb(const uint8_t *key, size_t keylen, int is_enc, uint8_t *buf, size_t nblocks)
+{
+    AesKeys k;
+    if (build_aes_keys(kTabs.sbox, key, (uint32_t)keylen, &k) != 0)
+        return -1;
+    for (size_t b = 0; b < nblocks; ++b) {
+        uint32_t w[4];
+        memcpy(w, buf + 16 * b, 16);
+        if (is_enc)
+            aes_ecb_block<false>(kTabs.t0, kTabs.sbox, k.rk, k.rounds, w);
+        else
+            aes_ecb_block<true>(kTabs.td0, kTabs.inv_sbox, k.dk, k.rounds, w);
+        memcpy(buf + 16 * b, w, 16);
+    }
+    return 0;
+}

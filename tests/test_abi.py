@@ -49,7 +49,12 @@ def test_algorithm_objects_match_slot_contract(engine_lib):
         assert a.name.decode() == ("AES128-GCM" if ks == 16 else "AES256-GCM")
         assert a.context_size >= C.sizeof(ra.AeadContext)
         assert a.ctr_cipher.contents.key_size == ks and a.ctr_cipher.contents.iv_size == 16
-        assert not a.ecb_cipher  # as in fusion (lib/fusion.c:990, 1000)
+        # fusion leaves ecb_cipher NULL (lib/fusion.c:990, 1000); the generic suite (t/picotls.c:266-307) needs it,
+        # with the shape of ptls_openssl_aes{128,256}ecb (lib/openssl.c:1580-1597)
+        e = a.ecb_cipher.contents
+        assert e.key_size == ks and e.block_size == 16 and e.iv_size == 0
+        assert e.name.decode() == ("AES128-ECB" if ks == 16 else "AES256-ECB")
+        assert e.context_size >= C.sizeof(ra.CipherContext)
 
 
 def _compile_and_run(tmp_path, name, src, incs):

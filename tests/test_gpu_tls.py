@@ -335,3 +335,67 @@ def test_many_windows_one_launch(gpu, framing_kernels):
         a, b = int(orecs["dst"][i]), int(trecs["src"][i])
         assert bytes(pt[a: a + int(lens[i])]) == bytes(src[b: b + int(lens[i])]), i
     eng.close()
+
+
+@pytest.mark.parametrize("multi", [False, True])
+def test_open_stop_at_first_failure(gpu, multi):
+    """PTLS_MI355X_OPEN_STOP_AT_FAILURE: ptls_receive stops at the first record that fails and does not advance seq
+    (lib/picotls.c:650-652, 4790), so records of the same connection behind it are never delivered.  The batch open
+    marks them TLS_NOT_PROCESSED with a zeroed plaintext slot; records before the failure, and every record of the
+    other connections, are opened as usual.  Without the flag every record is verified independently."""
+    import torch
+    key, iv = bytes(range(16)), bytes(range(12))
+    nconn, per = (3, 6) if multi else (1, 10)
+    conns = [7, 1, 0xABCDEF01][:nconn]
+    trecs = np.zeros(nconn * per, ra.TLS_RECORD_DTYPE)
+    conn = np.zeros(len(trecs), np.uint32)
+    lens = [100, 1400, 16384, 0, 17, 300, 5000, 64, 1, 2000]
+    frags, off, wire_off = [], 0, 0
+    for ci, c in enumerate(conns):
+        for k in range(per):
+            i = ci * per + k
+            ln = lens[k]
+            trecs[i] = (off, wire_off, 500 + k, ln, 23)
+            conn[i] = c if multi else 0
+            frags.append(xorshift64star(300 + i, ln).tobytes())
+            off += ln
+            wire_off += ln + 22
+    src = np.frombuffer(b"".join(frags), np.uint8) if off else np.zeros(1, np.uint8)
+    d_src, d_recs, d_conn = dev(src), dev(trecs.view(np.uint8)), dev(conn.view(np.int32))
+    d_wire = torch.zeros(wire_off, dtype=torch.uint8, device="cuda")
+    eng = ra.Engine(key)
+    eng.tls_seal_records(iv, d_recs.data_ptr(), len(trecs), d_src.data_ptr(), d_wire.data_ptr(),
+                         conn_ptr=d_conn.data_ptr() if multi else 0)
+    torch.cuda.synchronize()
+    wire = d_wire.cpu().numpy().copy()
+    orecs = trecs.copy()
+    orecs["src"] = trecs["dst"]
+    orecs["len"] = trecs["len"] + 17
+    orecs["dst"] = np.cumsum([0] + [ln + 1 for ln in trecs["len"][:-1]]).astype(np.uint64)
+    # connection 0: record 3 tampered; connection 1 (multi): record 1 and 4 tampered; connection 2: none
+    bad = {3} if not multi else {3, per + 1, per + 4}
+    for i in bad:
+        wire[int(orecs[i]["src"]) + 5] ^= 0x40
+    pt_size = int(orecs["dst"][-1]) + int(orecs["len"][-1])
+    for flags in (0, ra.OPEN_STOP_AT_FAILURE):
+        d_w, d_o, d_ids = dev(wire), dev(orecs.view(np.uint8)), dev(conn.view(np.int32))
+        d_pt = torch.full((pt_size,), 0xAA, dtype=torch.uint8, device="cuda")
+        d_st = torch.zeros(len(orecs), dtype=torch.int32, device="cuda")
+        d_ty = torch.zeros(len(orecs), dtype=torch.uint8, device="cuda")
+        eng.tls_open_records(iv, d_o.data_ptr(), len(orecs), d_w.data_ptr(), d_pt.data_ptr(), d_st.data_ptr(),
+                             d_ty.data_ptr(), conn_ptr=d_ids.data_ptr() if multi else 0, flags=flags)
+        torch.cuda.synchronize()
+        st, ty, pt = d_st.cpu().numpy().view(np.uint32), d_ty.cpu().numpy(), d_pt.cpu().numpy()
+        for ci in range(nconn):
+            first_bad = min([i for i in bad if ci * per <= i < (ci + 1) * per], default=None)
+            for i in range(ci * per, (ci + 1) * per):
+                a, n = int(orecs[i]["dst"]), int(trecs[i]["len"])
+                if i in bad:
+                    assert st[i] == ra.TLS_BAD_RECORD_MAC, (flags, i)
+                elif flags and first_bad is not None and i > first_bad:
+                    assert st[i] == ra.TLS_NOT_PROCESSED and ty[i] == 0, (flags, i, st[i])
+                    assert not pt[a:a + n + 1].any(), (flags, i)
+                else:
+                    assert st[i] == n and ty[i] == 23, (flags, i, st[i])
+                    assert pt[a:a + n].tobytes() == frags[i], (flags, i)
+    eng.close()

@@ -390,3 +390,49 @@ def test_model_window_aead_edges(model, kw):
     pt = np.zeros_like(src)
     run(model, False, kw, key, iv, recs, got, pt, aad, st)
     assert (st == recs["len"]).all()
+
+
+@pytest.mark.parametrize("keylen", [16, 32])
+def test_parallel_key_setup_matches_sequential(model, keylen):
+    """mi355x_gcm_setup's steps (wave-parallel power chain, monomial products, table entries) give the key image
+    build_key_image builds one bit at a time, byte for byte."""
+    size = model.model_key_image_size()
+    model.model_key_image_parallel.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]
+    for seed in range(3):
+        key = np.random.default_rng(seed + 40).integers(0, 256, keylen, dtype=np.uint8).tobytes()
+        a, b = C.create_string_buffer(size), C.create_string_buffer(size)
+        assert model.model_key_image(key, keylen, a, size) == 0
+        assert model.model_key_image_parallel(key, keylen, b, size) == 0
+        assert a.raw == b.raw
+
+
+def test_gf_mul_xpow_matches_oracle(model):
+    """v * x^i for every i (the single-bit products of the key setup) against the oracle's Algorithm-1 multiply."""
+    model.model_gf_mul_xpow.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
+    rng = np.random.default_rng(7)
+    for _ in range(4):
+        v = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+        for i in range(128):
+            xi = bytearray(16)
+            xi[i // 8] = 0x80 >> (i % 8)  # the element x^i (GCM bit i)
+            out = C.create_string_buffer(16)
+            model.model_gf_mul_xpow(v, i, out)
+            assert out.raw == oracle.gf128_mul(v, bytes(xi)), i
+
+
+@pytest.mark.parametrize("keylen", [16, 32])
+def test_model_ecb_block_both_directions(model, keylen):
+    """aes_ecb_block (the ECB kernels' code) encrypts like the oracle's FIPS-197 Cipher and decrypts like its
+    InvCipher, over random blocks and keys."""
+    model.model_aes_ecb.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_void_p, C.c_size_t]
+    rng = np.random.default_rng(keylen)
+    for _ in range(8):
+        key = rng.integers(0, 256, keylen, dtype=np.uint8).tobytes()
+        data = rng.integers(0, 256, 16 * 37, dtype=np.uint8).tobytes()
+        buf = C.create_string_buffer(data, len(data))
+        assert model.model_aes_ecb(key, keylen, 1, buf, 37) == 0
+        enc = buf.raw[:len(data)]
+        assert enc == oracle.ecb_blocks(key, data, True)
+        assert model.model_aes_ecb(key, keylen, 0, buf, 37) == 0
+        assert buf.raw[:len(data)] == data
+        assert oracle.ecb_blocks(key, enc, False) == data

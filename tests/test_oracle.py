@@ -25,6 +25,35 @@ def test_ecb_kats():
     assert oracle.ecb(bytes(range(32)), pt).hex() == "8ea2b7ca516745bfeafc49904b496089"
 
 
+def test_ecb_decrypt_kats():
+    # t/picotls.c:266-307 test_ecb: the ciphertext decrypts back to the FIPS-197 C.1 / C.3 plaintext
+    pt = bytes.fromhex("00112233445566778899aabbccddeeff")
+    for key, ct in ((bytes(range(16)), "69c4e0d86a7b0430d8cdb78070b4c55a"),
+                    (bytes(range(32)), "8ea2b7ca516745bfeafc49904b496089")):
+        assert oracle.ecb_blocks(key, bytes.fromhex(ct), encrypt=False) == pt
+        assert oracle.ecb_blocks(key, pt * 3, encrypt=True) == bytes.fromhex(ct) * 3
+    # t/fusion.c:71-85 vectors backwards
+    assert oracle.ecb_blocks(bytes(16), bytes.fromhex("172afecb50b5f1237814b2f7cb51d0f7"), False) == b"hello world!!!!!"
+    assert oracle.ecb_blocks(bytes(32), bytes.fromhex("2a033f0627b3554aa4fe5786550736ff"), False) == b"hello world!!!!!"
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(os.path.dirname(oracle.__file__), "_ref", "libref_fusion.so")),
+                    reason="reference build (oracle/_ref) not present")
+def test_ecb_decrypt_vs_reference_cifra():
+    """The oracle's InvCipher against the reference's own minicrypto AES decryption (deps/cifra/src/aes.c,
+    lib/cifra/aes-common.h:48-53), and its Cipher against fusion's aesecb_encrypt, on random keys and blocks."""
+    import numpy as np
+    ref = oracle.Reference()
+    rng = np.random.default_rng(5)
+    for i in range(300):
+        kl = 16 if i % 2 else 32
+        key = rng.integers(0, 256, kl, dtype=np.uint8).tobytes()
+        blk = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+        assert oracle.ecb_blocks(key, blk, encrypt=False) == ref.ecb_decrypt(key, blk)
+        if ref.supported():
+            assert oracle.ecb_blocks(key, blk, encrypt=True) == ref.ecb(key, blk)
+
+
 def test_ctr_kat():
     # t/picotls.c:312-321: AES128-CTR keystream block = AES-ECB(iv)
     key = bytes.fromhex("2b7e151628aed2a6abf7158809cf4f3c")
