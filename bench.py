@@ -1,6 +1,7 @@
 """Benchmark of the MI355X AES-GCM engine (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload 1400|16k|16k-aes128|ragged]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload 1400|16k|16k-aes128|ragged|...]
+                    [--workloads LIST | --no-workloads] [--no-cpu-baseline] [--no-e2e]
 
 One step = one pass of the hot path over one batch resident in HBM: seal every record
 of the batch (ptls_mi355x_seal_batch), then open the sealed batch
@@ -12,18 +13,25 @@ TLS records (5-byte TLS header AAD, seq = record index, 256-B aligned records). 
 N > 1 (torchrun, one rank per GPU) every rank seals/opens its own 1 M-record shard --
 configs[4], 8 M x 1400 B over 8 GPUs -- with no collective on the data path ("weak").
 
+At N=1 the same run also measures, each on its own batch and clock, the other single-GPU configs
+(`workloads`): the north-star config (AES-128-GCM, 256 K x 16 KiB), configs[2] (AES-256-GCM,
+256 K x 16 KiB) and configs[3] (AES-128-GCM, 1 M records U{64..16384} B, sorted inside the step).
+
 The JSON line also carries
   roofline      -- the dominant kernel's algorithmic HBM bytes per launch / its mean launch
                    time (HIP events on the launch stream) against the 8 TB/s HBM3E peak;
-                   `traffic` from rocprofv3 PMC counters when a profiles/ summary exists;
-  cpu_baseline  -- the reference engine (lib/fusion.c, built unmodified into oracle/_ref)
-                   on this host's cores with the t/ptlsbench.c methodology, bounded sample.
+                   `traffic` from rocprofv3 PMC counters (profiles/pmc_traffic.json);
+  cpu_baseline  -- the reference engine (lib/fusion.c, built unmodified into oracle/_ref) with the
+                   t/ptlsbench.c methodology: one pinned process per core, CLOCK_PROCESS_CPUTIME_ID,
+                   1400 B and 16 KiB, AES-128 and AES-256, 1 core and all usable cores; measured
+                   before the GPU is touched.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -34,6 +42,7 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH
 DESC_BYTES = 40         # sizeof(ptls_mi355x_record_t)
 LDS_CLOCK_GHZ = 2.4     # MI355X peak engine clock (the LDS roofline is priced at it, as HBM at its spec peak)
 GIB = float(1 << 30)
+METRIC = "device-resident AES-GCM GiB/s, 1.4 KB & 16 KiB record batches, 1/2/4/8 GPU"
 
 WORKLOADS = {
     "1400": dict(name="AES-128-GCM seal+open, 1M x 1400 B TLS records", key=16, n=1 << 20, length=1400),
@@ -45,6 +54,11 @@ WORKLOADS = {
                            length=16385),
     "ragged": dict(name="AES-128-GCM seal+open, 1M records U{64..16384} B", key=16, n=1 << 20, length=None),
 }
+# the single-GPU configs measured beside `value` at N=1: the north-star config first
+SIDE_WORKLOADS = "16k-aes128,16k,ragged"
+
+CPU_BENCH = os.path.join(ROOT, "oracle", "_ref", "ref_fusion_bench")
+PTLSBENCH = os.path.join(ROOT, "oracle", "_ref", "ptlsbench")
 
 
 def rank_shard(rank: int, world: int, n_per_rank: int):
@@ -74,85 +88,117 @@ def algorithmic_bytes(lengths_sum: int, n: int, aad_sum: int, seal: bool) -> int
     return lengths_sum + 16 * n + aad_sum + DESC_BYTES * n + lengths_sum + 4 * n
 
 
-def cpu_baseline(wl: dict, threads: int) -> dict:
-    """Reference fusion on host cores, t/ptlsbench.c methodology, ~10-30 s of CPU work."""
-    import oracle
-
-    length = wl["length"] or 8224  # ragged: the mean record size
+# ------------------------------------------------------------------------------------------- CPU baseline ----
+def _cgroup_cpus():
+    """CPUs' worth of the cgroup v2 quota (cpu.max), or None when unlimited."""
     try:
-        ref = oracle.Reference()
-        if not ref.supported():
-            raise RuntimeError("CPU lacks AES-NI/PCLMUL/AVX2")
-        per_thread = max(2000, int(3e9 / length))  # ~3 GB sealed (+ opened) per thread: ~10-20 s of CPU work
-        s1, o1, _, f1 = ref.bench(wl["key"], length, 5, per_thread, 1)
-        sN, oN, wall, fN = ref.bench(wl["key"], length, 5, per_thread, threads)
-        if f1 or fN:
-            raise RuntimeError("reference open failed")
-        # seal+open bytes per second (harmonic combination: each record is sealed then opened)
-        one = 2.0 / (1.0 / s1 + 1.0 / o1) / GIB
-        alln = 2.0 / (1.0 / sN + 1.0 / oN) / GIB
-        cpu = open("/proc/cpuinfo").read().split("model name")[1].split("\n")[0].strip(" :\t")
-        return {"value": round(alln, 3), "unit": "GiB/s", "cores": threads, "kind": "reference",
-                "value_1core": round(one, 3), "cpu": cpu,
-                "sample": f"lib/fusion.c AES-{8 * wl['key']}-GCM, {per_thread} x {length} B records per thread, "
-                          f"AAD 5 B, seal then open in 1000-record batches (t/ptlsbench.c:80-165), "
-                          f"{threads} threads each with its own context; 1-core run separately"}
-    except (FileNotFoundError, OSError, RuntimeError) as e:
-        # the CPU restatement (scalar, bit-serial GHASH): a much slower "port" baseline
-        import numpy as np
-        from rapido_amd import records
-
-        n = 256
-        recs, src, aad = records.tls_batch(np.full(n, length, dtype=np.uint64), seed=5)
-        dst = np.zeros_like(src)
-        t0 = time.perf_counter()
-        oracle.batch(True, bytes(wl["key"]), bytes(12), recs, src, dst, aad, nthreads=threads)
-        dt = time.perf_counter() - t0
-        return {"value": round(n * length / dt / GIB, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
-                "sample": f"oracle/aesgcm_oracle.c seal only, {n} x {length} B ({e})"}
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        return None if q == "max" else float(q) / float(period)
+    except (OSError, ValueError):
+        return None
 
 
-def main() -> None:
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="1400", choices=sorted(WORKLOADS))
-    ap.add_argument("--lanes", type=int, default=0, help="lanes per record (1/2/4/8); 0 = engine default")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--e2e", action="store_true", help="time the PCIe-inclusive path (pinned host in/out); default at N=1")
-    ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive path")
-    ap.add_argument("--check", type=int, default=64, help="records re-checked against the CPU oracle after timing")
-    args = ap.parse_args()
+def _physical_first(cpus):
+    """The CPUs ordered so that distinct physical cores come first (SMT siblings last)."""
+    seen, first, rest = set(), [], []
+    for c in sorted(cpus):
+        try:
+            core = (open(f"/sys/devices/system/cpu/cpu{c}/topology/physical_package_id").read().strip(),
+                    open(f"/sys/devices/system/cpu/cpu{c}/topology/core_id").read().strip())
+        except OSError:
+            core = (c,)
+        (rest if core in seen else first).append(c)
+        seen.add(core)
+    return first + rest, len(first)
 
+
+def _run_workers(keylen, length, nrec, cpus):
+    """One ref_fusion_bench process per CPU, all at once; -> (per-worker results, wall seconds)."""
+    t0 = time.perf_counter()
+    procs = [subprocess.Popen([CPU_BENCH, str(keylen), str(length), str(nrec), str(c)], stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True) for c in cpus]
+    outs = []
+    for p in procs:
+        o, e = p.communicate(timeout=300)
+        if p.returncode != 0:
+            raise RuntimeError(f"ref_fusion_bench rc={p.returncode}: {o.strip()[-200:]} {e.strip()[-200:]}")
+        outs.append(json.loads(o.strip().splitlines()[-1]))
+    return outs, time.perf_counter() - t0
+
+
+def cpu_baseline(main_key: int, main_length: int) -> dict:
+    """The reference lib/fusion.c on this host's cores, t/ptlsbench.c methodology (t/ptlsbench.c:80-175):
+    1 core and every usable core (one pinned process each), 1400 B and 16 KiB, AES-128 and AES-256.
+    Per worker: CLOCK_PROCESS_CPUTIME_ID rates, as ptlsbench; all cores: the sum of those rates, and the
+    wall-clock aggregate (total bytes / wall time of the whole run) beside it."""
+    if not os.path.exists(CPU_BENCH):
+        return {"value": None, "error": f"{CPU_BENCH} not built (oracle/Makefile needs /root/reference at build time)"}
+    avail = sorted(os.sched_getaffinity(0))
+    quota = _cgroup_cpus()
+    ordered, physical = _physical_first(avail)
+    usable = len(avail) if quota is None else max(1, min(len(avail), int(quota + 1e-6)))
+    workers = ordered[:usable]
+    cpu_model = open("/proc/cpuinfo").read().split("model name")[1].split("\n")[0].strip(" :\t")
+    configs = {}
+    for keylen in (16, 32):
+        for length in (1400, 16384):
+            target = 1.5e9 if keylen == 16 else 1.0e9  # bytes per worker: ~0.3-0.6 s of CPU time each
+            nrec = max(2000, int(target / length))
+            one, w1 = _run_workers(keylen, length, nrec, workers[:1])
+            alln, wall = _run_workers(keylen, length, nrec, workers)
+            r1 = one[0]
+
+            def so(r):  # seal+open bytes per CPU-second of one worker (each record sealed then opened)
+                return 2.0 * r["len"] * r["n"] / ((r["encrypt_us"] + r["decrypt_us"]) * 1e-6) / GIB
+
+            cput = sum(so(r) for r in alln)
+            wall_agg = 2.0 * length * nrec * len(alln) / wall / GIB
+            cpu_frac = sum((r["encrypt_us"] + r["decrypt_us"]) * 1e-6 for r in alln) / (wall * len(alln))
+            configs[f"aes{8 * keylen}-{length}"] = {
+                "seal_open_gibps_1core": round(so(r1), 3),
+                "seal_gibps_1core": round(r1["seal_gibps"], 3), "open_gibps_1core": round(r1["open_gibps"], 3),
+                "encrypt_mbps_1core": r1["encrypt_mbps"], "decrypt_mbps_1core": r1["decrypt_mbps"],
+                "seal_open_gibps_all_cputime": round(cput, 3),
+                "seal_open_gibps_all_wall": round(wall_agg, 3),
+                "scaling_cputime": round(cput / so(r1), 2),
+                "worker_cpu_time_per_wall": round(cpu_frac, 3),
+                "records_per_worker": nrec}
+    main = configs[f"aes{8 * main_key}-{main_length}"]
+    siblings = len(workers) - min(len(workers), physical)
+    note = (f"{len(avail)} CPUs in the affinity mask ({physical} physical cores), cgroup quota "
+            f"{'none' if quota is None else f'{quota:g} CPUs'}: {len(workers)} pinned workers ({siblings} on SMT "
+            f"siblings).  Per-worker rates use CLOCK_PROCESS_CPUTIME_ID as ptlsbench; the all-core value is their "
+            f"sum, and the wall-clock aggregate is given beside it (equal when every worker owns its core: "
+            f"worker_cpu_time_per_wall ~ 1).  The round-1 figure (6.4x on 16 threads) summed per-thread WALL "
+            f"rates of 16 threads in ONE process, so cgroup throttling and SMT sharing cut it; here each worker "
+            f"is its own process pinned to its own core.")
+    out = {"value": main["seal_open_gibps_all_cputime"], "unit": "GiB/s", "cores": len(workers), "kind": "reference",
+           "value_wall": main["seal_open_gibps_all_wall"], "value_1core": main["seal_open_gibps_1core"],
+           "cores_available": len(avail), "physical_cores_available": physical, "cgroup_quota_cpus": quota,
+           "cpu": cpu_model, "configs": configs, "scaling_note": note,
+           "sample": f"lib/fusion.c (unmodified), t/ptlsbench.c methodology: 1000-record batches sealed then opened, "
+                     f"32-B AAD = h[4] with seq, CLOCK_PROCESS_CPUTIME_ID; {len(workers)} pinned processes x "
+                     f"~1-1.5 GB each per config; value = AES-{8 * main_key} {main_length} B seal+open, all workers"}
+    if os.path.exists(PTLSBENCH):  # configs[0]-style unmodified run (L = 1500, the reference's own CSV)
+        try:
+            r = subprocess.run([PTLSBENCH], capture_output=True, text=True, timeout=120)
+            rows = [ln for ln in r.stdout.splitlines() if ", fusion," in ln]
+            out["ptlsbench_unmodified"] = {"rows": rows, "note": "t/ptlsbench.c as shipped: N=1000, L=1500, "
+                                                                 "AAD 32 B, 1 core, Mbps = 8 L N / us"}
+        except (OSError, subprocess.SubprocessError) as e:
+            out["ptlsbench_unmodified"] = {"error": str(e)}
+    return out
+
+
+# ------------------------------------------------------------------------------------------- GPU workload ----
+def measure(ra, wl_key, args, dev, rank, world, check):
+    """Times one workload: K steps (seal + open of the whole batch) after W warmups; -> result dict."""
     import numpy as np
     import torch
     import torch.distributed as dist
-
-    import rapido_amd as ra
     from rapido_amd import records
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    # rehearsal only (a 1-GPU box): RAPIDO_BENCH_SAME_DEVICE=1 puts every rank on cuda:0 and
-    # RAPIDO_BENCH_BACKEND=gloo replaces RCCL, which refuses two ranks on one GPU
-    dev_index = 0 if os.environ.get("RAPIDO_BENCH_SAME_DEVICE") == "1" else local_rank
-    if world > 1:
-        torch.cuda.set_device(dev_index)
-        backend = os.environ.get("RAPIDO_BENCH_BACKEND", "nccl")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
-        else:
-            dist.init_process_group(backend)
-    dev = torch.device("cuda", dev_index if world > 1 else 0)
-    torch.cuda.set_device(dev)
-    ra.require_gpu()
-    if args.lanes:
-        ra.set_lanes_per_record(args.lanes)
-
-    wl = WORKLOADS[args.workload]
+    wl = WORKLOADS[wl_key]
     n = wl["n"]
     rng = np.random.default_rng(1 + rank)
     if wl["length"] is None:
@@ -178,7 +224,6 @@ def main() -> None:
     eng = ra.Engine(key)
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
-
     ragged = wl["length"] is None
     d_order = torch.zeros(n, dtype=torch.int32, device=dev)
 
@@ -225,66 +270,37 @@ def main() -> None:
     # correctness after timing: every status verifies; a sample of records bit-exact vs the oracle
     st = d_st.cpu().numpy().view(np.uint32)
     if not (st == recs["len"]).all():
-        raise SystemExit("bench: open status mismatch -- results invalid")
-    if args.check and rank == 0:
+        raise SystemExit(f"bench: open status mismatch ({wl_key}) -- results invalid")
+    if check and rank == 0:
         import oracle
 
-        idx = rng.choice(n, size=min(args.check, n), replace=False)
-        sub = recs[idx].copy()
-        spans = [(int(r["src"]), int(r["len"])) for r in sub]
-        srcs = [d_src[a:a + ln].cpu().numpy() for a, ln in spans]
-        cts = [d_ct[a:a + ln + 16].cpu().numpy() for a, ln in spans]
-        for r, s_, c_ in zip(sub, srcs, cts):
+        idx = rng.choice(n, size=min(check, n), replace=False)
+        for r in recs[idx]:
+            a, ln = int(r["src"]), int(r["len"])
             want = oracle.seal(key, oracle.build_iv(iv, int(r["seq"])), aad[int(r["aad"]):int(r["aad"]) + 5].tobytes(),
-                               s_.tobytes())
-            if want != c_.tobytes():
-                raise SystemExit("bench: sealed record differs from the oracle -- results invalid")
+                               d_src[a:a + ln].cpu().numpy().tobytes())
+            if want != d_ct[a:a + ln + 16].cpu().numpy().tobytes():
+                raise SystemExit(f"bench: sealed record differs from the oracle ({wl_key}) -- results invalid")
 
     payload = float(lengths.sum())
-    total_bytes = 2.0 * payload * world  # sealed + opened, all ranks
-    value = total_bytes * args.steps / elapsed / GIB
+    value = 2.0 * payload * world * args.steps / elapsed / GIB  # sealed + opened, all ranks
     seal_b = algorithmic_bytes(int(payload), n, 5 * n, True)
     open_b = algorithmic_bytes(int(payload), n, 5 * n, False)
     dom_is_seal = seal_ms >= open_ms
     dom_ms = seal_ms if dom_is_seal else open_ms
     dom_bytes = seal_b if dom_is_seal else open_b
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
-    kname = ra.kernel_name(dom_is_seal, wl["key"])
+    kname = ra.kernel_name(dom_is_seal, wl["key"], n)
 
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_path):
         try:
-            pmc = json.load(open(pmc_path))
-            ent = pmc.get(args.workload, {}).get(kname)
+            ent = json.load(open(pmc_path)).get(wl_key, {}).get(kname)
             if ent:
                 traffic = ent["hbm_bytes_per_launch"]
         except (ValueError, KeyError):
             traffic = None
-
-    out = {
-        "metric": "device-resident AES-GCM GiB/s, 1.4 KB & 16 KiB record batches, 1/2/4/8 GPU",
-        "value": round(value, 2),
-        "unit": "GiB/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u8",
-        "data": "synthetic (device-generated random payload, TLS 1.3 record headers as AAD)",
-        "config": {"workload": wl["name"], "records_per_gpu": n,
-                   "record_bytes": wl["length"] if wl["length"] else "U{64..16384}",
-                   "aad_bytes": 5, "key_bits": 8 * wl["key"], "lanes_per_record": ra.lib().ptls_mi355x_get_lanes_per_record(),
-                   "parallelism": f"records sharded per GPU x{world}, no collective"},
-        "seal_gibps": round(payload / (seal_ms * 1e-3) / GIB, 2),
-        "open_gibps": round(payload / (open_ms * 1e-3) / GIB, 2),
-        "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                     "algorithmic_bytes_per_launch": dom_bytes, "launch_ms": round(dom_ms, 4)},
-    }
 
     # the kernels' binding resource: LDS-array cycles of the T-table AES + nibble-table GHASH reads
     # (MI355X_MICROARCH.md LDS table: ds_read_b32 2 clk, ds_read_b128 4 clk per wave)
@@ -293,92 +309,207 @@ def main() -> None:
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     lds_ceiling = ncu * LDS_CLOCK_GHZ * 1e9 / lds_cycles_per_block * 16 / 1e9  # payload GB/s
     dom_payload = payload / (dom_ms * 1e-3) / 1e9
-    out["lds_roofline"] = {"bound": "lds", "kernel": kname, "achieved": round(dom_payload, 1),
-                           "peak": round(lds_ceiling, 1), "unit": "GB/s payload", "frac": round(dom_payload / lds_ceiling, 4),
-                           "model": f"{b32_reads} ds_read_b32 + 32 ds_read_b128 per 16-B block = "
-                                    f"{lds_cycles_per_block:.2f} LDS clk/block/CU, {ncu} CU x {LDS_CLOCK_GHZ} GHz",
-                           "note": "this read mix alone sustains 0.78 of the nominal rate (profiles/r01c_lds_ceiling.json)"}
+    res = {
+        "workload": wl["name"], "records_per_gpu": n, "steps": args.steps, "warmup": args.warmup,
+        "value": round(value, 2), "unit": "GiB/s", "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "seal_gibps": round(payload / (seal_ms * 1e-3) / GIB, 2),
+        "open_gibps": round(payload / (open_ms * 1e-3) / GIB, 2),
+        "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                     "algorithmic_bytes_per_launch": dom_bytes, "launch_ms": round(dom_ms, 4)},
+        "lds_roofline": {"bound": "lds", "kernel": kname, "achieved": round(dom_payload, 1),
+                         "peak": round(lds_ceiling, 1), "unit": "GB/s payload",
+                         "frac": round(dom_payload / lds_ceiling, 4),
+                         "model": f"{b32_reads} ds_read_b32 + 32 ds_read_b128 per 16-B block = "
+                                  f"{lds_cycles_per_block:.2f} LDS clk/block/CU, {ncu} CU x {LDS_CLOCK_GHZ} GHz",
+                         "note": "this read mix alone sustains 0.78 of the nominal rate (profiles/r01c_lds_ceiling.json)"},
+    }
+    extra = dict(eng=eng, iv=iv, d_src=d_src, d_ct=d_ct, d_recs=d_recs, d_aad=d_aad, recs=recs, n=n,
+                 src_bytes=src_bytes, payload=payload, stream=stream, key=wl["key"])
+    return res, extra
 
-    if world == 1 and not args.no_e2e:
-        # latency side (not `value`): one rapido send window, 16 x 16 KiB records framed in one launch on the
-        # window kernels, device-resident, back-to-back launches timed with HIP events
-        WIN, FRAG = 16, 16384
-        t = np.zeros(WIN, ra.TLS_RECORD_DTYPE)
-        t["src"] = np.arange(WIN, dtype=np.uint64) * FRAG
-        t["dst"] = np.arange(WIN, dtype=np.uint64) * (FRAG + 22)
-        t["seq"] = np.arange(WIN, dtype=np.uint64)
-        t["len"], t["type"] = FRAG, 23
-        d_t = torch.from_numpy(t.view(np.uint8)).to(dev)
-        d_wire = torch.zeros(WIN * (FRAG + 22), dtype=torch.uint8, device=dev)
 
-        def window():
-            eng.tls_seal_records(iv, d_t.data_ptr(), WIN, d_src.data_ptr(), d_wire.data_ptr(), sh)
+def window_latency(ra, extra, dev):
+    """Latency side (not `value`): one rapido send window, 16 x 16 KiB records framed in one launch on the
+    window kernels, device-resident, back-to-back launches timed with HIP events."""
+    import numpy as np
+    import torch
+    WIN, FRAG = 16, 16384
+    eng, iv, stream = extra["eng"], extra["iv"], extra["stream"]
+    t = np.zeros(WIN, ra.TLS_RECORD_DTYPE)
+    t["src"] = np.arange(WIN, dtype=np.uint64) * FRAG
+    t["dst"] = np.arange(WIN, dtype=np.uint64) * (FRAG + 22)
+    t["seq"] = np.arange(WIN, dtype=np.uint64)
+    t["len"], t["type"] = FRAG, 23
+    d_t = torch.from_numpy(t.view(np.uint8)).to(dev)
+    d_wire = torch.zeros(WIN * (FRAG + 22), dtype=torch.uint8, device=dev)
 
-        for _ in range(5):
-            window()
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-        ev[0].record(stream)
-        for _ in range(100):
-            window()
-        ev[1].record(stream)
-        torch.cuda.synchronize(dev)
-        out["window_latency"] = {"us_per_window": round(ev[0].elapsed_time(ev[1]) * 10.0, 2),
-                                 "window": f"{WIN} x {FRAG} B TLS records sealed in one launch (rapido send window), "
-                                           f"AES-{8 * wl['key']}, device-resident, 100 back-to-back launches"}
+    def window():
+        eng.tls_seal_records(iv, d_t.data_ptr(), WIN, extra["d_src"].data_ptr(), d_wire.data_ptr(), stream.cuda_stream)
 
-    if (args.e2e or world == 1) and not args.no_e2e:
-        # PCIe-inclusive: records start and end in pinned host memory
-        h_src = torch.empty(src_bytes, dtype=torch.uint8, pin_memory=True)
-        h_dst = torch.empty(src_bytes, dtype=torch.uint8, pin_memory=True)
-        h_src.copy_(d_src.cpu())
-        torch.cuda.synchronize(dev)
-        reps = max(2, args.steps // 4)
-        t0 = time.perf_counter()
-        for _ in range(reps):  # serial: one H2D, the seal, one D2H
-            d_src.copy_(h_src, non_blocking=True)
-            eng.seal_batch(iv, d_recs.data_ptr(), n, d_src.data_ptr(), d_ct.data_ptr(), d_aad.data_ptr(), sh)
-            h_dst.copy_(d_ct, non_blocking=True)
-        torch.cuda.synchronize(dev)
-        serial = (time.perf_counter() - t0) / reps
-        # pipelined: the batch in chunks over 3 streams, so the H2D of chunk i+1 and the D2H of chunk i-1
-        # overlap the seal of chunk i (the copy engines run both directions at once)
-        nchunk = 16
-        bounds = np.linspace(0, n, nchunk + 1).astype(np.int64)
-        streams = [torch.cuda.Stream(dev) for _ in range(3)]
-        starts = recs["src"].astype(np.int64)
-        ends = starts + recs["len"].astype(np.int64) + 16
+    for _ in range(5):
+        window()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record(stream)
+    for _ in range(100):
+        window()
+    ev[1].record(stream)
+    torch.cuda.synchronize(dev)
+    return {"us_per_window": round(ev[0].elapsed_time(ev[1]) * 10.0, 2),
+            "kernel": ra.kernel_name(True, extra["key"], WIN, framing=True),
+            "window": f"{WIN} x {FRAG} B TLS records sealed in one launch (rapido send window), "
+                      f"AES-{8 * extra['key']}, device-resident, 100 back-to-back launches"}
 
-        def pipelined():
-            for c in range(nchunk):
-                r0, r1 = int(bounds[c]), int(bounds[c + 1])
-                a, b = int(starts[r0]), int(ends[r1 - 1])
-                st = streams[c % 3]
-                with torch.cuda.stream(st):
-                    d_src[a:b].copy_(h_src[a:b], non_blocking=True)
-                    eng.seal_batch(iv, d_recs.data_ptr() + r0 * DESC_BYTES, r1 - r0, d_src.data_ptr(), d_ct.data_ptr(),
-                                   d_aad.data_ptr(), st.cuda_stream)
-                    h_dst[a:b].copy_(d_ct[a:b], non_blocking=True)
 
+def e2e_pcie(ra, extra, dev, steps):
+    """PCIe-inclusive: records start and end in pinned host memory (never `value`)."""
+    import numpy as np
+    import torch
+    eng, iv, recs, n = extra["eng"], extra["iv"], extra["recs"], extra["n"]
+    d_src, d_ct, d_recs, d_aad = extra["d_src"], extra["d_ct"], extra["d_recs"], extra["d_aad"]
+    sh = extra["stream"].cuda_stream
+    h_src = torch.empty(extra["src_bytes"], dtype=torch.uint8, pin_memory=True)
+    h_dst = torch.empty(extra["src_bytes"], dtype=torch.uint8, pin_memory=True)
+    h_src.copy_(d_src.cpu())
+    torch.cuda.synchronize(dev)
+    reps = max(2, steps // 4)
+    t0 = time.perf_counter()
+    for _ in range(reps):  # serial: one H2D, the seal, one D2H
+        d_src.copy_(h_src, non_blocking=True)
+        eng.seal_batch(iv, d_recs.data_ptr(), n, d_src.data_ptr(), d_ct.data_ptr(), d_aad.data_ptr(), sh)
+        h_dst.copy_(d_ct, non_blocking=True)
+    torch.cuda.synchronize(dev)
+    serial = (time.perf_counter() - t0) / reps
+    # pipelined: the batch in chunks over 3 streams, so the H2D of chunk i+1 and the D2H of chunk i-1
+    # overlap the seal of chunk i (the copy engines run both directions at once)
+    nchunk = 16
+    bounds = np.linspace(0, n, nchunk + 1).astype(np.int64)
+    streams = [torch.cuda.Stream(dev) for _ in range(3)]
+    starts = recs["src"].astype(np.int64)
+    ends = starts + recs["len"].astype(np.int64) + 16
+
+    def pipelined():
+        for c in range(nchunk):
+            r0, r1 = int(bounds[c]), int(bounds[c + 1])
+            a, b = int(starts[r0]), int(ends[r1 - 1])
+            st = streams[c % 3]
+            with torch.cuda.stream(st):
+                d_src[a:b].copy_(h_src[a:b], non_blocking=True)
+                eng.seal_batch(iv, d_recs.data_ptr() + r0 * DESC_BYTES, r1 - r0, d_src.data_ptr(), d_ct.data_ptr(),
+                               d_aad.data_ptr(), st.cuda_stream)
+                h_dst[a:b].copy_(d_ct[a:b], non_blocking=True)
+
+    pipelined()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
         pipelined()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            pipelined()
-        torch.cuda.synchronize(dev)
-        piped = (time.perf_counter() - t0) / reps
-        # the pipelined output is the same ciphertext as the device-resident run
-        if not torch.equal(h_dst[: int(ends[-1])], d_ct[: int(ends[-1])].cpu()):
-            raise SystemExit("bench: pipelined PCIe seal differs from the device-resident seal -- results invalid")
-        out["e2e_pcie"] = {"seal_gibps_serial": round(payload / serial / GIB, 2),
-                           "seal_gibps_pipelined": round(payload / piped / GIB, 2),
-                           "note": "pinned host src -> H2D -> seal -> D2H -> pinned host dst; serial = one copy each way "
-                                   "around one launch; pipelined = 16 chunks over 3 streams"}
+    torch.cuda.synchronize(dev)
+    piped = (time.perf_counter() - t0) / reps
+    if not torch.equal(h_dst[: int(ends[-1])], d_ct[: int(ends[-1])].cpu()):
+        raise SystemExit("bench: pipelined PCIe seal differs from the device-resident seal -- results invalid")
+    return {"seal_gibps_serial": round(extra["payload"] / serial / GIB, 2),
+            "seal_gibps_pipelined": round(extra["payload"] / piped / GIB, 2),
+            "note": "pinned host src -> H2D -> seal -> D2H -> pinned host dst; serial = one copy each way "
+                    "around one launch; pipelined = 16 chunks over 3 streams"}
 
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="1400", choices=sorted(WORKLOADS))
+    ap.add_argument("--workloads", default=SIDE_WORKLOADS,
+                    help="comma-separated side workloads measured at N=1 after the main one")
+    ap.add_argument("--no-workloads", action="store_true", help="measure the main workload only")
+    ap.add_argument("--side-steps", type=int, default=10, help="timed steps of each side workload")
+    ap.add_argument("--lanes", type=int, default=0, help="lanes per record (1/2/4/8); 0 = engine default")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--e2e", action="store_true", help="time the PCIe-inclusive path (pinned host in/out); default at N=1")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive path")
+    ap.add_argument("--check", type=int, default=64, help="records re-checked against the CPU oracle after timing")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    wl = WORKLOADS[args.workload]
+
+    # the CPU baseline runs first: its worker processes start before this process touches the GPU
+    cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(wl, args.cpu_threads)
+        cpu = cpu_baseline(wl["key"], wl["length"] or 8224)
+
+    import torch
+    import torch.distributed as dist
+
+    import rapido_amd as ra
+
+    # rehearsal only (a 1-GPU box): RAPIDO_BENCH_SAME_DEVICE=1 puts every rank on cuda:0 and
+    # RAPIDO_BENCH_BACKEND=gloo replaces RCCL, which refuses two ranks on one GPU
+    dev_index = 0 if os.environ.get("RAPIDO_BENCH_SAME_DEVICE") == "1" else local_rank
+    if world > 1:
+        torch.cuda.set_device(dev_index)
+        backend = os.environ.get("RAPIDO_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", dev_index if world > 1 else 0)
+    torch.cuda.set_device(dev)
+    ra.require_gpu()
+    if args.lanes:
+        ra.set_lanes_per_record(args.lanes)
+
+    res, extra = measure(ra, args.workload, args, dev, rank, world, args.check)
+    out = {
+        "metric": METRIC,
+        "value": res["value"],
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": res["ms_per_step"],
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (device-generated random payload, TLS 1.3 record headers as AAD)",
+        "config": {"workload": wl["name"], "records_per_gpu": res["records_per_gpu"],
+                   "record_bytes": wl["length"] if wl["length"] else "U{64..16384}",
+                   "aad_bytes": 5, "key_bits": 8 * wl["key"], "lanes_per_record": ra.lib().ptls_mi355x_get_lanes_per_record(),
+                   "parallelism": f"records sharded per GPU x{world}, no collective"},
+        "seal_gibps": res["seal_gibps"],
+        "open_gibps": res["open_gibps"],
+        "roofline": res["roofline"],
+        "lds_roofline": res["lds_roofline"],
+    }
+    if world == 1 and not args.no_e2e:
+        out["window_latency"] = window_latency(ra, extra, dev)
+    if (args.e2e or world == 1) and not args.no_e2e:
+        out["e2e_pcie"] = e2e_pcie(ra, extra, dev, args.steps)
+    extra["eng"].close()
+    del extra
+    torch.cuda.empty_cache()
+
+    if world == 1 and not args.no_workloads:
+        side = {}
+        sargs = argparse.Namespace(**vars(args))
+        sargs.steps, sargs.warmup = args.side_steps, max(1, min(args.warmup, 2))
+        for w in [x for x in args.workloads.split(",") if x and x != args.workload]:
+            r, ex = measure(ra, w, sargs, dev, rank, world, min(args.check, 16))
+            r["config_key"] = w
+            side[w] = r
+            ex["eng"].close()
+            del ex
+            torch.cuda.empty_cache()
+        out["workloads"] = side
+
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(out), flush=True)
-    eng.close()
     if world > 1:
         dist.destroy_process_group()
 
