@@ -150,12 +150,13 @@ def lib() -> C.CDLL:
         L.ptls_mi355x_set_seg32_records.restype = sz
         L.ptls_mi355x_set_work_ticket_origin.restype = C.c_uint32
         L.ptls_mi355x_tls_open_records_multi.argtypes = [vp, vp, vp, vp, sz, vp, vp, vp, vp, vp]
-        L.ptls_mi355x_tls_open_records_ex.argtypes = [vp, vp, vp, vp, sz, vp, vp, vp, vp, C.c_int, vp]
-        L.ptls_mi355x_aes_new.argtypes = [vp, sz]
-        L.ptls_mi355x_aes_new.restype = vp
-        L.ptls_mi355x_aes_free.argtypes = [vp]
-        L.ptls_mi355x_aes_ecb.argtypes = [vp, C.c_int, vp, vp, sz]
-        L.ptls_mi355x_aes_ecb_batch.argtypes = [vp, C.c_int, vp, vp, sz, vp]
+        if hasattr(L, "ptls_mi355x_aes_new"):  # (absent from older builds used in A/B timing runs)
+            L.ptls_mi355x_tls_open_records_ex.argtypes = [vp, vp, vp, vp, sz, vp, vp, vp, vp, C.c_int, vp]
+            L.ptls_mi355x_aes_new.argtypes = [vp, sz]
+            L.ptls_mi355x_aes_new.restype = vp
+            L.ptls_mi355x_aes_free.argtypes = [vp]
+            L.ptls_mi355x_aes_ecb.argtypes = [vp, C.c_int, vp, vp, sz]
+            L.ptls_mi355x_aes_ecb_batch.argtypes = [vp, C.c_int, vp, vp, sz, vp]
         L.ptls_mi355x_tls_plan_send.argtypes = [sz, C.c_uint32, C.POINTER(u64), u64, u64, vp, sz, C.POINTER(sz)]
         L.ptls_mi355x_tls_plan_send.restype = sz
         L.ptls_mi355x_tls_parse_records.argtypes = [vp, sz, u64, C.POINTER(u64), u64, vp, sz, C.POINTER(sz),
