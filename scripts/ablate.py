@@ -39,7 +39,10 @@ VARIANTS = {
     "no_aes": ["-DGCM_ABLATE_AES=1"],
     "no_both": ["-DGCM_ABLATE_AES=1", "-DGCM_ABLATE_GHASH=1"],
     "fill16": ["-DGCM_WIN_FILL=16u"],
-    "w32t1024": ["-DMI355X_WIN32_THREADS=1024"],  # 32-position window kernels: 3 records per 1024-thread group  # window kernels: 16 vectors in flight per thread during the LDS fill
+    "w32t1024": ["-DMI355X_WIN32_THREADS=1024"],
+    # r02 experiments on the last AES round (last-round S-box lookups through the vector-memory path; two steps'
+    # last rounds bitsliced on the VALU; T1 moved to image B): scripts/experiments/r02_last_round_vmem_pair_t1b.patch
+    # holds the source, profiles/r02[c-e]_ablate_*.txt the measurements -- all slower, not in csrc/
 }
 if os.environ.get("ABLATE_VARIANTS"):
     VARIANTS = {k: v for k, v in VARIANTS.items() if k in os.environ["ABLATE_VARIANTS"].split(",")}

@@ -82,6 +82,63 @@ KERNEL(k_b3_2, OP_BITOP3_2)
 KERNEL(k_or3, OP_OR3)
 KERNEL(k_lshladd, OP_LSHLADD)
 
+
+/* explicit registers (clobbered), 8 chains v40..v47 and sources v48.., to see VGPR-bank effects (bank = reg % 4) */
+#define XR(NAME, BODY8)                                                                                                \
+    extern "C" __global__ __launch_bounds__(1024) void NAME(uint32_t iters, uint32_t *out, uint32_t sk)              \
+    {                                                                                                                  \
+        uint32_t r = 0;                                                                                                \
+        asm volatile("v_mov_b32 v40, %0\n v_mov_b32 v41, %0\n v_mov_b32 v42, %0\n v_mov_b32 v43, %0\n"                \
+                     "v_mov_b32 v44, %0\n v_mov_b32 v45, %0\n v_mov_b32 v46, %0\n v_mov_b32 v47, %0\n"                \
+                     "v_mov_b32 v48, %0\n v_mov_b32 v49, %0\n v_mov_b32 v50, %0\n v_mov_b32 v51, %0\n"                \
+                     "v_mov_b32 v52, %0\n v_mov_b32 v53, %0\n v_mov_b32 v54, %0\n v_mov_b32 v55, %0\n"                \
+                     :: "v"(threadIdx.x) : "v40","v41","v42","v43","v44","v45","v46","v47","v48","v49","v50","v51","v52","v53","v54","v55"); \
+        for (uint32_t it = 0; it < iters; ++it)                                                                        \
+            asm volatile(R64(BODY8) ::: "v40","v41","v42","v43","v44","v45","v46","v47","v48","v49","v50","v51","v52","v53","v54","v55"); \
+        asm volatile("v_mov_b32 %0, v40" : "=v"(r));                                                                  \
+        out[blockIdx.x * blockDim.x + threadIdx.x] = r;                                                                \
+    }
+/* chains v40..v47 (banks 0..3,0..3); sources chosen per variant */
+#define B3_DISTINCT "v_bitop3_b32 v40, v40, v49, v50 bitop3:0x96\n v_bitop3_b32 v41, v41, v50, v51 bitop3:0x96\n" \
+                    "v_bitop3_b32 v42, v42, v51, v48 bitop3:0x96\n v_bitop3_b32 v43, v43, v48, v49 bitop3:0x96\n" \
+                    "v_bitop3_b32 v44, v44, v49, v50 bitop3:0x96\n v_bitop3_b32 v45, v45, v50, v51 bitop3:0x96\n" \
+                    "v_bitop3_b32 v46, v46, v51, v48 bitop3:0x96\n v_bitop3_b32 v47, v47, v48, v49 bitop3:0x96\n"
+#define B3_SAMEBANK "v_bitop3_b32 v40, v40, v48, v52 bitop3:0x96\n v_bitop3_b32 v41, v41, v49, v53 bitop3:0x96\n" \
+                    "v_bitop3_b32 v42, v42, v50, v54 bitop3:0x96\n v_bitop3_b32 v43, v43, v51, v55 bitop3:0x96\n" \
+                    "v_bitop3_b32 v44, v44, v48, v52 bitop3:0x96\n v_bitop3_b32 v45, v45, v49, v53 bitop3:0x96\n" \
+                    "v_bitop3_b32 v46, v46, v50, v54 bitop3:0x96\n v_bitop3_b32 v47, v47, v51, v55 bitop3:0x96\n"
+#define B3_CONST    "v_bitop3_b32 v40, v40, v49, s0 bitop3:0x96\n v_bitop3_b32 v41, v41, v50, s0 bitop3:0x96\n" \
+                    "v_bitop3_b32 v42, v42, v51, s0 bitop3:0x96\n v_bitop3_b32 v43, v43, v48, s0 bitop3:0x96\n" \
+                    "v_bitop3_b32 v44, v44, v49, s0 bitop3:0x96\n v_bitop3_b32 v45, v45, v50, s0 bitop3:0x96\n" \
+                    "v_bitop3_b32 v46, v46, v51, s0 bitop3:0x96\n v_bitop3_b32 v47, v47, v48, s0 bitop3:0x96\n"
+#define B3_INL      "v_bitop3_b32 v40, v40, v49, 7 bitop3:0x96\n v_bitop3_b32 v41, v41, v50, 7 bitop3:0x96\n" \
+                    "v_bitop3_b32 v42, v42, v51, 7 bitop3:0x96\n v_bitop3_b32 v43, v43, v48, 7 bitop3:0x96\n" \
+                    "v_bitop3_b32 v44, v44, v49, 7 bitop3:0x96\n v_bitop3_b32 v45, v45, v50, 7 bitop3:0x96\n" \
+                    "v_bitop3_b32 v46, v46, v51, 7 bitop3:0x96\n v_bitop3_b32 v47, v47, v48, 7 bitop3:0x96\n"
+#define PERM_DISTINCT "v_perm_b32 v40, v40, v49, v50\n v_perm_b32 v41, v41, v50, v51\n" \
+                    "v_perm_b32 v42, v42, v51, v48\n v_perm_b32 v43, v43, v48, v49\n" \
+                    "v_perm_b32 v44, v44, v49, v50\n v_perm_b32 v45, v45, v50, v51\n" \
+                    "v_perm_b32 v46, v46, v51, v48\n v_perm_b32 v47, v47, v48, v49\n"
+#define XOR_SAMEBANK "v_xor_b32 v40, v40, v48\n v_xor_b32 v41, v41, v49\n v_xor_b32 v42, v42, v50\n v_xor_b32 v43, v43, v51\n" \
+                    "v_xor_b32 v44, v44, v48\n v_xor_b32 v45, v45, v49\n v_xor_b32 v46, v46, v50\n v_xor_b32 v47, v47, v51\n"
+#define XOR_SGPR    "v_xor_b32 v40, s0, v40\n v_xor_b32 v41, s0, v41\n v_xor_b32 v42, s0, v42\n v_xor_b32 v43, s0, v43\n" \
+                    "v_xor_b32 v44, s0, v44\n v_xor_b32 v45, s0, v45\n v_xor_b32 v46, s0, v46\n v_xor_b32 v47, s0, v47\n"
+#define AND_OR_DISTINCT "v_and_or_b32 v40, v40, v49, v50\n v_and_or_b32 v41, v41, v50, v51\n" \
+                    "v_and_or_b32 v42, v42, v51, v48\n v_and_or_b32 v43, v43, v48, v49\n" \
+                    "v_and_or_b32 v44, v44, v49, v50\n v_and_or_b32 v45, v45, v50, v51\n" \
+                    "v_and_or_b32 v46, v46, v51, v48\n v_and_or_b32 v47, v47, v48, v49\n"
+#define LSHR_ONLY   "v_lshrrev_b32 v40, 8, v49\n v_lshrrev_b32 v41, 8, v50\n v_lshrrev_b32 v42, 8, v51\n v_lshrrev_b32 v43, 8, v48\n" \
+                    "v_lshrrev_b32 v44, 8, v49\n v_lshrrev_b32 v45, 8, v50\n v_lshrrev_b32 v46, 8, v51\n v_lshrrev_b32 v47, 8, v48\n"
+XR(x_b3_distinct, B3_DISTINCT)
+XR(x_b3_samebank, B3_SAMEBANK)
+XR(x_b3_const, B3_CONST)
+XR(x_b3_inl, B3_INL)
+XR(x_perm_distinct, PERM_DISTINCT)
+XR(x_xor_samebank, XOR_SAMEBANK)
+XR(x_xor_sgpr, XOR_SGPR)
+XR(x_andor_distinct, AND_OR_DISTINCT)
+XR(x_lshr, LSHR_ONLY)
+
 typedef void (*kfn)(uint32_t, uint32_t *, uint32_t);
 struct Var {
     const char *name;
@@ -111,7 +168,16 @@ int main()
                         {"v_cndmask_b32 vcc", k_cnd},
                         {"v_mad_u32_u24 v,v,v", k_mad24},
                         {"v_lshrrev_b32 (VOP2)", k_lshr},
-                        {"v_xad_u32 v,v,v", k_xad}};
+                        {"v_xad_u32 v,v,v", k_xad},
+                        {"x: v_bitop3 3 distinct VGPR banks", x_b3_distinct},
+                        {"x: v_bitop3 3 VGPRs one bank", x_b3_samebank},
+                        {"x: v_bitop3 v,v,s0", x_b3_const},
+                        {"x: v_bitop3 v,v,inline const", x_b3_inl},
+                        {"x: v_perm 3 distinct VGPR banks", x_perm_distinct},
+                        {"x: v_xor_b32 2 VGPRs one bank", x_xor_samebank},
+                        {"x: v_xor_b32 s,v (VOP2 SGPR)", x_xor_sgpr},
+                        {"x: v_and_or_b32 3 distinct banks", x_andor_distinct},
+                        {"x: v_lshrrev_b32 (no dependency)", x_lshr}};
     int dev = 0, ncu = 0;
     hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     uint32_t *out = nullptr;

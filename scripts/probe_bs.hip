@@ -13,7 +13,7 @@
  */
 #include <hip/hip_runtime.h>
 #include "../rapido_amd/csrc/gcm_core.h"
-#include "../rapido_amd/csrc/gcm_bitslice.h"
+#include "gcm_bitslice.h"
 
 using namespace mi355x;
 

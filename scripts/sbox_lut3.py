@@ -1,6 +1,6 @@
 """Maps the Boyar-Peralta S-box circuit (scripts/sbox_circuit.py) onto 3-input LUTs (v_bitop3_b32):
 k = 3 cut enumeration + area-flow cover selection, then an exhaustive check of the mapped network.
-Prints the LUT count and, with --emit, the C++ body used by gcm_bitslice.h (sbox_bs).
+Prints the LUT count and, with --emit, the C++ body of sbox_bs (rapido_amd/csrc/gcm_sbox.h; two-input gates there are VOP2 ops).
 
 Truth-table convention: leaf 0 is the most significant bit of the table index (bitop3's src0).
 """

@@ -12,7 +12,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include "../../rapido_amd/csrc/gcm_core.h"
-#include "../../rapido_amd/csrc/gcm_bitslice.h"
+#include "../../scripts/gcm_bitslice.h"
 
 using namespace mi355x;
 
@@ -52,8 +52,8 @@ static void run(const KeyImage *ki, const uint8_t *lds, const uint8_t *static_iv
         uint32_t n1 = iv1 ^ bswap32((uint32_t)(r.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)r.seq);
         u32x4 tag = {0, 0, 0, 0};
         for (uint32_t j = 0; j < (uint32_t)K; ++j)
-            tag ^= lane_walk<NR, K, SEAL>(lds, 4u * (j & 31u) | 0x10000u, ki->rk, j, r, true, wk.T, iv0, n1, n2, src, dst, aad,
-                                          (const uint8_t *)recs);
+            tag ^= lane_walk<NR, K, SEAL>(lds, 4u * (j & 31u) | 0x10000u, ki->rk, j, r, true, wk.T, iv0, n1, n2, src, dst,
+                                          aad, (const uint8_t *)recs);
         if (SEAL) {
             memcpy(dst + r.dst + r.len, &tag, 16);
         } else {
@@ -474,3 +474,6 @@ extern "C" int model_aes_ecb(const uint8_t *key, size_t keylen, int is_enc, uint
     }
     return 0;
 }
+
+/* aes_last_round_bs2 on the host: two blocks' round-NR inputs a, b (LE words) -> outputs, with round key k */
+extern "C" void model_last_round_bs2(uint32_t *a, uint32_t *b, const uint32_t *k) { aes_last_round_bs2(a, b, k); }

@@ -436,3 +436,47 @@ def test_model_ecb_block_both_directions(model, keylen):
         assert model.model_aes_ecb(key, keylen, 0, buf, 37) == 0
         assert buf.raw[:len(data)] == data
         assert oracle.ecb_blocks(key, enc, False) == data
+
+
+def test_bitsliced_last_round_matches_sbox(model):
+    """aes_last_round_bs2 (gcm_sbox.h: 8x8 bit transposes + the S-box circuit, two blocks per lane) equals
+    SubBytes + ShiftRows + AddRoundKey computed byte by byte, on random states and keys."""
+    sbox = [oracle.ecb(bytes(16), bytes(16))]  # warm the oracle build
+    model.model_last_round_bs2.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    rng = np.random.default_rng(21)
+    # the S-box from the FIPS-197 definition: SubBytes(x) is the first byte of a one-round AES with zero keys
+    # would need internals; use the table of the kernel model's own T0 (byte 1 of T0[x] = S[x]) via the oracle
+    S = np.zeros(256, np.uint8)
+    inv = np.zeros(256, np.uint8)
+    for x in range(256):  # multiplicative inverse in GF(2^8), then the affine map (FIPS-197 5.1.1)
+        if x:
+            for y in range(1, 256):
+                a, b, p = x, y, 0
+                while b:
+                    if b & 1:
+                        p ^= a
+                    a = ((a << 1) ^ (0x1B if a & 0x80 else 0)) & 0xFF
+                    b >>= 1
+                if p == 1:
+                    inv[x] = y
+                    break
+        v = int(inv[x])
+        r = v
+        for k in range(1, 5):
+            r ^= ((v << k) | (v >> (8 - k))) & 0xFF
+        S[x] = r ^ 0x63
+    for _ in range(200):
+        a = rng.integers(0, 2 ** 32, 4, dtype=np.uint64).astype(np.uint32)
+        b = rng.integers(0, 2 ** 32, 4, dtype=np.uint64).astype(np.uint32)
+        k = rng.integers(0, 2 ** 32, 4, dtype=np.uint64).astype(np.uint32)
+        want = []
+        for st in (a, b):
+            by = st.view(np.uint8)  # byte r of column c at 4c + r
+            out = np.zeros(16, np.uint8)
+            for c in range(4):
+                for r in range(4):
+                    out[4 * c + r] = S[by[4 * ((c + r) & 3) + r]]
+            want.append(out.view(np.uint32) ^ k)
+        ga, gb = a.copy(), b.copy()
+        model.model_last_round_bs2(ga.ctypes.data, gb.ctypes.data, k.ctypes.data)
+        assert (ga == want[0]).all() and (gb == want[1]).all()
