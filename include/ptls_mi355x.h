@@ -312,6 +312,22 @@ size_t ptls_mi355x_set_slot_zero_copy_bytes(size_t n);
  */
 size_t ptls_mi355x_set_seg32_records(size_t n);
 /*
+ * Window batches of at most n records use the 16-lane single-record kernels instead: 32-position segments
+ * walked by 16 lanes in 2 steps, one record per 576-thread workgroup -- the latency
+ * kernels of a rapido send window.  Takes precedence over ptls_mi355x_set_seg32_records.
+ * SIZE_MAX (the default) means the device's CU count, 0 disables.  Returns the previous value.  Results are
+ * identical.
+ */
+size_t ptls_mi355x_set_win16_records(size_t n);
+/*
+ * Window batches of at most n records use the split kernels: every record's segments are cut into runs of 16, each
+ * walked by its own 256-thread workgroup on its own CU (3 per TLS record), the runs' partial GHASH sums joined by the
+ * last to arrive.  The lowest-latency family for a few records (a rapido send window).  Takes precedence over
+ * ptls_mi355x_set_win16_records.  SIZE_MAX (the default) means a third of the device's CU count, 0 disables.
+ * Returns the previous value.  Results are identical.
+ */
+size_t ptls_mi355x_set_split_records(size_t n);
+/*
  * Diagnostics: the batch kernels' work counters are never reset (each launch starts where the previous one
  * on its slot ended, modulo 2^32).  Contexts created after this call start their counters at `origin`
  * instead of 0, so a test can place the 2^32 wrap inside its first launches.  Returns the previous value.

@@ -61,7 +61,8 @@ EXPORTED_FUNCTIONS = (
     "ptls_mi355x_set_aead_window_records", "ptls_mi355x_set_slot_zero_copy_bytes",
     "ptls_mi355x_set_work_ticket_origin", "ptls_mi355x_set_seg32_records", "ptls_mi355x_tls_plan_send",
     "ptls_mi355x_tls_parse_records", "ptls_mi355x_tls_open_records_ex", "ptls_mi355x_aes_new", "ptls_mi355x_aes_free",
-    "ptls_mi355x_aes_ecb", "ptls_mi355x_aes_ecb_batch",
+    "ptls_mi355x_aes_ecb", "ptls_mi355x_aes_ecb_batch", "ptls_mi355x_set_win16_records",
+    "ptls_mi355x_set_split_records",
 )
 EXPORTED_OBJECTS = ("ptls_mi355x_aes128gcm", "ptls_mi355x_aes256gcm", "ptls_mi355x_aes128ctr",
                     "ptls_mi355x_aes256ctr", "ptls_mi355x_aes128ecb", "ptls_mi355x_aes256ecb")
@@ -150,6 +151,10 @@ def lib() -> C.CDLL:
         L.ptls_mi355x_set_seg32_records.restype = sz
         L.ptls_mi355x_set_work_ticket_origin.restype = C.c_uint32
         L.ptls_mi355x_tls_open_records_multi.argtypes = [vp, vp, vp, vp, sz, vp, vp, vp, vp, vp]
+        for name in ("ptls_mi355x_set_win16_records", "ptls_mi355x_set_split_records"):
+            if hasattr(L, name):  # (absent from older builds used in A/B timing runs)
+                getattr(L, name).argtypes = [sz]
+                getattr(L, name).restype = sz
         if hasattr(L, "ptls_mi355x_aes_new"):  # (absent from older builds used in A/B timing runs)
             L.ptls_mi355x_tls_open_records_ex.argtypes = [vp, vp, vp, vp, sz, vp, vp, vp, vp, C.c_int, vp]
             L.ptls_mi355x_aes_new.argtypes = [vp, sz]
@@ -480,6 +485,24 @@ SEG32_AUTO = (1 << 64) - 1  # SIZE_MAX: the device's CU count
 def set_seg32_records(n: int) -> int:
     """Window batches of at most n records use 32-position segments (0: never; SEG32_AUTO: one per CU)."""
     return lib().ptls_mi355x_set_seg32_records(n)
+
+
+def set_win16_records(n: int) -> int:
+    """Window batches of at most n records use the 16-lane single-record kernels (0: never; SEG32_AUTO: one per
+    CU); they take precedence over set_seg32_records."""
+    L = lib()
+    if not hasattr(L, "ptls_mi355x_set_win16_records"):
+        return 0
+    return L.ptls_mi355x_set_win16_records(n)
+
+
+def set_split_records(n: int) -> int:
+    """Window batches of at most n records use the split kernels (runs of 16 segments on separate CUs; 0: never;
+    SEG32_AUTO: a third of the CUs); they take precedence over set_win16_records."""
+    L = lib()
+    if not hasattr(L, "ptls_mi355x_set_split_records"):
+        return 0
+    return L.ptls_mi355x_set_split_records(n)
 
 
 def set_work_ticket_origin(origin: int) -> int:

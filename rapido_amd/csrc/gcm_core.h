@@ -61,6 +61,10 @@
 #define GCM_ABLATE_AES 0
 #endif
 
+#ifndef GCM_WALK_STAMP
+#define GCM_WALK_STAMP(i) ((void)0) /* timestamps inside lane_walk (measurement builds only, gcm_engine.hip) */
+#endif
+
 namespace mi355x {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -100,6 +104,7 @@ struct Layout {
     static constexpr uint32_t gh_base = aes_base + aes_bytes; /* nibble tables: slot s = H^(n_nibble - s) */
     static constexpr uint32_t n_nibble = gh5 ? 2u : (uint32_t)K;
     static constexpr uint32_t total = gh_base + n_nibble * GH_TABLE_BYTES;
+    static constexpr bool split_scale = false; /* lane scaling by one table H^(K - slot) (lane_walk) */
     static_assert(total <= 160u * 1024u, "LDS budget");
 };
 
@@ -834,6 +839,58 @@ GCM_HD u32x4 ghash_mul_lds_wide(const uint8_t *lds, uint32_t basereg, u32x4 x)
     return r;
 }
 
+/* ghash_mul_lds_wide in two halves of 16 reads (64 VGPRs in flight): kernels at three waves per SIMD */
+GCM_HD u32x4 ghash_mul_lds_half(const uint8_t *lds, uint32_t basereg, u32x4 x)
+{
+    u32x4 r = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        u32x4 e[16];
+#pragma unroll
+        for (int d = 2 * h; d < 2 * h + 2; ++d) {
+            const uint32_t lo = (x[d] << 4) & 0xf0f0f0f0u, hi = x[d] & 0xf0f0f0f0u;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const uint32_t sel = 0x0c020100u | (4u + (uint32_t)m);
+                e[8 * (d - 2 * h) + 2 * m] = lds_u32x4(lds, perm(lo, basereg, sel) + (uint32_t)(8 * d + 2 * m) * 256u);
+                e[8 * (d - 2 * h) + 2 * m + 1] =
+                    lds_u32x4(lds, perm(hi, basereg, sel) + (uint32_t)(8 * d + 2 * m + 1) * 256u);
+            }
+        }
+        GCM_SCHED_FENCE();
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) {
+            r[0] = xor3(r[0], e[i][0], e[i + 1][0]);
+            r[1] = xor3(r[1], e[i][1], e[i + 1][1]);
+            r[2] = xor3(r[2], e[i][2], e[i + 1][2]);
+            r[3] = xor3(r[3], e[i][3], e[i + 1][3]);
+        }
+    }
+    return r;
+}
+
+/* the window join's multiply: W = 2 all 32 reads in flight, 1 two halves of 16, 0 compiler-scheduled */
+template <int W>
+GCM_HD u32x4 ghash_mul_join(const uint8_t *lds, uint32_t basereg, u32x4 x)
+{
+    if constexpr (W == 2)
+        return ghash_mul_lds_wide(lds, basereg, x);
+    else if constexpr (W == 1)
+        return ghash_mul_lds_half(lds, basereg, x);
+    else
+        return ghash_mul_lds(lds, basereg, x);
+}
+
+/* the closing lane scaling of split_scale layouts: all 32 reads in flight when the kernel has the registers */
+template <bool WIDE>
+GCM_HD u32x4 ghash_mul_scale(const uint8_t *lds, uint32_t basereg, u32x4 x)
+{
+    if constexpr (WIDE)
+        return ghash_mul_lds_wide(lds, basereg, x);
+    else
+        return ghash_mul_lds(lds, basereg, x);
+}
+
 /* --------------------------------------------------------- GF(2^128) on byte strings ---- */
 
 /* SP 800-38D Algorithm 1 on stream-order bytes (used only by the key setup). */
@@ -889,12 +946,22 @@ struct KeyImage {
     uint32_t key_size;  /* 16 or 32 */
     uint32_t pad_[2];
     uint8_t H[16];      /* E_K(0^128) */
+    /*
+     * gh .. gh256 are contiguous, in this order: the 16-lane latency kernels copy them into LDS as one 96 KiB block
+     * behind the AES image (LayoutWin16).
+     */
     uint8_t gh[MAX_K][32][16][16]; /* gh[p-1] = nibble tables of H^p, p = 1..MAX_K */
-    uint8_t gh64[32][16][16];      /* nibble tables of H^64: joins the 64-position segments of the window kernels */
-    uint8_t gh256[32][16][16];     /* nibble tables of H^256: joins groups of 4 segments (window_join) */
-    uint8_t gh32[32][16][16];      /* H^32 and H^128: the same joins for the 32-position segments of the */
+    uint8_t gh16[32][16][16];      /* H^16: the Horner factor of 16 lanes per segment (LayoutWin16) */
+    uint8_t gh32[32][16][16];      /* H^32 and H^128: the joins of the 32-position segments of the */
     uint8_t gh128[32][16][16];     /* single-record latency kernels (window_body SEG = 32) */
+    uint8_t gh256[32][16][16];     /* nibble tables of H^256: joins groups of 4 segments (window_join) */
+    uint8_t gh64[32][16][16];      /* nibble tables of H^64: joins the 64-position segments of the window kernels */
+    uint8_t gh512[32][16][16];     /* H^512 and H^1024: scale a run of 16 segments to the record's end (the */
+    uint8_t gh1024[32][16][16];    /* split window kernels, LayoutSplit) */
 };
+static_assert(offsetof(KeyImage, gh16) == offsetof(KeyImage, gh) + MAX_K * 8192 &&
+                  offsetof(KeyImage, gh256) == offsetof(KeyImage, gh16) + 3 * 8192 && offsetof(KeyImage, gh) % 16 == 0,
+              "LayoutWin16 / LayoutSplit copy gh .. gh256 (gh128) as one block");
 
 /* ------------------------------------------------------------------ record walk ----------- */
 
@@ -1207,16 +1274,23 @@ GCM_HD Gf128 gf_mul_lane_share(Gf128 X, Gf128 Y, uint32_t lane)
     return acc;
 }
 
-/* The 13 multipliers of the key image, in KeyImage table order: H^1..H^8, H^64, H^256, H^32, H^128. */
-enum : uint32_t { KEY_IMAGE_TABLES = MAX_K + 4 };
+/* The 15 multipliers of the key image, by index s: H^1..H^8, then H^64, H^256, H^32, H^128, H^16, H^512, H^1024. */
+enum : uint32_t { KEY_IMAGE_TABLES = MAX_K + 7 };
 
 GCM_HD uint8_t (*key_image_table(KeyImage *ki, uint32_t s))[16][16]
 {
-    return s < (uint32_t)MAX_K ? ki->gh[s] : s == (uint32_t)MAX_K ? ki->gh64 : s == MAX_K + 1u ? ki->gh256 : s == MAX_K + 2u ? ki->gh32 : ki->gh128;
+    return s < (uint32_t)MAX_K      ? ki->gh[s]
+           : s == (uint32_t)MAX_K   ? ki->gh64
+           : s == MAX_K + 1u        ? ki->gh256
+           : s == MAX_K + 2u        ? ki->gh32
+           : s == MAX_K + 3u        ? ki->gh128
+           : s == MAX_K + 4u        ? ki->gh16
+           : s == MAX_K + 5u        ? ki->gh512
+                                    : ki->gh1024;
 }
 
 /*
- * Entry i of the 13 x 32 x 16 nibble-table entries: table s = i / 512, nibble t, value v; the XOR of the
+ * Entry i of the KEY_IMAGE_TABLES x 32 x 16 nibble-table entries: table s = i / 512, nibble t, value v; the XOR of the
  * single-bit products bits[s][k] = P_s x^k of v's set bits (bit b of nibble t is GCM bit nibble_bit_index(t, b)),
  * stored as its 16 stream bytes in LE dwords.
  */
@@ -1276,9 +1350,10 @@ GCM_HD int build_key_image(const uint8_t *sbox, const uint8_t *key, uint32_t key
             gf128_mul_bytes(hp, ki->H, hp);
         nibble_tables(hp, ki->gh[p - 1]);
     }
-    /* H^32 = ((H^8)^2)^2, H^64 = (H^32)^2, H^128 = (H^64)^2, H^256 = (H^128)^2 */
-    for (int sq = 0; sq < 2; ++sq)
-        gf128_mul_bytes(hp, hp, hp);
+    /* H^16 = (H^8)^2, H^32 = (H^16)^2, ... H^1024 = (H^512)^2 */
+    gf128_mul_bytes(hp, hp, hp);
+    nibble_tables(hp, ki->gh16);
+    gf128_mul_bytes(hp, hp, hp);
     nibble_tables(hp, ki->gh32);
     gf128_mul_bytes(hp, hp, hp);
     nibble_tables(hp, ki->gh64);
@@ -1286,6 +1361,10 @@ GCM_HD int build_key_image(const uint8_t *sbox, const uint8_t *key, uint32_t key
     nibble_tables(hp, ki->gh128);
     gf128_mul_bytes(hp, hp, hp);
     nibble_tables(hp, ki->gh256);
+    gf128_mul_bytes(hp, hp, hp);
+    nibble_tables(hp, ki->gh512);
+    gf128_mul_bytes(hp, hp, hp);
+    nibble_tables(hp, ki->gh1024);
     return 0;
 }
 
@@ -1362,6 +1441,35 @@ struct LayoutWin {
     static constexpr uint32_t gh256 = gh64 + GH_TABLE_BYTES;
     static constexpr uint32_t ghpair = gh256 + GH_TABLE_BYTES;
     static constexpr uint32_t parts = ghpair + (SEG == 32 ? GH_TABLE_BYTES : 0u);
+    static constexpr bool split_scale = false;
+    static constexpr bool parts_alias = false; /* the segment sums have their own LDS (after the tables) */
+};
+
+/*
+ * LDS map of the 16-lane single-record latency kernels (window_body KW = 16, SEG = 32: two steps per segment).
+ * 160 KiB, filled in one pass as two copies: the two-table AES image (the same rows as LayoutWin, kept once per
+ * device) and the key image's contiguous tables H^1..H^8, H^16, H^32, H^128, H^256.
+ *   [0, 64K)       AES image T0 | T1
+ *   [64K, 128K)    H^e at 64K + 8K (e - 1), e = 1..8 (lane scaling)
+ *   [128K, 136K)   H^16: the Horner factor (gh_base)
+ *   [136K, 160K)   H^32 (groups of 4 segments), H^128 (pairs of groups), H^256 (the chain of pairs)
+ * A lane's scaling H^e, e in 1..16, is one multiply for e <= 8 or e = 16, else H^8 then H^(e - 8) (split_scale).
+ * The segment sums alias the scaling tables: they are written after a barrier that ends every walk.
+ */
+struct LayoutWin16 {
+    static constexpr bool four_tables = false;
+    static constexpr bool gh5 = false;
+    static constexpr uint32_t aes_base = 0u;
+    static constexpr uint32_t gh_pow1 = 0x10000u; /* H^1; H^e at gh_pow1 + (e - 1) GH_TABLE_BYTES */
+    static constexpr uint32_t gh_base = 0x20000u; /* H^16 */
+    static constexpr uint32_t gh64 = 0x22000u;    /* window_body's within-group join table: H^32 */
+    static constexpr uint32_t gh256 = 0x24000u;   /* pairs of groups: H^128 */
+    static constexpr uint32_t ghpair = 0x26000u;  /* the chain of pairs: H^256 */
+    static constexpr uint32_t parts = 0x10000u;
+    static constexpr uint32_t bytes = 0x28000u;
+    static constexpr bool split_scale = true;
+    static constexpr bool wide_scale = false; /* 3 waves per SIMD: no registers for 32 reads in flight */
+    static constexpr bool parts_alias = true;
 };
 enum : uint32_t {
     WIN_SEG = 64,    /* GHASH positions per segment: 4 lanes x 16 steps */
@@ -1408,6 +1516,59 @@ GCM_HD void fill_lds_window(uint8_t *lds, const uint32_t *t0, const KeyImage *ki
             if (base + k * nthr < total)
                 *(u32x4 *)(lds + 16u * (base + k * nthr)) = v[k];
     }
+}
+
+/*
+ * LDS map of the split window kernels (gcm_engine.hip split_body): a record's 32-position segments are cut into runs
+ * of 16, each run walked by its own 256-thread workgroup (16 lanes per segment, 2 steps) on its own CU.  As
+ * LayoutWin16 up to 152K; the last table scales the run's sum to the record's end, H^(512 m) for the m runs after it.
+ *   [0, 64K) AES image; [64K, 128K) H^1..H^8; [128K) H^16 (Horner); [136K) H^32 (groups of 4 segments);
+ *   [144K) H^128 (the chain of groups); [152K) H^512 or H^1024 (gh_run)
+ */
+struct LayoutSplit {
+    static constexpr bool four_tables = false;
+    static constexpr bool gh5 = false;
+    static constexpr uint32_t aes_base = 0u;
+    static constexpr uint32_t gh_pow1 = 0x10000u;
+    static constexpr uint32_t gh_base = 0x20000u;  /* H^16 */
+    static constexpr uint32_t gh_group = 0x22000u; /* H^32 */
+    static constexpr uint32_t gh_chain = 0x24000u; /* H^128 */
+    static constexpr uint32_t gh_run = 0x26000u;   /* H^(512 m) */
+    static constexpr uint32_t parts = 0x10000u;    /* segment sums, after the walk (aliases H^1) */
+    static constexpr uint32_t bytes = 0x28000u;
+    static constexpr bool split_scale = true;
+    static constexpr bool wide_scale = true; /* one wave per SIMD: registers for 32 reads in flight */
+    static constexpr bool parts_alias = true;
+};
+enum : uint32_t {
+    SPLIT_RUNSEG = 16,  /* segments per run (one workgroup) */
+    SPLIT_MAXRUN = 3,   /* runs of a TLS record (33 segments); larger records are walked whole by run 0 */
+    SPLIT_THREADS = 256,
+};
+
+/* vector v of the LayoutSplit image for a run followed by m (0..2) runs: AES rows, gh[0] .. gh128, H^(512 m) */
+GCM_HD u32x4 split_image_vec(const uint32_t *t0, const KeyImage *ki, uint32_t v, uint32_t m)
+{
+    if (v < 0x10000u / 16u)
+        return window_image_vec(t0, ki, v, 8u, 32u);
+    if (v < LayoutSplit::gh_run / 16u)
+        return ((const u32x4 *)ki->gh)[v - 0x10000u / 16u];
+    return ((const u32x4 *)(m == 2u ? ki->gh1024 : ki->gh512))[v - LayoutSplit::gh_run / 16u];
+}
+
+/* vector v (16 B) of the LayoutWin16 image: the AES rows of window_image_vec, then the key image from gh[0] on */
+GCM_HD u32x4 win16_image_vec(const uint32_t *t0, const KeyImage *ki, uint32_t v)
+{
+    if (v < 0x10000u / 16u)
+        return window_image_vec(t0, ki, v, 8u, 32u);
+    return ((const u32x4 *)ki->gh)[v - 0x10000u / 16u];
+}
+
+/* the whole LayoutWin16 image, split over nthr threads (the host model; the kernels copy it, window_body) */
+GCM_HD void fill_lds_win16(uint8_t *lds, const uint32_t *t0, const KeyImage *ki, uint32_t tid, uint32_t nthr)
+{
+    for (uint32_t v = tid; v < LayoutWin16::bytes / 16u; v += nthr)
+        *(u32x4 *)(lds + 16u * v) = win16_image_vec(t0, ki, v);
 }
 
 /*
@@ -1539,6 +1700,36 @@ GCM_HD u32x4 shr_bytes(u32x4 v, uint32_t n)
 }
 
 /*
+ * Address of lane j's 16-byte load in step t of walk wk (lane_walk): the AAD or payload block at the lane's grid
+ * position, the received tag for the length block of an open, or `dummy` (steps with nothing to read).  A partial
+ * last AAD block is read as the AAD's last 16 bytes, a sealed partial payload block as the payload's last 16.
+ * in = src + rec.src, ad = aad + rec.aad, plen the GCM payload length.
+ */
+template <int K, bool SEAL, bool FRAME>
+GCM_HD const uint8_t *walk_fetch_ptr(uint32_t t, uint32_t j, const Walk &wk, const Record &rec, bool valid, uint32_t plen,
+                                     const uint8_t *in, const uint8_t *ad, const uint8_t *dummy)
+{
+    if (!valid || t >= wk.T)
+        return dummy;
+    const int32_t p = (int32_t)(j + K * t) - (int32_t)wk.pad;
+    if (p < 0)
+        return dummy;
+    if ((uint32_t)p < wk.A) {
+        if (FRAME)
+            return dummy;
+        if (16u * (uint32_t)p + 16u <= rec.aadlen)
+            return ad + 16u * (uint32_t)p;
+        return rec.aadlen >= 16u ? ad + rec.aadlen - 16u : dummy;
+    }
+    const uint32_t c = (uint32_t)p - wk.A;
+    if (c >= wk.C) /* the length block; open fetches the received tag into its slot */
+        return !SEAL && c == wk.C ? in + plen : dummy;
+    if (!SEAL || 16u * c + 16u <= rec.len)
+        return in + 16u * c;
+    return rec.len >= 16u ? in + rec.len - 16u : dummy;
+}
+
+/*
  * One lane's share of one record (see struct Walk).  Returns the lane's partial GHASH already
  * scaled by H^(K-j); the lane holding the length block has E_K(J0) folded in, so the XOR of the
  * K returned values is the tag (seal), or the tag XOR the received tag (open: the length
@@ -1562,11 +1753,12 @@ GCM_HD u32x4 shr_bytes(u32x4 v, uint32_t n)
  * LY: the LDS layout (T-table image count and GHASH table base).
  */
 template <int NR, int K, bool SEAL, bool FRAME = false, class LY = Layout<K>, int PF = 1>
-GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk, uint32_t j, const Record &rec, bool valid,
-                       uint32_t Tmax, uint32_t iv0, uint32_t iv1, uint32_t iv2, const uint8_t *src, uint8_t *dst,
-                       const uint8_t *aad, const uint8_t *dummy, uint32_t ctype = 0u, const Walk *seg = nullptr,
-                       uint32_t t0 = 0u)
+GCM_HD u32x4 lane_walk_seg(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk, uint32_t j, const Record &rec,
+                           bool valid, uint32_t Tmax, uint32_t iv0, uint32_t iv1, uint32_t iv2, const uint8_t *src,
+                           uint8_t *dst, const uint8_t *aad, const uint8_t *dummy, uint32_t ctype, bool use_seg,
+                           Walk segw, uint32_t t0)
 {
+    /* use_seg: walk the segment segw (window kernels); otherwise the whole record (make_walk) */
     /*
      * FRAME (TLS 1.3 record framing, lib/picotls.c:621-684 and :4779-4791): the AAD is the 5-byte
      * record header 17 03 03 BE16(plen + 16), built here in registers (build_aad), never read;
@@ -1575,15 +1767,15 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
      */
     const uint32_t plen = FRAME && SEAL ? rec.len + 1u : rec.len;
     const uint32_t aadlen = FRAME ? 5u : rec.aadlen;
-    const Walk wk = seg != nullptr ? *seg : make_walk(plen, aadlen, K, walk_out16(dst + rec.dst));
-    const uint32_t end_cap = seg != nullptr ? (uint32_t)K * seg->T : 0xffffffffu;
+    const Walk wk = use_seg ? segw : make_walk(plen, aadlen, K, walk_out16(dst + rec.dst));
+    const uint32_t end_cap = use_seg ? (uint32_t)K * segw.T : 0xffffffffu;
     const uint32_t gend = wk.A + wk.C + 1u; /* positions p >= gend are trailing pads */
     const uint8_t *in = src + rec.src;
     uint8_t *out = dst + rec.dst;
     const uint8_t *ad = aad + rec.aad;
     const uint32_t arem = rec.aadlen & 15u;
     u32x4 acc = {0u, 0u, 0u, 0u}, ek0 = {0u, 0u, 0u, 0u};
-    if (seg == nullptr && valid) {
+    if (!use_seg && valid) {
         /* hoisted AAD (make_walk): an AAD block at lane j's position before step 0 seeds its chain */
         const int32_t pv = (int32_t)j - (int32_t)K - (int32_t)wk.pad; /* record position of grid slot j - K */
         if (pv >= 0 && (uint32_t)pv < wk.A) {
@@ -1612,31 +1804,13 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
 #endif
 
     /*
-     * Address of the 16-byte load of step t.  The load is issued unconditionally (steps with
-     * nothing to read load 16 harmless bytes at `dummy`): with a load in every step the
-     * compiler can wait with vmcnt(1) for the current block while the next one is in flight,
-     * instead of vmcnt(0).
+     * Address of the 16-byte load of step t (walk_fetch_ptr).  The load is issued unconditionally (steps with
+     * nothing to read load 16 harmless bytes at `dummy`): with a load in every step the compiler can wait with
+     * vmcnt(1) for the current block while the next one is in flight, instead of vmcnt(0).
      */
     auto fetch_ptr = [&](uint32_t t) -> const uint8_t * {
         GCM_OPAQUE(t); /* recompute from t: no strength-reduced induction variables (VGPRs) */
-        if (!valid || t >= wk.T)
-            return dummy;
-        const int32_t p = (int32_t)(j + K * t) - (int32_t)wk.pad;
-        if (p < 0)
-            return dummy;
-        if ((uint32_t)p < wk.A) { /* a partial last AAD block is read as the AAD's last 16 bytes */
-            if (FRAME)
-                return dummy;
-            if (16u * (uint32_t)p + 16u <= rec.aadlen)
-                return ad + 16u * (uint32_t)p;
-            return rec.aadlen >= 16u ? ad + rec.aadlen - 16u : dummy;
-        }
-        const uint32_t c = (uint32_t)p - wk.A;
-        if (c >= wk.C) /* the length block; open fetches the received tag into its slot */
-            return !SEAL && c == wk.C ? in + plen : dummy;
-        if (!SEAL || 16u * c + 16u <= rec.len)
-            return in + 16u * c;
-        return rec.len >= 16u ? in + rec.len - 16u : dummy;
+        return walk_fetch_ptr<K, SEAL, FRAME>(t, j, wk, rec, valid, plen, in, ad, dummy);
     };
 
     /*
@@ -1723,7 +1897,7 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
                 const uint32_t reclen = plen + 16u;
                 X[0] = 0x00030317u | ((reclen >> 8) & 0xffu) << 24;
                 X[1] = reclen & 0xffu;
-            } else if (seg != nullptr && rec.aadlen < 16u) {
+            } else if (use_seg && rec.aadlen < 16u) {
                 X = load_partial(ad, rec.aadlen); /* segment walks: the short AAD may sit in any step */
             } else {
                 X = 16u * (uint32_t)p + 16u <= rec.aadlen || rec.aadlen < 16u ? cur : shr_bytes(cur, 16u - arem);
@@ -1753,8 +1927,9 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
      * t0 (even, segment walks): the first step with a real position in any lane of the wave.  Steps before
      * it hold only front padding, and a Horner chain stays 0 through leading zero blocks.
      */
+    GCM_WALK_STAMP(8);
     u32x4 bufA;
-    if (!FRAME && seg == nullptr && valid && rec.aadlen != 0u && rec.aadlen < 16u && j == wk.pad)
+    if (!FRAME && !use_seg && valid && rec.aadlen != 0u && rec.aadlen < 16u && j == wk.pad)
         bufA = load_partial(ad, rec.aadlen);
     else
         bufA = *(const u32x4_u *)fetch_ptr(t0);
@@ -1780,12 +1955,16 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
     } else {
         for (uint32_t t = t0; t < Tmax; t += 2u) {
             const u32x4 bufB = *(const u32x4_u *)fetch_ptr(t + 1u);
+            GCM_WALK_STAMP(9);
             step(t, bufA);
+            GCM_WALK_STAMP(10);
             bufA = *(const u32x4_u *)fetch_ptr(t + 2u);
             if (t + 1u < Tmax)
                 step(t + 1u, bufB);
+            GCM_WALK_STAMP(11);
         }
     }
+    GCM_WALK_STAMP(12);
     /* scale the chain by H^(pad + g - q_last(j)) (make_walk) */
     if (LY::gh5) {
         /* H^e, e = 4 - slot in 1..4, from the nibble tables of H^2 (slot 0) and H^1 (slot 1) */
@@ -1794,10 +1973,30 @@ GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk,
         const u32x4 y = ghash_mul_lds(lds, LY::gh_base + (e == 4u ? 0u : GH_TABLE_BYTES), acc);
         if (e >= 3u)
             acc = y;
+    } else if constexpr (LY::split_scale) {
+        /* H^e, e = K - slot in 1..16: H^16 (gh_base) or H^e directly, else H^8 then H^(e - 8) (LayoutWin16) */
+        uint32_t e = (uint32_t)K - walk_scale_slot(wk, j, K, end_cap);
+        if (e > 8u && e < 16u) {
+            acc = ghash_mul_scale<LY::wide_scale>(lds, LY::gh_pow1 + 7u * GH_TABLE_BYTES, acc);
+            e -= 8u;
+        }
+        acc = ghash_mul_scale<LY::wide_scale>(lds, e == 16u ? LY::gh_base : LY::gh_pow1 + (e - 1u) * GH_TABLE_BYTES, acc);
     } else {
         acc = ghash_mul_lds(lds, LY::gh_base + walk_scale_slot(wk, j, K, end_cap) * GH_TABLE_BYTES, acc);
     }
+    GCM_WALK_STAMP(13);
     return acc ^ ek0;
+}
+
+template <int NR, int K, bool SEAL, bool FRAME = false, class LY = Layout<K>, int PF = 1>
+GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk, uint32_t j, const Record &rec, bool valid,
+                       uint32_t Tmax, uint32_t iv0, uint32_t iv1, uint32_t iv2, const uint8_t *src, uint8_t *dst,
+                       const uint8_t *aad, const uint8_t *dummy, uint32_t ctype = 0u, const Walk *seg = nullptr,
+                       uint32_t t0 = 0u)
+{
+    return lane_walk_seg<NR, K, SEAL, FRAME, LY, PF>(lds, lanesel, rk, j, rec, valid, Tmax, iv0, iv1, iv2, src, dst, aad,
+                                                     dummy, ctype, seg != nullptr, seg != nullptr ? *seg : Walk{0, 0, 0, 0},
+                                                     t0);
 }
 
 } // namespace mi355x

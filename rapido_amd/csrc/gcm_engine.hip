@@ -25,6 +25,15 @@
 #include <rocprim/iterator/constant_iterator.hpp>
 #include <mutex>
 #include <new>
+#if defined(GCM_WIN_TIMING) && GCM_WIN_TIMING
+/* measurement build (scripts/window_phases.py): stamps inside the record walk of workgroup 0, thread 0 */
+__device__ uint64_t g_win_times[16];
+#define GCM_WALK_STAMP(i)                                                                                              \
+    do {                                                                                                               \
+        if (blockIdx.x == 0 && threadIdx.x == 0)                                                                       \
+            g_win_times[i] = __builtin_amdgcn_s_memrealtime();                                                         \
+    } while (0)
+#endif
 #include "gcm_core.h"
 #include "../../include/ptls_mi355x.h"
 
@@ -53,7 +62,6 @@ constexpr int WG_THREADS = MI355X_WG_THREADS; /* 16 waves: 4 per SIMD */
 #define GCM_WIN_TIMING 0
 #endif
 #if GCM_WIN_TIMING
-__device__ uint64_t g_win_times[8];
 #define WIN_STAMP(i)                                                                                                   \
     do {                                                                                                               \
         if (blockIdx.x == 0 && threadIdx.x == 0 && grp == blockIdx.x)                                                  \
@@ -64,6 +72,53 @@ __device__ uint64_t g_win_times[8];
 #endif
 
 __device__ __forceinline__ uint32_t shfl_xor_u32(uint32_t v, int mask) { return (uint32_t)__shfl_xor((int)v, mask, 64); }
+
+/*
+ * XOR of v over aligned groups of L lanes (L = 4, 8 or 16; a DPP row is 16 lanes), every lane receiving its group's
+ * XOR: quad_perm [1,0,3,2] and [2,3,0,1], then row_half_mirror (lane i <- 7 - i) and row_mirror (i <- 15 - i), each
+ * pairing lanes of the two halves of the previous level.  Register-to-register, unlike __shfl_xor (ds_bpermute).
+ */
+template <int L>
+__device__ __forceinline__ uint32_t dpp_xor_reduce(uint32_t v)
+{
+    static_assert(L == 4 || L == 8 || L == 16, "group of 4, 8 or 16 lanes");
+    v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);
+    v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true);
+    if constexpr (L >= 8)
+        v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, true);
+    if constexpr (L >= 16)
+        v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, true);
+    return v;
+}
+
+template <int L>
+__device__ __forceinline__ u32x4 dpp_xor_reduce4(u32x4 v)
+{
+    return u32x4{dpp_xor_reduce<L>(v[0]), dpp_xor_reduce<L>(v[1]), dpp_xor_reduce<L>(v[2]), dpp_xor_reduce<L>(v[3])};
+}
+
+/*
+ * x * c (nibble tables of c at basereg) computed by the L = 8 or 16 lanes of a window slot together, for the
+ * latency-bound segment join where one slot multiplies while the others wait: lane j reads the 2 x 16 / L table
+ * entries of byte pairs p = j, j + L (dword p / 4, byte p % 4: its low and high nibbles), then the group XOR-reduces
+ * (dpp_xor_reduce).  Every lane of the group returns the product; bit-identical to ghash_mul_lds.
+ */
+template <int L>
+__device__ __forceinline__ u32x4 ghash_mul_coop(const uint8_t *lds, uint32_t basereg, u32x4 x, uint32_t j)
+{
+    u32x4 r = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (uint32_t q = 0; q < 16u / (uint32_t)L; ++q) {
+        const uint32_t p = j + (uint32_t)L * q, d = p >> 2, m = p & 3u;
+        const uint32_t w = d == 0u ? x[0] : d == 1u ? x[1] : d == 2u ? x[2] : x[3];
+        const uint32_t lo = (w << 4) & 0xf0f0f0f0u, hi = w & 0xf0f0f0f0u, sel = 0x0c020100u | (4u + m);
+        const uint32_t off = (8u * d + 2u * m) * 256u;
+        const u32x4 e = lds_u32x4(lds, perm(lo, basereg, sel) + off);
+        const u32x4 f = lds_u32x4(lds, perm(hi, basereg, sel) + off + 256u);
+        r ^= e ^ f;
+    }
+    return dpp_xor_reduce4<L>(r);
+}
 
 __device__ __forceinline__ u32x4 shfl_xor_u32x4(u32x4 v, int mask)
 {
@@ -262,6 +317,66 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
 }
 
 /*
+ * The end of a record in the window kernels: seal writes the tag (and the TLS header), open verifies (acc = computed
+ * tag ^ received tag), zeroes a failed record's plaintext and writes the status (and strips the TLS padding).  Run by
+ * nt threads t = 0..nt-1 together; thread 0 does the single stores.
+ */
+template <bool SEAL, bool FRAME>
+__device__ __forceinline__ void window_finish(u32x4 acc, bool valid, const Record &rec, uint32_t plen, uint32_t r, uint32_t t,
+                                              uint32_t nt, uint8_t *dst, uint32_t *__restrict__ status,
+                                              uint8_t *__restrict__ types)
+{
+    if (SEAL) {
+        if (t == 0u && valid) {
+            *(u32x4_u *)(dst + rec.dst + plen) = acc;
+            if (FRAME) { /* 17 03 03 BE16(plen + 16) (lib/picotls.c:658-662) */
+                const uint32_t reclen = plen + 16u;
+                store_partial(dst + rec.dst - 5u, 5u,
+                              u32x4{0x00030317u | ((reclen >> 8) & 0xffu) << 24, reclen & 0xffu, 0u, 0u});
+            }
+        }
+    } else if (!valid || (acc[0] | acc[1] | acc[2] | acc[3]) != 0u) {
+        /* no unverified plaintext is released (fusion leaves it, lib/fusion.c:656-679) */
+        uint8_t *out = dst + rec.dst;
+        for (uint32_t off = 16u * t; off < rec.len; off += 16u * nt) {
+            const uint32_t n = rec.len - off;
+            if (n >= 16u)
+                *(u32x4_u *)(out + off) = u32x4{0u, 0u, 0u, 0u};
+            else
+                store_partial(out + off, n, u32x4{0u, 0u, 0u, 0u});
+        }
+        if (t == 0u) {
+            status[r] = 0xffffffffu; /* SIZE_MAX / PTLS_ALERT_BAD_RECORD_MAC */
+            if (FRAME)
+                types[r] = 0u;
+        }
+    } else if (!FRAME) {
+        if (t == 0u)
+            status[r] = rec.len;
+    } else if (t == 0u) {
+        /* padding strip + content-type pop (lib/picotls.c:4784-4791) over plaintext the other slots (workgroups) wrote */
+        __threadfence();
+        const uint8_t *pt = dst + rec.dst;
+        uint32_t n = plen, found = 0xfffffffeu, ty = 0u; /* PTLS_ALERT_UNEXPECTED_MESSAGE if all zero */
+        while (n != 0u && found == 0xfffffffeu) {
+            const uint32_t base = n >= 16u ? n - 16u : 0u;
+            const u32x4 v = n >= 16u ? *(const u32x4_u *)(pt + base) : load_partial(pt, n);
+#pragma unroll
+            for (int d = 3; d >= 0; --d) {
+                if (found == 0xfffffffeu && v[d] != 0u) {
+                    const uint32_t b = (31u - (uint32_t)__builtin_clz(v[d])) >> 3;
+                    found = base + 4u * (uint32_t)d + b;
+                    ty = (v[d] >> (8u * b)) & 0xffu;
+                }
+            }
+            n = base;
+        }
+        status[r] = found;
+        types[r] = (uint8_t)ty;
+    }
+}
+
+/*
  * Window kernels for SMALL framing batches (rapido's 16-record send / 32-record recv windows, a few
  * connections' windows at once).  The batch kernels above give a record 4 lanes, so a 16-record window
  * is one wave walking 257 steps.  Here every record is cut into 64-position GHASH segments (its
@@ -273,21 +388,29 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
  * H^4..H^1 (lane scaling) and of H^64.  A record of more than WIN_MAXSEG segments (larger than a TLS
  * record) is walked whole by its first slot instead.  Results are bit-identical to the batch kernels.
  */
-template <int NR, bool SEAL, bool FRAME, int THREADS, int KW, int SEG = 64>
+template <int NR, bool SEAL, bool FRAME, int THREADS, int KW, int SEG = 64, class LW = LayoutWin<KW, SEG>>
 __device__ __forceinline__ void window_body(const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2,
                                             const void *__restrict__ descs, uint32_t nrecs, const uint8_t *src, uint8_t *dst,
                                             const uint8_t *__restrict__ aad, uint32_t *__restrict__ status,
-                                            uint8_t *__restrict__ types, const uint32_t *__restrict__ conn)
+                                            uint8_t *__restrict__ types, const uint32_t *__restrict__ conn,
+                                            const u32x4 *__restrict__ win_aes)
 {
-    typedef LayoutWin<KW, SEG> LW;
     /* SEG = 32: half-length segments, twice as many, half the steps (single-record latency kernels) */
     static_assert(SEG == 64 || SEG == 32, "segment length");
     constexpr uint32_t MAXSEG = SEG == 64 ? WIN_MAXSEG : WIN_SEG32_MAXSEG;
     constexpr uint32_t SLOTS = THREADS / KW, RECS = SLOTS / MAXSEG; /* records per workgroup pass */
     static_assert(RECS >= 1, "a workgroup holds at least one record");
-    constexpr bool LATENCY = THREADS <= 512;   /* few records: up to 2 waves per SIMD */
-    constexpr int WIN_PF = LATENCY ? 3 : 1;    /* prefetch 3 steps ahead when little else hides a load (lane_walk) */
-    __shared__ __attribute__((aligned(16))) uint8_t lds[LW::parts + RECS * MAXSEG * 16u];
+    constexpr bool LATENCY = THREADS <= 576;   /* few records: up to 2-3 waves per SIMD */
+    /*
+     * join multiplies: the leader slot's KW lanes together (ghash_mul_coop) for 8 or 16 lanes per slot; otherwise
+     * each lane alone, all reads in flight at 2 waves per SIMD (256 VGPRs), compiler-scheduled at 4
+     */
+    constexpr int JW = !LATENCY ? 0 : THREADS <= 512 ? 2 : 1;
+    /* prefetch 3 steps ahead when little else hides a load (lane_walk); a 16-lane segment has only 2 steps */
+    constexpr int WIN_PF = LATENCY && KW <= 8 ? 3 : 1;
+    constexpr uint32_t LDS_BYTES = LW::parts_alias ? LayoutWin16::bytes : LW::parts + RECS * MAXSEG * 16u;
+    static_assert(!LW::parts_alias || (RECS == 1 && LW::parts + MAXSEG * 16u <= LW::gh_base), "segment sums alias H^1..");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
     const Record *__restrict__ recs = (const Record *)descs;
     const TlsRecord *__restrict__ trecs = (const TlsRecord *)descs;
     {
@@ -295,7 +418,103 @@ __device__ __forceinline__ void window_body(const KeyImage *__restrict__ ki, uin
         (void)grp;
         WIN_STAMP(0);
     }
-    fill_lds_window(lds, c_tabs.t0, ki, threadIdx.x, blockDim.x, (uint32_t)KW, (uint32_t)SEG);
+    const uint32_t lane = threadIdx.x & 63u, slot = threadIdx.x / KW, j = lane % KW;
+    const uint32_t lanesel = (lane & 31u) * 4u | 0x10000u;
+    const uint32_t rl = slot / MAXSEG, seg = slot % MAXSEG;
+    const uint32_t ngroups = (nrecs + RECS - 1u) / RECS;
+    auto join_mul = [&](uint32_t tab, u32x4 x) -> u32x4 {
+        if constexpr (KW >= 8)
+            return ghash_mul_coop<KW>(lds, tab, x, j);
+        else
+            return ghash_mul_join<JW>(lds, tab, x);
+    };
+    /* one record group's descriptor and segment walk */
+    struct Group {
+        Record rec;
+        Walk sw;
+        uint32_t r, ctype, plen, nseg, Tw, t0, n0, n1, n2;
+        bool in_batch, valid, whole, active;
+    };
+    auto setup = [&](uint32_t grp) -> Group {
+        Group g;
+        g.r = grp * RECS + rl;
+        g.in_batch = rl < RECS && g.r < nrecs;
+        g.rec = Record{0, 0, 0, 0, 0, FRAME ? 5u : 0u};
+        g.ctype = 0u;
+        g.valid = g.in_batch;
+        if (FRAME) {
+            if (g.in_batch) {
+                const TlsRecord t = trecs[g.r];
+                g.rec.seq = t.seq;
+                if (SEAL) {
+                    g.rec.src = t.src;
+                    g.rec.dst = t.dst + 5u;
+                    g.rec.len = t.len;
+                    g.ctype = t.type;
+                    g.valid = t.len <= PTLS_MI355X_TLS_MAX_FRAGMENT; /* larger: not a TLS record, nothing written */
+                } else {
+                    g.rec.src = t.src + 5u;
+                    g.rec.dst = t.dst;
+                    g.rec.len = t.len >= 16u ? t.len - 16u : 0u;
+                    g.valid = t.len >= 16u;
+                }
+            }
+        } else if (g.in_batch) {
+            g.rec = recs[g.r];
+        }
+        g.plen = FRAME && SEAL ? g.rec.len + 1u : g.rec.len;
+        const uint32_t A = FRAME ? 1u : (g.rec.aadlen + 15u) / 16u;
+        g.sw = window_segment(A, (g.plen + 15u) / 16u, seg, &g.nseg, (uint32_t)KW, (uint32_t)SEG);
+        g.whole = g.nseg > MAXSEG; /* larger than a TLS record: its first slot walks it all */
+        g.active = g.valid && (g.whole ? seg == 0u : seg < g.nseg);
+        uint32_t Tw = g.active ? (g.whole ? make_walk(g.plen, g.rec.aadlen, (uint32_t)KW, walk_out16(dst + g.rec.dst)).T
+                                          : g.sw.T)
+                               : 0u;
+        /* first step holding a real position (segments that are mostly front padding start late) */
+        uint32_t tf = g.active && !g.whole && (int32_t)g.sw.pad > 0 ? (uint32_t)(int32_t)g.sw.pad / (uint32_t)KW
+                                                                    : (g.active ? 0u : ~0u);
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            Tw = max(Tw, shfl_xor_u32(Tw, o));
+            tf = min(tf, shfl_xor_u32(tf, o));
+        }
+        g.Tw = Tw;
+        g.t0 = tf == ~0u ? 0u : tf & ~1u;
+        g.n1 = iv1 ^ bswap32((uint32_t)(g.rec.seq >> 32));
+        g.n2 = iv2 ^ bswap32((uint32_t)g.rec.seq);
+        g.n0 = conn != nullptr && g.in_batch ? iv0 ^ bswap32(conn[g.r]) : iv0;
+        return g;
+    };
+    /* latency kernels: the first group's descriptor is loaded before the LDS fill, its latency hidden under it (the
+     * wide kernels, at the 128-VGPR cap, keep nothing live across the fill) */
+    Group gr;
+    if constexpr (LATENCY)
+        gr = setup(blockIdx.x);
+    if constexpr (LW::parts_alias) {
+        /*
+         * One pass: every thread loads its <= 18 vectors of the image (the AES rows, kept once per device in win_aes,
+         * then the key image's tables from gh[0] on) before storing any, so the fill costs one memory latency.
+         * (LDS DMA, global_load_lds_dwordx4, measured 2.3 us for the same image but left the walk 24 VGPRs short at
+         * the 168-VGPR cap of 3 waves per SIMD, spilling inside the AES rounds.)
+         */
+        constexpr uint32_t NV = LayoutWin16::bytes / 16u, PER = (NV + THREADS - 1u) / THREADS;
+        const u32x4 *gk = (const u32x4 *)&ki->gh[0][0][0][0];
+        u32x4 v[PER];
+#pragma unroll
+        for (uint32_t k = 0; k < PER; ++k) {
+            const uint32_t i = threadIdx.x + k * THREADS;
+            if (i < NV)
+                v[k] = i < 0x1000u ? win_aes[i] : gk[i - 0x1000u];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < PER; ++k) {
+            const uint32_t i = threadIdx.x + k * THREADS;
+            if (i < NV)
+                *(u32x4 *)(lds + 16u * i) = v[k];
+        }
+    } else {
+        fill_lds_window(lds, c_tabs.t0, ki, threadIdx.x, blockDim.x, (uint32_t)KW, (uint32_t)SEG);
+    }
     uint32_t rk[4 * (NR + 1)];
 #pragma unroll
     for (int i = 0; i < 4 * (NR + 1); ++i)
@@ -307,61 +526,28 @@ __device__ __forceinline__ void window_body(const KeyImage *__restrict__ ki, uin
         WIN_STAMP(1);
     }
 
-    const uint32_t lane = threadIdx.x & 63u, slot = threadIdx.x / KW, j = lane % KW;
-    const uint32_t lanesel = (lane & 31u) * 4u | 0x10000u;
-    const uint32_t rl = slot / MAXSEG, seg = slot % MAXSEG;
-    const uint32_t ngroups = (nrecs + RECS - 1u) / RECS;
     /* persistent: the workgroup fills its LDS once and takes record groups with a grid stride */
     for (uint32_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
-        const uint32_t r = grp * RECS + rl;
-        const bool in_batch = rl < RECS && r < nrecs;
-        Record rec = {0, 0, 0, 0, 0, FRAME ? 5u : 0u};
-        uint32_t ctype = 0u;
-        bool valid = in_batch;
-        if (FRAME) {
-            if (in_batch) {
-                const TlsRecord t = trecs[r];
-                rec.seq = t.seq;
-                if (SEAL) {
-                    rec.src = t.src;
-                    rec.dst = t.dst + 5u;
-                    rec.len = t.len;
-                    ctype = t.type;
-                    valid = t.len <= PTLS_MI355X_TLS_MAX_FRAGMENT; /* larger: not a TLS record, nothing written */
-                } else {
-                    rec.src = t.src + 5u;
-                    rec.dst = t.dst;
-                    rec.len = t.len >= 16u ? t.len - 16u : 0u;
-                    valid = t.len >= 16u;
-                }
-            }
-        } else if (in_batch) {
-            rec = recs[r];
-        }
-        const uint32_t plen = FRAME && SEAL ? rec.len + 1u : rec.len;
-        const uint32_t A = FRAME ? 1u : (rec.aadlen + 15u) / 16u;
-        uint32_t nseg;
-        const Walk sw = window_segment(A, (plen + 15u) / 16u, seg, &nseg, (uint32_t)KW, (uint32_t)SEG);
-        const bool whole = nseg > MAXSEG; /* larger than a TLS record: its first slot walks it all */
-        const bool active = valid && (whole ? seg == 0u : seg < nseg);
-        uint32_t Tw = active ? (whole ? make_walk(plen, rec.aadlen, (uint32_t)KW, walk_out16(dst + rec.dst)).T : sw.T) : 0u;
-        /* first step holding a real position (segments that are mostly front padding start late) */
-        uint32_t tf = active && !whole && (int32_t)sw.pad > 0 ? (uint32_t)(int32_t)sw.pad / (uint32_t)KW : (active ? 0u : ~0u);
+        if (!LATENCY || grp != blockIdx.x)
+            gr = setup(grp);
+        const uint32_t r = gr.r, ctype = gr.ctype, plen = gr.plen, nseg = gr.nseg;
+        const bool in_batch = gr.in_batch, valid = gr.valid, whole = gr.whole, active = gr.active;
+        const Record &rec = gr.rec;
+        const Walk &sw = gr.sw;
+        (void)ctype;
+        u32x4 part = lane_walk_seg<NR, KW, SEAL, FRAME, LW, WIN_PF>(lds, lanesel, rk, j, rec, active, gr.Tw, gr.n0, gr.n1,
+                                                                  gr.n2, src, dst, aad, (const uint8_t *)descs, gr.ctype,
+                                                                  !whole, sw, gr.t0);
+        if constexpr (KW >= 4) {
+            part = dpp_xor_reduce4<KW>(part);
+        } else {
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            Tw = max(Tw, shfl_xor_u32(Tw, o));
-            tf = min(tf, shfl_xor_u32(tf, o));
+            for (int o = 1; o < KW; o <<= 1)
+                part ^= shfl_xor_u32x4(part, o);
         }
-        const uint32_t t0 = tf == ~0u ? 0u : tf & ~1u;
-        const uint32_t n1 = iv1 ^ bswap32((uint32_t)(rec.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)rec.seq);
-        const uint32_t n0 = conn != nullptr && in_batch ? iv0 ^ bswap32(conn[r]) : iv0;
-        u32x4 part = lane_walk<NR, KW, SEAL, FRAME, LW, WIN_PF>(lds, lanesel, rk, j, rec, active, Tw, n0, n1, n2, src, dst,
-                                                              aad, (const uint8_t *)descs, ctype, whole ? nullptr : &sw,
-                                                              t0);
-#pragma unroll
-        for (int o = 1; o < KW; o <<= 1)
-            part ^= shfl_xor_u32x4(part, o);
         WIN_STAMP(2);
+        if constexpr (LW::parts_alias)
+            __syncthreads(); /* every lane's scaling multiply is done: the sums may overwrite H^1.. */
         if (active && j == 0u)
             *(u32x4 *)(lds + LW::parts + (rl * MAXSEG + seg) * 16u) = part;
         __syncthreads();
@@ -372,7 +558,7 @@ __device__ __forceinline__ void window_body(const KeyImage *__restrict__ ki, uin
             u32x4 g = *(const u32x4 *)(lds + LW::parts + (rl * MAXSEG + seg) * 16u);
             const uint32_t gend = window_group_end(seg, ns);
             for (uint32_t k = seg + 1u; k < gend; ++k)
-                g = (LATENCY ? ghash_mul_lds_wide(lds, LW::gh64, g) : ghash_mul_lds(lds, LW::gh64, g)) ^
+                g = join_mul(LW::gh64, g) ^
                     *(const u32x4 *)(lds + LW::parts + (rl * MAXSEG + k) * 16u);
             *(u32x4 *)(lds + LW::parts + (rl * MAXSEG + seg) * 16u) = g;
         }
@@ -385,7 +571,7 @@ __device__ __forceinline__ void window_body(const KeyImage *__restrict__ ki, uin
                 if ((ng - g) % 2u == 0u) {
                     const u32x4 a = *(const u32x4 *)(lds + LW::parts + (rl * MAXSEG + seg) * 16u);
                     const u32x4 b = *(const u32x4 *)(lds + LW::parts + (rl * MAXSEG + window_group_start(g + 1u, ns)) * 16u);
-                    *(u32x4 *)(lds + LW::parts + (rl * MAXSEG + seg) * 16u) = ghash_mul_lds_wide(lds, LW::gh256, a) ^ b;
+                    *(u32x4 *)(lds + LW::parts + (rl * MAXSEG + seg) * 16u) = join_mul(LW::gh256, a) ^ b;
                 }
             }
             __syncthreads();
@@ -400,67 +586,180 @@ __device__ __forceinline__ void window_body(const KeyImage *__restrict__ ki, uin
                 acc = *(const u32x4 *)(lds + LW::parts + rl * MAXSEG * 16u);
                 if constexpr (SEG == 32) {
                     for (uint32_t g = 2u - ng % 2u; g < ng; g += 2u)
-                        acc = ghash_mul_lds_wide(lds, LW::ghpair, acc) ^
+                        acc = join_mul(LW::ghpair, acc) ^
                               *(const u32x4 *)(lds + LW::parts + (rl * MAXSEG + window_group_start(g, ns)) * 16u);
                 } else {
                     for (uint32_t k = window_group_end(0u, ns); k < ns; k += 4u)
-                        acc = (LATENCY ? ghash_mul_lds_wide(lds, LW::gh256, acc) : ghash_mul_lds(lds, LW::gh256, acc)) ^
+                        acc = join_mul(LW::gh256, acc) ^
                               *(const u32x4 *)(lds + LW::parts + (rl * MAXSEG + k) * 16u);
                 }
             }
             WIN_STAMP(4);
-            if (SEAL) {
-                if (j == 0u && valid) {
-                    *(u32x4_u *)(dst + rec.dst + plen) = acc;
-                    if (FRAME) { /* 17 03 03 BE16(plen + 16) (lib/picotls.c:658-662) */
-                        const uint32_t reclen = plen + 16u;
-                        store_partial(dst + rec.dst - 5u, 5u,
-                                      u32x4{0x00030317u | ((reclen >> 8) & 0xffu) << 24, reclen & 0xffu, 0u, 0u});
-                    }
-                }
-            } else if (!valid || (acc[0] | acc[1] | acc[2] | acc[3]) != 0u) {
-                /* no unverified plaintext is released (fusion leaves it, lib/fusion.c:656-679) */
-                uint8_t *out = dst + rec.dst;
-                for (uint32_t off = 16u * j; off < rec.len; off += 16u * KW) {
-                    const uint32_t n = rec.len - off;
-                    if (n >= 16u)
-                        *(u32x4_u *)(out + off) = u32x4{0u, 0u, 0u, 0u};
-                    else
-                        store_partial(out + off, n, u32x4{0u, 0u, 0u, 0u});
-                }
-                if (j == 0u) {
-                    status[r] = 0xffffffffu; /* SIZE_MAX / PTLS_ALERT_BAD_RECORD_MAC */
-                    if (FRAME)
-                        types[r] = 0u;
-                }
-            } else if (!FRAME) {
-                if (j == 0u)
-                    status[r] = rec.len;
-            } else if (j == 0u) {
-                /* padding strip + content-type pop (lib/picotls.c:4784-4791) over plaintext the other slots wrote */
-                __threadfence();
-                const uint8_t *pt = dst + rec.dst;
-                uint32_t n = plen, found = 0xfffffffeu, ty = 0u; /* PTLS_ALERT_UNEXPECTED_MESSAGE if all zero */
-                while (n != 0u && found == 0xfffffffeu) {
-                    const uint32_t base = n >= 16u ? n - 16u : 0u;
-                    const u32x4 v = n >= 16u ? *(const u32x4_u *)(pt + base) : load_partial(pt, n);
-#pragma unroll
-                    for (int d = 3; d >= 0; --d) {
-                        if (found == 0xfffffffeu && v[d] != 0u) {
-                            const uint32_t b = (31u - (uint32_t)__builtin_clz(v[d])) >> 3;
-                            found = base + 4u * (uint32_t)d + b;
-                            ty = (v[d] >> (8u * b)) & 0xffu;
-                        }
-                    }
-                    n = base;
-                }
-                status[r] = found;
-                types[r] = (uint8_t)ty;
-            }
+            window_finish<SEAL, FRAME>(acc, valid, rec, plen, r, j, (uint32_t)KW, dst, status, types);
         }
         __syncthreads(); /* the segment sums of this pass are consumed before the next pass writes them */
         WIN_STAMP(5);
     }
+}
+
+/*
+ * Split window kernels (single-record latency): a record's 32-position segments (16 lanes each, 2 steps) are cut into
+ * runs of SPLIT_RUNSEG = 16 aligned to the record's end, and each run is walked by its own 256-thread workgroup (one
+ * wave per SIMD) on its own CU: grid = records x SPLIT_MAXRUN, workgroup k of record r takes run k of R (idle if
+ * k >= R).  A run joins its segment sums locally (groups of 4 with H^32, the groups chained with H^128, all with the
+ * slot's 16 lanes cooperating, ghash_mul_coop) and scales the result by H^(512 m) to the record's end (m runs follow
+ * it).  The run then stores its partial, and the workgroup whose arrival ticket is the record's last XORs the R
+ * partials -- E_K(J0) and, for open, the received tag are already folded into the last run's -- and finishes the
+ * record (window_finish): tag and header, or verification, zeroing, status and padding strip.  The last arrival
+ * resets the record's ticket, so the counters are zero between launches.  No workgroup waits for another.
+ * A record of more than SPLIT_RUNSEG x SPLIT_MAXRUN segments (larger than a TLS record) is walked whole by run 0.
+ */
+template <int NR, bool SEAL, bool FRAME>
+__device__ __forceinline__ void split_body(const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2,
+                                           const void *__restrict__ descs, uint32_t nrecs, const uint8_t *src, uint8_t *dst,
+                                           const uint8_t *__restrict__ aad, uint32_t *__restrict__ status,
+                                           uint8_t *__restrict__ types, const uint32_t *__restrict__ conn,
+                                           const u32x4 *__restrict__ win_aes, u32x4 *__restrict__ partials,
+                                           uint32_t *__restrict__ tickets)
+{
+    typedef LayoutSplit LW;
+    constexpr int KW = 16;
+    constexpr uint32_t SEG = 32, THREADS = SPLIT_THREADS;
+    static_assert(THREADS / KW == SPLIT_RUNSEG, "one slot per segment of a run");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LW::bytes];
+    /* after the walk: the 16 segment sums, then the arrival ticket, over the (dead) H^1 table */
+    uint32_t *s_ticket = (uint32_t *)(lds + LW::parts + SPLIT_RUNSEG * 16u);
+    const uint32_t r = blockIdx.x / SPLIT_MAXRUN, k = blockIdx.x % SPLIT_MAXRUN;
+    if (r >= nrecs)
+        return;
+    /* the record (the same for every thread: scalar loads) */
+    Record rec = {0, 0, 0, 0, 0, FRAME ? 5u : 0u};
+    uint32_t ctype = 0u;
+    bool valid = true;
+    if (FRAME) {
+        const TlsRecord t = ((const TlsRecord *)descs)[r];
+        rec.seq = t.seq;
+        if (SEAL) {
+            rec.src = t.src;
+            rec.dst = t.dst + 5u;
+            rec.len = t.len;
+            ctype = t.type;
+            valid = t.len <= PTLS_MI355X_TLS_MAX_FRAGMENT;
+        } else {
+            rec.src = t.src + 5u;
+            rec.dst = t.dst;
+            rec.len = t.len >= 16u ? t.len - 16u : 0u;
+            valid = t.len >= 16u;
+        }
+    } else {
+        rec = ((const Record *)descs)[r];
+    }
+    const uint32_t plen = FRAME && SEAL ? rec.len + 1u : rec.len;
+    const uint32_t A = FRAME ? 1u : (rec.aadlen + 15u) / 16u, C = (plen + 15u) / 16u;
+    const uint32_t nseg = (A + C + 1u + SEG - 1u) / SEG;
+    const bool whole = nseg > SPLIT_RUNSEG * SPLIT_MAXRUN;
+    const uint32_t R = !valid || whole ? 1u : (nseg + SPLIT_RUNSEG - 1u) / SPLIT_RUNSEG;
+    if (k >= R)
+        return; /* uniform: the whole workgroup leaves before any barrier */
+    const uint32_t m = R - 1u - k; /* runs after this one */
+    /* segment of slot 0 (negative: run 0's leading slots are empty), and the run's real segments */
+    const int32_t first = (int32_t)nseg - (int32_t)(SPLIT_RUNSEG * (R - k));
+    const uint32_t ns_run = whole ? 1u : (uint32_t)((int32_t)SPLIT_RUNSEG + min(first, 0));
+    const uint32_t lane = threadIdx.x & 63u, slot = threadIdx.x / KW, j = lane % KW;
+    const uint32_t lanesel = (lane & 31u) * 4u | 0x10000u;
+    const int32_t segi = first + (int32_t)slot;
+    const bool active = valid && (whole ? slot == 0u : segi >= 0 && segi < (int32_t)nseg);
+    uint32_t nseg_chk;
+    const Walk sw = window_segment(A, C, segi >= 0 ? (uint32_t)segi : 0u, &nseg_chk, (uint32_t)KW, SEG);
+    uint32_t Tw = active ? (whole ? make_walk(plen, rec.aadlen, (uint32_t)KW, walk_out16(dst + rec.dst)).T : sw.T) : 0u;
+    uint32_t tf = active && !whole && (int32_t)sw.pad > 0 ? (uint32_t)(int32_t)sw.pad / (uint32_t)KW : (active ? 0u : ~0u);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        Tw = max(Tw, shfl_xor_u32(Tw, o));
+        tf = min(tf, shfl_xor_u32(tf, o));
+    }
+    const uint32_t t0 = tf == ~0u ? 0u : tf & ~1u;
+    {
+        /*
+         * One pass: each thread loads its 40 vectors of the image before storing any.  (Loading the tables only the
+         * scaling and the join read -- H^1..H^8, H^32, H^128, H^(512 m) -- by LDS DMA during the walk measured 2 us
+         * SLOWER per window: profiles/r02l_split_ab.txt.)
+         */
+        constexpr uint32_t NV = LW::bytes / 16u, PER = NV / THREADS;
+        static_assert(NV % THREADS == 0u, "whole passes");
+        const u32x4 *gk = (const u32x4 *)&ki->gh[0][0][0][0];
+        const u32x4 *gr = (const u32x4 *)(m == 2u ? &ki->gh1024[0][0][0] : &ki->gh512[0][0][0]);
+        u32x4 v[PER];
+#pragma unroll
+        for (uint32_t q = 0; q < PER; ++q) {
+            const uint32_t i = threadIdx.x + q * THREADS;
+            v[q] = i < 0x1000u ? win_aes[i] : i < LW::gh_run / 16u ? gk[i - 0x1000u] : gr[i - LW::gh_run / 16u];
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < PER; ++q)
+            *(u32x4 *)(lds + 16u * (threadIdx.x + q * THREADS)) = v[q];
+    }
+    uint32_t rk[4 * (NR + 1)];
+#pragma unroll
+    for (int i = 0; i < 4 * (NR + 1); ++i)
+        rk[i] = ki->rk[i];
+    __syncthreads();
+
+    const uint32_t n1 = iv1 ^ bswap32((uint32_t)(rec.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)rec.seq);
+    const uint32_t n0 = conn != nullptr ? iv0 ^ bswap32(conn[r]) : iv0;
+    u32x4 part = lane_walk_seg<NR, KW, SEAL, FRAME, LW, 1>(lds, lanesel, rk, j, rec, active, Tw, n0, n1, n2, src, dst, aad,
+                                                          (const uint8_t *)descs, ctype, !whole, sw, t0);
+    part = dpp_xor_reduce4<KW>(part);
+    if (R > 1u)
+        __threadfence(); /* this run's output reaches L2 before its arrival ticket (window_finish may overwrite it) */
+    __syncthreads(); /* every lane's scaling multiply is done: the sums may overwrite H^1.. */
+    if (active && j == 0u)
+        *(u32x4 *)(lds + LW::parts + slot * 16u) = part;
+    __syncthreads();
+    /* the run's local join over its ns_run real segments; li = slot - off is the index among them */
+    const uint32_t off = first < 0 ? (uint32_t)(-first) : 0u;
+    const uint32_t li = slot - off;
+    const bool real = valid && slot >= off && li < ns_run;
+    if (real && window_group_leader(li, ns_run)) {
+        u32x4 g = *(const u32x4 *)(lds + LW::parts + slot * 16u);
+        for (uint32_t q = li + 1u; q < window_group_end(li, ns_run); ++q)
+            g = ghash_mul_coop<KW>(lds, LW::gh_group, g, j) ^ *(const u32x4 *)(lds + LW::parts + (off + q) * 16u);
+        *(u32x4 *)(lds + LW::parts + slot * 16u) = g;
+    }
+    __syncthreads();
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    if (real && li == 0u) {
+        acc = *(const u32x4 *)(lds + LW::parts + off * 16u);
+        for (uint32_t q = window_group_end(0u, ns_run); q < ns_run; q += 4u)
+            acc = ghash_mul_coop<KW>(lds, LW::gh_chain, acc, j) ^ *(const u32x4 *)(lds + LW::parts + (off + q) * 16u);
+        if (m != 0u)
+            acc = ghash_mul_coop<KW>(lds, LW::gh_run, acc, j);
+        if (R > 1u && j == 0u) {
+            /* publish the run's partial, then take an arrival ticket (release: the partial and this run's output) */
+            partials[SPLIT_MAXRUN * r + k] = acc;
+            __threadfence();
+            *s_ticket = atomicAdd(&tickets[r], 1u);
+        }
+    }
+    if (R > 1u) {
+        __syncthreads();
+        if (*s_ticket != R - 1u)
+            return; /* not the last run of the record */
+        __threadfence(); /* acquire: every run's partial and output */
+        if (real && li == 0u) {
+            acc = u32x4{0u, 0u, 0u, 0u};
+            for (uint32_t q = 0; q < R; ++q)
+                acc ^= partials[SPLIT_MAXRUN * r + q];
+            if (j == 0u)
+                tickets[r] = 0u; /* every run has arrived: zero for the next launch */
+        }
+    }
+    /* the record's result to every thread (window_finish runs on all 256) */
+    if (real && li == 0u && j == 0u)
+        *(u32x4 *)(lds + LW::parts) = acc;
+    __syncthreads();
+    acc = *(const u32x4 *)(lds + LW::parts);
+    window_finish<SEAL, FRAME>(acc, valid, rec, plen, r, threadIdx.x, THREADS, dst, status, types);
 }
 
 } // namespace
@@ -504,9 +803,10 @@ MI355X_GCM_KERNEL_F(mi355x_tls_open_aes256_k4, 14, 4, false, true)
     extern "C" __global__ __launch_bounds__(THREADS) void NAME(                                                        \
         const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2, const void *__restrict__ descs,     \
         uint32_t nrecs, const uint8_t *src, uint8_t *dst, const uint8_t *__restrict__ aad, uint32_t *__restrict__ st,   \
-        uint8_t *__restrict__ types, const uint32_t *__restrict__ conn)                                                \
+        uint8_t *__restrict__ types, const uint32_t *__restrict__ conn, const u32x4 *__restrict__ win_aes)             \
     {                                                                                                                  \
-        window_body<NR, SEAL, FRAME, THREADS, KW>(ki, iv0, iv1, iv2, descs, nrecs, src, dst, aad, st, types, conn);        \
+        window_body<NR, SEAL, FRAME, THREADS, KW>(ki, iv0, iv1, iv2, descs, nrecs, src, dst, aad, st, types, conn,     \
+                                                  win_aes);                                                            \
     }
 /* single-record latency kernels: 32-position segments (4 steps of 8 lanes), one record per 512-thread group */
 #ifndef MI355X_WIN32_THREADS
@@ -516,10 +816,10 @@ MI355X_GCM_KERNEL_F(mi355x_tls_open_aes256_k4, 14, 4, false, true)
     extern "C" __global__ __launch_bounds__(MI355X_WIN32_THREADS) void NAME(                                           \
         const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2, const void *__restrict__ descs,     \
         uint32_t nrecs, const uint8_t *src, uint8_t *dst, const uint8_t *__restrict__ aad, uint32_t *__restrict__ st,   \
-        uint8_t *__restrict__ types, const uint32_t *__restrict__ conn)                                                \
+        uint8_t *__restrict__ types, const uint32_t *__restrict__ conn, const u32x4 *__restrict__ win_aes)             \
     {                                                                                                                  \
         window_body<NR, SEAL, FRAME, MI355X_WIN32_THREADS, 8, 32>(ki, iv0, iv1, iv2, descs, nrecs, src, dst, aad, st,  \
-                                                                  types, conn);                                      \
+                                                                  types, conn, win_aes);                             \
     }
 MI355X_WIN32_KERNEL(mi355x_tls_win32_seal_aes128, 10, true, true)
 MI355X_WIN32_KERNEL(mi355x_tls_win32_seal_aes256, 14, true, true)
@@ -529,6 +829,58 @@ MI355X_WIN32_KERNEL(mi355x_gcm_win32_seal_aes128, 10, true, false)
 MI355X_WIN32_KERNEL(mi355x_gcm_win32_seal_aes256, 14, true, false)
 MI355X_WIN32_KERNEL(mi355x_gcm_win32_open_aes128, 10, false, false)
 MI355X_WIN32_KERNEL(mi355x_gcm_win32_open_aes256, 14, false, false)
+/*
+ * 16-lane single-record latency kernels: 32-position segments walked by 16 lanes in 2 steps (LayoutWin16), one
+ * record (33 segments x 16 lanes = 528 lanes) per 576-thread group.
+ */
+#define MI355X_WIN16_KERNEL(NAME, NR, SEAL, FRAME)                                                                     \
+    extern "C" __global__ __launch_bounds__(576) void NAME(                                                            \
+        const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2, const void *__restrict__ descs,     \
+        uint32_t nrecs, const uint8_t *src, uint8_t *dst, const uint8_t *__restrict__ aad, uint32_t *__restrict__ st,   \
+        uint8_t *__restrict__ types, const uint32_t *__restrict__ conn, const u32x4 *__restrict__ win_aes)             \
+    {                                                                                                                  \
+        window_body<NR, SEAL, FRAME, 576, 16, 32, LayoutWin16>(ki, iv0, iv1, iv2, descs, nrecs, src, dst, aad, st,     \
+                                                               types, conn, win_aes);                                \
+    }
+MI355X_WIN16_KERNEL(mi355x_tls_win16_seal_aes128, 10, true, true)
+MI355X_WIN16_KERNEL(mi355x_tls_win16_seal_aes256, 14, true, true)
+MI355X_WIN16_KERNEL(mi355x_tls_win16_open_aes128, 10, false, true)
+MI355X_WIN16_KERNEL(mi355x_tls_win16_open_aes256, 14, false, true)
+MI355X_WIN16_KERNEL(mi355x_gcm_win16_seal_aes128, 10, true, false)
+MI355X_WIN16_KERNEL(mi355x_gcm_win16_seal_aes256, 14, true, false)
+MI355X_WIN16_KERNEL(mi355x_gcm_win16_open_aes128, 10, false, false)
+MI355X_WIN16_KERNEL(mi355x_gcm_win16_open_aes256, 14, false, false)
+
+/*
+ * Split window kernels (split_body): SPLIT_MAXRUN 256-thread workgroups per record, each walking one run of 16
+ * segments on its own CU; partials and arrival tickets in the context's split buffer.
+ */
+#define MI355X_SPLIT_KERNEL(NAME, NR, SEAL, FRAME)                                                                     \
+    extern "C" __global__ __launch_bounds__(SPLIT_THREADS) void NAME(                                                  \
+        const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2, const void *__restrict__ descs,     \
+        uint32_t nrecs, const uint8_t *src, uint8_t *dst, const uint8_t *__restrict__ aad, uint32_t *__restrict__ st,   \
+        uint8_t *__restrict__ types, const uint32_t *__restrict__ conn, const u32x4 *__restrict__ win_aes,             \
+        u32x4 *__restrict__ partials, uint32_t *__restrict__ tickets)                                                  \
+    {                                                                                                                  \
+        split_body<NR, SEAL, FRAME>(ki, iv0, iv1, iv2, descs, nrecs, src, dst, aad, st, types, conn, win_aes,           \
+                                    partials, tickets);                                                                \
+    }
+MI355X_SPLIT_KERNEL(mi355x_tls_wins_seal_aes128, 10, true, true)
+MI355X_SPLIT_KERNEL(mi355x_tls_wins_seal_aes256, 14, true, true)
+MI355X_SPLIT_KERNEL(mi355x_tls_wins_open_aes128, 10, false, true)
+MI355X_SPLIT_KERNEL(mi355x_tls_wins_open_aes256, 14, false, true)
+MI355X_SPLIT_KERNEL(mi355x_gcm_wins_seal_aes128, 10, true, false)
+MI355X_SPLIT_KERNEL(mi355x_gcm_wins_seal_aes256, 14, true, false)
+MI355X_SPLIT_KERNEL(mi355x_gcm_wins_open_aes128, 10, false, false)
+MI355X_SPLIT_KERNEL(mi355x_gcm_wins_open_aes256, 14, false, false)
+
+/* the AES rows of the window image (window_image_vec, v < 4096), once per device: the 16-lane kernels copy them */
+extern "C" __global__ void mi355x_win_aes_image(u32x4 *out)
+{
+    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v < 0x10000u / 16u)
+        out[v] = window_image_vec(c_tabs.t0, nullptr, v, 8u, 32u);
+}
 /* 256 threads (3 records per pass): a few records spread over many CUs; 1024 threads (15 records per pass,
  * persistent): hundreds of records */
 MI355X_WIN_KERNEL(mi355x_tls_win_seal_aes128, 10, true, true, 512, 8)
@@ -553,10 +905,10 @@ MI355X_WIN_KERNEL(mi355x_gcm_winw_open_aes256, 14, false, false, 1024, 4)
 /*
  * Key image setup (ptls_fusion_aesgcm_new, lib/fusion.c:775-795): one 1024-thread workgroup.
  *   1. thread 0: key expansion and H = E_K(0^128);
- *   2. wave 0: the 12 powers H^2..H^8, H^32, H^64, H^128, H^256 by wave-parallel multiplies
+ *   2. wave 0: the 14 powers H^2..H^8, H^16, H^32, ..., H^1024 by wave-parallel multiplies
  *      (lane l forms Y x^l and Y x^(l+64), masks them by bits l, l+64 of X, the wave XOR-reduces);
- *   3. all threads: the 13 x 128 single-bit products P x^k (gf_mul_xpow), into LDS;
- *   4. all threads: the 13 x 32 x 16 nibble-table entries, each the XOR of <= 4 single-bit products.
+ *   3. all threads: the 15 x 128 single-bit products P x^k (gf_mul_xpow), into LDS;
+ *   4. all threads: the 15 x 32 x 16 nibble-table entries, each the XOR of <= 4 single-bit products.
  * Bit-identical to build_key_image (tests/test_kernel_model.py checks the same steps on the host).
  */
 __device__ __forceinline__ Gf128 gf_wave_reduce(Gf128 v)
@@ -618,6 +970,8 @@ extern "C" __global__ __launch_bounds__(1024) void mi355x_gcm_setup(const uint8_
                 s_pow[e - 1] = p;
         }
         p = gf_mul_wave(p, p, lane); /* H^16 */
+        if (lane == 0)
+            s_pow[MAX_K + 4] = p;
         p = gf_mul_wave(p, p, lane); /* H^32 */
         if (lane == 0)
             s_pow[MAX_K + 2] = p;
@@ -630,6 +984,12 @@ extern "C" __global__ __launch_bounds__(1024) void mi355x_gcm_setup(const uint8_
         p = gf_mul_wave(p, p, lane); /* H^256 */
         if (lane == 0)
             s_pow[MAX_K + 1] = p;
+        p = gf_mul_wave(p, p, lane); /* H^512 */
+        if (lane == 0)
+            s_pow[MAX_K + 5] = p;
+        p = gf_mul_wave(p, p, lane); /* H^1024 */
+        if (lane == 0)
+            s_pow[MAX_K + 6] = p;
     }
     __syncthreads();
     for (uint32_t i = tid; i < KEY_IMAGE_TABLES * 128u; i += blockDim.x)
@@ -746,7 +1106,10 @@ typedef void (*batch_kernel_t)(const KeyImage *, uint32_t, uint32_t, uint32_t, c
                                const uint8_t *, uint8_t *, const uint8_t *, uint32_t *, uint8_t *, uint32_t *,
                                uint32_t, const uint32_t *);
 typedef void (*win_kernel_t)(const KeyImage *, uint32_t, uint32_t, uint32_t, const void *, uint32_t, const uint8_t *,
-                             uint8_t *, const uint8_t *, uint32_t *, uint8_t *, const uint32_t *);
+                             uint8_t *, const uint8_t *, uint32_t *, uint8_t *, const uint32_t *, const u32x4 *);
+typedef void (*split_kernel_t)(const KeyImage *, uint32_t, uint32_t, uint32_t, const void *, uint32_t, const uint8_t *,
+                               uint8_t *, const uint8_t *, uint32_t *, uint8_t *, const uint32_t *, const u32x4 *, u32x4 *,
+                               uint32_t *);
 
 constexpr uint32_t WORK_SLOTS = 256; /* per-context ring of work counters: one per launch in flight */
 
@@ -763,6 +1126,7 @@ struct DeviceShared {
     uint8_t *h_stage = nullptr;     /* pinned host staging (mapped, coherent) */
     uint8_t *h_stage_dev = nullptr; /* h_stage as the GPU addresses it */
     size_t cap = 0;
+    u32x4 *d_win_aes = nullptr;     /* the 64 KiB AES image of the 16-lane window kernels (mi355x_win_aes_image) */
 };
 
 struct st_ptls_mi355x_aesgcm_context {
@@ -778,6 +1142,10 @@ struct st_ptls_mi355x_aesgcm_context {
     hipEvent_t reuse_event;         /* orders a slot's reuse on another stream after its last launch */
     void *d_scratch;                /* order_by_length / stop-at-failure workspace */
     size_t scratch_cap;
+    u32x4 *d_split;                 /* split window kernels: SPLIT_MAXRUN partials per record, then the tickets */
+    size_t split_cap;               /* records the buffer holds */
+    hipStream_t split_stream;       /* stream of the last split launch */
+    hipEvent_t split_event;         /* orders a split launch on another stream after it */
 };
 
 struct st_ptls_mi355x_aes_context {
@@ -802,6 +1170,12 @@ static uint32_t g_ticket_origin = 0u;
 /* window batches of at most this many records use 32-position segments (ptls_mi355x_set_seg32_records;
  * SIZE_MAX = the device's CU count) */
 static size_t g_seg32_records = SIZE_MAX;
+/* window batches of at most this many records use the 16-lane single-record kernels (ptls_mi355x_set_win16_records;
+ * SIZE_MAX = the device's CU count); they take precedence over the 32-position 8-lane ones */
+static size_t g_win16_records = SIZE_MAX;
+/* window batches of at most this many records use the split kernels, SPLIT_MAXRUN workgroups per record
+ * (ptls_mi355x_set_split_records; SIZE_MAX = CU count / SPLIT_MAXRUN); they take precedence over the others */
+static size_t g_split_records = SIZE_MAX;
 
 static int fail(const char *what, hipError_t e)
 {
@@ -854,6 +1228,21 @@ static DeviceShared *device_shared(int dev)
             delete d;
             return nullptr;
         }
+        e = hipMalloc(&d->d_win_aes, 0x10000);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(mi355x_win_aes_image, dim3(16), dim3(256), 0, d->stream, d->d_win_aes);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess)
+            e = hipStreamSynchronize(d->stream);
+        if (e != hipSuccess) {
+            fail("window AES image", e);
+            if (d->d_win_aes)
+                (void)hipFree(d->d_win_aes);
+            (void)hipStreamDestroy(d->stream);
+            delete d;
+            return nullptr;
+        }
         g_shared[dev] = d;
     }
     return g_shared[dev];
@@ -889,6 +1278,7 @@ struct LaunchPlan {
     const char *name = "";
     batch_kernel_t batch = nullptr;
     win_kernel_t win = nullptr;
+    split_kernel_t split = nullptr;
     uint32_t blocks = 0, threads = 0;
 };
 
@@ -900,6 +1290,10 @@ struct BatchEntry {
 struct WinEntry {
     const char *name;
     win_kernel_t f;
+};
+struct SplitEntry {
+    const char *name;
+    split_kernel_t f;
 };
 
 /*
@@ -930,14 +1324,36 @@ static LaunchPlan plan_launch(bool seal, bool frame, uint32_t key_size, size_t n
              {KN(mi355x_gcm_win32_seal_aes128), KN(mi355x_gcm_win32_seal_aes256)}},
             {{KN(mi355x_tls_win32_open_aes128), KN(mi355x_tls_win32_open_aes256)},
              {KN(mi355x_tls_win32_seal_aes128), KN(mi355x_tls_win32_seal_aes256)}}};
+        static const WinEntry table16[2][2][2] = {
+            /* [frame][seal][aes256]: 32-position segments, 16 lanes each, one record per group */
+            {{KN(mi355x_gcm_win16_open_aes128), KN(mi355x_gcm_win16_open_aes256)},
+             {KN(mi355x_gcm_win16_seal_aes128), KN(mi355x_gcm_win16_seal_aes256)}},
+            {{KN(mi355x_tls_win16_open_aes128), KN(mi355x_tls_win16_open_aes256)},
+             {KN(mi355x_tls_win16_seal_aes128), KN(mi355x_tls_win16_seal_aes256)}}};
+        static const SplitEntry table_split[2][2][2] = {
+            /* [frame][seal][aes256]: runs of 16 segments, SPLIT_MAXRUN workgroups per record */
+            {{KN(mi355x_gcm_wins_open_aes128), KN(mi355x_gcm_wins_open_aes256)},
+             {KN(mi355x_gcm_wins_seal_aes128), KN(mi355x_gcm_wins_seal_aes256)}},
+            {{KN(mi355x_tls_wins_open_aes128), KN(mi355x_tls_wins_open_aes256)},
+             {KN(mi355x_tls_wins_seal_aes128), KN(mi355x_tls_wins_seal_aes256)}}};
+        if (n <= (g_split_records == SIZE_MAX ? (size_t)num_cu / SPLIT_MAXRUN : g_split_records) &&
+            n <= 0xffffffffu / SPLIT_MAXRUN) {
+            const SplitEntry &e = table_split[f][s][a256];
+            p.name = e.name;
+            p.split = e.f;
+            p.threads = SPLIT_THREADS;
+            p.blocks = (uint32_t)(n * SPLIT_MAXRUN);
+            return p;
+        }
         const bool wide = n > 15u * (uint64_t)num_cu; /* the wide groups (15 records) fill every CU */
         constexpr uint32_t per32 = (MI355X_WIN32_THREADS / 8u) / WIN_SEG32_MAXSEG; /* records per 32-position group */
-        const bool seg32 = !wide && n <= (g_seg32_records == SIZE_MAX ? (size_t)per32 * num_cu : g_seg32_records);
-        const WinEntry &e = seg32 ? table32[f][s][a256] : table[f][wide][s][a256];
+        const bool win16 = !wide && n <= (g_win16_records == SIZE_MAX ? (size_t)num_cu : g_win16_records);
+        const bool seg32 = !win16 && !wide && n <= (g_seg32_records == SIZE_MAX ? (size_t)per32 * num_cu : g_seg32_records);
+        const WinEntry &e = win16 ? table16[f][s][a256] : seg32 ? table32[f][s][a256] : table[f][wide][s][a256];
         p.name = e.name;
         p.win = e.f;
-        p.threads = seg32 ? (uint32_t)MI355X_WIN32_THREADS : wide ? 1024u : 512u;
-        const uint32_t per = seg32 ? per32 : (p.threads / (wide ? 4u : 8u)) / WIN_MAXSEG;
+        p.threads = win16 ? 576u : seg32 ? (uint32_t)MI355X_WIN32_THREADS : wide ? 1024u : 512u;
+        const uint32_t per = win16 ? 1u : seg32 ? per32 : (p.threads / (wide ? 4u : 8u)) / WIN_MAXSEG;
         uint64_t blocks = (n + per - 1) / per;
         if (wide && blocks > (uint64_t)num_cu)
             blocks = (uint64_t)num_cu;
@@ -988,9 +1404,42 @@ static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void
     const LaunchPlan p = plan_launch(seal, frame, ctx->key_size, n, ctx->num_cu);
     const uint8_t *iv = (const uint8_t *)static_iv12;
     DeviceGuard guard(ctx->device);
+    if (p.split != nullptr) {
+        /* partials and tickets for n records (tickets are zero between launches: each record's last run resets its) */
+        if (ctx->split_cap < n) {
+            if (ctx->d_split)
+                (void)hipFree(ctx->d_split); /* synchronises the device: no launch still uses it */
+            ctx->d_split = nullptr;
+            ctx->split_cap = 0;
+            const size_t cap = n < 64 ? 64 : n;
+            HIPCHK(hipMalloc(&ctx->d_split, cap * (SPLIT_MAXRUN * sizeof(u32x4) + sizeof(uint32_t))));
+            HIPCHK(hipMemsetAsync((uint8_t *)ctx->d_split + cap * SPLIT_MAXRUN * sizeof(u32x4), 0, cap * sizeof(uint32_t),
+                                  stream));
+            ctx->split_cap = cap;
+            ctx->split_stream = stream;
+        }
+        if (ctx->split_stream != stream) { /* the tickets are shared: order after the previous split launch */
+            if (ctx->split_event == nullptr)
+                HIPCHK(hipEventCreateWithFlags(&ctx->split_event, hipEventDisableTiming));
+            if (hipEventRecord(ctx->split_event, ctx->split_stream) == hipSuccess) {
+                HIPCHK(hipStreamWaitEvent(stream, ctx->split_event, 0));
+            } else {
+                (void)hipGetLastError();
+                HIPCHK(hipDeviceSynchronize());
+            }
+        }
+        uint32_t *tickets = (uint32_t *)((uint8_t *)ctx->d_split + ctx->split_cap * SPLIT_MAXRUN * sizeof(u32x4));
+        hipLaunchKernelGGL(p.split, dim3(p.blocks), dim3(p.threads), 0, stream, ctx->d_ki, le32(iv), le32(iv + 4),
+                           le32(iv + 8), recs, (uint32_t)n, src, dst, aad, status, types, conn,
+                           (const u32x4 *)ctx->shared->d_win_aes, ctx->d_split, tickets);
+        HIPCHK(hipGetLastError());
+        ctx->split_stream = stream;
+        return 0;
+    }
     if (p.win != nullptr) {
         hipLaunchKernelGGL(p.win, dim3(p.blocks), dim3(p.threads), 0, stream, ctx->d_ki, le32(iv), le32(iv + 4),
-                           le32(iv + 8), recs, (uint32_t)n, src, dst, aad, status, types, conn);
+                           le32(iv + 8), recs, (uint32_t)n, src, dst, aad, status, types, conn,
+                           (const u32x4 *)ctx->shared->d_win_aes);
         HIPCHK(hipGetLastError());
         return 0;
     }
@@ -1075,6 +1524,20 @@ size_t ptls_mi355x_set_aead_window_records(size_t n)
 {
     const size_t prev = g_aead_window_records;
     g_aead_window_records = n;
+    return prev;
+}
+
+size_t ptls_mi355x_set_split_records(size_t n)
+{
+    const size_t prev = g_split_records;
+    g_split_records = n;
+    return prev;
+}
+
+size_t ptls_mi355x_set_win16_records(size_t n)
+{
+    const size_t prev = g_win16_records;
+    g_win16_records = n;
     return prev;
 }
 
@@ -1175,6 +1638,10 @@ void ptls_mi355x_aesgcm_free(ptls_mi355x_aesgcm_context_t *ctx)
         (void)hipFree(ctx->d_scratch);
     if (ctx->reuse_event)
         (void)hipEventDestroy(ctx->reuse_event);
+    if (ctx->d_split)
+        (void)hipFree(ctx->d_split);
+    if (ctx->split_event)
+        (void)hipEventDestroy(ctx->split_event);
     free(ctx);
 }
 
@@ -1515,6 +1982,6 @@ int ptls_mi355x_aes_ecb_batch(ptls_mi355x_aes_context_t *ctx, int is_enc, uint8_
 /* measurement builds: the phase stamps of the last window launch (s_memrealtime ticks, 100 MHz) */
 extern "C" int ptls_mi355x_debug_window_times(uint64_t *out)
 {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_win_times), sizeof(uint64_t) * 8) == hipSuccess ? 0 : -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_win_times), sizeof(uint64_t) * 16) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -1,3 +1,4 @@
+import contextlib
 import os
 import sys
 
@@ -30,3 +31,28 @@ def gpu(engine_lib):
     import torch
     torch.cuda.init()
     return torch.device("cuda:0")
+
+
+# the kernel families every parity test runs on (rapido_amd/csrc/gcm_engine.hip plan_launch): the window kernels
+# with 64-position segments, with 32-position segments (8 lanes, 4 steps), with 32-position segments and 16 lanes
+# (2 steps), the split kernels (runs of 16 such segments on separate workgroups), and the batch kernels (K lanes per
+# record)
+FAMILIES = ["window", "window32", "window16", "split", "batch"]
+
+
+@contextlib.contextmanager
+def kernel_family(name: str, framing: bool):
+    """Routes every batch to the kernel family `name` (FAMILIES) for the duration of the block."""
+    import rapido_amd as ra
+    set_window = ra.set_tls_window_records if framing else ra.set_aead_window_records
+    prev = set_window(0 if name == "batch" else 1 << 30)
+    prev32 = ra.set_seg32_records(1 << 30 if name == "window32" else 0)
+    prev16 = ra.set_win16_records(1 << 30 if name == "window16" else 0)
+    prevs = ra.set_split_records(1 << 30 if name == "split" else 0)
+    try:
+        yield name
+    finally:
+        set_window(prev)
+        ra.set_seg32_records(prev32)
+        ra.set_win16_records(prev16)
+        ra.set_split_records(prevs)

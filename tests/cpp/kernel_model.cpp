@@ -11,6 +11,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <type_traits>
 #include "../../rapido_amd/csrc/gcm_core.h"
 #include "../../scripts/gcm_bitslice.h"
 
@@ -293,6 +294,126 @@ extern "C" int model_batch_window(int is_seal, const uint8_t *key, size_t keylen
     return 0;
 }
 
+/*
+ * The 16-lane latency kernels (window_body with LayoutWin16) and the split kernels (split_body, LayoutSplit) for AEAD
+ * records: 32-position segments walked by 16 lanes (2 steps; lane scaling H^(16 - j) as H^8 x H^(8 - j) for j < 8).
+ * win16 joins the segments as window_body does with SEG = 32 (groups of 4 with H^32, pairs of groups with H^128, the
+ * chain of pairs with H^256); split cuts them into runs of 16 aligned to the record's end, joins each run (groups of
+ * 4 with H^32, the chain of groups with H^128), scales it by H^(512 m) and XORs the runs.  Records of more than
+ * 33 (win16) / 48 (split) segments are walked whole by 16 lanes.
+ */
+template <int NR, bool SEAL, bool SPLIT>
+static void run_win16(const KeyImage *ki, uint8_t *lds, uint8_t *lds_m2, const uint8_t *static_iv, const Record *recs,
+                      size_t n, const uint8_t *src, uint8_t *dst, const uint8_t *aad, uint32_t *status)
+{
+    constexpr int KW = 16;
+    typedef typename std::conditional<SPLIT, LayoutSplit, LayoutWin16>::type LW;
+    uint32_t iv0, iv1, iv2;
+    memcpy(&iv0, static_iv, 4);
+    memcpy(&iv1, static_iv + 4, 4);
+    memcpy(&iv2, static_iv + 8, 4);
+    const uint32_t maxseg = SPLIT ? SPLIT_RUNSEG * SPLIT_MAXRUN : WIN_SEG32_MAXSEG;
+    for (size_t i = 0; i < n; ++i) {
+        const Record &r = recs[i];
+        const uint32_t n1 = iv1 ^ bswap32((uint32_t)(r.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)r.seq);
+        const uint32_t A = (r.aadlen + 15) / 16, C = (r.len + 15) / 16;
+        uint32_t nseg;
+        window_segment(A, C, 0, &nseg, KW, 32);
+        u32x4 acc = {0, 0, 0, 0};
+        if (nseg > maxseg) {
+            const Walk wk = make_walk(r.len, r.aadlen, KW, walk_out16(dst + r.dst));
+            for (uint32_t j = 0; j < (uint32_t)KW; ++j)
+                acc ^= lane_walk<NR, KW, SEAL, false, LW, 1>(lds, 4u * j | 0x10000u, ki->rk, j, r, true, wk.T, iv0, n1, n2, src,
+                                                            dst, aad, (const uint8_t *)recs);
+        } else {
+            u32x4 parts[64];
+            for (uint32_t sg = 0; sg < nseg; ++sg) {
+                const Walk sw = window_segment(A, C, sg, &nseg, KW, 32);
+                u32x4 part = {0, 0, 0, 0};
+                for (uint32_t j = 0; j < (uint32_t)KW; ++j)
+                    part ^= lane_walk<NR, KW, SEAL, false, LW, 1>(lds, 4u * j | 0x10000u, ki->rk, j, r, true, sw.T, iv0, n1,
+                                                                 n2, src, dst, aad, (const uint8_t *)recs, 0u, &sw);
+                parts[sg] = part;
+            }
+            if (!SPLIT) {
+                /* window_body, SEG = 32: the LDS slots gh64 / gh256 / ghpair hold H^32 / H^128 / H^256 */
+                for (uint32_t sg = 0; sg < nseg; ++sg)
+                    if (window_group_leader(sg, nseg))
+                        for (uint32_t k = sg + 1; k < window_group_end(sg, nseg); ++k)
+                            parts[sg] = ghash_mul_lds_wide(lds, LayoutWin16::gh64, parts[sg]) ^ parts[k];
+                const uint32_t ng = window_group_count(nseg);
+                for (uint32_t g = 0; g + 1 < ng; ++g)
+                    if ((ng - g) % 2u == 0u)
+                        parts[window_group_start(g, nseg)] =
+                            ghash_mul_lds_wide(lds, LayoutWin16::gh256, parts[window_group_start(g, nseg)]) ^
+                            parts[window_group_start(g + 1, nseg)];
+                acc = parts[0];
+                for (uint32_t g = 2 - ng % 2; g < ng; g += 2)
+                    acc = ghash_mul_lds_wide(lds, LayoutWin16::ghpair, acc) ^ parts[window_group_start(g, nseg)];
+            } else {
+                /* split_body: runs of 16 aligned to the end, each joined, scaled by H^(512 m), XORed */
+                const uint32_t R = (nseg + SPLIT_RUNSEG - 1) / SPLIT_RUNSEG;
+                for (uint32_t k = 0; k < R; ++k) {
+                    const int32_t first = (int32_t)nseg - (int32_t)(SPLIT_RUNSEG * (R - k));
+                    const uint32_t lo = first < 0 ? 0u : (uint32_t)first, ns = (uint32_t)((int32_t)SPLIT_RUNSEG + (first < 0 ? first : 0));
+                    u32x4 *p = parts + lo;
+                    for (uint32_t li = 0; li < ns; ++li)
+                        if (window_group_leader(li, ns))
+                            for (uint32_t q = li + 1; q < window_group_end(li, ns); ++q)
+                                p[li] = ghash_mul_lds_wide(lds, LayoutSplit::gh_group, p[li]) ^ p[q];
+                    u32x4 run = p[0];
+                    for (uint32_t q = window_group_end(0, ns); q < ns; q += 4)
+                        run = ghash_mul_lds_wide(lds, LayoutSplit::gh_chain, run) ^ p[q];
+                    const uint32_t m = R - 1 - k;
+                    if (m != 0)
+                        run = ghash_mul_lds_wide(m == 2 ? lds_m2 : lds, LayoutSplit::gh_run, run);
+                    acc ^= run;
+                }
+            }
+        }
+        if (SEAL)
+            memcpy(dst + r.dst + r.len, &acc, 16);
+        else
+            status[i] = (acc[0] | acc[1] | acc[2] | acc[3]) ? 0xffffffffu : r.len;
+    }
+}
+
+/* the 16-lane (split = 0) or split (split = 1) window kernels' math for an AEAD batch */
+extern "C" int model_batch_win16(int is_seal, int split, const uint8_t *key, size_t keylen, const uint8_t *static_iv,
+                                 const Record *recs, size_t n, const uint8_t *src, uint8_t *dst, const uint8_t *aad,
+                                 uint32_t *status)
+{
+    KeyImage *ki = (KeyImage *)aligned_alloc(64, sizeof(KeyImage));
+    uint8_t *lds = (uint8_t *)aligned_alloc(256, 160u * 1024u), *lds2 = (uint8_t *)aligned_alloc(256, 160u * 1024u);
+    if (build_key_image(kTabs.sbox, key, (uint32_t)keylen, ki) != 0) {
+        free(ki);
+        free(lds);
+        free(lds2);
+        return -1;
+    }
+    if (split) { /* the image of a run followed by one run (H^512), and by two (H^1024) */
+        for (uint32_t v = 0; v < LayoutSplit::bytes / 16u; ++v) {
+            *(u32x4 *)(lds + 16u * v) = split_image_vec(kTabs.t0, ki, v, 1u);
+            *(u32x4 *)(lds2 + 16u * v) = split_image_vec(kTabs.t0, ki, v, 2u);
+        }
+    } else {
+        fill_lds_win16(lds, kTabs.t0, ki, 0, 1);
+    }
+#define W16_CASE(NRV, SP)                                                                                              \
+    if (ki->rounds == NRV && (split != 0) == SP) {                                                                     \
+        if (is_seal)                                                                                                   \
+            run_win16<NRV, true, SP>(ki, lds, lds2, static_iv, recs, n, src, dst, aad, status);                       \
+        else                                                                                                           \
+            run_win16<NRV, false, SP>(ki, lds, lds2, static_iv, recs, n, src, dst, aad, status);                      \
+    }
+    W16_CASE(10, false) W16_CASE(14, false) W16_CASE(10, true) W16_CASE(14, true)
+#undef W16_CASE
+    free(ki);
+    free(lds);
+    free(lds2);
+    return 0;
+}
+
 extern "C" int model_tls_window(int is_seal, const uint8_t *key, size_t keylen, const uint8_t *static_iv,
                                 const TlsRecord *trecs, size_t n, const uint8_t *src, uint8_t *dst, uint32_t *status,
                                 uint8_t *types, const uint32_t *conn)
@@ -416,7 +537,7 @@ extern "C" int model_bs_keystream(const uint8_t *key, size_t keylen, const uint8
 
 /*
  * The parallel key setup of mi355x_gcm_setup, step by step on the host: the wave multiplies as the XOR of
- * the 64 lane shares (gf_mul_lane_share), the 13 x 128 single-bit products, then every table entry
+ * the 64 lane shares (gf_mul_lane_share), the KEY_IMAGE_TABLES x 128 single-bit products, then every table entry
  * (key_image_store_entry).  Must equal build_key_image byte for byte.
  */
 extern "C" int model_key_image_parallel(const uint8_t *key, size_t keylen, void *out, size_t outlen)
@@ -441,11 +562,13 @@ extern "C" int model_key_image_parallel(const uint8_t *key, size_t keylen, void 
     Gf128 p = h;
     for (int e = 2; e <= MAX_K; ++e)
         pw[e - 1] = p = wave_mul(p, h);
-    p = wave_mul(p, p);                    /* H^16 */
+    pw[MAX_K + 4] = p = wave_mul(p, p);    /* H^16 */
     pw[MAX_K + 2] = p = wave_mul(p, p);    /* H^32 */
     pw[MAX_K] = p = wave_mul(p, p);        /* H^64 */
     pw[MAX_K + 3] = p = wave_mul(p, p);    /* H^128 */
     pw[MAX_K + 1] = p = wave_mul(p, p);    /* H^256 */
+    pw[MAX_K + 5] = p = wave_mul(p, p);    /* H^512 */
+    pw[MAX_K + 6] = p = wave_mul(p, p);    /* H^1024 */
     static Gf128 bits[KEY_IMAGE_TABLES][128];
     for (uint32_t i = 0; i < KEY_IMAGE_TABLES * 128u; ++i)
         bits[i >> 7][i & 127u] = gf_mul_xpow(pw[i >> 7], i & 127u);

@@ -6,6 +6,7 @@ import pytest
 
 import oracle
 import rapido_amd as ra
+from conftest import FAMILIES, kernel_family
 from rapido_amd import records
 
 pytestmark = pytest.mark.gpu
@@ -106,19 +107,16 @@ def test_parallel_key_setup_all_tables(gpu, keylen):
     oracle.batch(True, key, iv, recs, src, want, aad)
     eng = ra.Engine(key)
     d_recs, d_src, d_aad = (torch.from_numpy(a).cuda() for a in (recs.view(np.uint8), src, aad))
-    configs = [("batch", k, None) for k in (1, 2, 4, 8)] + [("window", 4, 0), ("window32", 4, 1 << 30)]
-    for family, k, seg32 in configs:
+    configs = [("batch", k) for k in (1, 2, 4, 8)] + [(f, 4) for f in FAMILIES if f != "batch"]
+    for family, k in configs:
         prev_k = ra.set_lanes_per_record(k)
-        prev_w = ra.set_aead_window_records(0 if family == "batch" else 1 << 30)
-        prev_s = ra.set_seg32_records(seg32 if seg32 is not None else 0)
         try:
-            d_dst = torch.zeros_like(d_src)
-            eng.seal_batch(iv, d_recs.data_ptr(), len(recs), d_src.data_ptr(), d_dst.data_ptr(), d_aad.data_ptr())
-            torch.cuda.synchronize()
+            with kernel_family(family, framing=False):
+                d_dst = torch.zeros_like(d_src)
+                eng.seal_batch(iv, d_recs.data_ptr(), len(recs), d_src.data_ptr(), d_dst.data_ptr(), d_aad.data_ptr())
+                torch.cuda.synchronize()
         finally:
             ra.set_lanes_per_record(prev_k)
-            ra.set_aead_window_records(prev_w)
-            ra.set_seg32_records(prev_s)
         got = d_dst.cpu().numpy()
         for r in recs:
             a, n = int(r["dst"]), int(r["len"]) + 16
@@ -130,8 +128,20 @@ def test_kernel_name_reports_the_launched_family(gpu):
     """ptls_mi355x_kernel_name takes n and the framing flag and names the kernel launch_batch picks."""
     import torch
     ncu = torch.cuda.get_device_properties(0).multi_processor_count
-    assert ra.kernel_name(True, 16, 1) == "mi355x_gcm_win32_seal_aes128"
-    assert ra.kernel_name(False, 32, 1, framing=True) == "mi355x_tls_win32_open_aes256"
+    assert ra.kernel_name(True, 16, 1) == "mi355x_gcm_wins_seal_aes128"
+    assert ra.kernel_name(False, 32, ncu // 3, framing=True) == "mi355x_tls_wins_open_aes256"
+    assert ra.kernel_name(False, 32, ncu, framing=True) == "mi355x_tls_win16_open_aes256"
+    prevs = ra.set_split_records(0)
+    try:
+        assert ra.kernel_name(True, 16, 1) == "mi355x_gcm_win16_seal_aes128"
+        prev16 = ra.set_win16_records(0)
+        try:
+            assert ra.kernel_name(True, 16, 1) == "mi355x_gcm_win32_seal_aes128"
+            assert ra.kernel_name(False, 32, 1, framing=True) == "mi355x_tls_win32_open_aes256"
+        finally:
+            ra.set_win16_records(prev16)
+    finally:
+        ra.set_split_records(prevs)
     assert ra.kernel_name(True, 16, 16 * ncu, framing=True) == "mi355x_tls_winw_seal_aes128"
     assert ra.kernel_name(True, 16, 3 * ncu, framing=True) == "mi355x_tls_win_seal_aes128"
     assert ra.kernel_name(True, 16, 1 << 20) == "mi355x_gcm_seal_aes128_k4"

@@ -11,6 +11,7 @@ import pytest
 
 import oracle
 import rapido_amd as ra
+from conftest import FAMILIES, kernel_family
 from rapido_amd import RECORD_DTYPE
 
 pytestmark = pytest.mark.gpu
@@ -33,40 +34,37 @@ def make_batch(rng, n):
     return recs, src, aad
 
 
-@pytest.mark.parametrize("family", ["window", "window32", "batch"])
+@pytest.mark.parametrize("family", FAMILIES)
 @pytest.mark.parametrize("lanes", [1, 2, 4, 8])
 @pytest.mark.parametrize("keylen", [16, 32])
 def test_fuzz_seal_open(gpu, family, lanes, keylen):
     import torch
-    rng = np.random.default_rng(7000 + 10 * lanes + keylen + {"batch": 0, "window": 1, "window32": 2}[family])
+    rng = np.random.default_rng(7000 + 10 * lanes + keylen + FAMILIES.index(family))
     recs, src, aad = make_batch(rng, 120)
     key = rng.integers(0, 256, keylen, dtype=np.uint8).tobytes()
     iv = rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
-    prev_w = ra.set_aead_window_records(0 if family == "batch" else 1 << 30)
-    prev_32 = ra.set_seg32_records(1 << 30 if family == "window32" else 0)
     prev_k = ra.set_lanes_per_record(lanes)
     try:
-        eng = ra.Engine(key)
-        d_recs = torch.from_numpy(recs.view(np.uint8)).cuda()
-        d_src = torch.from_numpy(src).cuda()
-        d_aad = torch.from_numpy(aad).cuda()
-        d_ct = torch.zeros_like(d_src)
-        d_pt = torch.zeros_like(d_src)
-        d_st = torch.zeros(len(recs), dtype=torch.int32, device="cuda")
-        eng.seal_batch(iv, d_recs.data_ptr(), len(recs), d_src.data_ptr(), d_ct.data_ptr(), d_aad.data_ptr())
-        eng.open_batch(iv, d_recs.data_ptr(), len(recs), d_ct.data_ptr(), d_pt.data_ptr(), d_aad.data_ptr(),
-                       d_st.data_ptr())
-        torch.cuda.synchronize()
-        ct, pt, st = d_ct.cpu().numpy(), d_pt.cpu().numpy(), d_st.cpu().numpy().view(np.uint32)
-        want = np.zeros_like(src)
-        oracle.batch(True, key, iv, recs, src, want, aad)
-        for i, r in enumerate(recs):
-            a, n = int(r["dst"]), int(r["len"])
-            assert bytes(ct[a: a + n + 16]) == bytes(want[a: a + n + 16]), (i, n, int(r["aadlen"]))
-            assert bytes(pt[a: a + n]) == bytes(src[a: a + n]), (i, n)
-        assert (st == recs["len"]).all()
-        eng.close()
+        with kernel_family(family, framing=False):
+            eng = ra.Engine(key)
+            d_recs = torch.from_numpy(recs.view(np.uint8)).cuda()
+            d_src = torch.from_numpy(src).cuda()
+            d_aad = torch.from_numpy(aad).cuda()
+            d_ct = torch.zeros_like(d_src)
+            d_pt = torch.zeros_like(d_src)
+            d_st = torch.zeros(len(recs), dtype=torch.int32, device="cuda")
+            eng.seal_batch(iv, d_recs.data_ptr(), len(recs), d_src.data_ptr(), d_ct.data_ptr(), d_aad.data_ptr())
+            eng.open_batch(iv, d_recs.data_ptr(), len(recs), d_ct.data_ptr(), d_pt.data_ptr(), d_aad.data_ptr(),
+                           d_st.data_ptr())
+            torch.cuda.synchronize()
+            ct, pt, st = d_ct.cpu().numpy(), d_pt.cpu().numpy(), d_st.cpu().numpy().view(np.uint32)
+            want = np.zeros_like(src)
+            oracle.batch(True, key, iv, recs, src, want, aad)
+            for i, r in enumerate(recs):
+                a, n = int(r["dst"]), int(r["len"])
+                assert bytes(ct[a: a + n + 16]) == bytes(want[a: a + n + 16]), (i, n, int(r["aadlen"]))
+                assert bytes(pt[a: a + n]) == bytes(src[a: a + n]), (i, n)
+            assert (st == recs["len"]).all()
+            eng.close()
     finally:
-        ra.set_aead_window_records(prev_w)
-        ra.set_seg32_records(prev_32)
         ra.set_lanes_per_record(prev_k)

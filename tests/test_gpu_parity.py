@@ -7,21 +7,19 @@ import pytest
 
 import oracle
 import rapido_amd as ra
+from conftest import FAMILIES, kernel_family
 from rapido_amd import records
 
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["window", "window32", "batch"])
+@pytest.fixture(autouse=True, params=FAMILIES)
 def aead_kernels(request, engine_lib):
-    """Every test here runs on each kernel family: the window kernels with 64-block segments walked in parallel
-    (the default for batches up to 2048 records), the same with 32-block segments (the default up to one record
-    per CU, so the slot calls), and the batch kernels (K lanes per record)."""
-    prev = ra.set_aead_window_records(0 if request.param == "batch" else 1 << 30)
-    prev32 = ra.set_seg32_records(1 << 30 if request.param == "window32" else 0)
-    yield request.param
-    ra.set_aead_window_records(prev)
-    ra.set_seg32_records(prev32)
+    """Every test here runs on each kernel family (conftest.FAMILIES): the window kernels with 64-block segments
+    walked in parallel, the same with 32-block segments of 8 or of 16 lanes (the default up to one record per CU,
+    so the slot calls), and the batch kernels (K lanes per record)."""
+    with kernel_family(request.param, framing=False):
+        yield request.param
 
 
 def to_dev(a: np.ndarray):

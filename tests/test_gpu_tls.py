@@ -11,22 +11,20 @@ import pytest
 
 import oracle
 import rapido_amd as ra
+from conftest import FAMILIES, kernel_family
 from rapido_amd.records import xorshift64star
 
 pytestmark = pytest.mark.gpu
 GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "tls_records.json")))
 
 
-@pytest.fixture(autouse=True, params=["window", "window32", "batch"])
+@pytest.fixture(autouse=True, params=FAMILIES)
 def framing_kernels(request, engine_lib):
-    """Every framing test runs on each kernel family: the window kernels (64-block segments in parallel, the
-    default for batches up to 16384 records), the same with 32-block segments (the default up to one record per
-    CU) and the batch kernels (4 lanes per record)."""
-    prev = ra.set_tls_window_records(0 if request.param == "batch" else 1 << 30)
-    prev32 = ra.set_seg32_records(1 << 30 if request.param == "window32" else 0)
-    yield request.param
-    ra.set_tls_window_records(prev)
-    ra.set_seg32_records(prev32)
+    """Every framing test runs on each kernel family (conftest.FAMILIES): the window kernels (64-block segments in
+    parallel), the same with 32-block segments, with 32-block segments of 16 lanes (the default up to one record
+    per CU) and the batch kernels (4 lanes per record)."""
+    with kernel_family(request.param, framing=True):
+        yield request.param
 
 
 def dev(a):

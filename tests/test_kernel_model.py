@@ -26,7 +26,12 @@ def model():
 def run(lib, is_seal, K, key, iv, recs, src, dst, aad, st):
     """K = "w4" / "w8": the window kernels' math (64-position segments of 4 / 8 lanes joined with H^64);
     else the K-lane batch walk."""
-    if isinstance(K, str):  # "w4", "w8", or "w8s32" (32-position segments: the single-record latency kernels)
+    if K in ("w16", "split"):  # the 16-lane latency kernels and the split kernels (32-position segments, 2 steps)
+        lib.model_batch_win16.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p,
+                                          C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        rc = lib.model_batch_win16(1 if is_seal else 0, 1 if K == "split" else 0, key, len(key), iv, recs.ctypes.data,
+                                   len(recs), src.ctypes.data, dst.ctypes.data, aad.ctypes.data, st.ctypes.data)
+    elif isinstance(K, str):  # "w4", "w8", or "w8s32" (32-position segments: the single-record latency kernels)
         lanes, _, seglen = K[1:].partition("s")
         assert lib.model_set_window_lanes(int(lanes)) > 0
         assert lib.model_set_window_seglen(int(seglen or 64)) > 0
@@ -59,10 +64,11 @@ def spans(buf, recs, extra):
     return [bytes(buf[int(r["dst"]): int(r["dst"]) + int(r["len"]) + extra]) for r in recs]
 
 
-@pytest.mark.parametrize("K", [1, 2, 4, 8, "w4", "w8", "w8s32"])
+@pytest.mark.parametrize("K", [1, 2, 4, 8, "w4", "w8", "w8s32", "w16", "split"])
 @pytest.mark.parametrize("keylen", [16, 32])
 def test_model_matches_oracle(model, K, keylen):
-    rng = np.random.default_rng((K if isinstance(K, int) else 900 + int(K[1:].replace("s", ""))) * 100 + keylen)
+    seed = K if isinstance(K, int) else {"w16": 9016, "split": 9017}.get(K) or 900 + int(K[1:].replace("s", ""))
+    rng = np.random.default_rng(seed * 100 + keylen)
     recs, src, aad = batch(rng, 150, 700, 48)
     key = rng.integers(0, 256, keylen, dtype=np.uint8).tobytes()
     iv = rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
@@ -78,6 +84,30 @@ def test_model_matches_oracle(model, K, keylen):
     got[int(recs[20]["dst"]) + 1] ^= 0x40
     run(model, False, K, key, iv, recs, got, pt, aad, st)
     assert st[20] == 0xFFFFFFFF and (np.delete(st, 20) == np.delete(recs["len"], 20)).all()
+
+
+@pytest.mark.parametrize("K", ["w16", "split"])
+def test_model_long_records_16_lanes(model, K):
+    """Records of 1..3 runs of 16 segments and beyond (walked whole): the 16-lane and split kernels' joins and the
+    H^8 x H^(8 - j) lane scaling, seal and open against the oracle."""
+    rng = np.random.default_rng(77 if K == "w16" else 78)
+    lens = np.array([0, 15, 496, 497, 1000, 8150, 8190, 8200, 16383, 16384, 16385, 24000, 24560, 24600, 30000, 40000],
+                    np.uint64)
+    aadlens = np.array([0, 13, 5, 31, 16, 5, 17, 0, 5, 13, 5, 3, 16, 40, 5, 20], np.uint64)
+    recs, src_bytes, aad_bytes = records.layout(lens, aadlens, align=16)
+    recs["seq"] = rng.integers(0, 2 ** 63, len(lens), dtype=np.uint64)
+    src = rng.integers(0, 256, src_bytes, dtype=np.uint8)
+    aad = rng.integers(0, 256, aad_bytes, dtype=np.uint8)
+    key = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+    iv = rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    got, want = np.zeros_like(src), np.zeros_like(src)
+    st = np.zeros(len(recs), np.uint32)
+    run(model, True, K, key, iv, recs, src, got, aad, st)
+    oracle.batch(True, key, iv, recs, src, want, aad)
+    assert spans(got, recs, 16) == spans(want, recs, 16)
+    pt = np.zeros_like(src)
+    run(model, False, K, key, iv, recs, got, pt, aad, st)
+    assert (st == recs["len"]).all()
 
 
 def test_model_tls_records_all_sizes(model):
