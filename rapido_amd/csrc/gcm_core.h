@@ -997,6 +997,9 @@ struct Record {
  * lanes that hold them; payload block 0 goes to its aligned grid position q0 = out16 mod K at the
  * minimal step count ceil((q0 + C + 1) / K).
  */
+#ifndef GCM_PAIR_STORES
+#define GCM_PAIR_STORES 0 /* 1: K = 4 walks store whole 128-byte lines (lane_walk; measured slower) */
+#endif
 #ifndef GCM_ALIGN_MIN_T
 #define GCM_ALIGN_MIN_T 32u
 #endif
@@ -1699,6 +1702,20 @@ GCM_HD u32x4 shr_bytes(u32x4 v, uint32_t n)
     return o;
 }
 
+#ifndef GCM_NT_LOADS
+#define GCM_NT_LOADS 0
+#endif
+/* a record block's 16-byte load (GCM_NT_LOADS: marked non-temporal, so the streamed input does not displace the
+ * half-written output lines from L2) */
+GCM_HD u32x4 walk_load(const uint8_t *p)
+{
+#if defined(__HIP_DEVICE_COMPILE__) && GCM_NT_LOADS
+    return __builtin_nontemporal_load((const u32x4_u *)p);
+#else
+    return *(const u32x4_u *)p;
+#endif
+}
+
 /*
  * Address of lane j's 16-byte load in step t of walk wk (lane_walk): the AAD or payload block at the lane's grid
  * position, the received tag for the length block of an open, or `dummy` (steps with nothing to read).  A partial
@@ -1818,6 +1835,36 @@ GCM_HD u32x4 lane_walk_seg(const uint8_t *lds, uint32_t lanesel, const uint32_t 
      * value, P = A_(t-1) * H^K, runs inside the AES of step t (aes_ghash_fused), then
      * A_t = P ^ X_t.  A_(-1) = 0, and A_(T-1) is the lane's sum.
      */
+    /*
+     * Paired stores (K = 4): a step writes a 64-byte piece of a record, half of a 128-byte line.  Lines left half
+     * written are written back as two partial requests, which measured 1.12-1.20x the algorithmic write traffic
+     * (scripts/pmc_lengths.py; K = 8, whole lines per step, 1.00x).  A lane therefore holds a block that falls in the
+     * first half of a line and stores it together with the next step's block, the second half (its address + 64).
+     */
+    constexpr bool PAIRST = GCM_PAIR_STORES && K == 4;
+    u32x4 pend_v = {0u, 0u, 0u, 0u};
+    uint32_t pend_c = 0xffffffffu; /* payload block of the held store (none: ~0) */
+    /*
+     * The schedule is static: blocks of even steps are held, odd steps store the held block and their own.  t is
+     * wave-uniform, so this is a scalar branch; walks start on even steps (t0), and a record whose payload is 128-byte
+     * aligned (every 256-byte record slot) then pairs exactly the two halves of each line.
+     */
+    auto put = [&](uint32_t t, uint32_t c, u32x4 o) {
+        if constexpr (PAIRST) {
+            if ((t & 1u) == 0u) {
+                if (pend_c != 0xffffffffu) /* (a lane's payload blocks are consecutive steps: not reached) */
+                    *(u32x4_u *)(out + 16u * pend_c) = pend_v;
+                pend_v = o;
+                pend_c = c;
+                return;
+            }
+            if (pend_c != 0xffffffffu) {
+                *(u32x4_u *)(out + 16u * pend_c) = pend_v;
+                pend_c = 0xffffffffu;
+            }
+        }
+        *(u32x4_u *)(out + 16u * c) = o;
+    };
     auto step = [&](uint32_t t, u32x4 cur) {
         GCM_OPAQUE(t);
         const int32_t p = (int32_t)(j + K * t) - (int32_t)wk.pad;
@@ -1873,13 +1920,13 @@ GCM_HD u32x4 lane_walk_seg(const uint8_t *lds, uint32_t lanesel, const uint32_t 
                 data = insert_byte(data, flen, ctype);
                 const u32x4 o = data ^ ks;
                 if (clen == 16u)
-                    *(u32x4_u *)(out + 16u * c) = o;
+                    put(t, c, o);
                 else
                     store_partial(out + 16u * c, clen, o);
                 X = mask_tail(o, clen);
             } else if (clen >= 16u) {
                 const u32x4 o = data ^ ks;
-                *(u32x4_u *)(out + 16u * c) = o;
+                put(t, c, o);
                 X = SEAL ? o : data;
             } else {
                 if (SEAL) {
@@ -1932,39 +1979,43 @@ GCM_HD u32x4 lane_walk_seg(const uint8_t *lds, uint32_t lanesel, const uint32_t 
     if (!FRAME && !use_seg && valid && rec.aadlen != 0u && rec.aadlen < 16u && j == wk.pad)
         bufA = load_partial(ad, rec.aadlen);
     else
-        bufA = *(const u32x4_u *)fetch_ptr(t0);
+        bufA = walk_load(fetch_ptr(t0));
     if (PF >= 3) {
         /*
          * Prefetch three steps ahead (window kernels at one wave per SIMD, where nothing else hides a load's
          * latency behind a step): four buffers, four steps per trip.
          */
-        u32x4 b1 = *(const u32x4_u *)fetch_ptr(t0 + 1u), b2 = *(const u32x4_u *)fetch_ptr(t0 + 2u);
+        u32x4 b1 = walk_load(fetch_ptr(t0 + 1u)), b2 = walk_load(fetch_ptr(t0 + 2u));
         for (uint32_t t = t0; t < Tmax; t += 4u) {
-            const u32x4 b3 = *(const u32x4_u *)fetch_ptr(t + 3u);
+            const u32x4 b3 = walk_load(fetch_ptr(t + 3u));
             step(t, bufA);
-            bufA = *(const u32x4_u *)fetch_ptr(t + 4u);
+            bufA = walk_load(fetch_ptr(t + 4u));
             if (t + 1u < Tmax)
                 step(t + 1u, b1);
-            b1 = *(const u32x4_u *)fetch_ptr(t + 5u);
+            b1 = walk_load(fetch_ptr(t + 5u));
             if (t + 2u < Tmax)
                 step(t + 2u, b2);
-            b2 = *(const u32x4_u *)fetch_ptr(t + 6u);
+            b2 = walk_load(fetch_ptr(t + 6u));
             if (t + 3u < Tmax)
                 step(t + 3u, b3);
         }
     } else {
         for (uint32_t t = t0; t < Tmax; t += 2u) {
-            const u32x4 bufB = *(const u32x4_u *)fetch_ptr(t + 1u);
+            const u32x4 bufB = walk_load(fetch_ptr(t + 1u));
             GCM_WALK_STAMP(9);
             step(t, bufA);
             GCM_WALK_STAMP(10);
-            bufA = *(const u32x4_u *)fetch_ptr(t + 2u);
+            bufA = walk_load(fetch_ptr(t + 2u));
             if (t + 1u < Tmax)
                 step(t + 1u, bufB);
             GCM_WALK_STAMP(11);
         }
     }
     GCM_WALK_STAMP(12);
+    if constexpr (PAIRST) {
+        if (pend_c != 0xffffffffu) /* a first half with no second half in this walk */
+            *(u32x4_u *)(out + 16u * pend_c) = pend_v;
+    }
     /* scale the chain by H^(pad + g - q_last(j)) (make_walk) */
     if (LY::gh5) {
         /* H^e, e = 4 - slot in 1..4, from the nibble tables of H^2 (slot 0) and H^1 (slot 1) */

@@ -22,9 +22,11 @@ from rapido_amd import records  # noqa: E402
 LENGTHS = [int(x) for x in os.environ.get("PMC_LENGTHS", "1392,1400,1408,1424,16384,16368").split(",")]
 TOTAL = int(os.environ.get("PMC_BYTES", str(1 << 30)))
 ALIGN = int(os.environ.get("PMC_ALIGN", "256"))
+LANES = [int(x) for x in os.environ.get("PMC_LANES", "4").split(",")]
 
 out = []
-for L in LENGTHS:
+for K, L in [(k, l) for k in LANES for l in LENGTHS]:
+    ra.set_lanes_per_record(K)
     n = max(1, TOTAL // L)
     lengths = np.full(n, L, dtype=np.uint64)
     recs, src_bytes, aad_bytes = records.layout(lengths, np.full(n, 5, dtype=np.uint64), align=ALIGN)
@@ -45,7 +47,7 @@ for L in LENGTHS:
     ev[1].record()
     torch.cuda.synchronize()
     ms = ev[0].elapsed_time(ev[1])
-    out.append({"len": L, "n": n, "read": n * (L + 5 + 40), "write": n * (L + 16), "ms": round(ms, 4),
+    out.append({"lanes": K, "len": L, "n": n, "read": n * (L + 5 + 40), "write": n * (L + 16), "ms": round(ms, 4),
                 "gibps": round(n * L / 2 ** 30 / (ms / 1e3), 1), "launches": 3})
     del d_src, d_dst, d_recs, d_aad
     eng.close()
