@@ -285,6 +285,41 @@ size_t ptls_mi355x_tls_plan_send(size_t len, uint32_t type, uint64_t *seq, uint6
 int ptls_mi355x_tls_parse_records(const uint8_t *wire, size_t len, uint64_t src_off, uint64_t *seq, uint64_t dst_off,
                                   ptls_mi355x_tls_record_t *recs, size_t max, size_t *nrecs, size_t *consumed);
 
+/* ---- 5. batched record layer over host buffers (csrc/record_layer.c) ----
+ * One traffic direction of one connection, for an application with its own record layer: picotls hands such an
+ * application the traffic secret through its update_traffic_key callback (lib/picotls.c:1206-1211), and rapido
+ * derives each connection's key and IV from it (ptls_hkdf_expand_label "key"/"iv", then derive_connection_aead_iv,
+ * lib/rapido.c:127-150); INTEGRATION.md section 4 shows the callback.  Each call moves a whole window between
+ * host memory and the GPU in one copy each way and seals or opens all its records in one launch; it returns when
+ * the results are in the caller's buffer.  A layer is used by one host thread at a time. */
+typedef struct st_ptls_mi355x_record_layer_t ptls_mi355x_record_layer_t;
+typedef struct st_ptls_mi355x_iovec_t { /* layout of ptls_iovec_t (include/picotls.h) */
+    const uint8_t *base;
+    size_t len;
+} ptls_mi355x_iovec_t;
+/* a layer for key (16 or 32 bytes) and the 12-byte static IV, starting at record sequence number seq; NULL on error
+ * (ptls_mi355x_record_layer_last_error) */
+ptls_mi355x_record_layer_t *ptls_mi355x_record_layer_new(const void *key, size_t key_size, const void *iv12, uint64_t seq);
+void ptls_mi355x_record_layer_free(ptls_mi355x_record_layer_t *rl);
+uint64_t ptls_mi355x_record_layer_get_seq(const ptls_mi355x_record_layer_t *rl);
+void ptls_mi355x_record_layer_set_seq(ptls_mi355x_record_layer_t *rl, uint64_t seq);
+/* ptls_send (lib/picotls.c:4969-4988) for a window: every fragment is framed as records of <= 16384 bytes of inner
+ * content type `type` (buffer_push_encrypted_records, :664-684), all sealed in one launch; the records go to out
+ * back to back (*outlen bytes, *nrecords records; each record is fragment + 22 bytes) and seq advances past them.
+ * Returns 0, or -1 (capacity below the wire size, or an engine error; nothing written, seq unchanged). */
+int ptls_mi355x_record_layer_seal(ptls_mi355x_record_layer_t *rl, const ptls_mi355x_iovec_t *frags, size_t nfrags,
+                                  uint8_t type, void *out, size_t capacity, size_t *outlen, size_t *nrecords);
+/* ptls_receive / handle_input (lib/picotls.c:4757-4842, 4913-4947) for a window: the complete application_data
+ * records at the start of in are opened in one launch; their plaintexts (padding and content type removed) go to out
+ * back to back, in order, up to the first record that fails (its alert is returned: 20 BAD_RECORD_MAC, 10
+ * UNEXPECTED_MESSAGE; 50 DECODE_ERROR for a bad length field), the first record of another inner content type, an
+ * incomplete record or a record of another outer type -- those are left for the caller's picotls path.
+ * *consumed = wire bytes of the delivered records, seq advances by *nrecords.  -1: engine error or out too small
+ * for the first record. */
+int ptls_mi355x_record_layer_open(ptls_mi355x_record_layer_t *rl, const void *in, size_t inlen, size_t *consumed,
+                                  void *out, size_t capacity, size_t *outlen, size_t *nrecords);
+const char *ptls_mi355x_record_layer_last_error(void);
+
 /* ---- tuning / introspection ---- */
 /* lanes per record used by the batch kernels (1, 2, 4 or 8; default 4); returns the previous value, or -1 */
 int ptls_mi355x_set_lanes_per_record(int k);

@@ -62,7 +62,9 @@ EXPORTED_FUNCTIONS = (
     "ptls_mi355x_set_work_ticket_origin", "ptls_mi355x_set_seg32_records", "ptls_mi355x_tls_plan_send",
     "ptls_mi355x_tls_parse_records", "ptls_mi355x_tls_open_records_ex", "ptls_mi355x_aes_new", "ptls_mi355x_aes_free",
     "ptls_mi355x_aes_ecb", "ptls_mi355x_aes_ecb_batch", "ptls_mi355x_set_win16_records",
-    "ptls_mi355x_set_split_records",
+    "ptls_mi355x_set_split_records", "ptls_mi355x_record_layer_new", "ptls_mi355x_record_layer_free",
+    "ptls_mi355x_record_layer_get_seq", "ptls_mi355x_record_layer_set_seq", "ptls_mi355x_record_layer_seal",
+    "ptls_mi355x_record_layer_open", "ptls_mi355x_record_layer_last_error",
 )
 EXPORTED_OBJECTS = ("ptls_mi355x_aes128gcm", "ptls_mi355x_aes256gcm", "ptls_mi355x_aes128ctr",
                     "ptls_mi355x_aes256ctr", "ptls_mi355x_aes128ecb", "ptls_mi355x_aes256ecb")
@@ -151,6 +153,16 @@ def lib() -> C.CDLL:
         L.ptls_mi355x_set_seg32_records.restype = sz
         L.ptls_mi355x_set_work_ticket_origin.restype = C.c_uint32
         L.ptls_mi355x_tls_open_records_multi.argtypes = [vp, vp, vp, vp, sz, vp, vp, vp, vp, vp]
+        if hasattr(L, "ptls_mi355x_record_layer_new"):  # (absent from older builds used in A/B timing runs)
+            L.ptls_mi355x_record_layer_new.argtypes = [vp, sz, vp, u64]
+            L.ptls_mi355x_record_layer_new.restype = vp
+            L.ptls_mi355x_record_layer_free.argtypes = [vp]
+            L.ptls_mi355x_record_layer_get_seq.argtypes = [vp]
+            L.ptls_mi355x_record_layer_get_seq.restype = u64
+            L.ptls_mi355x_record_layer_set_seq.argtypes = [vp, u64]
+            L.ptls_mi355x_record_layer_seal.argtypes = [vp, vp, sz, C.c_uint8, vp, sz, C.POINTER(sz), C.POINTER(sz)]
+            L.ptls_mi355x_record_layer_open.argtypes = [vp, vp, sz, C.POINTER(sz), vp, sz, C.POINTER(sz), C.POINTER(sz)]
+            L.ptls_mi355x_record_layer_last_error.restype = C.c_char_p
         for name in ("ptls_mi355x_set_win16_records", "ptls_mi355x_set_split_records"):
             if hasattr(L, name):  # (absent from older builds used in A/B timing runs)
                 getattr(L, name).argtypes = [sz]
@@ -420,6 +432,69 @@ class AesKeys:
     def close(self) -> None:
         if self.handle:
             lib().ptls_mi355x_aes_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class _IoVec(C.Structure):
+    _fields_ = [("base", C.c_void_p), ("len", C.c_size_t)]
+
+
+class RecordLayer:
+    """ptls_mi355x_record_layer_t: one traffic direction of a connection, windows of records between host memory
+    and the GPU (include/ptls_mi355x.h section 5)."""
+
+    def __init__(self, key: bytes, static_iv: bytes, seq: int = 0):
+        assert len(static_iv) == 12
+        self.handle = lib().ptls_mi355x_record_layer_new(_cbuf(key), len(key), _cbuf(static_iv), seq)
+        if not self.handle:
+            raise RuntimeError("ptls_mi355x_record_layer_new failed: " + lib().ptls_mi355x_record_layer_last_error().decode())
+
+    @property
+    def seq(self) -> int:
+        return lib().ptls_mi355x_record_layer_get_seq(self.handle)
+
+    @seq.setter
+    def seq(self, v: int) -> None:
+        lib().ptls_mi355x_record_layer_set_seq(self.handle, v)
+
+    def seal(self, fragments, content_type: int = 23, capacity: int = None):
+        """-> (wire bytes, record count); every fragment framed as records of <= 16384 bytes."""
+        bufs = [_cbuf(f) for f in fragments]
+        iov = (_IoVec * max(len(fragments), 1))()
+        for i, (b, f) in enumerate(zip(bufs, fragments)):
+            iov[i].base = C.cast(b, C.c_void_p)
+            iov[i].len = len(f)
+        if capacity is None:
+            capacity = sum(len(f) + (len(f) + 16383) // 16384 * TLS_OVERHEAD for f in fragments)
+        out = C.create_string_buffer(max(capacity, 1))
+        olen, nrec = sz(), sz()
+        rc = lib().ptls_mi355x_record_layer_seal(self.handle, iov, len(fragments), content_type, out, capacity,
+                                                 C.byref(olen), C.byref(nrec))
+        if rc != 0:
+            raise RuntimeError("record_layer_seal failed: " + lib().ptls_mi355x_record_layer_last_error().decode())
+        return out.raw[:olen.value], nrec.value
+
+    def open(self, wire: bytes, capacity: int = None):
+        """-> (return code: 0 or a TLS alert, plaintext, wire bytes consumed, record count)."""
+        if capacity is None:
+            capacity = len(wire)
+        out = C.create_string_buffer(max(capacity, 1))
+        cons, olen, nrec = sz(), sz(), sz()
+        rc = lib().ptls_mi355x_record_layer_open(self.handle, _cbuf(wire), len(wire), C.byref(cons), out, capacity,
+                                                 C.byref(olen), C.byref(nrec))
+        if rc < 0:
+            raise RuntimeError("record_layer_open failed: " + lib().ptls_mi355x_record_layer_last_error().decode())
+        return rc, out.raw[:olen.value], cons.value, nrec.value
+
+    def close(self) -> None:
+        if self.handle:
+            lib().ptls_mi355x_record_layer_free(self.handle)
             self.handle = None
 
     def __del__(self):

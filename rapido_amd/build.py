@@ -1,7 +1,7 @@
 """Builds the MI355X engine library in-tree (no JIT cache, so the .so travels with the repo).
 
     rapido_amd/_lib/libptls_mi355x.so  <- csrc/gcm_engine.hip (hipcc, --offload-arch=gfx950)
-                                         + csrc/aead_slot.c, csrc/tls_records.c (host C, gcc)
+                                         + csrc/aead_slot.c, csrc/tls_records.c, csrc/record_layer.c (host C, gcc)
     tests/cpp/_build/libkernel_model.so <- tests/cpp/kernel_model.cpp (host clang++, test only)
 
 Rebuilds only when a source or header is newer than the output.
@@ -48,7 +48,8 @@ def _run(cmd, verbose):
     return r
 
 
-C_SRCS = [os.path.join(CSRC, f) for f in ("aead_slot.c", "tls_records.c")]
+C_SRCS = [os.path.join(CSRC, f) for f in ("aead_slot.c", "tls_records.c", "record_layer.c")]
+ROCM_INCLUDE = "/opt/rocm/include"
 C_OBJS = [os.path.join(OBJDIR, os.path.basename(f)[:-2] + ".o") for f in C_SRCS]
 
 
@@ -61,8 +62,8 @@ def build_engine(verbose: bool = False, force: bool = False) -> str:
              verbose)
     for c_src, c_obj in zip(C_SRCS, C_OBJS):
         if force or _newer(c_obj, [c_src] + HEADERS):
-            _run([CC, "-std=gnu99", "-O2", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter", "-c", c_src, "-o",
-                  c_obj], verbose)
+            _run([CC, "-std=gnu99", "-O2", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter", "-D__HIP_PLATFORM_AMD__",
+                  "-I" + ROCM_INCLUDE, "-c", c_src, "-o", c_obj], verbose)
     if force or _newer(LIB, [hip_obj] + C_OBJS):
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, hip_obj] + C_OBJS, verbose)
     return LIB

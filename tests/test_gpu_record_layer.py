@@ -1,0 +1,137 @@
+"""The batched record layer over host buffers (include/ptls_mi355x.h section 5, rapido_amd/csrc/record_layer.c)
+against the oracle's TLS 1.3 record functions, which reproduce the reference ptls_send / ptls_receive outputs
+(tests/test_tls_records.py, tests/golden/tls_records.json).
+
+A rapido send window is up to 16 records of 16 KiB (lib/rapido.c:2115-2126), each record one cleartext that
+rapido_prepare_record produced; a connection's key and IV come from the traffic secret (lib/rapido.c:135-150),
+with the connection id XORed into the IV's first four bytes (derive_connection_aead_iv, lib/rapido.c:123-133)."""
+import struct
+
+import numpy as np
+import pytest
+
+import oracle
+import rapido_amd as ra
+from conftest import FAMILIES, kernel_family
+
+pytestmark = pytest.mark.gpu
+
+
+def conn_iv(iv: bytes, conn_id: int) -> bytes:
+    """derive_connection_aead_iv (lib/rapido.c:123-133): BE32(first 4 IV bytes) ^ connection id."""
+    msb = struct.unpack(">I", iv[:4])[0] ^ conn_id
+    return struct.pack(">I", msb) + iv[4:]
+
+
+def oracle_window(key, iv, seq, frags, ctype=23):
+    out = b""
+    for f in frags:
+        for off in range(0, max(len(f), 1), 16384):
+            if not f:
+                break
+            out += oracle.tls_seal_record(key, iv, seq, ctype, f[off:off + 16384])
+            seq += 1
+    return out, seq
+
+
+@pytest.fixture(params=["split", "window16", "batch"])
+def family(request, gpu):
+    with kernel_family(request.param, framing=True):
+        yield request.param
+
+
+@pytest.mark.parametrize("keylen", [16, 32])
+def test_send_window_matches_ptls_send(family, keylen):
+    rng = np.random.default_rng(keylen)
+    key = rng.integers(0, 256, keylen, dtype=np.uint8).tobytes()
+    iv = conn_iv(rng.integers(0, 256, 12, dtype=np.uint8).tobytes(), 3)
+    frags = [rng.integers(0, 256, 16384, dtype=np.uint8).tobytes() for _ in range(16)]
+    rl = ra.RecordLayer(key, iv, seq=41)
+    wire, n = rl.seal(frags)
+    want, seq = oracle_window(key, iv, 41, frags)
+    assert n == 16 and rl.seq == seq == 57
+    assert wire == want
+    # ragged fragments, one over 16 KiB (two records), empty ones (no record), in the same call
+    frags2 = [b"", rng.integers(0, 256, 1, dtype=np.uint8).tobytes(), rng.integers(0, 256, 40000, dtype=np.uint8).tobytes(),
+              rng.integers(0, 256, 1399, dtype=np.uint8).tobytes(), b""]
+    wire2, n2 = rl.seal(frags2)
+    want2, seq2 = oracle_window(key, iv, 57, frags2)
+    assert wire2 == want2 and n2 == 1 + 3 + 1 and rl.seq == seq2
+    rl.close()
+
+
+@pytest.mark.parametrize("keylen", [16, 32])
+def test_receive_window_round_trip(family, keylen):
+    rng = np.random.default_rng(100 + keylen)
+    key = rng.integers(0, 256, keylen, dtype=np.uint8).tobytes()
+    iv = rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    frags = [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in rng.integers(1, 16385, 32)]
+    wire, _ = oracle_window(key, iv, 7, frags)
+    rx = ra.RecordLayer(key, iv, seq=7)
+    rc, pt, consumed, n = rx.open(wire)
+    assert (rc, consumed, n) == (0, len(wire), 32)
+    assert pt == b"".join(frags) and rx.seq == 39
+    # a window that ends inside a record: the complete ones only
+    wire2, _ = oracle_window(key, iv, 39, frags[:3])
+    rc, pt, consumed, n = rx.open(wire2[:-10])
+    assert (rc, n) == (0, 2) and consumed == len(oracle_window(key, iv, 39, frags[:2])[0])
+    assert pt == frags[0] + frags[1] and rx.seq == 41
+    rx.close()
+
+
+def test_receive_stops_at_first_failure(family):
+    """picotls returns the alert of the first bad record and does not advance seq past it (lib/picotls.c:650-652);
+    the records before it are delivered."""
+    rng = np.random.default_rng(5)
+    key, iv = bytes(range(16)), bytes(range(12))
+    frags = [rng.integers(0, 256, 3000, dtype=np.uint8).tobytes() for _ in range(8)]
+    wire = bytearray(oracle_window(key, iv, 0, frags)[0])
+    rec = 5 + 3000 + 1 + 16
+    wire[5 * rec + 100] ^= 1  # record 5's ciphertext
+    rx = ra.RecordLayer(key, iv)
+    rc, pt, consumed, n = rx.open(bytes(wire))
+    assert rc == 20 and n == 5 and consumed == 5 * rec and pt == b"".join(frags[:5]) and rx.seq == 5
+    # the window resent intact from record 5 on continues the stream
+    rc, pt, consumed, n = rx.open(oracle_window(key, iv, 5, frags[5:])[0])
+    assert rc == 0 and n == 3 and pt == b"".join(frags[5:]) and rx.seq == 8
+
+
+def test_receive_leaves_other_content_types(family):
+    """A handshake record (post-handshake message, inner type 22) or an alert record (outer type 21) ends the
+    delivered run: it is left, with its seq, for the caller's picotls path."""
+    key, iv = bytes(range(32)), bytes(range(12))
+    a, b, c = b"a" * 1000, b"b" * 2000, b"c" * 300
+    w_a, s = oracle_window(key, iv, 0, [a])
+    w_hs = oracle.tls_seal_record(key, iv, s, 22, b"\x04\x00\x00\x00")
+    w_c, _ = oracle_window(key, iv, s + 1, [c])
+    rx = ra.RecordLayer(key, iv)
+    rc, pt, consumed, n = rx.open(w_a + w_hs + w_c)
+    assert (rc, pt, consumed, n, rx.seq) == (0, a, len(w_a), 1, 1)
+    alert = bytes([21, 3, 3, 0, 2, 2, 40])
+    rx.seq = 0
+    rc, pt, consumed, n = rx.open(w_a + alert + w_c)
+    assert (rc, pt, consumed, n, rx.seq) == (0, a, len(w_a), 1, 1)
+    # padding and the all-zero record (no content type: UNEXPECTED_MESSAGE)
+    padded = oracle.tls_seal_record(key, iv, 1, 23, b, pad=100)
+    nothing = oracle.tls_seal_record(key, iv, 2, 0, b"", pad=8)
+    rx.seq = 1
+    rc, pt, consumed, n = rx.open(padded + nothing)
+    assert (rc, pt, n, rx.seq) == (10, b, 1, 2)
+
+
+def test_capacity_and_errors(gpu):
+    key, iv = bytes(16), bytes(12)
+    rl = ra.RecordLayer(key, iv)
+    with pytest.raises(RuntimeError):
+        rl.seal([b"x" * 100], capacity=100)
+    assert rl.seq == 0
+    wire, n = rl.seal([b"x" * 100])
+    assert n == 1 and len(wire) == 122
+    rx = ra.RecordLayer(key, iv)
+    with pytest.raises(RuntimeError):
+        rx.open(wire, capacity=50)
+    assert rx.seq == 0
+    rc, pt, consumed, n = rx.open(wire[:3])
+    assert (rc, pt, consumed, n) == (0, b"", 0, 0)
+    rc, pt, consumed, n = rx.open(bytes([23, 3, 3, 0xff, 0xff]) + bytes(10))
+    assert rc == 50 and n == 0  # DECODE_ERROR: length field above 16640
