@@ -79,9 +79,13 @@ def main(tag, label):
             others.setdefault(w, {})[k] = {"FETCH_SIZE_kB": fw[k]["FETCH_SIZE"],
                                            "WRITE_SIZE_kB": ww.get(k, {}).get("WRITE_SIZE"), "hbm_bytes_per_launch": b}
         allt[w] = t
+    sq16 = {}
+    p16 = os.path.join(src, "pmc_sq_16k-aes128", "run_counter_collection.csv")
+    if os.path.exists(p16):
+        sq16 = {k: v for k, v in counters(p16).items() if "setup" not in k}
     with open(os.path.join(dst, f"{label}_pmc.json"), "w") as f:
         json.dump({"workload": "1400 (bench.py default)", "correction": "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024",
-                   "kernels": pmc, "other_workloads": others}, f, indent=1)
+                   "kernels": pmc, "other_workloads": others, "sq_16k-aes128": sq16}, f, indent=1)
     with open(tpath, "w") as f:
         json.dump(allt, f, indent=1)
     print(json.dumps(pmc, indent=1))
