@@ -289,9 +289,9 @@ int ptls_mi355x_tls_parse_records(const uint8_t *wire, size_t len, uint64_t src_
  * One traffic direction of one connection, for an application with its own record layer: picotls hands such an
  * application the traffic secret through its update_traffic_key callback (lib/picotls.c:1206-1211), and rapido
  * derives each connection's key and IV from it (ptls_hkdf_expand_label "key"/"iv", then derive_connection_aead_iv,
- * lib/rapido.c:127-150); INTEGRATION.md section 4 shows the callback.  Each call moves a whole window between
- * host memory and the GPU in one copy each way and seals or opens all its records in one launch; it returns when
- * the results are in the caller's buffer.  A layer is used by one host thread at a time. */
+ * lib/rapido.c:127-150); INTEGRATION.md section 4 shows the callback.  Each call seals or opens all the records of
+ * a whole window in one launch; it returns when the results are in the caller's buffer.  A layer is used by one host
+ * thread at a time. */
 typedef struct st_ptls_mi355x_record_layer_t ptls_mi355x_record_layer_t;
 typedef struct st_ptls_mi355x_iovec_t { /* layout of ptls_iovec_t (include/picotls.h) */
     const uint8_t *base;
@@ -319,6 +319,21 @@ int ptls_mi355x_record_layer_seal(ptls_mi355x_record_layer_t *rl, const ptls_mi3
 int ptls_mi355x_record_layer_open(ptls_mi355x_record_layer_t *rl, const void *in, size_t inlen, size_t *consumed,
                                   void *out, size_t capacity, size_t *outlen, size_t *nrecords);
 const char *ptls_mi355x_record_layer_last_error(void);
+/* How the bytes travel (record_layer.c): a call whose fragments and output (seal), or input and output (open; out
+ * at least as large as the records' ciphertexts), all lie in ranges registered below runs DIRECT: the kernel reads
+ * and writes them in place, no copy.  Otherwise a window of at most `zero copy bytes` (descriptors, input and
+ * output) is copied into the layer's pinned, mapped staging, which the kernel reads and writes over PCIe (one
+ * launch, one synchronisation); larger windows move by one H2D and one D2H DMA copy.  Results are identical. */
+/* registers host memory [base, base+len) that stays allocated (a connection's socket buffers) for direct calls
+ * (hipHostRegister, mapped); up to 8 ranges per layer.  A range that is already registered (by the application, or
+ * by the layer of the other direction sharing a buffer) is used as it is and left registered on unregister; it must
+ * stay registered while this layer uses it.  0, or -1 (ptls_mi355x_record_layer_last_error). */
+int ptls_mi355x_record_layer_register(ptls_mi355x_record_layer_t *rl, void *base, size_t len);
+/* unregisters a range given to ptls_mi355x_record_layer_register (by its base); 0 or -1.  The layer unregisters
+ * its ranges when freed. */
+int ptls_mi355x_record_layer_unregister(ptls_mi355x_record_layer_t *rl, void *base);
+/* zero-copy limit in bytes (default 4 MiB; 0 = always DMA copies); returns the previous value */
+size_t ptls_mi355x_record_layer_set_zero_copy_bytes(ptls_mi355x_record_layer_t *rl, size_t n);
 
 /* ---- tuning / introspection ---- */
 /* lanes per record used by the batch kernels (1, 2, 4 or 8; default 4); returns the previous value, or -1 */

@@ -64,7 +64,8 @@ EXPORTED_FUNCTIONS = (
     "ptls_mi355x_aes_ecb", "ptls_mi355x_aes_ecb_batch", "ptls_mi355x_set_win16_records",
     "ptls_mi355x_set_split_records", "ptls_mi355x_record_layer_new", "ptls_mi355x_record_layer_free",
     "ptls_mi355x_record_layer_get_seq", "ptls_mi355x_record_layer_set_seq", "ptls_mi355x_record_layer_seal",
-    "ptls_mi355x_record_layer_open", "ptls_mi355x_record_layer_last_error",
+    "ptls_mi355x_record_layer_open", "ptls_mi355x_record_layer_last_error", "ptls_mi355x_record_layer_register",
+    "ptls_mi355x_record_layer_unregister", "ptls_mi355x_record_layer_set_zero_copy_bytes",
 )
 EXPORTED_OBJECTS = ("ptls_mi355x_aes128gcm", "ptls_mi355x_aes256gcm", "ptls_mi355x_aes128ctr",
                     "ptls_mi355x_aes256ctr", "ptls_mi355x_aes128ecb", "ptls_mi355x_aes256ecb")
@@ -163,6 +164,10 @@ def lib() -> C.CDLL:
             L.ptls_mi355x_record_layer_seal.argtypes = [vp, vp, sz, C.c_uint8, vp, sz, C.POINTER(sz), C.POINTER(sz)]
             L.ptls_mi355x_record_layer_open.argtypes = [vp, vp, sz, C.POINTER(sz), vp, sz, C.POINTER(sz), C.POINTER(sz)]
             L.ptls_mi355x_record_layer_last_error.restype = C.c_char_p
+            L.ptls_mi355x_record_layer_register.argtypes = [vp, vp, sz]
+            L.ptls_mi355x_record_layer_unregister.argtypes = [vp, vp]
+            L.ptls_mi355x_record_layer_set_zero_copy_bytes.argtypes = [vp, sz]
+            L.ptls_mi355x_record_layer_set_zero_copy_bytes.restype = sz
         for name in ("ptls_mi355x_set_win16_records", "ptls_mi355x_set_split_records"):
             if hasattr(L, name):  # (absent from older builds used in A/B timing runs)
                 getattr(L, name).argtypes = [sz]
@@ -451,6 +456,7 @@ class RecordLayer:
 
     def __init__(self, key: bytes, static_iv: bytes, seq: int = 0):
         assert len(static_iv) == 12
+        self._registered = {}
         self.handle = lib().ptls_mi355x_record_layer_new(_cbuf(key), len(key), _cbuf(static_iv), seq)
         if not self.handle:
             raise RuntimeError("ptls_mi355x_record_layer_new failed: " + lib().ptls_mi355x_record_layer_last_error().decode())
@@ -492,9 +498,48 @@ class RecordLayer:
             raise RuntimeError("record_layer_open failed: " + lib().ptls_mi355x_record_layer_last_error().decode())
         return rc, out.raw[:olen.value], cons.value, nrec.value
 
+    def set_zero_copy_bytes(self, n: int) -> int:
+        """Windows of at most n staged bytes run zero-copy on the pinned staging (0: DMA copies); -> previous."""
+        return lib().ptls_mi355x_record_layer_set_zero_copy_bytes(self.handle, n)
+
+    def register(self, buf: np.ndarray) -> None:
+        """Registers a long-lived host buffer (a uint8 numpy array) for direct calls: seal_into / open_into on
+        views of registered buffers run with no copy (ptls_mi355x_record_layer_register)."""
+        self._check(lib().ptls_mi355x_record_layer_register(self.handle, buf.ctypes.data, buf.nbytes), "register")
+        self._registered[buf.ctypes.data] = buf  # keeps the memory alive while registered
+
+    def unregister(self, buf: np.ndarray) -> None:
+        self._check(lib().ptls_mi355x_record_layer_unregister(self.handle, buf.ctypes.data), "unregister")
+        self._registered.pop(buf.ctypes.data, None)
+
+    def _check(self, rc: int, what: str) -> None:
+        if rc != 0:
+            raise RuntimeError(f"record_layer_{what} failed: " + lib().ptls_mi355x_record_layer_last_error().decode())
+
+    def seal_into(self, fragments, out: np.ndarray, content_type: int = 23):
+        """seal with the fragments (uint8 numpy views) and the output written in place -> (wire bytes, records)."""
+        iov = (_IoVec * max(len(fragments), 1))()
+        for i, f in enumerate(fragments):
+            iov[i].base = C.c_void_p(f.ctypes.data)
+            iov[i].len = f.nbytes
+        olen, nrec = sz(), sz()
+        self._check(lib().ptls_mi355x_record_layer_seal(self.handle, iov, len(fragments), content_type, out.ctypes.data,
+                                                        out.nbytes, C.byref(olen), C.byref(nrec)), "seal")
+        return olen.value, nrec.value
+
+    def open_into(self, wire: np.ndarray, out: np.ndarray):
+        """open of the records in `wire` (a uint8 numpy view) into `out` -> (rc, plaintext bytes, consumed, records)."""
+        cons, olen, nrec = sz(), sz(), sz()
+        rc = lib().ptls_mi355x_record_layer_open(self.handle, wire.ctypes.data, wire.nbytes, C.byref(cons),
+                                                 out.ctypes.data, out.nbytes, C.byref(olen), C.byref(nrec))
+        if rc < 0:
+            self._check(rc, "open")
+        return rc, olen.value, cons.value, nrec.value
+
     def close(self) -> None:
         if self.handle:
-            lib().ptls_mi355x_record_layer_free(self.handle)
+            lib().ptls_mi355x_record_layer_free(self.handle)  # unregisters its ranges
+            self._registered.clear()
             self.handle = None
 
     def __del__(self):

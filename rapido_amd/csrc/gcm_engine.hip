@@ -1584,6 +1584,7 @@ ptls_mi355x_aesgcm_context_t *ptls_mi355x_aesgcm_new(const void *key, size_t key
     int rc = -1;
     hipDeviceProp_t prop;
     DeviceShared *d = nullptr;
+    g_err[0] = 0;
     if (hipGetDevice(&ctx->device) != hipSuccess || hipGetDeviceProperties(&prop, ctx->device) != hipSuccess ||
         (d = device_shared(ctx->device)) == nullptr)
         goto Fail;
@@ -1591,8 +1592,10 @@ ptls_mi355x_aesgcm_context_t *ptls_mi355x_aesgcm_new(const void *key, size_t key
     ctx->num_cu = prop.multiProcessorCount;
     if (hipMalloc(&ctx->d_ki, sizeof(KeyImage)) != hipSuccess ||
         hipMalloc(&ctx->d_work, WORK_SLOTS * sizeof(uint32_t)) != hipSuccess ||
-        hipEventCreateWithFlags(&ctx->reuse_event, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&ctx->reuse_event, hipEventDisableTiming) != hipSuccess) {
+        snprintf(g_err, sizeof(g_err), "context allocation: %s", hipGetErrorString(hipGetLastError()));
         goto Fail;
+    }
     for (uint32_t i = 0; i < WORK_SLOTS; ++i) {
         ctx->work_base[i] = g_ticket_origin;
         ctx->work_stream[i] = nullptr;
@@ -1604,15 +1607,21 @@ ptls_mi355x_aesgcm_context_t *ptls_mi355x_aesgcm_new(const void *key, size_t key
             goto Fail;
         memcpy(d->h_stage, key, key_size);
         *(volatile int *)(d->h_stage + 64) = -2;
-        if (hipMemsetD32Async((hipDeviceptr_t)ctx->d_work, (int)g_ticket_origin, WORK_SLOTS, d->stream) != hipSuccess)
+        if (hipMemsetD32Async((hipDeviceptr_t)ctx->d_work, (int)g_ticket_origin, WORK_SLOTS, d->stream) != hipSuccess) {
+            snprintf(g_err, sizeof(g_err), "work counters: %s", hipGetErrorString(hipGetLastError()));
             goto Fail;
+        }
+        (void)hipGetLastError(); /* a stale error of an unrelated earlier call is not this launch's */
         hipLaunchKernelGGL(mi355x_gcm_setup, dim3(1), dim3(1024), 0, d->stream, d->h_stage_dev, (uint32_t)key_size,
                            ctx->d_ki, (int *)(d->h_stage_dev + 64));
         const hipError_t e1 = hipGetLastError(), e2 = hipStreamSynchronize(d->stream);
         memset(d->h_stage, 0, key_size);
         rc = *(volatile int *)(d->h_stage + 64);
-        if (e1 != hipSuccess || e2 != hipSuccess || rc != 0)
+        if (e1 != hipSuccess || e2 != hipSuccess || rc != 0) {
+            snprintf(g_err, sizeof(g_err), "key setup kernel: launch %s, synchronize %s, status %d",
+                     hipGetErrorString(e1), hipGetErrorString(e2), rc);
             goto Fail;
+        }
     }
     return ctx;
 Fail:
@@ -1921,6 +1930,7 @@ ptls_mi355x_aes_context_t *ptls_mi355x_aes_new(const void *key, size_t key_size)
             goto Fail;
         memcpy(d->h_stage, key, key_size);
         *(volatile int *)(d->h_stage + 64) = -2;
+        (void)hipGetLastError();
         hipLaunchKernelGGL(mi355x_aes_setup, dim3(1), dim3(64), 0, d->stream, d->h_stage_dev, (uint32_t)key_size,
                            ctx->d_keys, (int *)(d->h_stage_dev + 64));
         const hipError_t e1 = hipGetLastError(), e2 = hipStreamSynchronize(d->stream);

@@ -1,10 +1,13 @@
 """Host-to-host latency of the batched record layer (include/ptls_mi355x.h section 5): one rapido send window
 (16 records of 16 KiB, lib/rapido.c:2115-2126) sealed from host memory into host memory, and the same window opened
-back, through ptls_mi355x_record_layer_seal / _open (pinned staging, one H2D copy, one launch, one D2H copy).
+back, through ptls_mi355x_record_layer_seal / _open, for each way the bytes can travel (record_layer.c):
+  copy      -- the Python bytes go through the layer's pinned staging, one H2D and one D2H DMA copy;
+  zero_copy -- the same staging, read and written by the kernel over PCIe (the default up to 4 MiB);
+  direct    -- fragments, wire and plaintext in registered host buffers, no copy at all (seal_into / open_into).
 
     python scripts/record_layer_latency.py [--reps 50] [--records 16] [--size 16384]
 
-Prints one JSON line: median microseconds per window for seal and open, and the payload rate.
+Prints one JSON line per mode: median microseconds per window for seal and open, and the payload rate.
 """
 import argparse
 import json
@@ -32,28 +35,52 @@ def main():
     key = rng.integers(0, 256, a.keylen, dtype=np.uint8).tobytes()
     iv = rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
     frags = [rng.integers(0, 256, a.size, dtype=np.uint8).tobytes() for _ in range(a.records)]
-    tx, rx = ra.RecordLayer(key, iv), ra.RecordLayer(key, iv)
-    seal_us, open_us = [], []
-    for i in range(a.reps + 5):
-        t0 = time.perf_counter()
-        wire, n = tx.seal(frags)
-        t1 = time.perf_counter()
-        rc, pt, consumed, m = rx.open(wire)
-        t2 = time.perf_counter()
-        assert rc == 0 and m == n == a.records and consumed == len(wire)
-        if i >= 5:
-            seal_us.append((t1 - t0) * 1e6)
-            open_us.append((t2 - t1) * 1e6)
-    assert pt == b"".join(frags)
-    s, o = statistics.median(seal_us), statistics.median(open_us)
     payload = a.records * a.size
-    print(json.dumps({"what": f"record layer, {a.records} x {a.size} B window, host buffers in and out (median of "
-                              f"{a.reps}, us, including the Python binding's buffer copies)",
-                      "kernel": ra.kernel_name(True, a.keylen, a.records, framing=True),
-                      "seal_us": round(s, 1), "open_us": round(o, 1),
-                      "seal_gibps": round(payload / 2 ** 30 / (s / 1e6), 2),
-                      "open_gibps": round(payload / 2 ** 30 / (o / 1e6), 2)}))
-
+    for mode in ("copy", "zero_copy", "direct"):
+        tx, rx = ra.RecordLayer(key, iv), ra.RecordLayer(key, iv)
+        if mode == "copy":
+            tx.set_zero_copy_bytes(0)
+            rx.set_zero_copy_bytes(0)
+        if mode == "direct":
+            send = np.frombuffer(b"".join(frags), np.uint8).copy()
+            views = [send[i * a.size:(i + 1) * a.size] for i in range(a.records)]
+            wirebuf = np.zeros(payload + a.records * 64, np.uint8)
+            ptbuf = np.zeros(payload + a.records * 64, np.uint8)
+            tx.register(send)
+            tx.register(wirebuf)
+            rx.register(wirebuf)
+            rx.register(ptbuf)
+        seal_us, open_us = [], []
+        for i in range(a.reps + 5):
+            if mode == "direct":
+                t0 = time.perf_counter()
+                wlen, n = tx.seal_into(views, wirebuf)
+                t1 = time.perf_counter()
+                rc, olen, consumed, m = rx.open_into(wirebuf[:wlen], ptbuf)
+                t2 = time.perf_counter()
+                assert rc == 0 and m == n == a.records and consumed == wlen and olen == payload
+            else:
+                t0 = time.perf_counter()
+                wire, n = tx.seal(frags)
+                t1 = time.perf_counter()
+                rc, pt, consumed, m = rx.open(wire)
+                t2 = time.perf_counter()
+                assert rc == 0 and m == n == a.records and consumed == len(wire)
+            rx.seq = tx.seq
+            if i >= 5:
+                seal_us.append((t1 - t0) * 1e6)
+                open_us.append((t2 - t1) * 1e6)
+        got = ptbuf[:payload].tobytes() if mode == "direct" else pt
+        assert got == b"".join(frags)
+        s, o = statistics.median(seal_us), statistics.median(open_us)
+        print(json.dumps({"what": f"record layer, {a.records} x {a.size} B window, host buffers in and out (median of "
+                                  f"{a.reps}, us, including the Python binding)", "mode": mode,
+                          "kernel": ra.kernel_name(True, a.keylen, a.records, framing=True),
+                          "seal_us": round(s, 1), "open_us": round(o, 1),
+                          "seal_gibps": round(payload / 2 ** 30 / (s / 1e6), 2),
+                          "open_gibps": round(payload / 2 ** 30 / (o / 1e6), 2)}), flush=True)
+        tx.close()
+        rx.close()
 
 if __name__ == "__main__":
     main()

@@ -40,13 +40,26 @@ def family(request, gpu):
         yield request.param
 
 
+@pytest.fixture(params=["zero_copy", "copy"])
+def transport(request, gpu):
+    return request.param
+
+
+def layer(transport, key, iv, seq=0):
+    """A record layer whose windows go through the pinned staging zero-copy (the default) or by DMA copies."""
+    rl = ra.RecordLayer(key, iv, seq=seq)
+    if transport == "copy":
+        rl.set_zero_copy_bytes(0)
+    return rl
+
+
 @pytest.mark.parametrize("keylen", [16, 32])
-def test_send_window_matches_ptls_send(family, keylen):
+def test_send_window_matches_ptls_send(family, transport, keylen):
     rng = np.random.default_rng(keylen)
     key = rng.integers(0, 256, keylen, dtype=np.uint8).tobytes()
     iv = conn_iv(rng.integers(0, 256, 12, dtype=np.uint8).tobytes(), 3)
     frags = [rng.integers(0, 256, 16384, dtype=np.uint8).tobytes() for _ in range(16)]
-    rl = ra.RecordLayer(key, iv, seq=41)
+    rl = layer(transport, key, iv, seq=41)
     wire, n = rl.seal(frags)
     want, seq = oracle_window(key, iv, 41, frags)
     assert n == 16 and rl.seq == seq == 57
@@ -61,13 +74,13 @@ def test_send_window_matches_ptls_send(family, keylen):
 
 
 @pytest.mark.parametrize("keylen", [16, 32])
-def test_receive_window_round_trip(family, keylen):
+def test_receive_window_round_trip(family, transport, keylen):
     rng = np.random.default_rng(100 + keylen)
     key = rng.integers(0, 256, keylen, dtype=np.uint8).tobytes()
     iv = rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
     frags = [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in rng.integers(1, 16385, 32)]
     wire, _ = oracle_window(key, iv, 7, frags)
-    rx = ra.RecordLayer(key, iv, seq=7)
+    rx = layer(transport, key, iv, seq=7)
     rc, pt, consumed, n = rx.open(wire)
     assert (rc, consumed, n) == (0, len(wire), 32)
     assert pt == b"".join(frags) and rx.seq == 39
@@ -79,7 +92,7 @@ def test_receive_window_round_trip(family, keylen):
     rx.close()
 
 
-def test_receive_stops_at_first_failure(family):
+def test_receive_stops_at_first_failure(family, transport):
     """picotls returns the alert of the first bad record and does not advance seq past it (lib/picotls.c:650-652);
     the records before it are delivered."""
     rng = np.random.default_rng(5)
@@ -88,7 +101,7 @@ def test_receive_stops_at_first_failure(family):
     wire = bytearray(oracle_window(key, iv, 0, frags)[0])
     rec = 5 + 3000 + 1 + 16
     wire[5 * rec + 100] ^= 1  # record 5's ciphertext
-    rx = ra.RecordLayer(key, iv)
+    rx = layer(transport, key, iv)
     rc, pt, consumed, n = rx.open(bytes(wire))
     assert rc == 20 and n == 5 and consumed == 5 * rec and pt == b"".join(frags[:5]) and rx.seq == 5
     # the window resent intact from record 5 on continues the stream
@@ -96,7 +109,7 @@ def test_receive_stops_at_first_failure(family):
     assert rc == 0 and n == 3 and pt == b"".join(frags[5:]) and rx.seq == 8
 
 
-def test_receive_leaves_other_content_types(family):
+def test_receive_leaves_other_content_types(family, transport):
     """A handshake record (post-handshake message, inner type 22) or an alert record (outer type 21) ends the
     delivered run: it is left, with its seq, for the caller's picotls path."""
     key, iv = bytes(range(32)), bytes(range(12))
@@ -104,7 +117,7 @@ def test_receive_leaves_other_content_types(family):
     w_a, s = oracle_window(key, iv, 0, [a])
     w_hs = oracle.tls_seal_record(key, iv, s, 22, b"\x04\x00\x00\x00")
     w_c, _ = oracle_window(key, iv, s + 1, [c])
-    rx = ra.RecordLayer(key, iv)
+    rx = layer(transport, key, iv)
     rc, pt, consumed, n = rx.open(w_a + w_hs + w_c)
     assert (rc, pt, consumed, n, rx.seq) == (0, a, len(w_a), 1, 1)
     alert = bytes([21, 3, 3, 0, 2, 2, 40])
@@ -135,3 +148,66 @@ def test_capacity_and_errors(gpu):
     assert (rc, pt, consumed, n) == (0, b"", 0, 0)
     rc, pt, consumed, n = rx.open(bytes([23, 3, 3, 0xff, 0xff]) + bytes(10))
     assert rc == 50 and n == 0  # DECODE_ERROR: length field above 16640
+
+
+def page_buffer(nbytes: int) -> np.ndarray:
+    """A page-aligned uint8 host buffer (a long-lived socket buffer to register)."""
+    raw = np.zeros(nbytes + 4096, np.uint8)
+    off = (-raw.ctypes.data) % 4096
+    return raw[off:off + nbytes]
+
+
+@pytest.mark.parametrize("keylen", [16, 32])
+def test_direct_window_in_registered_buffers(family, keylen):
+    """Fragments, wire and plaintext in registered host buffers: the kernels read and write them in place over
+    PCIe (no staging copy); same bytes as ptls_send / ptls_receive."""
+    rng = np.random.default_rng(200 + keylen)
+    key = rng.integers(0, 256, keylen, dtype=np.uint8).tobytes()
+    iv = conn_iv(rng.integers(0, 256, 12, dtype=np.uint8).tobytes(), 9)
+    sizes = [16384] * 12 + [1, 40000, 1399, 0]
+    sendbuf, wirebuf, ptbuf = page_buffer(sum(sizes) + 4096), page_buffer(1 << 20), page_buffer(1 << 20)
+    frags, pos = [], 0
+    for n in sizes:  # fragments scattered through the send buffer, out of order
+        pos += int(rng.integers(0, 64))
+        sendbuf[pos:pos + n] = rng.integers(0, 256, n, dtype=np.uint8)
+        frags.append(sendbuf[pos:pos + n])
+        pos += n
+    frags = frags[::-1]
+    tx, rx = ra.RecordLayer(key, iv, seq=3), ra.RecordLayer(key, iv, seq=3)
+    for b in (sendbuf, wirebuf):
+        tx.register(b)
+    for b in (wirebuf, ptbuf):
+        rx.register(b)
+    out = wirebuf[100:]  # an unaligned start inside the registered range
+    wlen, nrec = tx.seal_into(frags, out)
+    want, seq = oracle_window(key, iv, 3, [f.tobytes() for f in frags])
+    assert out[:wlen].tobytes() == want and nrec == seq - 3 and tx.seq == seq
+    # open in place: plaintexts closed up at the start of ptbuf, the rest of the slots zeroed
+    ptbuf[:] = 0xee
+    rc, olen, consumed, n = rx.open_into(out[:wlen], ptbuf)
+    assert (rc, consumed, n) == (0, wlen, nrec) and rx.seq == seq
+    assert ptbuf[:olen].tobytes() == b"".join(f.tobytes() for f in frags)
+    slots = wlen - 21 * nrec  # the records' plaintext slots (type byte included): zeroed past the plaintext
+    assert not ptbuf[olen:slots].any() and (ptbuf[slots:] == 0xee).all()
+    # a tampered record: the ones before it delivered, nothing of it or behind it left in the buffer
+    rx.seq = 3
+    wire = out[:wlen].copy()
+    before, seq_before = oracle_window(key, iv, 3, [f.tobytes() for f in frags[:3]])
+    tampered = wire.copy()
+    tampered[len(before) + 10] ^= 0x80  # the tag of the record of frags[3] (1 byte)
+    wirebuf[:wlen] = tampered
+    ptbuf[:] = 0xee
+    rc, olen, consumed, n = rx.open_into(wirebuf[:wlen], ptbuf)
+    assert (rc, n, consumed, rx.seq) == (20, seq_before - 3, len(before), seq_before)
+    assert ptbuf[:olen].tobytes() == b"".join(f.tobytes() for f in frags[:3])
+    assert not ptbuf[olen:slots].any()
+    # input and output outside the registered ranges: through the staging, same bytes
+    plain = np.zeros(wlen, np.uint8)
+    rx.seq = 3
+    rc, olen2, consumed, n = rx.open_into(wire, plain)
+    assert rc == 0 and plain[:olen2].tobytes() == b"".join(f.tobytes() for f in frags)
+    tx.unregister(sendbuf)
+    with pytest.raises(RuntimeError):
+        tx.unregister(sendbuf)
+    tx.close()
+    rx.close()
