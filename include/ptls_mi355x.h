@@ -272,7 +272,7 @@ int ptls_mi355x_tls_open_records_ex(ptls_mi355x_aesgcm_context_t *ctx, const voi
  *  plan_send: splits len bytes at src_off into <= 16384-byte fragments with consecutive seq
  *    from *seq, records laid out back to back from dst_off (buffer_push_encrypted_records,
  *    lib/picotls.c:664-684).  Returns the number of records (recs may be NULL to count);
- *    *wire_len = bytes the records occupy; *seq advanced past them.  Writes at most max.
+ *    *wire_len = bytes the records occupy; *seq advanced past them (unchanged when counting).  Writes at most max.
  *  parse_records: walks the complete records at the start of wire[0..len) (parse_record +
  *    parse_record_header fast path, lib/picotls.c:4243-4268): type 23 records only, one
  *    descriptor each (src = src_off + offset, plaintext slots back to back from dst_off,

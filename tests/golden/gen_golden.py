@@ -25,7 +25,8 @@ through oracle/ref_fusion_harness.c:
                           records (their wire bytes built by oracle.tls_seal_record).
 
 The known-answer vectors transcribed from the reference's own tests (t/fusion.c,
-t/picotls.c, deps/cifra/src/testmodes.c) live in kats.json and are data only.
+t/picotls.c, deps/cifra/src/testmodes.c) are data inlined in tests/test_oracle.py and
+tests/test_gpu_cipher.py, not generated here.
 """
 import hashlib
 import json
