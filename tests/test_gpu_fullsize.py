@@ -112,3 +112,62 @@ def test_full_size_round_trip(gpu, name, keylen, n, length):
         a, ln = int(recs[i]["src"]), int(recs[i]["len"])
         assert not d_pt[a: a + ln].any()
     eng.close()
+
+
+def test_configs4_sharded_batch_equals_whole(gpu):
+    """BASELINE.json configs[4] on one device: 8 M x 1400 B AES-128 records cut into the 8 per-GPU shards bench.py's
+    ranks take (bench.rank_shard: 1 M each, no collective), each sealed by its own context on its own stream, give
+    exactly the bytes of one launch over the whole batch; every shard then opens with every record verified."""
+    import os
+    import sys
+
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import rank_shard
+
+    world, per = 8, 1 << 20
+    n = world * per
+    lengths = np.full(n, 1400, np.uint64)
+    recs, src_bytes, aad_bytes = records.layout(lengths, np.full(n, 5, dtype=np.uint64), align=256)
+    recs["seq"] = np.arange(n, dtype=np.uint64)  # rank r's first seq is its first global record (bench.measure)
+    aad = np.zeros(aad_bytes, dtype=np.uint8)
+    aad[: 5 * n] = records.tls_aad(lengths)
+    key, iv = bytes(range(16)), bytes(range(0xA0, 0xAC))
+    dev = gpu
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(4)
+    d_src = torch.randint(0, 256, (src_bytes,), dtype=torch.uint8, device=dev, generator=gen)
+    d_whole = torch.zeros_like(d_src)
+    d_shard = torch.zeros_like(d_src)
+    d_recs = torch.from_numpy(recs.view(np.uint8)).to(dev)
+    d_aad = torch.from_numpy(aad).to(dev)
+    dsize = recs.dtype.itemsize
+    whole = ra.Engine(key)
+    whole.seal_batch(iv, d_recs.data_ptr(), n, d_src.data_ptr(), d_whole.data_ptr(), d_aad.data_ptr())
+    ranks = [(ra.Engine(key), torch.cuda.Stream(dev)) for _ in range(world)]
+    torch.cuda.synchronize(dev)  # the buffers' fills on torch's stream precede the shard streams' launches
+    for r, (eng, s) in enumerate(ranks):
+        first, cnt = rank_shard(r, world, per)
+        eng.seal_batch(iv, d_recs.data_ptr() + first * dsize, cnt, d_src.data_ptr(), d_shard.data_ptr(),
+                       d_aad.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize(dev)
+    assert torch.equal(d_whole, d_shard)
+    d_pt = torch.zeros_like(d_src)
+    d_st = torch.zeros(n, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)
+    for r, (eng, s) in enumerate(ranks):
+        first, cnt = rank_shard(r, world, per)
+        eng.open_batch(iv, d_recs.data_ptr() + first * dsize, cnt, d_shard.data_ptr(), d_pt.data_ptr(),
+                       d_aad.data_ptr(), d_st.data_ptr() + 4 * first, s.cuda_stream)
+    torch.cuda.synchronize(dev)
+    assert (d_st.cpu().numpy().view(np.uint32) == 1400).all()
+    # one sampled record of every shard is bit-exact against the oracle
+    for r in range(world):
+        i = r * per + int(np.random.default_rng(r).integers(0, per))
+        a = int(recs[i]["src"])
+        want = oracle.seal(key, oracle.build_iv(iv, i), aad[int(recs[i]["aad"]): int(recs[i]["aad"]) + 5].tobytes(),
+                           d_src[a: a + 1400].cpu().numpy().tobytes())
+        assert d_shard[a: a + 1416].cpu().numpy().tobytes() == want
+    for eng, _ in ranks:
+        eng.close()
+    whole.close()
