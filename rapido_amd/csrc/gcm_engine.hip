@@ -53,6 +53,9 @@ constexpr int WG_THREADS = MI355X_WG_THREADS; /* 16 waves: 4 per SIMD */
 #ifndef GCM_LANE_MAJOR
 #define GCM_LANE_MAJOR 1
 #endif
+#ifndef GCM_SPLIT_GLDS
+#define GCM_SPLIT_GLDS 1 /* split window kernels fill their LDS image by LDS DMA (split_body) */
+#endif
 /*
  * Phase timestamps of the window kernels' first workgroup (measurement builds only, scripts/window_phases.py):
  * s_memrealtime (100 MHz) at entry, after the LDS fill, after the first pass's walk, after its barrier,
@@ -689,6 +692,23 @@ __device__ __forceinline__ void split_body(const KeyImage *__restrict__ ki, uint
         static_assert(NV % THREADS == 0u, "whole passes");
         const u32x4 *gk = (const u32x4 *)&ki->gh[0][0][0][0];
         const u32x4 *gr = (const u32x4 *)(m == 2u ? &ki->gh1024[0][0][0] : &ki->gh512[0][0][0]);
+#if GCM_SPLIT_GLDS
+        /*
+         * LDS DMA (global_load_lds_dwordx4): a wave-instruction writes 64 x 16 B contiguously at a wave-uniform LDS
+         * base, lane l's vector from its own global address, with no VGPR round trip and no ds_write transfer.  At one
+         * wave per SIMD the walk has registers to spare, so nothing spills (unlike the 3-wave win16 layout).
+         */
+        const uint32_t wbase = __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
+#pragma unroll
+        for (uint32_t q = 0; q < PER; ++q) {
+            const uint32_t i = threadIdx.x + q * THREADS;
+            const u32x4 *g = i < 0x1000u ? win_aes + i : i < LW::gh_run / 16u ? gk + (i - 0x1000u) : gr + (i - LW::gh_run / 16u);
+            __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1))) *)g,
+                                             (void __attribute__((address_space(3))) *)(lds + 16u * (q * THREADS + wbase)),
+                                             16, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* this wave's DMA has landed; the barrier below covers the rest */
+#else
         u32x4 v[PER];
 #pragma unroll
         for (uint32_t q = 0; q < PER; ++q) {
@@ -698,6 +718,7 @@ __device__ __forceinline__ void split_body(const KeyImage *__restrict__ ki, uint
 #pragma unroll
         for (uint32_t q = 0; q < PER; ++q)
             *(u32x4 *)(lds + 16u * (threadIdx.x + q * THREADS)) = v[q];
+#endif
     }
     uint32_t rk[4 * (NR + 1)];
 #pragma unroll
