@@ -28,11 +28,24 @@
 #if defined(GCM_WIN_TIMING) && GCM_WIN_TIMING
 /* measurement build (scripts/window_phases.py): stamps inside the record walk of workgroup 0, thread 0 */
 __device__ uint64_t g_win_times[16];
+#ifndef GCM_STAMP_BLOCK
+#define GCM_STAMP_BLOCK 0 /* the workgroup whose phases are stamped (split kernels: 3 r + k for run k of record r) */
+#endif
 #define GCM_WALK_STAMP(i)                                                                                              \
     do {                                                                                                               \
-        if (blockIdx.x == 0 && threadIdx.x == 0)                                                                       \
+        if (blockIdx.x == GCM_STAMP_BLOCK && threadIdx.x == 0)                                                         \
             g_win_times[i] = __builtin_amdgcn_s_memrealtime();                                                         \
     } while (0)
+/* split kernels: stamps of workgroup GCM_STAMP_BLOCK, and (6, 7) of the run that finishes record 0 */
+#define SPLIT_STAMP(i) GCM_WALK_STAMP(i)
+#define SPLIT_STAMP_LAST(i)                                                                                            \
+    do {                                                                                                               \
+        if (r == 0u && threadIdx.x == 0)                                                                               \
+            g_win_times[i] = __builtin_amdgcn_s_memrealtime();                                                         \
+    } while (0)
+#else
+#define SPLIT_STAMP(i) ((void)0)
+#define SPLIT_STAMP_LAST(i) ((void)0)
 #endif
 #include "gcm_core.h"
 #include "../../include/ptls_mi355x.h"
@@ -664,6 +677,7 @@ __device__ __forceinline__ void split_body(const KeyImage *__restrict__ ki, uint
     const uint32_t R = !valid || whole ? 1u : (nseg + SPLIT_RUNSEG - 1u) / SPLIT_RUNSEG;
     if (k >= R)
         return; /* uniform: the whole workgroup leaves before any barrier */
+    SPLIT_STAMP(0);
     const uint32_t m = R - 1u - k; /* runs after this one */
     /* segment of slot 0 (negative: run 0's leading slots are empty), and the run's real segments */
     const int32_t first = (int32_t)nseg - (int32_t)(SPLIT_RUNSEG * (R - k));
@@ -725,18 +739,27 @@ __device__ __forceinline__ void split_body(const KeyImage *__restrict__ ki, uint
     for (int i = 0; i < 4 * (NR + 1); ++i)
         rk[i] = ki->rk[i];
     __syncthreads();
+    SPLIT_STAMP(1);
 
     const uint32_t n1 = iv1 ^ bswap32((uint32_t)(rec.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)rec.seq);
     const uint32_t n0 = conn != nullptr ? iv0 ^ bswap32(conn[r]) : iv0;
     u32x4 part = lane_walk_seg<NR, KW, SEAL, FRAME, LW, 1>(lds, lanesel, rk, j, rec, active, Tw, n0, n1, n2, src, dst, aad,
                                                           (const uint8_t *)descs, ctype, !whole, sw, t0);
+    SPLIT_STAMP(2);
     part = dpp_xor_reduce4<KW>(part);
-    if (R > 1u)
-        __threadfence(); /* this run's output reaches L2 before its arrival ticket (window_finish may overwrite it) */
+    /*
+     * open: this run's plaintext reaches L2 before its arrival ticket, since the last run's window_finish reads it back
+     * (padding strip) or zeroes it (failure).  seal: window_finish writes only the tag and the header, bytes no run
+     * writes, so nothing orders this run's ciphertext (kernel completion does); the publishing lane's fence below
+     * still orders its partial before its ticket.  Waiting for the stores here cost ~1.3 us per window.
+     */
+    if (R > 1u && !SEAL)
+        __threadfence();
     __syncthreads(); /* every lane's scaling multiply is done: the sums may overwrite H^1.. */
     if (active && j == 0u)
         *(u32x4 *)(lds + LW::parts + slot * 16u) = part;
     __syncthreads();
+    SPLIT_STAMP(3);
     /* the run's local join over its ns_run real segments; li = slot - off is the index among them */
     const uint32_t off = first < 0 ? (uint32_t)(-first) : 0u;
     const uint32_t li = slot - off;
@@ -762,10 +785,13 @@ __device__ __forceinline__ void split_body(const KeyImage *__restrict__ ki, uint
             *s_ticket = atomicAdd(&tickets[r], 1u);
         }
     }
+    SPLIT_STAMP(4);
     if (R > 1u) {
         __syncthreads();
+        SPLIT_STAMP(5);
         if (*s_ticket != R - 1u)
             return; /* not the last run of the record */
+        SPLIT_STAMP_LAST(6);
         __threadfence(); /* acquire: every run's partial and output */
         if (real && li == 0u) {
             acc = u32x4{0u, 0u, 0u, 0u};
@@ -781,6 +807,7 @@ __device__ __forceinline__ void split_body(const KeyImage *__restrict__ ki, uint
     __syncthreads();
     acc = *(const u32x4 *)(lds + LW::parts);
     window_finish<SEAL, FRAME>(acc, valid, rec, plen, r, threadIdx.x, THREADS, dst, status, types);
+    SPLIT_STAMP_LAST(7);
 }
 
 } // namespace
