@@ -309,6 +309,16 @@ void ptls_mi355x_record_layer_set_seq(ptls_mi355x_record_layer_t *rl, uint64_t s
  * Returns 0, or -1 (capacity below the wire size, or an engine error; nothing written, seq unchanged). */
 int ptls_mi355x_record_layer_seal(ptls_mi355x_record_layer_t *rl, const ptls_mi355x_iovec_t *frags, size_t nfrags,
                                   uint8_t type, void *out, size_t capacity, size_t *outlen, size_t *nrecords);
+/* The send windows of several connections of one session in ONE launch: layers[l] seals frags[l][0..nfrags[l]) into
+ * out[l] (capacity[l]) exactly as ptls_mi355x_record_layer_seal would, outlen[l] / nrecords[l] its results, each
+ * layer's seq advanced.  The layers must share the key and IV bytes 4..11: rapido's connections of a session, whose
+ * IVs differ by the connection id in bytes 0..3 (derive_connection_aead_iv, lib/rapido.c:123-133); the kernel applies
+ * each record's difference (ptls_mi355x_tls_seal_records_multi).  Runs on layers[0]'s stream and staging; direct when
+ * every fragment and output lies in a range registered with any of the layers.  0, or -1 (nothing written, no seq
+ * advanced: a capacity, a layer with another key or IV, or an engine error). */
+int ptls_mi355x_record_layer_seal_multi(ptls_mi355x_record_layer_t *const *layers, size_t nlayers,
+                                        const ptls_mi355x_iovec_t *const *frags, const size_t *nfrags, uint8_t type,
+                                        void *const *out, const size_t *capacity, size_t *outlen, size_t *nrecords);
 /* ptls_receive / handle_input (lib/picotls.c:4757-4842, 4913-4947) for a window: the complete application_data
  * records at the start of in are opened in one launch; their plaintexts (padding and content type removed) go to out
  * back to back, in order, up to the first record that fails (its alert is returned: 20 BAD_RECORD_MAC, 10
@@ -318,6 +328,14 @@ int ptls_mi355x_record_layer_seal(ptls_mi355x_record_layer_t *rl, const ptls_mi3
  * for the first record. */
 int ptls_mi355x_record_layer_open(ptls_mi355x_record_layer_t *rl, const void *in, size_t inlen, size_t *consumed,
                                   void *out, size_t capacity, size_t *outlen, size_t *nrecords);
+/* The receive windows of several connections of one session in ONE launch: layers[l] opens in[l][0..inlen[l]) into
+ * out[l] (capacity[l]) exactly as ptls_mi355x_record_layer_open would; alerts[l] is what that call would have
+ * returned (0, a TLS alert, or -1 for out[l] too small for its first record), consumed[l] / outlen[l] / nrecords[l]
+ * its results.  Same session rule and stream as ptls_mi355x_record_layer_seal_multi.  0, or -1 (engine error: nothing
+ * consumed, no seq advanced). */
+int ptls_mi355x_record_layer_open_multi(ptls_mi355x_record_layer_t *const *layers, size_t nlayers, const void *const *in,
+                                        const size_t *inlen, size_t *consumed, void *const *out, const size_t *capacity,
+                                        size_t *outlen, size_t *nrecords, int *alerts);
 const char *ptls_mi355x_record_layer_last_error(void);
 /* How the bytes travel (record_layer.c): a call whose fragments and output (seal), or input and output (open; out
  * at least as large as the records' ciphertexts), all lie in ranges registered below runs DIRECT: the kernel reads

@@ -66,6 +66,7 @@ EXPORTED_FUNCTIONS = (
     "ptls_mi355x_record_layer_get_seq", "ptls_mi355x_record_layer_set_seq", "ptls_mi355x_record_layer_seal",
     "ptls_mi355x_record_layer_open", "ptls_mi355x_record_layer_last_error", "ptls_mi355x_record_layer_register",
     "ptls_mi355x_record_layer_unregister", "ptls_mi355x_record_layer_set_zero_copy_bytes",
+    "ptls_mi355x_record_layer_seal_multi", "ptls_mi355x_record_layer_open_multi",
 )
 EXPORTED_OBJECTS = ("ptls_mi355x_aes128gcm", "ptls_mi355x_aes256gcm", "ptls_mi355x_aes128ctr",
                     "ptls_mi355x_aes256ctr", "ptls_mi355x_aes128ecb", "ptls_mi355x_aes256ecb")
@@ -168,6 +169,8 @@ def lib() -> C.CDLL:
             L.ptls_mi355x_record_layer_unregister.argtypes = [vp, vp]
             L.ptls_mi355x_record_layer_set_zero_copy_bytes.argtypes = [vp, sz]
             L.ptls_mi355x_record_layer_set_zero_copy_bytes.restype = sz
+            L.ptls_mi355x_record_layer_seal_multi.argtypes = [vp, sz, vp, vp, C.c_uint8, vp, vp, vp, vp]
+            L.ptls_mi355x_record_layer_open_multi.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, vp, vp]
         for name in ("ptls_mi355x_set_win16_records", "ptls_mi355x_set_split_records"):
             if hasattr(L, name):  # (absent from older builds used in A/B timing runs)
                 getattr(L, name).argtypes = [sz]
@@ -547,6 +550,60 @@ class RecordLayer:
             self.close()
         except Exception:
             pass
+
+
+def record_layer_seal_multi(layers, windows, content_type: int = 23, outs=None):
+    """One launch for the send windows of several connections of a session (ptls_mi355x_record_layer_seal_multi):
+    windows[l] is a list of fragments for layers[l], bytes or uint8 numpy views (for direct calls, with `outs` a
+    list of uint8 numpy output buffers) -> [(wire bytes, record count)] per layer (wire length with `outs`)."""
+    n = len(layers)
+    keep, iov_arrays = [], []
+    for frags in windows:
+        iov = (_IoVec * max(len(frags), 1))()
+        for i, f in enumerate(frags):
+            if isinstance(f, np.ndarray):
+                iov[i].base = C.c_void_p(f.ctypes.data)
+                iov[i].len = f.nbytes
+            else:
+                b = _cbuf(f)
+                keep.append(b)
+                iov[i].base = C.cast(b, C.c_void_p)
+                iov[i].len = len(f)
+        iov_arrays.append(iov)
+    frag_ptrs = (C.c_void_p * n)(*[C.cast(a, C.c_void_p) for a in iov_arrays])
+    nfr = (sz * n)(*[len(w) for w in windows])
+    if outs is None:
+        caps = [sum(len(f) + (len(f) + 16383) // 16384 * TLS_OVERHEAD for f in w) for w in windows]
+        bufs = [C.create_string_buffer(max(c, 1)) for c in caps]
+        out_ptrs = (C.c_void_p * n)(*[C.cast(o, C.c_void_p) for o in bufs])
+    else:
+        caps = [o.nbytes for o in outs]
+        out_ptrs = (C.c_void_p * n)(*[o.ctypes.data for o in outs])
+    capv = (sz * n)(*caps)
+    olen, nrec = (sz * n)(), (sz * n)()
+    handles = (C.c_void_p * n)(*[lr.handle for lr in layers])
+    if lib().ptls_mi355x_record_layer_seal_multi(handles, n, frag_ptrs, nfr, content_type, out_ptrs, capv, olen, nrec):
+        raise RuntimeError("record_layer_seal_multi failed: " + lib().ptls_mi355x_record_layer_last_error().decode())
+    if outs is None:
+        return [(bufs[i].raw[:olen[i]], nrec[i]) for i in range(n)]
+    return [(olen[i], nrec[i]) for i in range(n)]
+
+
+def record_layer_open_multi(layers, wires):
+    """One launch for the receive windows of several connections of a session (ptls_mi355x_record_layer_open_multi):
+    wires[l] (bytes) for layers[l] -> [(alert, plaintext, wire bytes consumed, record count)] per layer."""
+    n = len(layers)
+    bufs = [_cbuf(w) for w in wires]
+    in_ptrs = (C.c_void_p * n)(*[C.cast(b, C.c_void_p) for b in bufs])
+    inl = (sz * n)(*[len(w) for w in wires])
+    outs = [C.create_string_buffer(max(len(w), 1)) for w in wires]
+    out_ptrs = (C.c_void_p * n)(*[C.cast(o, C.c_void_p) for o in outs])
+    caps = (sz * n)(*[len(w) for w in wires])
+    cons, olen, nrec, alerts = (sz * n)(), (sz * n)(), (sz * n)(), (C.c_int * n)()
+    handles = (C.c_void_p * n)(*[lr.handle for lr in layers])
+    if lib().ptls_mi355x_record_layer_open_multi(handles, n, in_ptrs, inl, cons, out_ptrs, caps, olen, nrec, alerts):
+        raise RuntimeError("record_layer_open_multi failed: " + lib().ptls_mi355x_record_layer_last_error().decode())
+    return [(alerts[i], outs[i].raw[:olen[i]], cons[i], nrec[i]) for i in range(n)]
 
 
 def tls_plan_send(length: int, seq: int, content_type: int = 23, src_off: int = 0, dst_off: int = 0):

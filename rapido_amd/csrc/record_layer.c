@@ -46,6 +46,8 @@ typedef struct {
 
 struct st_ptls_mi355x_record_layer_t {
     ptls_mi355x_aesgcm_context_t *ctx;
+    uint8_t key[32]; /* the key, to check that the layers of a _multi call share it (zeroed on free) */
+    size_t key_size;
     uint8_t iv[12];
     uint64_t seq;
     hipStream_t stream;
@@ -156,6 +158,8 @@ ptls_mi355x_record_layer_t *ptls_mi355x_record_layer_new(const void *key, size_t
         free(rl);
         return NULL;
     }
+    memcpy(rl->key, key, key_size);
+    rl->key_size = key_size;
     memcpy(rl->iv, iv12, 12);
     rl->seq = seq;
     rl->zero_copy_bytes = RL_ZERO_COPY_DEFAULT;
@@ -182,6 +186,7 @@ void ptls_mi355x_record_layer_free(ptls_mi355x_record_layer_t *rl)
     }
     free(rl->recs);
     ptls_mi355x_aesgcm_free(rl->ctx);
+    memset(rl->key, 0, sizeof(rl->key));
     memset(rl->iv, 0, sizeof(rl->iv));
     free(rl);
 }
@@ -239,174 +244,374 @@ int ptls_mi355x_record_layer_unregister(ptls_mi355x_record_layer_t *rl, void *ba
     return -1;
 }
 
-int ptls_mi355x_record_layer_seal(ptls_mi355x_record_layer_t *rl, const ptls_mi355x_iovec_t *frags, size_t nfrags,
-                                  uint8_t type, void *out, size_t capacity, size_t *outlen, size_t *nrecords)
+/* device address of [p, p+len) inside a range registered with any of the layers, else NULL */
+static uint8_t *dev_addr_any(ptls_mi355x_record_layer_t *const *layers, size_t n, const void *p, size_t len)
 {
-    size_t nrec = 0, srcbytes = 0, wire = 0;
-    for (size_t f = 0; f < nfrags; ++f) {
-        uint64_t s = 0;
-        size_t w = 0;
-        nrec += ptls_mi355x_tls_plan_send(frags[f].len, type, &s, 0, 0, NULL, 0, &w);
-        srcbytes += frags[f].len;
-        wire += w;
+    for (size_t i = 0; i < n; ++i) {
+        uint8_t *d = dev_addr(layers[i], p, len);
+        if (d != NULL)
+            return d;
     }
-    *outlen = 0;
-    if (nrecords != NULL)
-        *nrecords = 0;
-    if (wire > capacity) {
-        snprintf(rl_err, sizeof(rl_err), "record layer: %zu wire bytes exceed the output capacity %zu", wire, capacity);
-        return -1;
-    }
-    if (nrec == 0)
+    return NULL;
+}
+
+static uint32_t be32(const uint8_t *b) { return (uint32_t)b[0] << 24 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 8 | b[3]; }
+
+int ptls_mi355x_record_layer_seal_multi(ptls_mi355x_record_layer_t *const *layers, size_t nlayers,
+                                        const ptls_mi355x_iovec_t *const *frags, const size_t *nfrags, uint8_t type,
+                                        void *const *out, const size_t *capacity, size_t *outlen, size_t *nrecords)
+{
+    if (nlayers == 0)
         return 0;
-    if (reserve_recs(rl, nrec) != 0)
-        return -1;
-    /* direct: every non-empty fragment and the output in registered ranges; fragments addressed from the lowest */
-    uint8_t *out_dev = dev_addr(rl, out, wire), *src_base = NULL;
-    int direct = out_dev != NULL;
-    for (size_t f = 0; direct && f < nfrags; ++f) {
-        if (frags[f].len == 0)
-            continue;
-        uint8_t *d = dev_addr(rl, frags[f].base, frags[f].len);
-        if (d == NULL)
-            direct = 0;
-        else if (src_base == NULL || d < src_base)
-            src_base = d;
+    ptls_mi355x_record_layer_t *rl = layers[0];
+    size_t nrec = 0, srcbytes = 0, wire = 0;
+    for (size_t l = 0; l < nlayers; ++l) {
+        const ptls_mi355x_record_layer_t *x = layers[l];
+        outlen[l] = 0;
+        if (nrecords != NULL)
+            nrecords[l] = 0;
+        /* one launch, one key image: the connections of one session (rapido: the session key, the IV differing in
+         * bytes 0..3 only, derive_connection_aead_iv lib/rapido.c:123-133) */
+        if (x->key_size != rl->key_size || memcmp(x->key, rl->key, rl->key_size) != 0 ||
+            memcmp(x->iv + 4, rl->iv + 4, 8) != 0) {
+            snprintf(rl_err, sizeof(rl_err), "record layer: layer %zu has another key or IV bytes 4..11", l);
+            return -1;
+        }
+        size_t wl = 0;
+        for (size_t f = 0; f < nfrags[l]; ++f) {
+            uint64_t sq = 0;
+            size_t w = 0;
+            nrec += ptls_mi355x_tls_plan_send(frags[l][f].len, type, &sq, 0, 0, NULL, 0, &w);
+            srcbytes += frags[l][f].len;
+            wl += w;
+        }
+        if (wl > capacity[l]) {
+            snprintf(rl_err, sizeof(rl_err), "record layer: %zu wire bytes exceed the output capacity %zu (layer %zu)",
+                     wl, capacity[l], l);
+            return -1;
+        }
+        outlen[l] = wl; /* provisional: reset below unless the call succeeds */
+        wire += wl;
     }
-    const size_t off_src = up16(nrec * sizeof(ptls_mi355x_tls_record_t));
+    if (nrec == 0) {
+        for (size_t l = 0; l < nlayers; ++l)
+            outlen[l] = 0;
+        return 0;
+    }
+    if (reserve_recs(rl, nrec) != 0)
+        goto Fail;
+    /* direct: every non-empty fragment and every output in registered ranges; addressed from the lowest of each */
+    uint8_t *src_base = NULL, *dst_base = NULL;
+    int direct = 1;
+    for (size_t l = 0; direct && l < nlayers; ++l) {
+        uint8_t *d = outlen[l] != 0 ? dev_addr_any(layers, nlayers, out[l], outlen[l]) : NULL;
+        if (outlen[l] != 0 && d == NULL)
+            direct = 0;
+        else if (d != NULL && (dst_base == NULL || d < dst_base))
+            dst_base = d;
+        for (size_t f = 0; direct && f < nfrags[l]; ++f) {
+            if (frags[l][f].len == 0)
+                continue;
+            if ((d = dev_addr_any(layers, nlayers, frags[l][f].base, frags[l][f].len)) == NULL)
+                direct = 0;
+            else if (src_base == NULL || d < src_base)
+                src_base = d;
+        }
+    }
+    const size_t off_conn = up16(nrec * sizeof(ptls_mi355x_tls_record_t));
+    const size_t off_src = off_conn + (nlayers > 1 ? up16(nrec * 4) : 0);
     const size_t off_dst = off_src + (direct ? 0 : up16(srcbytes)), total = off_dst + (direct ? 0 : up16(wire));
     const int zero_copy = direct || total <= rl->zero_copy_bytes;
     if (reserve_stage(rl, total) != 0 || (!zero_copy && reserve_device(rl, total) != 0))
-        return -1;
-    /* descriptors (offsets relative to the src / dst bases) and, unless direct, the fragments back to back */
+        goto Fail;
+    /* descriptors (offsets relative to the src / dst bases), the per-record IV differences and, unless direct, the
+     * fragments back to back */
+    uint32_t *conn = (uint32_t *)(rl->h_buf + off_conn);
+    uint64_t *seqs = (uint64_t *)malloc(nlayers * sizeof(uint64_t));
+    if (seqs == NULL) {
+        snprintf(rl_err, sizeof(rl_err), "record layer: out of memory");
+        goto Fail;
+    }
     size_t k = 0, src_off = 0, dst_off = 0;
-    uint64_t seq = rl->seq;
-    for (size_t f = 0; f < nfrags; ++f) {
-        size_t w = 0;
-        if (direct && frags[f].len != 0)
-            src_off = (size_t)(dev_addr(rl, frags[f].base, frags[f].len) - src_base);
-        k += ptls_mi355x_tls_plan_send(frags[f].len, type, &seq, src_off, dst_off, rl->recs + k, nrec - k, &w);
-        if (!direct) {
-            if (frags[f].len != 0)
-                memcpy(rl->h_buf + off_src + src_off, frags[f].base, frags[f].len);
-            src_off += frags[f].len;
+    for (size_t l = 0; l < nlayers; ++l) {
+        seqs[l] = layers[l]->seq;
+        if (direct && outlen[l] != 0)
+            dst_off = (size_t)(dev_addr_any(layers, nlayers, out[l], outlen[l]) - dst_base);
+        const uint32_t cid = be32(layers[l]->iv) ^ be32(rl->iv); /* BE32(cid) ^ IV[0..3] of layer 0 = layer l's */
+        const size_t k0 = k;
+        for (size_t f = 0; f < nfrags[l]; ++f) {
+            const ptls_mi355x_iovec_t *fr = &frags[l][f];
+            size_t w = 0;
+            if (direct && fr->len != 0)
+                src_off = (size_t)(dev_addr_any(layers, nlayers, fr->base, fr->len) - src_base);
+            k += ptls_mi355x_tls_plan_send(fr->len, type, &seqs[l], src_off, dst_off, rl->recs + k, nrec - k, &w);
+            if (!direct) {
+                if (fr->len != 0)
+                    memcpy(rl->h_buf + off_src + src_off, fr->base, fr->len);
+                src_off += fr->len;
+            }
+            dst_off += w;
         }
-        dst_off += w;
+        if (nlayers > 1)
+            for (size_t i = k0; i < k; ++i)
+                conn[i] = cid;
     }
     memcpy(rl->h_buf, rl->recs, nrec * sizeof(ptls_mi355x_tls_record_t));
     uint8_t *base = zero_copy ? rl->h_dev : rl->d_buf;
     hipError_t e;
+    int rc;
     if (!zero_copy &&
-        (e = hipMemcpyAsync(rl->d_buf, rl->h_buf, off_src + srcbytes, hipMemcpyHostToDevice, rl->stream)) != hipSuccess)
-        return rl_fail("H2D", e);
-    if (ptls_mi355x_tls_seal_records(rl->ctx, rl->iv, (const ptls_mi355x_tls_record_t *)base, nrec,
-                                     direct ? src_base : base + off_src, direct ? out_dev : base + off_dst,
-                                     rl->stream) != 0) {
+        (e = hipMemcpyAsync(rl->d_buf, rl->h_buf, off_src + srcbytes, hipMemcpyHostToDevice, rl->stream)) != hipSuccess) {
+        free(seqs);
+        rl_fail("H2D", e);
+        goto Fail;
+    }
+    if (nlayers == 1)
+        rc = ptls_mi355x_tls_seal_records(rl->ctx, rl->iv, (const ptls_mi355x_tls_record_t *)base, nrec,
+                                          direct ? src_base : base + off_src, direct ? dst_base : base + off_dst,
+                                          rl->stream);
+    else
+        rc = ptls_mi355x_tls_seal_records_multi(rl->ctx, rl->iv, (const ptls_mi355x_tls_record_t *)base,
+                                                (const uint32_t *)(base + off_conn), nrec,
+                                                direct ? src_base : base + off_src, direct ? dst_base : base + off_dst,
+                                                rl->stream);
+    if (rc != 0) {
+        free(seqs);
         snprintf(rl_err, sizeof(rl_err), "record layer: %s", ptls_mi355x_last_error());
+        goto Fail;
+    }
+    if ((!zero_copy && (e = hipMemcpyAsync(rl->h_buf + off_dst, rl->d_buf + off_dst, wire, hipMemcpyDeviceToHost,
+                                           rl->stream)) != hipSuccess) ||
+        (e = hipStreamSynchronize(rl->stream)) != hipSuccess) {
+        free(seqs);
+        rl_fail("synchronize", e);
+        goto Fail;
+    }
+    for (size_t l = 0, off = 0; l < nlayers; ++l) {
+        if (!direct) {
+            memcpy(out[l], rl->h_buf + off_dst + off, outlen[l]);
+            off += outlen[l];
+        }
+        if (nrecords != NULL)
+            nrecords[l] = (size_t)(seqs[l] - layers[l]->seq);
+        layers[l]->seq = seqs[l];
+    }
+    free(seqs);
+    if (!direct)
+        memset(rl->h_buf + off_src, 0, srcbytes); /* no plaintext left in the staging */
+    return 0;
+Fail:
+    for (size_t l = 0; l < nlayers; ++l)
+        outlen[l] = 0;
+    return -1;
+}
+
+int ptls_mi355x_record_layer_seal(ptls_mi355x_record_layer_t *rl, const ptls_mi355x_iovec_t *frags, size_t nfrags,
+                                  uint8_t type, void *out, size_t capacity, size_t *outlen, size_t *nrecords)
+{
+    return ptls_mi355x_record_layer_seal_multi(&rl, 1, &frags, &nfrags, type, &out, &capacity, outlen, nrecords);
+}
+
+/* the layers of one launch share the key and IV bytes 4..11 (the connections of a session) */
+static int same_session(ptls_mi355x_record_layer_t *const *layers, size_t nlayers)
+{
+    const ptls_mi355x_record_layer_t *rl = layers[0];
+    for (size_t l = 1; l < nlayers; ++l) {
+        const ptls_mi355x_record_layer_t *x = layers[l];
+        if (x->key_size != rl->key_size || memcmp(x->key, rl->key, rl->key_size) != 0 ||
+            memcmp(x->iv + 4, rl->iv + 4, 8) != 0) {
+            snprintf(rl_err, sizeof(rl_err), "record layer: layer %zu has another key or IV bytes 4..11", l);
+            return 0;
+        }
+    }
+    return 1;
+}
+
+typedef struct {
+    size_t k0, n, cons, ptbytes; /* its descriptors rl->recs[k0 .. k0 + n), wire bytes parsed, plaintext slot bytes */
+    uint64_t src_add, dst_add;   /* added to its descriptors' offsets (its position in the launch's src / dst) */
+    int perr;
+} rl_open_part_t;
+
+int ptls_mi355x_record_layer_open_multi(ptls_mi355x_record_layer_t *const *layers, size_t nlayers, const void *const *in,
+                                        const size_t *inlen, size_t *consumed, void *const *out, const size_t *capacity,
+                                        size_t *outlen, size_t *nrecords, int *alerts)
+{
+    for (size_t l = 0; l < nlayers; ++l) {
+        consumed[l] = outlen[l] = 0;
+        alerts[l] = 0;
+        if (nrecords != NULL)
+            nrecords[l] = 0;
+    }
+    if (nlayers == 0)
+        return 0;
+    ptls_mi355x_record_layer_t *rl = layers[0];
+    if (!same_session(layers, nlayers))
+        return -1;
+    rl_open_part_t *part = (rl_open_part_t *)calloc(nlayers, sizeof(*part));
+    if (part == NULL) {
+        snprintf(rl_err, sizeof(rl_err), "record layer: out of memory");
         return -1;
     }
-    if (!zero_copy &&
-        (e = hipMemcpyAsync(rl->h_buf + off_dst, rl->d_buf + off_dst, wire, hipMemcpyDeviceToHost, rl->stream)) !=
-            hipSuccess)
-        return rl_fail("D2H", e);
-    if ((e = hipStreamSynchronize(rl->stream)) != hipSuccess)
-        return rl_fail("synchronize", e);
-    if (!direct) {
-        memcpy(out, rl->h_buf + off_dst, wire);
-        memset(rl->h_buf + off_src, 0, srcbytes); /* no plaintext left in the staging */
+    int ret = -1;
+    size_t max = 0, nrec = 0, srcbytes = 0, ptbytes = 0;
+    for (size_t l = 0; l < nlayers; ++l)
+        max += inlen[l] / (PTLS_MI355X_TLS_HEADER_SIZE + 16) + 1;
+    if (reserve_recs(rl, max) != 0)
+        goto Exit;
+    /* the complete application_data records at the start of every input, offsets local to it for now */
+    for (size_t l = 0; l < nlayers; ++l) {
+        uint64_t seq = layers[l]->seq;
+        part[l].k0 = nrec;
+        part[l].perr = ptls_mi355x_tls_parse_records((const uint8_t *)in[l], inlen[l], 0, &seq, 0, rl->recs + nrec,
+                                                     max - nrec, &part[l].n, &part[l].cons);
+        if (part[l].n != 0) {
+            const ptls_mi355x_tls_record_t *last = rl->recs + nrec + part[l].n - 1;
+            part[l].ptbytes = last->dst + (last->len >= 16u ? last->len - 16u : 0u);
+        }
+        nrec += part[l].n;
+        srcbytes += up16(part[l].cons);
+        ptbytes += up16(part[l].ptbytes);
     }
-    rl->seq = seq;
-    *outlen = wire;
-    if (nrecords != NULL)
-        *nrecords = nrec;
-    return 0;
+    if (nrec == 0) {
+        for (size_t l = 0; l < nlayers; ++l)
+            alerts[l] = part[l].perr;
+        ret = 0;
+        goto Exit;
+    }
+    /* direct: every input and every plaintext buffer (at least as large as its slots) in registered ranges */
+    uint8_t *src_base = NULL, *dst_base = NULL;
+    int direct = 1;
+    for (size_t l = 0; direct && l < nlayers; ++l) {
+        if (part[l].n == 0)
+            continue;
+        uint8_t *di = dev_addr_any(layers, nlayers, in[l], part[l].cons);
+        uint8_t *dout = capacity[l] >= part[l].ptbytes ? dev_addr_any(layers, nlayers, out[l], part[l].ptbytes) : NULL;
+        if (di == NULL || dout == NULL) {
+            direct = 0;
+            break;
+        }
+        if (src_base == NULL || di < src_base)
+            src_base = di;
+        if (dst_base == NULL || dout < dst_base)
+            dst_base = dout;
+    }
+    const size_t off_conn = up16(nrec * sizeof(ptls_mi355x_tls_record_t));
+    const size_t off_src = off_conn + (nlayers > 1 ? up16(nrec * 4) : 0);
+    const size_t off_dst = off_src + (direct ? 0 : srcbytes), off_st = off_dst + (direct ? 0 : ptbytes);
+    const size_t off_ty = off_st + up16(nrec * 4), total = off_ty + up16(nrec);
+    const int zero_copy = direct || total <= rl->zero_copy_bytes;
+    if (reserve_stage(rl, total) != 0 || (!zero_copy && reserve_device(rl, total) != 0))
+        goto Exit;
+    uint32_t *conn = (uint32_t *)(rl->h_buf + off_conn);
+    for (size_t l = 0, so = 0, dso = 0; l < nlayers; ++l) {
+        if (part[l].n == 0)
+            continue;
+        if (direct) {
+            part[l].src_add = (uint64_t)(dev_addr_any(layers, nlayers, in[l], part[l].cons) - src_base);
+            part[l].dst_add = (uint64_t)(dev_addr_any(layers, nlayers, out[l], part[l].ptbytes) - dst_base);
+        } else {
+            part[l].src_add = so;
+            part[l].dst_add = dso;
+            memcpy(rl->h_buf + off_src + so, in[l], part[l].cons);
+            so += up16(part[l].cons);
+            dso += up16(part[l].ptbytes);
+        }
+        const uint32_t cid = be32(layers[l]->iv) ^ be32(rl->iv);
+        for (size_t i = part[l].k0; i < part[l].k0 + part[l].n; ++i) {
+            rl->recs[i].src += part[l].src_add;
+            rl->recs[i].dst += part[l].dst_add;
+            if (nlayers > 1)
+                conn[i] = cid;
+        }
+    }
+    memcpy(rl->h_buf, rl->recs, nrec * sizeof(ptls_mi355x_tls_record_t));
+    uint8_t *base = zero_copy ? rl->h_dev : rl->d_buf;
+    hipError_t e;
+    int rc;
+    if (!zero_copy && (e = hipMemcpyAsync(rl->d_buf, rl->h_buf, off_src + srcbytes, hipMemcpyHostToDevice,
+                                          rl->stream)) != hipSuccess) {
+        rl_fail("H2D", e);
+        goto Exit;
+    }
+    /* every record verified independently; the stop at a connection's first failure is the host loop below */
+    if (nlayers == 1)
+        rc = ptls_mi355x_tls_open_records(rl->ctx, rl->iv, (const ptls_mi355x_tls_record_t *)base, nrec,
+                                          direct ? src_base : base + off_src, direct ? dst_base : base + off_dst,
+                                          (uint32_t *)(base + off_st), base + off_ty, rl->stream);
+    else
+        rc = ptls_mi355x_tls_open_records_multi(rl->ctx, rl->iv, (const ptls_mi355x_tls_record_t *)base,
+                                                (const uint32_t *)(base + off_conn), nrec,
+                                                direct ? src_base : base + off_src, direct ? dst_base : base + off_dst,
+                                                (uint32_t *)(base + off_st), base + off_ty, rl->stream);
+    if (rc != 0) {
+        snprintf(rl_err, sizeof(rl_err), "record layer: %s", ptls_mi355x_last_error());
+        goto Exit;
+    }
+    if ((!zero_copy && (e = hipMemcpyAsync(rl->h_buf + off_dst, rl->d_buf + off_dst, off_ty + nrec - off_dst,
+                                           hipMemcpyDeviceToHost, rl->stream)) != hipSuccess) ||
+        (e = hipStreamSynchronize(rl->stream)) != hipSuccess) {
+        rl_fail("synchronize", e);
+        goto Exit;
+    }
+    const uint32_t *status = (const uint32_t *)(rl->h_buf + off_st);
+    const uint8_t *types = rl->h_buf + off_ty;
+    for (size_t l = 0; l < nlayers; ++l) {
+        if (part[l].n == 0) {
+            alerts[l] = part[l].perr;
+            continue;
+        }
+        /* slot i of this layer at its local plaintext offset: in out[l] (direct) or in the staging */
+        uint8_t *slots = direct ? (uint8_t *)out[l] : rl->h_buf + off_dst + part[l].dst_add;
+        size_t done = 0, wire_done = 0, olen = 0;
+        int a = 0;
+        for (size_t i = part[l].k0; i < part[l].k0 + part[l].n; ++i) {
+            if (status[i] == PTLS_MI355X_TLS_BAD_RECORD_MAC) {
+                a = 20; /* PTLS_ALERT_BAD_RECORD_MAC */
+                break;
+            }
+            if (status[i] == PTLS_MI355X_TLS_UNEXPECTED_MESSAGE) {
+                a = 10; /* PTLS_ALERT_UNEXPECTED_MESSAGE: no content type */
+                break;
+            }
+            if (types[i] != 23) /* a handshake / alert record inside: the caller's picotls path re-opens it */
+                break;
+            if (olen + status[i] > capacity[l]) {
+                if (done == 0) {
+                    snprintf(rl_err, sizeof(rl_err), "record layer: %u plaintext bytes exceed the output capacity %zu",
+                             status[i], capacity[l]);
+                    a = -1;
+                }
+                break;
+            }
+            /* direct: slot i starts at or after olen, so the delivered plaintexts close up in place */
+            memmove((uint8_t *)out[l] + olen, slots + (rl->recs[i].dst - part[l].dst_add), status[i]);
+            olen += status[i];
+            wire_done += PTLS_MI355X_TLS_HEADER_SIZE + (rl->recs[i].len);
+            ++done;
+        }
+        if (direct)
+            memset((uint8_t *)out[l] + olen, 0, part[l].ptbytes - olen); /* padding, types, records not delivered */
+        else
+            memset(slots, 0, part[l].ptbytes); /* no plaintext left in the staging */
+        layers[l]->seq += done;
+        consumed[l] = wire_done;
+        outlen[l] = olen;
+        if (nrecords != NULL)
+            nrecords[l] = done;
+        alerts[l] = a == 0 && done == part[l].n ? part[l].perr : a; /* a DECODE_ERROR behind the parsed records */
+    }
+    ret = 0;
+Exit:
+    free(part);
+    return ret;
 }
 
 int ptls_mi355x_record_layer_open(ptls_mi355x_record_layer_t *rl, const void *in, size_t inlen, size_t *consumed,
                                   void *out, size_t capacity, size_t *outlen, size_t *nrecords)
 {
-    *consumed = 0;
-    *outlen = 0;
-    if (nrecords != NULL)
-        *nrecords = 0;
-    const size_t max = inlen / (PTLS_MI355X_TLS_HEADER_SIZE + 16) + 1;
-    if (reserve_recs(rl, max) != 0)
+    int alert = 0;
+    if (ptls_mi355x_record_layer_open_multi(&rl, 1, &in, &inlen, consumed, &out, &capacity, outlen, nrecords, &alert) != 0)
         return -1;
-    uint64_t seq = rl->seq;
-    size_t nrec = 0, cons = 0;
-    const int perr = ptls_mi355x_tls_parse_records((const uint8_t *)in, inlen, 0, &seq, 0, rl->recs, max, &nrec, &cons);
-    if (nrec == 0)
-        return perr;
-    const ptls_mi355x_tls_record_t *last = rl->recs + nrec - 1;
-    const size_t ptbytes = last->dst + (last->len >= 16u ? last->len - 16u : 0u); /* the plaintext slots */
-    /* direct: the input and the slots (capacity permitting) in registered ranges; the kernel writes the slots into out */
-    uint8_t *in_dev = dev_addr(rl, in, cons), *out_dev = capacity >= ptbytes ? dev_addr(rl, out, ptbytes) : NULL;
-    const int direct = in_dev != NULL && out_dev != NULL;
-    const size_t off_src = up16(nrec * sizeof(ptls_mi355x_tls_record_t));
-    const size_t off_dst = off_src + (direct ? 0 : up16(cons)), off_st = off_dst + (direct ? 0 : up16(ptbytes));
-    const size_t off_ty = off_st + up16(nrec * 4), total = off_ty + up16(nrec);
-    const int zero_copy = direct || total <= rl->zero_copy_bytes;
-    if (reserve_stage(rl, total) != 0 || (!zero_copy && reserve_device(rl, total) != 0))
-        return -1;
-    memcpy(rl->h_buf, rl->recs, nrec * sizeof(ptls_mi355x_tls_record_t));
-    if (!direct)
-        memcpy(rl->h_buf + off_src, in, cons);
-    uint8_t *base = zero_copy ? rl->h_dev : rl->d_buf;
-    hipError_t e;
-    if (!zero_copy && (e = hipMemcpyAsync(rl->d_buf, rl->h_buf, off_src + cons, hipMemcpyHostToDevice, rl->stream)) !=
-                          hipSuccess)
-        return rl_fail("H2D", e);
-    if (ptls_mi355x_tls_open_records(rl->ctx, rl->iv, (const ptls_mi355x_tls_record_t *)base, nrec,
-                                     direct ? in_dev : base + off_src, direct ? out_dev : base + off_dst,
-                                     (uint32_t *)(base + off_st), base + off_ty, rl->stream) != 0) {
-        snprintf(rl_err, sizeof(rl_err), "record layer: %s", ptls_mi355x_last_error());
-        return -1;
-    }
-    if (!zero_copy && (e = hipMemcpyAsync(rl->h_buf + off_dst, rl->d_buf + off_dst, off_ty + nrec - off_dst,
-                                          hipMemcpyDeviceToHost, rl->stream)) != hipSuccess)
-        return rl_fail("D2H", e);
-    if ((e = hipStreamSynchronize(rl->stream)) != hipSuccess)
-        return rl_fail("synchronize", e);
-    const uint32_t *status = (const uint32_t *)(rl->h_buf + off_st);
-    const uint8_t *types = rl->h_buf + off_ty;
-    uint8_t *slots = direct ? (uint8_t *)out : rl->h_buf + off_dst;
-    size_t done = 0, wire_done = 0, olen = 0;
-    int ret = 0;
-    for (size_t i = 0; i < nrec; ++i) {
-        if (status[i] == PTLS_MI355X_TLS_BAD_RECORD_MAC) {
-            ret = 20; /* PTLS_ALERT_BAD_RECORD_MAC */
-            break;
-        }
-        if (status[i] == PTLS_MI355X_TLS_UNEXPECTED_MESSAGE) {
-            ret = 10; /* PTLS_ALERT_UNEXPECTED_MESSAGE: no content type */
-            break;
-        }
-        if (types[i] != 23) /* a handshake / alert record inside: the caller's picotls path re-opens it */
-            break;
-        if (olen + status[i] > capacity) {
-            if (done == 0) {
-                snprintf(rl_err, sizeof(rl_err), "record layer: %u plaintext bytes exceed the output capacity %zu",
-                         status[i], capacity);
-                ret = -1;
-            }
-            break;
-        }
-        /* direct: slot i starts at or after olen, so the delivered plaintexts close up in place */
-        memmove((uint8_t *)out + olen, slots + rl->recs[i].dst, status[i]);
-        olen += status[i];
-        wire_done += PTLS_MI355X_TLS_HEADER_SIZE + rl->recs[i].len;
-        ++done;
-    }
-    if (direct)
-        memset((uint8_t *)out + olen, 0, ptbytes - olen); /* padding, types and records not delivered */
-    else
-        memset(rl->h_buf + off_dst, 0, ptbytes); /* no plaintext left in the staging */
-    rl->seq += done;
-    *consumed = wire_done;
-    *outlen = olen;
-    if (nrecords != NULL)
-        *nrecords = done;
-    if (ret == 0 && done == nrec)
-        ret = perr; /* a DECODE_ERROR behind the parsed records */
-    return ret;
+    return alert;
 }

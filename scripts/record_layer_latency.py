@@ -81,6 +81,50 @@ def main():
                           "open_gibps": round(payload / 2 ** 30 / (o / 1e6), 2)}), flush=True)
         tx.close()
         rx.close()
+    # the send windows of C connections of one session: one seal_multi launch vs C seal calls, on registered buffers
+    # (direct) and through the zero-copy staging
+    for conns in (4, 8):
+        for direct in (True, False):
+            ivs = [bytes([i]) + iv[1:] for i in range(conns)]
+            layers = [ra.RecordLayer(key, v) for v in ivs]
+            if direct:
+                send = np.frombuffer(b"".join(frags), np.uint8).copy()
+                wins = [[send[i * a.size:(i + 1) * a.size] for i in range(a.records)]] * conns
+                per = payload + a.records * 64
+                wirebuf = np.zeros(conns * per, np.uint8)
+                outs = [wirebuf[c * per:(c + 1) * per] for c in range(conns)]
+                for lr in layers:  # the first registers, the others find the ranges already registered
+                    lr.register(send)
+                    lr.register(wirebuf)
+            else:
+                wins, outs = [frags] * conns, None
+            one, each = [], []
+            for i in range(a.reps + 5):
+                t0 = time.perf_counter()
+                res = ra.record_layer_seal_multi(layers, wins, outs=outs)
+                t1 = time.perf_counter()
+                for c, (lr, w) in enumerate(zip(layers, wins)):
+                    if direct:
+                        ra.record_layer_seal_multi([lr], [w], outs=[outs[c]])
+                    else:
+                        lr.seal(w)
+                t2 = time.perf_counter()
+                assert all(n == a.records for _, n in res)
+                if i >= 5:
+                    one.append((t1 - t0) * 1e6)
+                    each.append((t2 - t1) * 1e6)
+            s1, s2 = statistics.median(one), statistics.median(each)
+            print(json.dumps({"what": f"{conns} connections x {a.records} x {a.size} B send windows, host buffers in and "
+                                      f"out (median of {a.reps}, us, Python binding, "
+                                      f"{'registered buffers (direct)' if direct else 'zero-copy staging'})",
+                              "mode": "seal_multi" + ("_direct" if direct else ""), "one_launch_us": round(s1, 1),
+                              "per_connection_calls_us": round(s2, 1),
+                              "one_launch_gibps": round(conns * payload / 2 ** 30 / (s1 / 1e6), 2),
+                              "per_connection_calls_gibps": round(conns * payload / 2 ** 30 / (s2 / 1e6), 2)}),
+                  flush=True)
+            for lr in layers[::-1]:  # layers[0] owns the registrations: it goes last
+                lr.close()
+
 
 if __name__ == "__main__":
     main()

@@ -211,3 +211,84 @@ def test_direct_window_in_registered_buffers(family, keylen):
         tx.unregister(sendbuf)
     tx.close()
     rx.close()
+
+
+@pytest.mark.parametrize("keylen", [16, 32])
+def test_seal_multi_session_windows(family, transport, keylen):
+    """The send windows of four connections of one session (session key, per-connection IV: the connection id in IV
+    bytes 0..3, lib/rapido.c:123-133) sealed in one launch: every connection's wire bytes are its own ptls_send
+    output, every seq advances by its record count."""
+    rng = np.random.default_rng(300 + keylen)
+    key = rng.integers(0, 256, keylen, dtype=np.uint8).tobytes()
+    iv = rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    cids, seqs = [0, 3, 7, 0x01020304], [5, 0, 1000, 2 ** 40]
+    layers = [layer(transport, key, conn_iv(iv, c), seq=s) for c, s in zip(cids, seqs)]
+    windows = [[rng.integers(0, 256, 16384, dtype=np.uint8).tobytes() for _ in range(16)],
+               [b"", rng.integers(0, 256, 40000, dtype=np.uint8).tobytes()],
+               [],
+               [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in rng.integers(1, 3000, 9)]]
+    got = ra.record_layer_seal_multi(layers, windows)
+    for lr, c, s, w, (wire, n) in zip(layers, cids, seqs, windows, got):
+        want, end = oracle_window(key, conn_iv(iv, c), s, w)
+        assert wire == want and n == end - s and lr.seq == end
+    # a layer with another key: refused, nothing advanced
+    other = layer(transport, bytes(keylen), conn_iv(iv, 1), seq=9)
+    before = [lr.seq for lr in layers]
+    with pytest.raises(RuntimeError):
+        ra.record_layer_seal_multi(layers[:2] + [other], windows[:2] + [[b"x" * 10]])
+    assert [lr.seq for lr in layers] == before and other.seq == 9
+    for lr in layers + [other]:
+        lr.close()
+
+
+def test_seal_multi_direct(family):
+    """The same, direct: every connection's fragments and output in registered host buffers."""
+    rng = np.random.default_rng(400)
+    key, iv = rng.integers(0, 256, 16, dtype=np.uint8).tobytes(), rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    cids = [11, 12, 13]
+    layers = [ra.RecordLayer(key, conn_iv(iv, c), seq=c) for c in cids]
+    sendbuf, wirebuf = page_buffer(1 << 20), page_buffer(1 << 20)
+    sendbuf[:] = rng.integers(0, 256, sendbuf.size, dtype=np.uint8)
+    layers[0].register(sendbuf)
+    layers[1].register(wirebuf)
+    sizes = [[16384, 100, 0], [40000], [1, 2, 3, 16385]]
+    windows, pos = [], 0
+    for w in sizes:
+        frags = []
+        for n in w:
+            frags.append(sendbuf[pos:pos + n])
+            pos += n + 7
+        windows.append(frags)
+    outs = [wirebuf[300000:600000], wirebuf[17:200000], wirebuf[700000:]]  # out of order in the buffer
+    got = ra.record_layer_seal_multi(layers, windows, outs=outs)
+    for lr, c, w, o, (wlen, n) in zip(layers, cids, windows, outs, got):
+        want, end = oracle_window(key, conn_iv(iv, c), c, [f.tobytes() for f in w])
+        assert o[:wlen].tobytes() == want and lr.seq == end and n == end - c
+    for lr in layers:
+        lr.close()
+
+
+def test_open_multi_session_windows(family, transport):
+    """The receive windows of four connections of one session opened in one launch: each connection gets exactly
+    what its own ptls_receive would have delivered, alerts and stops included, and only its seq advances."""
+    rng = np.random.default_rng(500)
+    key, iv = rng.integers(0, 256, 32, dtype=np.uint8).tobytes(), rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    cids, seqs = [2, 9, 0x7fffffff, 40], [0, 17, 5, 2 ** 33]
+    layers = [layer(transport, key, conn_iv(iv, c), seq=s) for c, s in zip(cids, seqs)]
+    frags = [[rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in rng.integers(1, 16385, k)]
+             for k in (16, 3, 0, 5)]
+    wires = [oracle_window(key, conn_iv(iv, c), s, f)[0] for c, s, f in zip(cids, seqs, frags)]
+    # connection 1: its second record tampered (delivers the first, alert 20); connection 3: ends inside a record
+    bad = bytearray(wires[1])
+    first = 5 + len(frags[1][0]) + 17
+    bad[first + 5] ^= 4  # the first ciphertext byte of record 2
+    wires[1] = bytes(bad)
+    wires[3] = wires[3][:-9]
+    got = ra.record_layer_open_multi(layers, wires)
+    assert got[0] == (0, b"".join(frags[0]), len(wires[0]), 16) and layers[0].seq == 16
+    assert got[1] == (20, frags[1][0], first, 1) and layers[1].seq == 18
+    assert got[2] == (0, b"", 0, 0) and layers[2].seq == 5
+    whole4 = len(oracle_window(key, conn_iv(iv, 40), 2 ** 33, frags[3][:4])[0])
+    assert got[3] == (0, b"".join(frags[3][:4]), whole4, 4) and layers[3].seq == 2 ** 33 + 4
+    for lr in layers:
+        lr.close()
