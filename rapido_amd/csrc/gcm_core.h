@@ -105,6 +105,7 @@ struct Layout {
     static constexpr uint32_t n_nibble = gh5 ? 2u : (uint32_t)K;
     static constexpr uint32_t total = gh_base + n_nibble * GH_TABLE_BYTES;
     static constexpr bool split_scale = false; /* lane scaling by one table H^(K - slot) (lane_walk) */
+    static constexpr bool x2_walk = false;
     static_assert(total <= 160u * 1024u, "LDS budget");
 };
 
@@ -561,6 +562,137 @@ __device__ __forceinline__ void aes_round_tt2_asm(uint32_t ls, uint32_t s0, uint
           [a3] "s"(0x0c0c0700u), [o0] "i"(BASE), [o1] "i"(BASE + 128u)
         : "memory");
 }
+/*
+ * One middle round of the two-table layout (aes_round_tt2_asm) for TWO independent states A and B, as one asm block:
+ * A's 16 reads go out first, B's 16 addresses are formed while they are in flight, and each of A's columns is
+ * finished as its reads return, followed by one column of B's reads, so at most 16 reads are outstanding (the LDS
+ * counter's reach) and B's reads overlap A's XORs.  For the latency-bound split walk, where one wave per SIMD has
+ * nothing else to hide an LDS round trip behind: two counter blocks per lane per step instead of one.
+ */
+template <uint32_t BASE>
+__device__ __forceinline__ void aes_round_tt2_asm_x2(uint32_t ls, const uint32_t sA[4], const uint32_t sB[4],
+                                                     const uint32_t *k, uint32_t nA[4], uint32_t nB[4])
+{
+    uint32_t tA1, tA2, tA3, tA5, tA6, tA7, tA9, tA10, tA11, tA13, tA14, tA15, tB1, tB2, tB3, tB5, tB6, tB7, tB9, tB10, tB11, tB13, tB14, tB15;
+    asm volatile(
+        "v_perm_b32 %[nA0], %[sA0], %[ls], %[a0]\n\t"
+        "v_perm_b32 %[tA1], %[sA1], %[ls], %[a1]\n\t"
+        "v_perm_b32 %[tA2], %[sA2], %[ls], %[a2]\n\t"
+        "v_perm_b32 %[tA3], %[sA3], %[ls], %[a3]\n\t"
+        "ds_read_b32 %[nA0], %[nA0] offset:%[o0]\n\t"
+        "ds_read_b32 %[tA1], %[tA1] offset:%[o1]\n\t"
+        "ds_read_b32 %[tA2], %[tA2] offset:%[o0]\n\t"
+        "ds_read_b32 %[tA3], %[tA3] offset:%[o1]\n\t"
+        "v_perm_b32 %[nA1], %[sA1], %[ls], %[a0]\n\t"
+        "v_perm_b32 %[tA5], %[sA2], %[ls], %[a1]\n\t"
+        "v_perm_b32 %[tA6], %[sA3], %[ls], %[a2]\n\t"
+        "v_perm_b32 %[tA7], %[sA0], %[ls], %[a3]\n\t"
+        "ds_read_b32 %[nA1], %[nA1] offset:%[o0]\n\t"
+        "ds_read_b32 %[tA5], %[tA5] offset:%[o1]\n\t"
+        "ds_read_b32 %[tA6], %[tA6] offset:%[o0]\n\t"
+        "ds_read_b32 %[tA7], %[tA7] offset:%[o1]\n\t"
+        "v_perm_b32 %[nA2], %[sA2], %[ls], %[a0]\n\t"
+        "v_perm_b32 %[tA9], %[sA3], %[ls], %[a1]\n\t"
+        "v_perm_b32 %[tA10], %[sA0], %[ls], %[a2]\n\t"
+        "v_perm_b32 %[tA11], %[sA1], %[ls], %[a3]\n\t"
+        "ds_read_b32 %[nA2], %[nA2] offset:%[o0]\n\t"
+        "ds_read_b32 %[tA9], %[tA9] offset:%[o1]\n\t"
+        "ds_read_b32 %[tA10], %[tA10] offset:%[o0]\n\t"
+        "ds_read_b32 %[tA11], %[tA11] offset:%[o1]\n\t"
+        "v_perm_b32 %[nA3], %[sA3], %[ls], %[a0]\n\t"
+        "v_perm_b32 %[tA13], %[sA0], %[ls], %[a1]\n\t"
+        "v_perm_b32 %[tA14], %[sA1], %[ls], %[a2]\n\t"
+        "v_perm_b32 %[tA15], %[sA2], %[ls], %[a3]\n\t"
+        "ds_read_b32 %[nA3], %[nA3] offset:%[o0]\n\t"
+        "ds_read_b32 %[tA13], %[tA13] offset:%[o1]\n\t"
+        "ds_read_b32 %[tA14], %[tA14] offset:%[o0]\n\t"
+        "ds_read_b32 %[tA15], %[tA15] offset:%[o1]\n\t"
+        "v_perm_b32 %[nB0], %[sB0], %[ls], %[a0]\n\t"
+        "v_perm_b32 %[tB1], %[sB1], %[ls], %[a1]\n\t"
+        "v_perm_b32 %[tB2], %[sB2], %[ls], %[a2]\n\t"
+        "v_perm_b32 %[tB3], %[sB3], %[ls], %[a3]\n\t"
+        "v_perm_b32 %[nB1], %[sB1], %[ls], %[a0]\n\t"
+        "v_perm_b32 %[tB5], %[sB2], %[ls], %[a1]\n\t"
+        "v_perm_b32 %[tB6], %[sB3], %[ls], %[a2]\n\t"
+        "v_perm_b32 %[tB7], %[sB0], %[ls], %[a3]\n\t"
+        "v_perm_b32 %[nB2], %[sB2], %[ls], %[a0]\n\t"
+        "v_perm_b32 %[tB9], %[sB3], %[ls], %[a1]\n\t"
+        "v_perm_b32 %[tB10], %[sB0], %[ls], %[a2]\n\t"
+        "v_perm_b32 %[tB11], %[sB1], %[ls], %[a3]\n\t"
+        "v_perm_b32 %[nB3], %[sB3], %[ls], %[a0]\n\t"
+        "v_perm_b32 %[tB13], %[sB0], %[ls], %[a1]\n\t"
+        "v_perm_b32 %[tB14], %[sB1], %[ls], %[a2]\n\t"
+        "v_perm_b32 %[tB15], %[sB2], %[ls], %[a3]\n\t"
+        "s_waitcnt lgkmcnt(12)\n\t"
+        "v_xor_b32 %[tA2], %[tA2], %[tA3]\n\t"
+        "v_bitop3_b32 %[nA0], %[nA0], %[tA1], %[k0] bitop3:0x96\n\t"
+        "v_alignbit_b32 %[tA2], %[tA2], %[tA2], 16\n\t"
+        "v_xor_b32 %[nA0], %[nA0], %[tA2]\n\t"
+        "ds_read_b32 %[nB0], %[nB0] offset:%[o0]\n\t"
+        "ds_read_b32 %[tB1], %[tB1] offset:%[o1]\n\t"
+        "ds_read_b32 %[tB2], %[tB2] offset:%[o0]\n\t"
+        "ds_read_b32 %[tB3], %[tB3] offset:%[o1]\n\t"
+        "s_waitcnt lgkmcnt(12)\n\t"
+        "v_xor_b32 %[tA6], %[tA6], %[tA7]\n\t"
+        "v_bitop3_b32 %[nA1], %[nA1], %[tA5], %[k1] bitop3:0x96\n\t"
+        "v_alignbit_b32 %[tA6], %[tA6], %[tA6], 16\n\t"
+        "v_xor_b32 %[nA1], %[nA1], %[tA6]\n\t"
+        "ds_read_b32 %[nB1], %[nB1] offset:%[o0]\n\t"
+        "ds_read_b32 %[tB5], %[tB5] offset:%[o1]\n\t"
+        "ds_read_b32 %[tB6], %[tB6] offset:%[o0]\n\t"
+        "ds_read_b32 %[tB7], %[tB7] offset:%[o1]\n\t"
+        "s_waitcnt lgkmcnt(12)\n\t"
+        "v_xor_b32 %[tA10], %[tA10], %[tA11]\n\t"
+        "v_bitop3_b32 %[nA2], %[nA2], %[tA9], %[k2] bitop3:0x96\n\t"
+        "v_alignbit_b32 %[tA10], %[tA10], %[tA10], 16\n\t"
+        "v_xor_b32 %[nA2], %[nA2], %[tA10]\n\t"
+        "ds_read_b32 %[nB2], %[nB2] offset:%[o0]\n\t"
+        "ds_read_b32 %[tB9], %[tB9] offset:%[o1]\n\t"
+        "ds_read_b32 %[tB10], %[tB10] offset:%[o0]\n\t"
+        "ds_read_b32 %[tB11], %[tB11] offset:%[o1]\n\t"
+        "s_waitcnt lgkmcnt(12)\n\t"
+        "v_xor_b32 %[tA14], %[tA14], %[tA15]\n\t"
+        "v_bitop3_b32 %[nA3], %[nA3], %[tA13], %[k3] bitop3:0x96\n\t"
+        "v_alignbit_b32 %[tA14], %[tA14], %[tA14], 16\n\t"
+        "v_xor_b32 %[nA3], %[nA3], %[tA14]\n\t"
+        "ds_read_b32 %[nB3], %[nB3] offset:%[o0]\n\t"
+        "ds_read_b32 %[tB13], %[tB13] offset:%[o1]\n\t"
+        "ds_read_b32 %[tB14], %[tB14] offset:%[o0]\n\t"
+        "ds_read_b32 %[tB15], %[tB15] offset:%[o1]\n\t"
+        "s_waitcnt lgkmcnt(12)\n\t"
+        "v_xor_b32 %[tB2], %[tB2], %[tB3]\n\t"
+        "v_bitop3_b32 %[nB0], %[nB0], %[tB1], %[k0] bitop3:0x96\n\t"
+        "v_alignbit_b32 %[tB2], %[tB2], %[tB2], 16\n\t"
+        "v_xor_b32 %[nB0], %[nB0], %[tB2]\n\t"
+        "s_waitcnt lgkmcnt(8)\n\t"
+        "v_xor_b32 %[tB6], %[tB6], %[tB7]\n\t"
+        "v_bitop3_b32 %[nB1], %[nB1], %[tB5], %[k1] bitop3:0x96\n\t"
+        "v_alignbit_b32 %[tB6], %[tB6], %[tB6], 16\n\t"
+        "v_xor_b32 %[nB1], %[nB1], %[tB6]\n\t"
+        "s_waitcnt lgkmcnt(4)\n\t"
+        "v_xor_b32 %[tB10], %[tB10], %[tB11]\n\t"
+        "v_bitop3_b32 %[nB2], %[nB2], %[tB9], %[k2] bitop3:0x96\n\t"
+        "v_alignbit_b32 %[tB10], %[tB10], %[tB10], 16\n\t"
+        "v_xor_b32 %[nB2], %[nB2], %[tB10]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_xor_b32 %[tB14], %[tB14], %[tB15]\n\t"
+        "v_bitop3_b32 %[nB3], %[nB3], %[tB13], %[k3] bitop3:0x96\n\t"
+        "v_alignbit_b32 %[tB14], %[tB14], %[tB14], 16\n\t"
+        "v_xor_b32 %[nB3], %[nB3], %[tB14]"
+        : [nA0] "=&v"(nA[0]), [nA1] "=&v"(nA[1]), [nA2] "=&v"(nA[2]), [nA3] "=&v"(nA[3]), [nB0] "=&v"(nB[0]),
+          [nB1] "=&v"(nB[1]), [nB2] "=&v"(nB[2]), [nB3] "=&v"(nB[3]), [tA1] "=&v"(tA1), [tA2] "=&v"(tA2),
+          [tA3] "=&v"(tA3), [tA5] "=&v"(tA5), [tA6] "=&v"(tA6), [tA7] "=&v"(tA7), [tA9] "=&v"(tA9),
+          [tA10] "=&v"(tA10), [tA11] "=&v"(tA11), [tA13] "=&v"(tA13), [tA14] "=&v"(tA14), [tA15] "=&v"(tA15),
+          [tB1] "=&v"(tB1), [tB2] "=&v"(tB2), [tB3] "=&v"(tB3), [tB5] "=&v"(tB5), [tB6] "=&v"(tB6), [tB7] "=&v"(tB7),
+          [tB9] "=&v"(tB9), [tB10] "=&v"(tB10), [tB11] "=&v"(tB11), [tB13] "=&v"(tB13), [tB14] "=&v"(tB14),
+          [tB15] "=&v"(tB15)
+        : [sA0] "v"(sA[0]), [sA1] "v"(sA[1]), [sA2] "v"(sA[2]), [sA3] "v"(sA[3]), [sB0] "v"(sB[0]), [sB1] "v"(sB[1]),
+          [sB2] "v"(sB[2]), [sB3] "v"(sB[3]), [ls] "v"(ls), [k0] "s"(k[0]), [k1] "s"(k[1]), [k2] "s"(k[2]),
+          [k3] "s"(k[3]), [a0] "s"(0x0c0c0400u), [a1] "s"(0x0c0c0500u), [a2] "s"(0x0c0c0600u), [a3] "s"(0x0c0c0700u),
+          [o0] "i"(BASE), [o1] "i"(BASE + 128u)
+        : "memory");
+}
+
 #endif
 
 /*
@@ -779,6 +911,62 @@ GCM_HD u32x4 aes_ghash_fused_h(const uint8_t *lds, uint32_t lanesel, const uint3
         }
     }
     return P;
+#undef GCM_TA
+}
+
+/*
+ * Keystreams of two counter blocks of one record (ctrA, ctrB) with the two-table layout, their rounds interleaved
+ * (aes_round_tt2_asm_x2): rounds 1-2 from the window constants cA / cB (aes_round12_consts of each block's window),
+ * rounds 3..NR-1 two states per asm block, the last round for both.  Bit-identical to two aes_ghash_fused_h calls'
+ * keystreams; no GHASH.
+ */
+template <int NR, uint32_t AES_BASE = 0u>
+GCM_HD void aes_ctr_x2_h(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk, const uint32_t *cA, const uint32_t *cB,
+                         uint32_t ctrA, uint32_t ctrB, uint32_t wA[4], uint32_t wB[4])
+{
+#define GCM_TA(x, k) perm((x), lanesel, 0x0c0c0400u | ((4u + (k)) << 8))
+    const uint8_t *la = lds + AES_BASE;
+    uint32_t sA[4], sB[4];
+    {
+        const uint32_t a3 = bswap32(ctrA) ^ rk[3], b3 = bswap32(ctrB) ^ rk[3];
+        const uint32_t a0 = cA[0] ^ tlook<false>(la, lanesel, a3, 3, 3), b0 = cB[0] ^ tlook<false>(la, lanesel, b3, 3, 3);
+        sA[0] = cA[4] ^ tlook<false>(la, lanesel, a0, 0, 0);
+        sB[0] = cB[4] ^ tlook<false>(la, lanesel, b0, 0, 0);
+        sA[1] = cA[5] ^ tlook<false>(la, lanesel, a0, 3, 3);
+        sB[1] = cB[5] ^ tlook<false>(la, lanesel, b0, 3, 3);
+        sA[2] = cA[6] ^ tlook<false>(la, lanesel, a0, 2, 2);
+        sB[2] = cB[6] ^ tlook<false>(la, lanesel, b0, 2, 2);
+        sA[3] = cA[7] ^ tlook<false>(la, lanesel, a0, 1, 1);
+        sB[3] = cB[7] ^ tlook<false>(la, lanesel, b0, 1, 1);
+    }
+#pragma unroll
+    for (int r = 3; r < NR; ++r) {
+        uint32_t nA[4], nB[4];
+#if defined(__HIP_DEVICE_COMPILE__) && GCM_ROUND_ASM
+        aes_round_tt2_asm_x2<AES_BASE>(lanesel, sA, sB, rk + 4 * r, nA, nB);
+#else
+        const uint32_t *k = rk + 4 * r;
+        for (int c = 0; c < 4; ++c) {
+            nA[c] = aes_col<false>(la, lanesel, sA[c], sA[(c + 1) & 3], sA[(c + 2) & 3], sA[(c + 3) & 3], k[c]);
+            nB[c] = aes_col<false>(la, lanesel, sB[c], sB[(c + 1) & 3], sB[(c + 2) & 3], sB[(c + 3) & 3], k[c]);
+        }
+#endif
+        GCM_SCHED_FENCE();
+        for (int c = 0; c < 4; ++c) {
+            sA[c] = nA[c];
+            sB[c] = nB[c];
+        }
+    }
+    const uint32_t *k = rk + 4 * NR;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t ra = lds_u32(la, GCM_TA(sA[j], 0)), rb = lds_u32(la, GCM_TA(sA[(j + 1) & 3], 1));
+        const uint32_t rc = lds_u32(la, GCM_TA(sA[(j + 2) & 3], 2)), rd = lds_u32(la, GCM_TA(sA[(j + 3) & 3], 3));
+        const uint32_t qa = lds_u32(la, GCM_TA(sB[j], 0)), qb = lds_u32(la, GCM_TA(sB[(j + 1) & 3], 1));
+        const uint32_t qc = lds_u32(la, GCM_TA(sB[(j + 2) & 3], 2)), qd = lds_u32(la, GCM_TA(sB[(j + 3) & 3], 3));
+        wA[j] = xor3(perm(rb, ra, 0x0c0c0501u), perm(rd, rc, 0x06020c0cu), k[j]);
+        wB[j] = xor3(perm(qb, qa, 0x0c0c0501u), perm(qd, qc, 0x06020c0cu), k[j]);
+    }
 #undef GCM_TA
 }
 
@@ -1445,6 +1633,7 @@ struct LayoutWin {
     static constexpr uint32_t ghpair = gh256 + GH_TABLE_BYTES;
     static constexpr uint32_t parts = ghpair + (SEG == 32 ? GH_TABLE_BYTES : 0u);
     static constexpr bool split_scale = false;
+    static constexpr bool x2_walk = false;
     static constexpr bool parts_alias = false; /* the segment sums have their own LDS (after the tables) */
 };
 
@@ -1471,6 +1660,7 @@ struct LayoutWin16 {
     static constexpr uint32_t parts = 0x10000u;
     static constexpr uint32_t bytes = 0x28000u;
     static constexpr bool split_scale = true;
+    static constexpr bool x2_walk = false;
     static constexpr bool wide_scale = false; /* 3 waves per SIMD: no registers for 32 reads in flight */
     static constexpr bool parts_alias = true;
 };
@@ -1501,6 +1691,9 @@ GCM_HD u32x4 window_image_vec(const uint32_t *t0, const KeyImage *ki, uint32_t v
  * Fills the window image, split over nthr threads.  Eight vectors per thread are loaded before any is
  * stored: a fill pass is one memory latency, and with 256 threads the image takes 26 vectors per thread.
  */
+#ifndef GCM_SPLIT_X2
+#define GCM_SPLIT_X2 1 /* split kernels: a segment's two steps as one interleaved two-block AES (lane_walk) */
+#endif
 #ifndef GCM_WIN_FILL
 #define GCM_WIN_FILL 8u /* vectors loaded per thread before any is stored (one memory latency per pass) */
 #endif
@@ -1540,6 +1733,7 @@ struct LayoutSplit {
     static constexpr uint32_t parts = 0x10000u;    /* segment sums, after the walk (aliases H^1) */
     static constexpr uint32_t bytes = 0x28000u;
     static constexpr bool split_scale = true;
+    static constexpr bool x2_walk = true; /* a segment's two steps in one trip (lane_walk) */
     static constexpr bool wide_scale = true; /* one wave per SIMD: registers for 32 reads in flight */
     static constexpr bool parts_alias = true;
 };
@@ -1865,8 +2059,15 @@ GCM_HD u32x4 lane_walk_seg(const uint8_t *lds, uint32_t lanesel, const uint32_t 
         }
         *(u32x4_u *)(out + 16u * c) = o;
     };
-    auto step = [&](uint32_t t, u32x4 cur) {
-        GCM_OPAQUE(t);
+    /* the block a lane consumes in step t: its counter (payload c + 2, otherwise J0, counter 1) */
+    auto step_ctr = [&](uint32_t t) -> uint32_t {
+        const int32_t p = (int32_t)(j + K * t) - (int32_t)wk.pad;
+        const bool is_pay = valid && t < wk.T && p < (int32_t)gend && p >= 0 && (uint32_t)p >= wk.A &&
+                            (uint32_t)p < wk.A + wk.C;
+        return is_pay ? (uint32_t)p - wk.A + 2u : 1u;
+    };
+    /* everything of step t after its keystream ks and its Horner product P = A_(t-1) * H^K */
+    auto finish = [&](uint32_t t, u32x4 cur, u32x4 ks, u32x4 P) {
         const int32_t p = (int32_t)(j + K * t) - (int32_t)wk.pad;
         const bool active = valid && t < wk.T && p < (int32_t)gend;
         const bool is_aad = active && p >= 0 && (uint32_t)p < wk.A;
@@ -1875,37 +2076,6 @@ GCM_HD u32x4 lane_walk_seg(const uint8_t *lds, uint32_t lanesel, const uint32_t 
         const uint32_t c = (uint32_t)p - wk.A;
         const uint32_t clen = plen - 16u * c;    /* bytes of this payload block if < 16 */
         const uint32_t flen = rec.len - 16u * c; /* of them from the input (FRAME seal: all but the type byte) */
-
-        /* one AES per lane per step: payload counter c + 2, otherwise J0 (counter 1) */
-        uint32_t ctr = is_pay ? c + 2u : 1u;
-        uint32_t w[4] = {iv0, iv1, iv2, bswap32(ctr)};
-#if GCM_ABLATE_AES && GCM_ABLATE_GHASH
-        const u32x4 P = acc;
-#elif GCM_ABLATE_AES
-        const u32x4 P = LY::gh5 ? ghash5_mul_lds(lds, acc) : ghash_mul_lds(lds, LY::gh_base, acc);
-#elif GCM_ABLATE_GHASH
-        aes_encrypt_tt<NR, LY::four_tables>(lds + LY::aes_base, lanesel, rk, w);
-        const u32x4 P = acc;
-#else
-        if ((ctr & WIN) != c1_hi) { /* a record crossing a counter window (>= 2^8 blocks with GCM_R2CACHE) */
-            c1_hi = ctr & WIN;
-            /* opaque inputs: keeps LICM from parking this rare path's 16 LDS addresses in VGPRs */
-            uint32_t o0 = iv0, o1 = iv1, o2 = iv2, ol = lanesel;
-            GCM_OPAQUE(o0);
-            GCM_OPAQUE(o1);
-            GCM_OPAQUE(o2);
-            GCM_OPAQUE(ol);
-#if GCM_R2CACHE
-            aes_round12_consts<LY::four_tables>(lds + LY::aes_base, ol, rk, o0, o1, o2, c1_hi, c1);
-#else
-            aes_round1_consts<LY::four_tables>(lds + LY::aes_base, ol, rk, o0, o1, o2, c1_hi, c1);
-#endif
-        }
-        const u32x4 P =
-            aes_ghash_fused_h<NR, LY::four_tables, LY::gh5, LY::aes_base>(lds, lanesel, rk, c1, ctr, w, LY::gh_base, acc);
-#endif
-        const u32x4 ks = {w[0], w[1], w[2], w[3]};
-
         u32x4 X = {0u, 0u, 0u, 0u};
         if (is_pay) {
             u32x4 data = cur;
@@ -1960,6 +2130,37 @@ GCM_HD u32x4 lane_walk_seg(const uint8_t *lds, uint32_t lanesel, const uint32_t 
         if (active)
             acc = P ^ X;
     };
+    auto step = [&](uint32_t t, u32x4 cur) {
+        GCM_OPAQUE(t);
+        const uint32_t ctr = step_ctr(t);
+        uint32_t w[4] = {iv0, iv1, iv2, bswap32(ctr)};
+#if GCM_ABLATE_AES && GCM_ABLATE_GHASH
+        const u32x4 P = acc;
+#elif GCM_ABLATE_AES
+        const u32x4 P = LY::gh5 ? ghash5_mul_lds(lds, acc) : ghash_mul_lds(lds, LY::gh_base, acc);
+#elif GCM_ABLATE_GHASH
+        aes_encrypt_tt<NR, LY::four_tables>(lds + LY::aes_base, lanesel, rk, w);
+        const u32x4 P = acc;
+#else
+        if ((ctr & WIN) != c1_hi) { /* a record crossing a counter window (>= 2^8 blocks with GCM_R2CACHE) */
+            c1_hi = ctr & WIN;
+            /* opaque inputs: keeps LICM from parking this rare path's 16 LDS addresses in VGPRs */
+            uint32_t o0 = iv0, o1 = iv1, o2 = iv2, ol = lanesel;
+            GCM_OPAQUE(o0);
+            GCM_OPAQUE(o1);
+            GCM_OPAQUE(o2);
+            GCM_OPAQUE(ol);
+#if GCM_R2CACHE
+            aes_round12_consts<LY::four_tables>(lds + LY::aes_base, ol, rk, o0, o1, o2, c1_hi, c1);
+#else
+            aes_round1_consts<LY::four_tables>(lds + LY::aes_base, ol, rk, o0, o1, o2, c1_hi, c1);
+#endif
+        }
+        const u32x4 P =
+            aes_ghash_fused_h<NR, LY::four_tables, LY::gh5, LY::aes_base>(lds, lanesel, rk, c1, ctr, w, LY::gh_base, acc);
+#endif
+        finish(t, cur, u32x4{w[0], w[1], w[2], w[3]}, P);
+    };
 
     /*
      * Two steps per trip with two load buffers: the block of step t+1 is in flight during step
@@ -1980,6 +2181,36 @@ GCM_HD u32x4 lane_walk_seg(const uint8_t *lds, uint32_t lanesel, const uint32_t 
         bufA = load_partial(ad, rec.aadlen);
     else
         bufA = walk_load(fetch_ptr(t0));
+#if GCM_SPLIT_X2 && !GCM_ABLATE_AES && !GCM_ABLATE_GHASH
+    if constexpr (LY::x2_walk) {
+        static_assert(GCM_R2CACHE && !LY::four_tables, "the x2 walk runs the two-table rounds with round-2 caching");
+        if (use_seg && Tmax == t0 + 2u) { /* wave-uniform: a whole segment in one trip */
+            /*
+             * Both steps' counter blocks in one interleaved AES (aes_ctr_x2_h): the walk's two dependent AES chains
+             * become one, at the price of exposing the one Horner multiply (the chain is 0 before the segment's
+             * first step, so that step's product is 0 and only the second one multiplies).
+             */
+            const u32x4 bufB = walk_load(fetch_ptr(t0 + 1u));
+            const uint32_t ctrA = step_ctr(t0), ctrB = step_ctr(t0 + 1u);
+            uint32_t o0 = iv0, o1 = iv1, o2 = iv2, ol = lanesel;
+            if ((ctrA & WIN) != c1_hi) {
+                c1_hi = ctrA & WIN;
+                aes_round12_consts<false>(lds + LY::aes_base, ol, rk, o0, o1, o2, c1_hi, c1);
+            }
+            uint32_t c2[8];
+            for (int i = 0; i < 8; ++i)
+                c2[i] = c1[i];
+            if ((ctrB & WIN) != c1_hi) /* the two blocks straddle a counter window */
+                aes_round12_consts<false>(lds + LY::aes_base, ol, rk, o0, o1, o2, ctrB & WIN, c2);
+            uint32_t wA[4] = {iv0, iv1, iv2, bswap32(ctrA)}, wB[4] = {iv0, iv1, iv2, bswap32(ctrB)};
+            aes_ctr_x2_h<NR, LY::aes_base>(lds, lanesel, rk, c1, c2, ctrA, ctrB, wA, wB);
+            finish(t0, bufA, u32x4{wA[0], wA[1], wA[2], wA[3]}, u32x4{0u, 0u, 0u, 0u});
+            const u32x4 P = ghash_mul_scale<LY::wide_scale>(lds, LY::gh_base, acc);
+            finish(t0 + 1u, bufB, u32x4{wB[0], wB[1], wB[2], wB[3]}, P);
+            goto Scale;
+        }
+    }
+#endif
     if (PF >= 3) {
         /*
          * Prefetch three steps ahead (window kernels at one wave per SIMD, where nothing else hides a load's
@@ -2011,6 +2242,9 @@ GCM_HD u32x4 lane_walk_seg(const uint8_t *lds, uint32_t lanesel, const uint32_t 
             GCM_WALK_STAMP(11);
         }
     }
+#if GCM_SPLIT_X2 && !GCM_ABLATE_AES && !GCM_ABLATE_GHASH
+Scale:
+#endif
     GCM_WALK_STAMP(12);
     if constexpr (PAIRST) {
         if (pend_c != 0xffffffffu) /* a first half with no second half in this walk */

@@ -43,7 +43,8 @@ VARIANTS = {
     # K = 4 walks storing whole 128-byte lines (lane_walk PAIRST, r02) vs one 64-byte piece per step
     "pair": ["-DGCM_PAIR_STORES=1"],
     "ntload": ["-DGCM_NT_LOADS=1"],
-    "noglds": ["-DGCM_SPLIT_GLDS=0"],  # split window kernels: register-staged LDS fill instead of LDS DMA  # non-temporal input loads (keep the half-written output lines in L2)
+    "noglds": ["-DGCM_SPLIT_GLDS=0"],
+    "nox2": ["-DGCM_SPLIT_X2=0"],  # split kernels: a segment's two steps one after the other (one AES chain each)  # split window kernels: register-staged LDS fill instead of LDS DMA  # non-temporal input loads (keep the half-written output lines in L2)
     # r02 experiments on the last AES round (last-round S-box lookups through the vector-memory path; two steps'
     # last rounds bitsliced on the VALU; T1 moved to image B): scripts/experiments/r02_last_round_vmem_pair_t1b.patch
     # holds the source, profiles/r02[c-e]_ablate_*.txt the measurements -- all slower, not in csrc/
