@@ -2059,7 +2059,12 @@ GCM_HD u32x4 lane_walk_seg(const uint8_t *lds, uint32_t lanesel, const uint32_t 
         }
         *(u32x4_u *)(out + 16u * c) = o;
     };
-    /* the block a lane consumes in step t: its counter (payload c + 2, otherwise J0, counter 1) */
+    /*
+     * step_ctr and finish: step() below cut at its keystream, for the split kernels' two-step trip (x2 walk).  step()
+     * keeps its own copy of both halves: expressed through these two lambdas it measured 2-3% slower in the batch
+     * kernels at 1400 B (codegen), so the same logic is written twice; tests/test_kernel_model.py and the GPU suites
+     * check both against the oracle.
+     */
     auto step_ctr = [&](uint32_t t) -> uint32_t {
         const int32_t p = (int32_t)(j + K * t) - (int32_t)wk.pad;
         const bool is_pay = valid && t < wk.T && p < (int32_t)gend && p >= 0 && (uint32_t)p >= wk.A &&
@@ -2132,7 +2137,17 @@ GCM_HD u32x4 lane_walk_seg(const uint8_t *lds, uint32_t lanesel, const uint32_t 
     };
     auto step = [&](uint32_t t, u32x4 cur) {
         GCM_OPAQUE(t);
-        const uint32_t ctr = step_ctr(t);
+        const int32_t p = (int32_t)(j + K * t) - (int32_t)wk.pad;
+        const bool active = valid && t < wk.T && p < (int32_t)gend;
+        const bool is_aad = active && p >= 0 && (uint32_t)p < wk.A;
+        const bool is_pay = active && (uint32_t)p >= wk.A && (uint32_t)p < wk.A + wk.C && p >= 0;
+        const bool is_len = active && (uint32_t)p == wk.A + wk.C;
+        const uint32_t c = (uint32_t)p - wk.A;
+        const uint32_t clen = plen - 16u * c;    /* bytes of this payload block if < 16 */
+        const uint32_t flen = rec.len - 16u * c; /* of them from the input (FRAME seal: all but the type byte) */
+
+        /* one AES per lane per step: payload counter c + 2, otherwise J0 (counter 1) */
+        uint32_t ctr = is_pay ? c + 2u : 1u;
         uint32_t w[4] = {iv0, iv1, iv2, bswap32(ctr)};
 #if GCM_ABLATE_AES && GCM_ABLATE_GHASH
         const u32x4 P = acc;
@@ -2159,7 +2174,61 @@ GCM_HD u32x4 lane_walk_seg(const uint8_t *lds, uint32_t lanesel, const uint32_t 
         const u32x4 P =
             aes_ghash_fused_h<NR, LY::four_tables, LY::gh5, LY::aes_base>(lds, lanesel, rk, c1, ctr, w, LY::gh_base, acc);
 #endif
-        finish(t, cur, u32x4{w[0], w[1], w[2], w[3]}, P);
+        const u32x4 ks = {w[0], w[1], w[2], w[3]};
+
+        u32x4 X = {0u, 0u, 0u, 0u};
+        if (is_pay) {
+            u32x4 data = cur;
+            if (FRAME && SEAL && flen < 16u) {
+                /* the last block: fb = flen fragment bytes (0..15), then the content type */
+                if (flen == 0u)
+                    data = u32x4{0u, 0u, 0u, 0u};
+                else if (rec.len >= 16u)
+                    data = shr_bytes(data, 16u - flen);
+                else /* rare: a fragment under 16 bytes, read in place */
+                    data = load_partial(in, rec.len);
+                data = insert_byte(data, flen, ctype);
+                const u32x4 o = data ^ ks;
+                if (clen == 16u)
+                    put(t, c, o);
+                else
+                    store_partial(out + 16u * c, clen, o);
+                X = mask_tail(o, clen);
+            } else if (clen >= 16u) {
+                const u32x4 o = data ^ ks;
+                put(t, c, o);
+                X = SEAL ? o : data;
+            } else {
+                if (SEAL) {
+                    if (rec.len >= 16u)
+                        data = shr_bytes(data, 16u - clen);
+                    else /* rare: a whole payload under 16 bytes, read in place */
+                        data = load_partial(in, rec.len);
+                }
+                const u32x4 o = data ^ ks;
+                store_partial(out + 16u * c, clen, o);
+                X = mask_tail(SEAL ? o : data, clen);
+            }
+        } else if (is_aad) {
+            if (FRAME) { /* 17 03 03 BE16(plen + 16) */
+                const uint32_t reclen = plen + 16u;
+                X[0] = 0x00030317u | ((reclen >> 8) & 0xffu) << 24;
+                X[1] = reclen & 0xffu;
+            } else if (use_seg && rec.aadlen < 16u) {
+                X = load_partial(ad, rec.aadlen); /* segment walks: the short AAD may sit in any step */
+            } else {
+                X = 16u * (uint32_t)p + 16u <= rec.aadlen || rec.aadlen < 16u ? cur : shr_bytes(cur, 16u - arem);
+            }
+        } else if (is_len) {
+            uint64_t abits = (uint64_t)aadlen * 8u, cbits = (uint64_t)plen * 8u;
+            X[0] = bswap32((uint32_t)(abits >> 32));
+            X[1] = bswap32((uint32_t)abits);
+            X[2] = bswap32((uint32_t)(cbits >> 32));
+            X[3] = bswap32((uint32_t)cbits);
+            ek0 = SEAL ? ks : ks ^ cur; /* open: E(J0) ^ received tag */
+        }
+        if (active)
+            acc = P ^ X;
     };
 
     /*
