@@ -388,10 +388,10 @@ size_t ptls_mi355x_set_seg32_records(size_t n);
  */
 size_t ptls_mi355x_set_win16_records(size_t n);
 /*
- * Window batches of at most n records use the split kernels: every record's segments are cut into runs of 16, each
- * walked by its own 256-thread workgroup on its own CU (3 per TLS record), the runs' partial GHASH sums joined by the
+ * Window batches of at most n records use the split kernels: every record's segments are cut into runs of 8, each
+ * walked by its own 128-thread workgroup on its own CU (5 per TLS record), the runs' partial GHASH sums joined by the
  * last to arrive.  The lowest-latency family for a few records (a rapido send window).  Takes precedence over
- * ptls_mi355x_set_win16_records.  SIZE_MAX (the default) means a third of the device's CU count, 0 disables.
+ * ptls_mi355x_set_win16_records.  SIZE_MAX (the default) means a fifth of the device's CU count, 0 disables.
  * Returns the previous value.  Results are identical.
  */
 size_t ptls_mi355x_set_split_records(size_t n);

@@ -674,8 +674,8 @@ def set_win16_records(n: int) -> int:
 
 
 def set_split_records(n: int) -> int:
-    """Window batches of at most n records use the split kernels (runs of 16 segments on separate CUs; 0: never;
-    SEG32_AUTO: a third of the CUs); they take precedence over set_win16_records."""
+    """Window batches of at most n records use the split kernels (runs of 8 segments on separate CUs; 0: never;
+    SEG32_AUTO: a fifth of the CUs); they take precedence over set_win16_records."""
     L = lib()
     if not hasattr(L, "ptls_mi355x_set_split_records"):
         return 0

@@ -1144,8 +1144,9 @@ struct KeyImage {
     uint8_t gh128[32][16][16];     /* single-record latency kernels (window_body SEG = 32) */
     uint8_t gh256[32][16][16];     /* nibble tables of H^256: joins groups of 4 segments (window_join) */
     uint8_t gh64[32][16][16];      /* nibble tables of H^64: joins the 64-position segments of the window kernels */
-    uint8_t gh512[32][16][16];     /* H^512 and H^1024: scale a run of 16 segments to the record's end (the */
-    uint8_t gh1024[32][16][16];    /* split window kernels, LayoutSplit) */
+    uint8_t gh512[32][16][16];     /* H^256 m, m = 1..4 (gh256, gh512, gh768, gh1024): scale a run of 8 segments */
+    uint8_t gh1024[32][16][16];    /* to the record's end, m runs after it (the split window kernels, LayoutSplit) */
+    uint8_t gh768[32][16][16];
 };
 static_assert(offsetof(KeyImage, gh16) == offsetof(KeyImage, gh) + MAX_K * 8192 &&
                   offsetof(KeyImage, gh256) == offsetof(KeyImage, gh16) + 3 * 8192 && offsetof(KeyImage, gh) % 16 == 0,
@@ -1465,8 +1466,9 @@ GCM_HD Gf128 gf_mul_lane_share(Gf128 X, Gf128 Y, uint32_t lane)
     return acc;
 }
 
-/* The 15 multipliers of the key image, by index s: H^1..H^8, then H^64, H^256, H^32, H^128, H^16, H^512, H^1024. */
-enum : uint32_t { KEY_IMAGE_TABLES = MAX_K + 7 };
+/* The 16 multipliers of the key image, by index s: H^1..H^8, then H^64, H^256, H^32, H^128, H^16, H^512, H^1024,
+ * H^768. */
+enum : uint32_t { KEY_IMAGE_TABLES = MAX_K + 8 };
 
 GCM_HD uint8_t (*key_image_table(KeyImage *ki, uint32_t s))[16][16]
 {
@@ -1477,7 +1479,8 @@ GCM_HD uint8_t (*key_image_table(KeyImage *ki, uint32_t s))[16][16]
            : s == MAX_K + 3u        ? ki->gh128
            : s == MAX_K + 4u        ? ki->gh16
            : s == MAX_K + 5u        ? ki->gh512
-                                    : ki->gh1024;
+           : s == MAX_K + 6u        ? ki->gh1024
+                                    : ki->gh768;
 }
 
 /*
@@ -1552,8 +1555,13 @@ GCM_HD int build_key_image(const uint8_t *sbox, const uint8_t *key, uint32_t key
     nibble_tables(hp, ki->gh128);
     gf128_mul_bytes(hp, hp, hp);
     nibble_tables(hp, ki->gh256);
+    uint8_t h256[16], h768[16];
+    for (int k = 0; k < 16; ++k)
+        h256[k] = hp[k];
     gf128_mul_bytes(hp, hp, hp);
     nibble_tables(hp, ki->gh512);
+    gf128_mul_bytes(hp, h256, h768); /* H^768 = H^512 H^256 */
+    nibble_tables(h768, ki->gh768);
     gf128_mul_bytes(hp, hp, hp);
     nibble_tables(hp, ki->gh1024);
     return 0;
@@ -1716,10 +1724,10 @@ GCM_HD void fill_lds_window(uint8_t *lds, const uint32_t *t0, const KeyImage *ki
 
 /*
  * LDS map of the split window kernels (gcm_engine.hip split_body): a record's 32-position segments are cut into runs
- * of 16, each run walked by its own 256-thread workgroup (16 lanes per segment, 2 steps) on its own CU.  As
- * LayoutWin16 up to 152K; the last table scales the run's sum to the record's end, H^(512 m) for the m runs after it.
+ * of 8, each run walked by its own 128-thread workgroup (16 lanes per segment, one two-block trip) on its own CU.  As
+ * LayoutWin16 up to 152K; the last table scales the run's sum to the record's end, H^(256 m) for the m runs after it.
  *   [0, 64K) AES image; [64K, 128K) H^1..H^8; [128K) H^16 (Horner); [136K) H^32 (groups of 4 segments);
- *   [144K) H^128 (the chain of groups); [152K) H^512 or H^1024 (gh_run)
+ *   [144K) H^128 (the chain of groups); [152K) H^256, H^512, H^768 or H^1024 (gh_run)
  */
 struct LayoutSplit {
     static constexpr bool four_tables = false;
@@ -1738,19 +1746,26 @@ struct LayoutSplit {
     static constexpr bool parts_alias = true;
 };
 enum : uint32_t {
-    SPLIT_RUNSEG = 16,  /* segments per run (one workgroup) */
-    SPLIT_MAXRUN = 3,   /* runs of a TLS record (33 segments); larger records are walked whole by run 0 */
-    SPLIT_THREADS = 256,
+    SPLIT_RUNSEG = 8,   /* segments per run (one workgroup) */
+    SPLIT_MAXRUN = 5,   /* runs of a TLS record (33 segments); larger records are walked whole by run 0 */
+    SPLIT_THREADS = 128,
 };
 
-/* vector v of the LayoutSplit image for a run followed by m (0..2) runs: AES rows, gh[0] .. gh128, H^(512 m) */
+/* H^(256 m): scales a run of SPLIT_RUNSEG 32-position segments over the m runs after it (m = 1..4; any for m = 0) */
+GCM_HD const u32x4 *split_run_table(const KeyImage *ki, uint32_t m)
+{
+    return (const u32x4 *)(m <= 1u ? &ki->gh256[0][0][0] : m == 2u ? &ki->gh512[0][0][0]
+                                                         : m == 3u ? &ki->gh768[0][0][0] : &ki->gh1024[0][0][0]);
+}
+
+/* vector v of the LayoutSplit image for a run followed by m (0..4) runs: AES rows, gh[0] .. gh128, H^(256 m) */
 GCM_HD u32x4 split_image_vec(const uint32_t *t0, const KeyImage *ki, uint32_t v, uint32_t m)
 {
     if (v < 0x10000u / 16u)
         return window_image_vec(t0, ki, v, 8u, 32u);
     if (v < LayoutSplit::gh_run / 16u)
         return ((const u32x4 *)ki->gh)[v - 0x10000u / 16u];
-    return ((const u32x4 *)(m == 2u ? ki->gh1024 : ki->gh512))[v - LayoutSplit::gh_run / 16u];
+    return split_run_table(ki, m)[v - LayoutSplit::gh_run / 16u];
 }
 
 /* vector v (16 B) of the LayoutWin16 image: the AES rows of window_image_vec, then the key image from gh[0] on */

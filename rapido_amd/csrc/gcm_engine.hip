@@ -619,12 +619,12 @@ __device__ __forceinline__ void window_body(const KeyImage *__restrict__ ki, uin
 }
 
 /*
- * Split window kernels (single-record latency): a record's 32-position segments (16 lanes each, 2 steps) are cut into
- * runs of SPLIT_RUNSEG = 16 aligned to the record's end, and each run is walked by its own 256-thread workgroup (one
- * wave per SIMD) on its own CU: grid = records x SPLIT_MAXRUN, workgroup k of record r takes run k of R (idle if
- * k >= R).  A run joins its segment sums locally (groups of 4 with H^32, the groups chained with H^128, all with the
- * slot's 16 lanes cooperating, ghash_mul_coop) and scales the result by H^(512 m) to the record's end (m runs follow
- * it).  The run then stores its partial, and the workgroup whose arrival ticket is the record's last XORs the R
+ * Split window kernels (single-record latency): a record's 32-position segments (16 lanes each, one two-block trip) are
+ * cut into runs of SPLIT_RUNSEG = 8 aligned to the record's end, and each run is walked by its own 128-thread
+ * workgroup (one wave per SIMD) on its own CU: grid = records x SPLIT_MAXRUN, workgroup k of record r takes run k of R
+ * (idle if k >= R).  A run joins its segment sums locally (groups of 4 with H^32, the two groups chained with H^128,
+ * all with the slot's 16 lanes cooperating, ghash_mul_coop) and scales the result by H^(256 m) to the record's end
+ * (m runs follow it).  The run then stores its partial, and the workgroup whose arrival ticket is the record's last XORs the R
  * partials -- E_K(J0) and, for open, the received tag are already folded into the last run's -- and finishes the
  * record (window_finish): tag and header, or verification, zeroing, status and padding strip.  The last arrival
  * resets the record's ticket, so the counters are zero between launches.  No workgroup waits for another.
@@ -699,13 +699,13 @@ __device__ __forceinline__ void split_body(const KeyImage *__restrict__ ki, uint
     {
         /*
          * One pass: each thread loads its 40 vectors of the image before storing any.  (Loading the tables only the
-         * scaling and the join read -- H^1..H^8, H^32, H^128, H^(512 m) -- by LDS DMA during the walk measured 2 us
+         * scaling and the join read -- H^1..H^8, H^32, H^128, H^(256 m) -- by LDS DMA during the walk measured 2 us
          * SLOWER per window: profiles/r02l_split_ab.txt.)
          */
         constexpr uint32_t NV = LW::bytes / 16u, PER = NV / THREADS;
         static_assert(NV % THREADS == 0u, "whole passes");
         const u32x4 *gk = (const u32x4 *)&ki->gh[0][0][0][0];
-        const u32x4 *gr = (const u32x4 *)(m == 2u ? &ki->gh1024[0][0][0] : &ki->gh512[0][0][0]);
+        const u32x4 *gr = split_run_table(ki, m);
 #if GCM_SPLIT_GLDS
         /*
          * LDS DMA (global_load_lds_dwordx4): a wave-instruction writes 64 x 16 B contiguously at a wave-uniform LDS
@@ -900,7 +900,7 @@ MI355X_WIN16_KERNEL(mi355x_gcm_win16_open_aes128, 10, false, false)
 MI355X_WIN16_KERNEL(mi355x_gcm_win16_open_aes256, 14, false, false)
 
 /*
- * Split window kernels (split_body): SPLIT_MAXRUN 256-thread workgroups per record, each walking one run of 16
+ * Split window kernels (split_body): SPLIT_MAXRUN 128-thread workgroups per record, each walking one run of 8
  * segments on its own CU; partials and arrival tickets in the context's split buffer.
  */
 #define MI355X_SPLIT_KERNEL(NAME, NR, SEAL, FRAME)                                                                     \
@@ -1032,9 +1032,13 @@ extern "C" __global__ __launch_bounds__(1024) void mi355x_gcm_setup(const uint8_
         p = gf_mul_wave(p, p, lane); /* H^256 */
         if (lane == 0)
             s_pow[MAX_K + 1] = p;
+        const Gf128 p256 = p;
         p = gf_mul_wave(p, p, lane); /* H^512 */
         if (lane == 0)
             s_pow[MAX_K + 5] = p;
+        const Gf128 p768 = gf_mul_wave(p, p256, lane); /* H^768 */
+        if (lane == 0)
+            s_pow[MAX_K + 7] = p768;
         p = gf_mul_wave(p, p, lane); /* H^1024 */
         if (lane == 0)
             s_pow[MAX_K + 6] = p;
@@ -1379,7 +1383,7 @@ static LaunchPlan plan_launch(bool seal, bool frame, uint32_t key_size, size_t n
             {{KN(mi355x_tls_win16_open_aes128), KN(mi355x_tls_win16_open_aes256)},
              {KN(mi355x_tls_win16_seal_aes128), KN(mi355x_tls_win16_seal_aes256)}}};
         static const SplitEntry table_split[2][2][2] = {
-            /* [frame][seal][aes256]: runs of 16 segments, SPLIT_MAXRUN workgroups per record */
+            /* [frame][seal][aes256]: runs of SPLIT_RUNSEG segments, SPLIT_MAXRUN workgroups per record */
             {{KN(mi355x_gcm_wins_open_aes128), KN(mi355x_gcm_wins_open_aes256)},
              {KN(mi355x_gcm_wins_seal_aes128), KN(mi355x_gcm_wins_seal_aes256)}},
             {{KN(mi355x_tls_wins_open_aes128), KN(mi355x_tls_wins_open_aes256)},

@@ -351,7 +351,7 @@ static void run_win16(const KeyImage *ki, uint8_t *lds, uint8_t *lds_m2, const u
                 for (uint32_t g = 2 - ng % 2; g < ng; g += 2)
                     acc = ghash_mul_lds_wide(lds, LayoutWin16::ghpair, acc) ^ parts[window_group_start(g, nseg)];
             } else {
-                /* split_body: runs of 16 aligned to the end, each joined, scaled by H^(512 m), XORed */
+                /* split_body: runs of SPLIT_RUNSEG aligned to the end, each joined, scaled by H^(256 m), XORed */
                 const uint32_t R = (nseg + SPLIT_RUNSEG - 1) / SPLIT_RUNSEG;
                 for (uint32_t k = 0; k < R; ++k) {
                     const int32_t first = (int32_t)nseg - (int32_t)(SPLIT_RUNSEG * (R - k));
@@ -365,8 +365,11 @@ static void run_win16(const KeyImage *ki, uint8_t *lds, uint8_t *lds_m2, const u
                     for (uint32_t q = window_group_end(0, ns); q < ns; q += 4)
                         run = ghash_mul_lds_wide(lds, LayoutSplit::gh_chain, run) ^ p[q];
                     const uint32_t m = R - 1 - k;
-                    if (m != 0)
-                        run = ghash_mul_lds_wide(m == 2 ? lds_m2 : lds, LayoutSplit::gh_run, run);
+                    if (m != 0) { /* H^(256 m): the run's workgroup holds that table in its gh_run slot */
+                        memcpy(lds_m2, lds, LayoutSplit::bytes);
+                        memcpy(lds_m2 + LayoutSplit::gh_run, split_run_table(ki, m), GH_TABLE_BYTES);
+                        run = ghash_mul_lds_wide(lds_m2, LayoutSplit::gh_run, run);
+                    }
                     acc ^= run;
                 }
             }
@@ -391,11 +394,9 @@ extern "C" int model_batch_win16(int is_seal, int split, const uint8_t *key, siz
         free(lds2);
         return -1;
     }
-    if (split) { /* the image of a run followed by one run (H^512), and by two (H^1024) */
-        for (uint32_t v = 0; v < LayoutSplit::bytes / 16u; ++v) {
+    if (split) { /* the image of a run followed by one run (H^256); run_win16 swaps the gh_run table per run */
+        for (uint32_t v = 0; v < LayoutSplit::bytes / 16u; ++v)
             *(u32x4 *)(lds + 16u * v) = split_image_vec(kTabs.t0, ki, v, 1u);
-            *(u32x4 *)(lds2 + 16u * v) = split_image_vec(kTabs.t0, ki, v, 2u);
-        }
     } else {
         fill_lds_win16(lds, kTabs.t0, ki, 0, 1);
     }
@@ -567,7 +568,9 @@ extern "C" int model_key_image_parallel(const uint8_t *key, size_t keylen, void 
     pw[MAX_K] = p = wave_mul(p, p);        /* H^64 */
     pw[MAX_K + 3] = p = wave_mul(p, p);    /* H^128 */
     pw[MAX_K + 1] = p = wave_mul(p, p);    /* H^256 */
+    const Gf128 p256 = p;
     pw[MAX_K + 5] = p = wave_mul(p, p);    /* H^512 */
+    pw[MAX_K + 7] = wave_mul(p, p256);     /* H^768 */
     pw[MAX_K + 6] = p = wave_mul(p, p);    /* H^1024 */
     static Gf128 bits[KEY_IMAGE_TABLES][128];
     for (uint32_t i = 0; i < KEY_IMAGE_TABLES * 128u; ++i)
