@@ -1749,6 +1749,7 @@ enum : uint32_t {
     SPLIT_RUNSEG = 8,   /* segments per run (one workgroup) */
     SPLIT_MAXRUN = 5,   /* runs of a TLS record (33 segments); larger records are walked whole by run 0 */
     SPLIT_THREADS = 128,
+    SPLIT_PSLOTS = SPLIT_MAXRUN,     /* u32x4 slots per record in the split buffer: the runs' partials */
 };
 
 /* H^(256 m): scales a run of SPLIT_RUNSEG 32-position segments over the m runs after it (m = 1..4; any for m = 0) */

@@ -333,14 +333,40 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
 }
 
 /*
+ * The TLS 1.3 padding strip (lib/picotls.c:4784-4791) over plaintext bytes [lo, n) of a record at pt: the position of
+ * the last non-zero byte (the inner content type; the inner plaintext's length) and that byte, scanning back 16 bytes at
+ * a time; found = 0xfffffffe if the bytes are all zero.
+ */
+__device__ __forceinline__ void strip_scan(const uint8_t *pt, uint32_t lo, uint32_t n, uint32_t &found, uint32_t &ty)
+{
+    found = 0xfffffffeu;
+    ty = 0u;
+    while (n > lo && found == 0xfffffffeu) {
+        const uint32_t base = n - lo >= 16u ? n - 16u : lo;
+        const u32x4 v = n - base == 16u ? *(const u32x4_u *)(pt + base) : load_partial(pt + base, n - base);
+#pragma unroll
+        for (int d = 3; d >= 0; --d) {
+            if (found == 0xfffffffeu && v[d] != 0u) {
+                const uint32_t b = (31u - (uint32_t)__builtin_clz(v[d])) >> 3;
+                found = base + 4u * (uint32_t)d + b;
+                ty = (v[d] >> (8u * b)) & 0xffu;
+            }
+        }
+        n = base;
+    }
+}
+
+/*
  * The end of a record in the window kernels: seal writes the tag (and the TLS header), open verifies (acc = computed
  * tag ^ received tag), zeroes a failed record's plaintext and writes the status (and strips the TLS padding).  Run by
  * nt threads t = 0..nt-1 together; thread 0 does the single stores.
+ * hint_found / hint_type: the strip's result if the caller already has it (split kernels), else 0xffffffff.
  */
 template <bool SEAL, bool FRAME>
 __device__ __forceinline__ void window_finish(u32x4 acc, bool valid, const Record &rec, uint32_t plen, uint32_t r, uint32_t t,
                                               uint32_t nt, uint8_t *dst, uint32_t *__restrict__ status,
-                                              uint8_t *__restrict__ types)
+                                              uint8_t *__restrict__ types, uint32_t hint_found = 0xffffffffu,
+                                              uint32_t hint_type = 0u)
 {
     if (SEAL) {
         if (t == 0u && valid) {
@@ -371,21 +397,10 @@ __device__ __forceinline__ void window_finish(u32x4 acc, bool valid, const Recor
             status[r] = rec.len;
     } else if (t == 0u) {
         /* padding strip + content-type pop (lib/picotls.c:4784-4791) over plaintext the other slots (workgroups) wrote */
-        __threadfence();
-        const uint8_t *pt = dst + rec.dst;
-        uint32_t n = plen, found = 0xfffffffeu, ty = 0u; /* PTLS_ALERT_UNEXPECTED_MESSAGE if all zero */
-        while (n != 0u && found == 0xfffffffeu) {
-            const uint32_t base = n >= 16u ? n - 16u : 0u;
-            const u32x4 v = n >= 16u ? *(const u32x4_u *)(pt + base) : load_partial(pt, n);
-#pragma unroll
-            for (int d = 3; d >= 0; --d) {
-                if (found == 0xfffffffeu && v[d] != 0u) {
-                    const uint32_t b = (31u - (uint32_t)__builtin_clz(v[d])) >> 3;
-                    found = base + 4u * (uint32_t)d + b;
-                    ty = (v[d] >> (8u * b)) & 0xffu;
-                }
-            }
-            n = base;
+        uint32_t found = hint_found, ty = hint_type;
+        if (found == 0xffffffffu) {
+            __threadfence();
+            strip_scan(dst + rec.dst, 0u, plen, found, ty); /* PTLS_ALERT_UNEXPECTED_MESSAGE (0xfffffffe) if all zero */
         }
         status[r] = found;
         types[r] = (uint8_t)ty;
@@ -645,6 +660,7 @@ __device__ __forceinline__ void split_body(const KeyImage *__restrict__ ki, uint
     __shared__ __attribute__((aligned(16))) uint8_t lds[LW::bytes];
     /* after the walk: the 16 segment sums, then the arrival ticket, over the (dead) H^1 table */
     uint32_t *s_ticket = (uint32_t *)(lds + LW::parts + SPLIT_RUNSEG * 16u);
+    uint32_t *s_hint = s_ticket + 1; /* the strip hint of open (two words) */
     const uint32_t r = blockIdx.x / SPLIT_MAXRUN, k = blockIdx.x % SPLIT_MAXRUN;
     if (r >= nrecs)
         return;
@@ -780,7 +796,7 @@ __device__ __forceinline__ void split_body(const KeyImage *__restrict__ ki, uint
             acc = ghash_mul_coop<KW>(lds, LW::gh_run, acc, j);
         if (R > 1u && j == 0u) {
             /* publish the run's partial, then take an arrival ticket (release: the partial and this run's output) */
-            partials[SPLIT_MAXRUN * r + k] = acc;
+            partials[SPLIT_PSLOTS * r + k] = acc;
             __threadfence();
             *s_ticket = atomicAdd(&tickets[r], 1u);
         }
@@ -796,7 +812,18 @@ __device__ __forceinline__ void split_body(const KeyImage *__restrict__ ki, uint
         if (real && li == 0u) {
             acc = u32x4{0u, 0u, 0u, 0u};
             for (uint32_t q = 0; q < R; ++q)
-                acc ^= partials[SPLIT_MAXRUN * r + q];
+                acc ^= partials[SPLIT_PSLOTS * r + q];
+            if (FRAME && !SEAL && j == 1u) {
+                /*
+                 * The padding strip's first 16 bytes, loaded beside the partials (one L2 round trip for both, instead of
+                 * a second one in window_finish): almost every record's content type is in its last 16 bytes.  If they
+                 * are all zero the finish scans the whole record (0xffffffff).
+                 */
+                uint32_t found, ty;
+                strip_scan(dst + rec.dst, plen >= 16u ? plen - 16u : 0u, plen, found, ty);
+                s_hint[0] = found == 0xfffffffeu && plen > 16u ? 0xffffffffu : found;
+                s_hint[1] = ty;
+            }
             if (j == 0u)
                 tickets[r] = 0u; /* every run has arrived: zero for the next launch */
         }
@@ -806,7 +833,9 @@ __device__ __forceinline__ void split_body(const KeyImage *__restrict__ ki, uint
         *(u32x4 *)(lds + LW::parts) = acc;
     __syncthreads();
     acc = *(const u32x4 *)(lds + LW::parts);
-    window_finish<SEAL, FRAME>(acc, valid, rec, plen, r, threadIdx.x, THREADS, dst, status, types);
+    const bool hinted = FRAME && !SEAL && R > 1u; /* s_hint written by the last-arrival block above */
+    window_finish<SEAL, FRAME>(acc, valid, rec, plen, r, threadIdx.x, THREADS, dst, status, types,
+                               hinted ? s_hint[0] : 0xffffffffu, hinted ? s_hint[1] : 0u);
     SPLIT_STAMP_LAST(7);
 }
 
@@ -1464,8 +1493,8 @@ static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void
             ctx->d_split = nullptr;
             ctx->split_cap = 0;
             const size_t cap = n < 64 ? 64 : n;
-            HIPCHK(hipMalloc(&ctx->d_split, cap * (SPLIT_MAXRUN * sizeof(u32x4) + sizeof(uint32_t))));
-            HIPCHK(hipMemsetAsync((uint8_t *)ctx->d_split + cap * SPLIT_MAXRUN * sizeof(u32x4), 0, cap * sizeof(uint32_t),
+            HIPCHK(hipMalloc(&ctx->d_split, cap * (SPLIT_PSLOTS * sizeof(u32x4) + sizeof(uint32_t))));
+            HIPCHK(hipMemsetAsync((uint8_t *)ctx->d_split + cap * SPLIT_PSLOTS * sizeof(u32x4), 0, cap * sizeof(uint32_t),
                                   stream));
             ctx->split_cap = cap;
             ctx->split_stream = stream;
@@ -1480,7 +1509,7 @@ static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void
                 HIPCHK(hipDeviceSynchronize());
             }
         }
-        uint32_t *tickets = (uint32_t *)((uint8_t *)ctx->d_split + ctx->split_cap * SPLIT_MAXRUN * sizeof(u32x4));
+        uint32_t *tickets = (uint32_t *)((uint8_t *)ctx->d_split + ctx->split_cap * SPLIT_PSLOTS * sizeof(u32x4));
         hipLaunchKernelGGL(p.split, dim3(p.blocks), dim3(p.threads), 0, stream, ctx->d_ki, le32(iv), le32(iv + 4),
                            le32(iv + 8), recs, (uint32_t)n, src, dst, aad, status, types, conn,
                            (const u32x4 *)ctx->shared->d_win_aes, ctx->d_split, tickets);
