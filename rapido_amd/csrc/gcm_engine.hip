@@ -1115,11 +1115,12 @@ __device__ __forceinline__ void aes_ecb_body(const uint32_t *__restrict__ k, uin
     for (uint32_t i = 0; i < 4u * (nr + 1u); ++i)
         rk[i] = k[i];
     __syncthreads();
-    for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < nblocks; b += gridDim.x * blockDim.x) {
-        const u32x4 v = *(const u32x4_u *)(in + 16u * b);
+    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nblocks; b += (uint64_t)gridDim.x * blockDim.x) {
+        const size_t off = (size_t)b * 16u; /* 64-bit: a batch may reach 2^32 - 1 blocks (64 GiB) */
+        const u32x4 v = *(const u32x4_u *)(in + off);
         uint32_t w[4] = {v[0], v[1], v[2], v[3]};
         aes_ecb_block<DEC>(s_t, s_s, rk, nr, w);
-        *(u32x4_u *)(out + 16u * b) = u32x4{w[0], w[1], w[2], w[3]};
+        *(u32x4_u *)(out + off) = u32x4{w[0], w[1], w[2], w[3]};
     }
 }
 
@@ -1223,6 +1224,9 @@ struct st_ptls_mi355x_aesgcm_context {
     hipEvent_t reuse_event;         /* orders a slot's reuse on another stream after its last launch */
     void *d_scratch;                /* order_by_length / stop-at-failure workspace */
     size_t scratch_cap;
+    hipStream_t scratch_stream;     /* stream of the last use of d_scratch (valid once scratch_used) */
+    bool scratch_used;
+    hipEvent_t scratch_event;       /* orders a use of d_scratch on another stream after it */
     u32x4 *d_split;                 /* split window kernels: SPLIT_MAXRUN partials per record, then the tickets */
     size_t split_cap;               /* records the buffer holds */
     hipStream_t split_stream;       /* stream of the last split launch */
@@ -1555,12 +1559,32 @@ static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void
 
 static inline size_t up16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-static int ensure_scratch(ptls_mi355x_aesgcm_context_t *ctx, size_t need)
+/*
+ * The workspace of order_by_length and the stop-at-failure scan, for a use on `stream`.  Launches of one context may
+ * go to any streams, and they share this buffer: a use on another stream than the last one first waits for
+ * everything queued on that one (scratch_event), as the split tickets and the work slots do.  Growing it waits for
+ * the last use before the old buffer is freed.
+ */
+static int ensure_scratch(ptls_mi355x_aesgcm_context_t *ctx, size_t need, hipStream_t stream)
 {
+    if (ctx->scratch_used && ctx->scratch_stream != stream) {
+        if (ctx->scratch_event == nullptr)
+            HIPCHK(hipEventCreateWithFlags(&ctx->scratch_event, hipEventDisableTiming));
+        if (hipEventRecord(ctx->scratch_event, ctx->scratch_stream) == hipSuccess) {
+            HIPCHK(hipStreamWaitEvent(stream, ctx->scratch_event, 0));
+        } else { /* that stream is gone (its work with it) or unusable: wait for the device instead */
+            (void)hipGetLastError();
+            HIPCHK(hipDeviceSynchronize());
+        }
+    }
+    ctx->scratch_stream = stream;
+    ctx->scratch_used = true;
     if (need <= ctx->scratch_cap)
         return 0;
-    if (ctx->d_scratch)
+    if (ctx->d_scratch) {
+        HIPCHK(hipStreamSynchronize(stream)); /* the last use (ordered before this stream's queue above) is done */
         (void)hipFree(ctx->d_scratch);
+    }
     ctx->d_scratch = nullptr;
     ctx->scratch_cap = 0;
     HIPCHK(hipMalloc(&ctx->d_scratch, need));
@@ -1726,6 +1750,8 @@ void ptls_mi355x_aesgcm_free(ptls_mi355x_aesgcm_context_t *ctx)
         (void)hipFree(ctx->d_work);
     if (ctx->d_scratch)
         (void)hipFree(ctx->d_scratch);
+    if (ctx->scratch_event)
+        (void)hipEventDestroy(ctx->scratch_event);
     if (ctx->reuse_event)
         (void)hipEventDestroy(ctx->reuse_event);
     if (ctx->d_split)
@@ -1825,7 +1851,7 @@ int ptls_mi355x_tls_open_records_ex(ptls_mi355x_aesgcm_context_t *ctx, const voi
         HIPCHK(hipcub::DeviceScan::InclusiveScanByKey(nullptr, temp, one_conn, (uint32_t *)nullptr, (uint32_t *)nullptr,
                                                       hipcub::Min(), (uint32_t)n, hipcub::Equality(), stream));
     const size_t arr = ((n * sizeof(uint32_t)) + 255) & ~(size_t)255;
-    if (ensure_scratch(ctx, 2 * arr + temp) != 0)
+    if (ensure_scratch(ctx, 2 * arr + temp, stream) != 0)
         return -1;
     uint8_t *base = (uint8_t *)ctx->d_scratch;
     uint32_t *pos = (uint32_t *)base, *first = (uint32_t *)(base + arr);
@@ -1859,7 +1885,7 @@ int ptls_mi355x_order_by_length(ptls_mi355x_aesgcm_context_t *ctx, const ptls_mi
     HIPCHK(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, temp, (uint32_t *)nullptr, (uint32_t *)nullptr,
                                                         (uint32_t *)nullptr, (uint32_t *)nullptr, (int)n, 0, 24, stream));
     const size_t arr = ((n * sizeof(uint32_t)) + 255) & ~(size_t)255;
-    if (ensure_scratch(ctx, 3 * arr + temp) != 0)
+    if (ensure_scratch(ctx, 3 * arr + temp, stream) != 0)
         return -1;
     uint8_t *base = (uint8_t *)ctx->d_scratch;
     uint32_t *keys_in = (uint32_t *)base, *keys_out = (uint32_t *)(base + arr), *vals_in = (uint32_t *)(base + 2 * arr);
