@@ -411,6 +411,24 @@ def e2e_pcie(ra, extra, dev, steps):
                     "around one launch; pipelined = 16 chunks over 3 streams"}
 
 
+def record_layer_stream(key_bytes: int = 16, nwin: int = 64, depth: int = 4, transport: str = "direct"):
+    """Host-to-host side figure (never `value`): rapido send and receive windows (16 x 16 KiB records, lib/rapido.c
+    :2115-2126) through the asynchronous record layer (include/ptls_mi355x.h section 5) on registered host buffers
+    (direct: the kernels read and write the socket buffers in place over PCIe), `depth` windows in flight.  Driven
+    from C (scripts/rl_stream.c), as rapido would drive it; timed on the host clock from the first submit to the last
+    wait; every opened window is compared with its fragments.  *_sync: one window at a time."""
+    exe = os.path.join(ROOT, "scripts", "_build", "rl_stream")
+    r = subprocess.run([exe, str(nwin), str(depth), str(key_bytes), transport], capture_output=True, text=True,
+                       timeout=120)
+    if r.returncode != 0:
+        raise SystemExit("bench: record-layer stream failed -- " + r.stderr.strip())
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    res["note"] = (f"{nwin} back-to-back windows of 16 x 16384 B records, AES-{8 * key_bytes}, host memory to host "
+                   f"memory ({transport}), {depth} windows in flight (record_layer_seal_submit / open_submit + wait), "
+                   "C driver scripts/rl_stream.c; *_sync: one window at a time")
+    return res
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -486,6 +504,8 @@ def main() -> None:
         out["window_latency"] = window_latency(ra, extra, dev)
     if (args.e2e or world == 1) and not args.no_e2e:
         out["e2e_pcie"] = e2e_pcie(ra, extra, dev, args.steps)
+    if world == 1 and not args.no_e2e:
+        out["record_layer_stream"] = record_layer_stream(16)
     extra["eng"].close()
     del extra
     torch.cuda.empty_cache()

@@ -306,7 +306,17 @@ void ptls_mi355x_record_layer_set_seq(ptls_mi355x_record_layer_t *rl, uint64_t s
 /* ptls_send (lib/picotls.c:4969-4988) for a window: every fragment is framed as records of <= 16384 bytes of inner
  * content type `type` (buffer_push_encrypted_records, :664-684), all sealed in one launch; the records go to out
  * back to back (*outlen bytes, *nrecords records; each record is fragment + 22 bytes) and seq advances past them.
- * Returns 0, or -1 (capacity below the wire size, or an engine error; nothing written, seq unchanged). */
+ * A fragment is one ptls_send call: ptls_send forces a key update once seq >= 2^24 (:4976-4977), so an application
+ * data fragment (type 23) is sealed only if seq is below PTLS_MI355X_RECORD_LAYER_SEQ_LIMIT when it starts.  The
+ * window stops before the first fragment at or past the limit and the call returns
+ * PTLS_MI355X_RECORD_LAYER_KEY_UPDATE: the records of the fragments before it are written (*outlen, *nrecords; a
+ * fragment of n bytes is max(1, ceil(n / 16384)) records, none when empty), nothing after it.  The caller then sends
+ * the KeyUpdate message (type 22, sealed past the limit under the old key, as update_send_key does, :4949-4962),
+ * installs the next traffic key (ptls_mi355x_record_layer_rekey: seq restarts at 0) and seals the rest.
+ * Returns 0, PTLS_MI355X_RECORD_LAYER_KEY_UPDATE, or -1 (capacity below the wire size, or an engine error; nothing
+ * written, seq unchanged). */
+#define PTLS_MI355X_RECORD_LAYER_SEQ_LIMIT (1ull << 24)
+#define PTLS_MI355X_RECORD_LAYER_KEY_UPDATE 1
 int ptls_mi355x_record_layer_seal(ptls_mi355x_record_layer_t *rl, const ptls_mi355x_iovec_t *frags, size_t nfrags,
                                   uint8_t type, void *out, size_t capacity, size_t *outlen, size_t *nrecords);
 /* The send windows of several connections of one session in ONE launch: layers[l] seals frags[l][0..nfrags[l]) into
@@ -336,6 +346,45 @@ int ptls_mi355x_record_layer_open(ptls_mi355x_record_layer_t *rl, const void *in
 int ptls_mi355x_record_layer_open_multi(ptls_mi355x_record_layer_t *const *layers, size_t nlayers, const void *const *in,
                                         const size_t *inlen, size_t *consumed, void *const *out, const size_t *capacity,
                                         size_t *outlen, size_t *nrecords, int *alerts);
+/* ptls_receive for ONE record of any inner content type at the start of in (the handshake / alert record a window
+ * open stopped at, e.g. a KeyUpdate): its plaintext (padding and type removed) to out, its inner type to
+ * *content_type, seq advanced by one.  Returns 0 (*consumed == 0: no complete application_data-framed record), a TLS
+ * alert, or -1. */
+int ptls_mi355x_record_layer_open_record(ptls_mi355x_record_layer_t *rl, const void *in, size_t inlen, size_t *consumed,
+                                         void *out, size_t capacity, size_t *outlen, uint8_t *content_type);
+/* a new traffic key for this direction (the update_traffic_key callback of a KeyUpdate epoch change,
+ * INTEGRATION.md section 5): key and static IV replaced, seq restarts at 0 (setup_traffic_protection,
+ * lib/picotls.c:1217).  No window may be outstanding.  0 or -1. */
+int ptls_mi355x_record_layer_rekey(ptls_mi355x_record_layer_t *rl, const void *key, size_t key_size, const void *iv12);
+/*
+ * Asynchronous windows: a submit plans and stages the window and launches it on the next of the layer's (layers[0]'s)
+ * 4 slots -- each its own stream, staging and engine context -- and returns at once; so consecutive windows of one
+ * connection, and windows of several connections, overlap their PCIe transfers and kernels.  Windows complete in
+ * submission order: ptls_mi355x_record_layer_wait(rl, ticket, ...) for the oldest ticket of rl, then the next.  At
+ * most 4 windows per layer are outstanding (a fifth submit returns -1).  A synchronous call on a layer with windows
+ * outstanding returns -1.  Buffers (fragments, inputs, outputs) must stay untouched until the window's wait.
+ *
+ *  seal_submit: the records take their seq at submit (get_seq includes them).  Its wait gives per layer outlen[l],
+ *               nrecords[l], consumed[l] = fragments sealed, alerts[l] = 0 or PTLS_MI355X_RECORD_LAYER_KEY_UPDATE.
+ *  open_submit: parsed[l] = the wire bytes of the complete records taken from in[l] (the next window starts behind
+ *               them).  The records take the seq that follows the windows in flight before them; their wait gives
+ *               what ptls_mi355x_record_layer_open_multi would (consumed[l], outlen[l], nrecords[l], alerts[l]).  When a
+ *               window stops before its last parsed record (an alert, another content type, a full output), seq
+ *               stays at the stop and every window submitted behind it completes with alerts[l] =
+ *               PTLS_MI355X_RECORD_LAYER_STALE, nothing consumed: resubmit from the stop.
+ * Returns 0 or -1 (ptls_mi355x_record_layer_last_error).
+ */
+#define PTLS_MI355X_RECORD_LAYER_STALE (-2)
+int ptls_mi355x_record_layer_seal_submit(ptls_mi355x_record_layer_t *const *layers, size_t nlayers,
+                                         const ptls_mi355x_iovec_t *const *frags, const size_t *nfrags, uint8_t type,
+                                         void *const *out, const size_t *capacity, uint64_t *ticket);
+int ptls_mi355x_record_layer_open_submit(ptls_mi355x_record_layer_t *const *layers, size_t nlayers, const void *const *in,
+                                         const size_t *inlen, void *const *out, const size_t *capacity, size_t *parsed,
+                                         uint64_t *ticket);
+int ptls_mi355x_record_layer_wait(ptls_mi355x_record_layer_t *rl, uint64_t ticket, size_t *outlen, size_t *nrecords,
+                                  size_t *consumed, int *alerts);
+/* windows submitted and not yet waited for */
+size_t ptls_mi355x_record_layer_pending(const ptls_mi355x_record_layer_t *rl);
 const char *ptls_mi355x_record_layer_last_error(void);
 /* How the bytes travel (record_layer.c): a call whose fragments and output (seal), or input and output (open; out
  * at least as large as the records' ciphertexts), all lie in ranges registered below runs DIRECT: the kernel reads

@@ -67,6 +67,8 @@ EXPORTED_FUNCTIONS = (
     "ptls_mi355x_record_layer_open", "ptls_mi355x_record_layer_last_error", "ptls_mi355x_record_layer_register",
     "ptls_mi355x_record_layer_unregister", "ptls_mi355x_record_layer_set_zero_copy_bytes",
     "ptls_mi355x_record_layer_seal_multi", "ptls_mi355x_record_layer_open_multi",
+    "ptls_mi355x_record_layer_open_record", "ptls_mi355x_record_layer_rekey", "ptls_mi355x_record_layer_seal_submit",
+    "ptls_mi355x_record_layer_open_submit", "ptls_mi355x_record_layer_wait", "ptls_mi355x_record_layer_pending",
 )
 EXPORTED_OBJECTS = ("ptls_mi355x_aes128gcm", "ptls_mi355x_aes256gcm", "ptls_mi355x_aes128ctr",
                     "ptls_mi355x_aes256ctr", "ptls_mi355x_aes128ecb", "ptls_mi355x_aes256ecb")
@@ -171,6 +173,15 @@ def lib() -> C.CDLL:
             L.ptls_mi355x_record_layer_set_zero_copy_bytes.restype = sz
             L.ptls_mi355x_record_layer_seal_multi.argtypes = [vp, sz, vp, vp, C.c_uint8, vp, vp, vp, vp]
             L.ptls_mi355x_record_layer_open_multi.argtypes = [vp, sz, vp, vp, vp, vp, vp, vp, vp, vp]
+        if hasattr(L, "ptls_mi355x_record_layer_rekey"):
+            L.ptls_mi355x_record_layer_open_record.argtypes = [vp, vp, sz, C.POINTER(sz), vp, sz, C.POINTER(sz),
+                                                               C.POINTER(C.c_uint8)]
+            L.ptls_mi355x_record_layer_rekey.argtypes = [vp, vp, sz, vp]
+            L.ptls_mi355x_record_layer_seal_submit.argtypes = [vp, sz, vp, vp, C.c_uint8, vp, vp, C.POINTER(u64)]
+            L.ptls_mi355x_record_layer_open_submit.argtypes = [vp, sz, vp, vp, vp, vp, vp, C.POINTER(u64)]
+            L.ptls_mi355x_record_layer_wait.argtypes = [vp, u64, vp, vp, vp, vp]
+            L.ptls_mi355x_record_layer_pending.argtypes = [vp]
+            L.ptls_mi355x_record_layer_pending.restype = sz
         for name in ("ptls_mi355x_set_win16_records", "ptls_mi355x_set_split_records"):
             if hasattr(L, name):  # (absent from older builds used in A/B timing runs)
                 getattr(L, name).argtypes = [sz]
@@ -453,6 +464,11 @@ class _IoVec(C.Structure):
     _fields_ = [("base", C.c_void_p), ("len", C.c_size_t)]
 
 
+RECORD_LAYER_SEQ_LIMIT = 1 << 24  # ptls_send's key-update threshold (lib/picotls.c:4976-4977)
+RECORD_LAYER_KEY_UPDATE = 1
+RECORD_LAYER_STALE = -2
+
+
 class RecordLayer:
     """ptls_mi355x_record_layer_t: one traffic direction of a connection, windows of records between host memory
     and the GPU (include/ptls_mi355x.h section 5)."""
@@ -473,7 +489,8 @@ class RecordLayer:
         lib().ptls_mi355x_record_layer_set_seq(self.handle, v)
 
     def seal(self, fragments, content_type: int = 23, capacity: int = None):
-        """-> (wire bytes, record count); every fragment framed as records of <= 16384 bytes."""
+        """-> (wire bytes, record count); every fragment framed as records of <= 16384 bytes.  self.key_update is set
+        when the window stopped at the 2^24-record limit (RECORD_LAYER_KEY_UPDATE)."""
         bufs = [_cbuf(f) for f in fragments]
         iov = (_IoVec * max(len(fragments), 1))()
         for i, (b, f) in enumerate(zip(bufs, fragments)):
@@ -485,8 +502,9 @@ class RecordLayer:
         olen, nrec = sz(), sz()
         rc = lib().ptls_mi355x_record_layer_seal(self.handle, iov, len(fragments), content_type, out, capacity,
                                                  C.byref(olen), C.byref(nrec))
-        if rc != 0:
+        if rc not in (0, RECORD_LAYER_KEY_UPDATE):
             raise RuntimeError("record_layer_seal failed: " + lib().ptls_mi355x_record_layer_last_error().decode())
+        self.key_update = rc == RECORD_LAYER_KEY_UPDATE
         return out.raw[:olen.value], nrec.value
 
     def open(self, wire: bytes, capacity: int = None):
@@ -526,8 +544,11 @@ class RecordLayer:
             iov[i].base = C.c_void_p(f.ctypes.data)
             iov[i].len = f.nbytes
         olen, nrec = sz(), sz()
-        self._check(lib().ptls_mi355x_record_layer_seal(self.handle, iov, len(fragments), content_type, out.ctypes.data,
-                                                        out.nbytes, C.byref(olen), C.byref(nrec)), "seal")
+        rc = lib().ptls_mi355x_record_layer_seal(self.handle, iov, len(fragments), content_type, out.ctypes.data,
+                                                 out.nbytes, C.byref(olen), C.byref(nrec))
+        if rc != RECORD_LAYER_KEY_UPDATE:
+            self._check(rc, "seal")
+        self.key_update = rc == RECORD_LAYER_KEY_UPDATE
         return olen.value, nrec.value
 
     def open_into(self, wire: np.ndarray, out: np.ndarray):
@@ -538,6 +559,57 @@ class RecordLayer:
         if rc < 0:
             self._check(rc, "open")
         return rc, olen.value, cons.value, nrec.value
+
+    def open_record(self, wire: bytes, capacity: int = None):
+        """ONE record of any inner content type (ptls_mi355x_record_layer_open_record)
+        -> (rc: 0 or a TLS alert, plaintext, wire bytes consumed, content type)."""
+        if capacity is None:
+            capacity = len(wire)
+        out = C.create_string_buffer(max(capacity, 1))
+        cons, olen, ty = sz(), sz(), C.c_uint8()
+        rc = lib().ptls_mi355x_record_layer_open_record(self.handle, _cbuf(wire), len(wire), C.byref(cons), out,
+                                                        capacity, C.byref(olen), C.byref(ty))
+        if rc < 0:
+            self._check(rc, "open_record")
+        return rc, out.raw[:olen.value], cons.value, ty.value
+
+    def rekey(self, key: bytes, static_iv: bytes) -> None:
+        """A new traffic key and IV for this direction; seq restarts at 0 (ptls_mi355x_record_layer_rekey)."""
+        assert len(static_iv) == 12
+        self._check(lib().ptls_mi355x_record_layer_rekey(self.handle, _cbuf(key), len(key), _cbuf(static_iv)), "rekey")
+
+    @property
+    def pending(self) -> int:
+        return lib().ptls_mi355x_record_layer_pending(self.handle)
+
+    def seal_submit(self, fragments, out: np.ndarray, content_type: int = 23) -> int:
+        """Asynchronous seal of the fragments (uint8 numpy views) into `out` -> ticket (wait() completes it)."""
+        iov = (_IoVec * max(len(fragments), 1))()
+        for i, f in enumerate(fragments):
+            iov[i].base = C.c_void_p(f.ctypes.data)
+            iov[i].len = f.nbytes
+        frag_ptrs = (C.c_void_p * 1)(C.cast(iov, C.c_void_p))
+        nfr, outp, cap, t = (sz * 1)(len(fragments)), (C.c_void_p * 1)(out.ctypes.data), (sz * 1)(out.nbytes), u64()
+        handles = (C.c_void_p * 1)(self.handle)
+        self._check(lib().ptls_mi355x_record_layer_seal_submit(handles, 1, frag_ptrs, nfr, content_type, outp, cap,
+                                                               C.byref(t)), "seal_submit")
+        return t.value
+
+    def open_submit(self, wire: np.ndarray, out: np.ndarray):
+        """Asynchronous open of the records in `wire` into `out` -> (ticket, wire bytes parsed into the window)."""
+        inp, inl = (C.c_void_p * 1)(wire.ctypes.data), (sz * 1)(wire.nbytes)
+        outp, cap, parsed, t = (C.c_void_p * 1)(out.ctypes.data), (sz * 1)(out.nbytes), (sz * 1)(), u64()
+        handles = (C.c_void_p * 1)(self.handle)
+        self._check(lib().ptls_mi355x_record_layer_open_submit(handles, 1, inp, inl, outp, cap, parsed, C.byref(t)),
+                    "open_submit")
+        return t.value, parsed[0]
+
+    def wait(self, ticket: int):
+        """Completes the oldest window -> (outlen, records, consumed, alert); seal: consumed = fragments sealed,
+        alert = RECORD_LAYER_KEY_UPDATE at the limit; open: alert = a TLS alert or RECORD_LAYER_STALE."""
+        olen, nrec, cons, al = (sz * 1)(), (sz * 1)(), (sz * 1)(), (C.c_int * 1)()
+        self._check(lib().ptls_mi355x_record_layer_wait(self.handle, ticket, olen, nrec, cons, al), "wait")
+        return olen[0], nrec[0], cons[0], al[0]
 
     def close(self) -> None:
         if self.handle:
@@ -582,7 +654,8 @@ def record_layer_seal_multi(layers, windows, content_type: int = 23, outs=None):
     capv = (sz * n)(*caps)
     olen, nrec = (sz * n)(), (sz * n)()
     handles = (C.c_void_p * n)(*[lr.handle for lr in layers])
-    if lib().ptls_mi355x_record_layer_seal_multi(handles, n, frag_ptrs, nfr, content_type, out_ptrs, capv, olen, nrec):
+    if lib().ptls_mi355x_record_layer_seal_multi(handles, n, frag_ptrs, nfr, content_type, out_ptrs, capv, olen,
+                                                 nrec) not in (0, RECORD_LAYER_KEY_UPDATE):
         raise RuntimeError("record_layer_seal_multi failed: " + lib().ptls_mi355x_record_layer_last_error().decode())
     if outs is None:
         return [(bufs[i].raw[:olen[i]], nrec[i]) for i in range(n)]

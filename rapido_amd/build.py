@@ -3,6 +3,8 @@
     rapido_amd/_lib/libptls_mi355x.so  <- csrc/gcm_engine.hip (hipcc, --offload-arch=gfx950)
                                          + csrc/aead_slot.c, csrc/tls_records.c, csrc/record_layer.c (host C, gcc)
     tests/cpp/_build/libkernel_model.so <- tests/cpp/kernel_model.cpp (host clang++, test only)
+    scripts/_build/rl_stream            <- scripts/rl_stream.c (gcc, against the library: bench.py's host-to-host
+                                           record-layer stream driver, a measurement tool)
 
 Rebuilds only when a source or header is newer than the output.
 """
@@ -77,9 +79,23 @@ def build_model(verbose: bool = False, force: bool = False) -> str:
     return MODEL_LIB
 
 
+RL_STREAM_SRC = os.path.join(ROOT, "scripts", "rl_stream.c")
+RL_STREAM = os.path.join(ROOT, "scripts", "_build", "rl_stream")
+
+
+def build_rl_stream(verbose: bool = False, force: bool = False) -> str:
+    """The C driver of bench.py's record_layer_stream (measurement, not part of the product)."""
+    os.makedirs(os.path.dirname(RL_STREAM), exist_ok=True)
+    if force or _newer(RL_STREAM, [RL_STREAM_SRC, LIB] + HEADERS):
+        _run([CC, "-std=gnu99", "-O2", "-Wall", "-o", RL_STREAM, RL_STREAM_SRC, "-L" + LIBDIR, "-lptls_mi355x",
+              "-Wl,-rpath,$ORIGIN/../../rapido_amd/_lib"], verbose)
+    return RL_STREAM
+
+
 def build_all(verbose: bool = False, force: bool = False) -> None:
     build_engine(verbose, force)
     build_model(verbose, force)
+    build_rl_stream(verbose, force)
 
 
 if __name__ == "__main__":

@@ -10,22 +10,34 @@
  *
  *   seal: the fragments are planned into records (ptls_mi355x_tls_plan_send, <= 16384 bytes each, consecutive
  *         seq), sealed by ptls_mi355x_tls_seal_records; seq advances by the record count, as ptls_send's does.
+ *         A fragment is one ptls_send call: it is sealed only if seq is below 2^24 when it starts (ptls_send forces a
+ *         key update there, lib/picotls.c:4976-4977); the window stops before the first fragment at or past the
+ *         limit and reports PTLS_MI355X_RECORD_LAYER_KEY_UPDATE.  Records of other content types (the KeyUpdate
+ *         message itself, update_send_key :4949-4962) are sealed past it.
  *   open: the complete application_data records at the start of the input are parsed (ptls_mi355x_tls_parse_
  *         records) and opened by ptls_mi355x_tls_open_records.  Records are then delivered in order until the first
  *         failure (its alert is returned, as ptls_receive returns it, lib/picotls.c:650-652) or the first record
- *         whose inner type is not application_data (left unconsumed, seq not advanced, for the caller's picotls
- *         slot path).  Every record is verified independently by the kernel; the stop at the first failure is this
- *         host loop, and nothing behind it reaches the caller (slots are zeroed).
+ *         whose inner type is not application_data (left unconsumed, seq not advanced, for open_record below).
+ *         Every record is verified independently by the kernel; the stop at the first failure is this host loop,
+ *         and nothing behind it reaches the caller (slots are zeroed).
  *
- * Where the bytes travel, per call (the first that applies):
+ * Windows are asynchronous: a submit plans, stages and launches a window on one of the layer's RL_SLOTS slots and
+ * returns; wait (in submission order) completes it.  Each slot has its own stream, staging, device buffer and engine
+ * context (the split kernels' arrival tickets and the batch kernels' work counters are per context, so windows on
+ * different slots never wait for each other).  A send window's records take their seq at submit.  A receive window
+ * takes the seq that follows the windows before it (speculatively: they are not verified yet); if one of them stops
+ * early (a failure, a non-application_data record, a full output), the windows submitted behind it are stale and
+ * their wait reports PTLS_MI355X_RECORD_LAYER_STALE with nothing delivered.  The synchronous calls are a submit and
+ * its wait.
+ *
+ * Where the bytes travel, per window (the first that applies):
  *   direct     -- the fragments and the output (seal), or the input and the output (open), all lie in host ranges
- *                 the caller registered (ptls_mi355x_record_layer_register: long-lived socket buffers): the kernel
- *                 reads and writes them in place over PCIe.  Only the descriptors (and statuses) pass through the
- *                 layer's staging.  No copy at all.
- *   zero-copy  -- the window fits the zero-copy limit: fragments / input are copied into the layer's pinned,
- *                 mapped, coherent staging and the kernel works on it over PCIe; one launch, one synchronisation.
+ *                 the caller registered (ptls_mi355x_record_layer_register: long-lived socket buffers) and the
+ *                 inputs do not overlap the outputs: the kernel reads and writes them in place over PCIe.  Only the
+ *                 descriptors (and statuses) pass through the slot's staging.  No copy at all.
+ *   zero-copy  -- the window fits the zero-copy limit: fragments / input are copied into the slot's pinned,
+ *                 mapped, coherent staging and the kernel works on it over PCIe.
  *   copy       -- larger windows: staging -> one H2D copy -> launch -> one D2H copy (DMA at the link rate).
- * Everything runs on the layer's own stream and the call returns when the results are in the caller's buffer.
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -36,6 +48,7 @@
 
 #define RL_MAX_REGIONS 8
 #define RL_ZERO_COPY_DEFAULT ((size_t)4 << 20)
+#define RL_SLOTS 4 /* windows in flight per layer */
 
 typedef struct {
     uint8_t *base; /* host address as registered */
@@ -44,23 +57,56 @@ typedef struct {
     int owned;     /* registered by this layer (not already registered, e.g. by the other direction's layer) */
 } rl_region_t;
 
-struct st_ptls_mi355x_record_layer_t {
+/* one layer's part of a window */
+typedef struct {
+    /* seal */
+    size_t nfrags, wire; /* fragments taken (before the key-update limit), their wire bytes */
+    int stopped;         /* stopped at the limit */
+    /* open */
+    size_t k0, n, cons, ptbytes; /* descriptors recs[k0 .. k0 + n), wire bytes parsed, plaintext slot bytes */
+    uint64_t src_add, dst_add;   /* added to its descriptors' offsets (its position in the launch's src / dst) */
+    int perr;
+    /* both */
+    uint64_t seq0; /* seq of its first record */
+    size_t nrec;   /* records in the launch */
+} rl_part_t;
+
+typedef struct {
+    int busy, is_seal, any_type; /* any_type: open_record (one record of any inner content type) */
+    uint64_t ticket;
+    size_t nlayers;
+    ptls_mi355x_record_layer_t **layers;
+    void **out;
+    size_t *capacity;
+    rl_part_t *part;
+    int direct, zero_copy;
+    size_t nrec, off_src, srcbytes, off_dst, dstbytes, off_st, off_ty;
+} rl_op_t;
+
+typedef struct {
+    hipStream_t stream;
     ptls_mi355x_aesgcm_context_t *ctx;
-    uint8_t key[32]; /* the key, to check that the layers of a _multi call share it (zeroed on free) */
+    uint8_t *h_buf; /* pinned, mapped, coherent staging: [descriptors | conn ids | input | output | status | types] */
+    uint8_t *h_dev; /* the staging's device address (zero-copy and direct windows) */
+    size_t cap;
+    uint8_t *d_buf; /* device copy of the staging layout (copy windows), allocated on first use */
+    size_t d_cap;
+    ptls_mi355x_tls_record_t *recs; /* host descriptors */
+    size_t recs_cap;
+    rl_op_t op;
+} rl_slot_t;
+
+struct st_ptls_mi355x_record_layer_t {
+    uint8_t key[32]; /* the key, for the slots' contexts and to check that the layers of a _multi call share it */
     size_t key_size;
     uint8_t iv[12];
-    uint64_t seq;
-    hipStream_t stream;
-    uint8_t *h_buf; /* pinned, mapped, coherent staging: [descriptors | input | output | status | types] */
-    uint8_t *h_dev; /* the staging's device address (zero-copy and direct calls) */
-    size_t cap;
-    uint8_t *d_buf; /* device copy of the staging layout (copy calls), allocated on first use */
-    size_t d_cap;
+    uint64_t seq;      /* seal: the next record's seq; open: the seq of the next record to deliver */
+    uint64_t spec_seq; /* open: the seq of the next record to submit (ahead of seq while windows are in flight) */
     size_t zero_copy_bytes;
     rl_region_t reg[RL_MAX_REGIONS];
     size_t nreg;
-    ptls_mi355x_tls_record_t *recs; /* host descriptors */
-    size_t recs_cap;
+    rl_slot_t slot[RL_SLOTS];
+    uint64_t next_ticket, oldest; /* tickets [oldest, next_ticket) are outstanding */
 };
 
 static char rl_err[160];
@@ -74,59 +120,99 @@ static int rl_fail(const char *what, hipError_t e)
     return -1;
 }
 
+static int rl_msg(const char *msg)
+{
+    snprintf(rl_err, sizeof(rl_err), "record layer: %s", msg);
+    return -1;
+}
+
 const char *ptls_mi355x_record_layer_last_error(void) { return rl_err; }
 
-static int reserve_recs(ptls_mi355x_record_layer_t *rl, size_t nrecs)
+static int reserve_recs(rl_slot_t *s, size_t nrecs)
 {
-    if (nrecs <= rl->recs_cap)
+    if (nrecs <= s->recs_cap)
         return 0;
-    size_t c = rl->recs_cap ? rl->recs_cap : 64;
+    size_t c = s->recs_cap ? s->recs_cap : 64;
     while (c < nrecs)
         c *= 2;
-    ptls_mi355x_tls_record_t *r = realloc(rl->recs, c * sizeof(*r));
-    if (r == NULL) {
-        snprintf(rl_err, sizeof(rl_err), "record layer: out of memory");
-        return -1;
-    }
-    rl->recs = r;
-    rl->recs_cap = c;
+    ptls_mi355x_tls_record_t *r = realloc(s->recs, c * sizeof(*r));
+    if (r == NULL)
+        return rl_msg("out of memory");
+    s->recs = r;
+    s->recs_cap = c;
     return 0;
 }
 
-static int reserve_stage(ptls_mi355x_record_layer_t *rl, size_t bytes)
+static int reserve_stage(rl_slot_t *s, size_t bytes)
 {
-    if (bytes <= rl->cap)
+    if (bytes <= s->cap)
         return 0;
-    size_t c = rl->cap ? rl->cap : 1 << 16;
+    size_t c = s->cap ? s->cap : 1 << 16;
     while (c < bytes)
         c *= 2;
     hipError_t e;
-    if (rl->h_buf != NULL)
-        (void)hipHostFree(rl->h_buf);
-    rl->h_buf = rl->h_dev = NULL;
-    rl->cap = 0;
+    if (s->h_buf != NULL) {
+        memset(s->h_buf, 0, s->cap);
+        (void)hipHostFree(s->h_buf);
+    }
+    s->h_buf = s->h_dev = NULL;
+    s->cap = 0;
     /* coherent: the kernel's zero-copy reads never see stale lines of an earlier window */
-    if ((e = hipHostMalloc((void **)&rl->h_buf, c, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
+    if ((e = hipHostMalloc((void **)&s->h_buf, c, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
         return rl_fail("hipHostMalloc", e);
-    if ((e = hipHostGetDevicePointer((void **)&rl->h_dev, rl->h_buf, 0)) != hipSuccess)
+    if ((e = hipHostGetDevicePointer((void **)&s->h_dev, s->h_buf, 0)) != hipSuccess)
         return rl_fail("hipHostGetDevicePointer", e);
-    rl->cap = c;
+    s->cap = c;
     return 0;
 }
 
-static int reserve_device(ptls_mi355x_record_layer_t *rl, size_t bytes)
+static int reserve_device(rl_slot_t *s)
 {
-    if (bytes <= rl->d_cap)
+    if (s->cap <= s->d_cap)
         return 0;
     hipError_t e;
-    if (rl->d_buf != NULL)
-        (void)hipFree(rl->d_buf);
-    rl->d_buf = NULL;
-    rl->d_cap = 0;
-    if ((e = hipMalloc((void **)&rl->d_buf, rl->cap)) != hipSuccess)
+    if (s->d_buf != NULL) {
+        (void)hipMemset(s->d_buf, 0, s->d_cap);
+        (void)hipFree(s->d_buf);
+    }
+    s->d_buf = NULL;
+    s->d_cap = 0;
+    if ((e = hipMalloc((void **)&s->d_buf, s->cap)) != hipSuccess)
         return rl_fail("hipMalloc", e);
-    rl->d_cap = rl->cap;
+    s->d_cap = s->cap;
     return 0;
+}
+
+/* the slot's stream and engine context, created on first use (a synchronous layer only ever uses slot 0) */
+static int slot_ready(ptls_mi355x_record_layer_t *rl, rl_slot_t *s)
+{
+    hipError_t e;
+    if (s->stream == NULL && (e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)) != hipSuccess) {
+        s->stream = NULL;
+        return rl_fail("hipStreamCreateWithFlags", e);
+    }
+    if (s->ctx == NULL && (s->ctx = ptls_mi355x_aesgcm_new(rl->key, rl->key_size, 0)) == NULL)
+        return rl_msg(ptls_mi355x_last_error());
+    return 0;
+}
+
+static void slot_release(rl_slot_t *s)
+{
+    if (s->stream != NULL) {
+        (void)hipStreamSynchronize(s->stream);
+        (void)hipStreamDestroy(s->stream);
+    }
+    if (s->h_buf != NULL) {
+        memset(s->h_buf, 0, s->cap); /* plaintexts passed through the staging */
+        (void)hipHostFree(s->h_buf);
+    }
+    if (s->d_buf != NULL) {
+        (void)hipMemset(s->d_buf, 0, s->d_cap);
+        (void)hipFree(s->d_buf);
+    }
+    free(s->recs);
+    ptls_mi355x_aesgcm_free(s->ctx);
+    memset(s, 0, sizeof(*s));
 }
 
 /* device address of host range [p, p+len) if it lies inside one registered range, else NULL */
@@ -143,26 +229,24 @@ static uint8_t *dev_addr(const ptls_mi355x_record_layer_t *rl, const void *p, si
 
 ptls_mi355x_record_layer_t *ptls_mi355x_record_layer_new(const void *key, size_t key_size, const void *iv12, uint64_t seq)
 {
+    if (key_size != 16 && key_size != 32) {
+        rl_msg("key size must be 16 or 32");
+        return NULL;
+    }
     ptls_mi355x_record_layer_t *rl = calloc(1, sizeof(*rl));
     if (rl == NULL)
         return NULL;
-    hipError_t e;
-    if ((rl->ctx = ptls_mi355x_aesgcm_new(key, key_size, 0)) == NULL) {
-        snprintf(rl_err, sizeof(rl_err), "record layer: %s", ptls_mi355x_last_error());
-        free(rl);
-        return NULL;
-    }
-    if ((e = hipStreamCreateWithFlags(&rl->stream, hipStreamNonBlocking)) != hipSuccess) {
-        rl_fail("hipStreamCreateWithFlags", e);
-        ptls_mi355x_aesgcm_free(rl->ctx);
-        free(rl);
-        return NULL;
-    }
     memcpy(rl->key, key, key_size);
     rl->key_size = key_size;
     memcpy(rl->iv, iv12, 12);
-    rl->seq = seq;
+    rl->seq = rl->spec_seq = seq;
     rl->zero_copy_bytes = RL_ZERO_COPY_DEFAULT;
+    if (slot_ready(rl, &rl->slot[0]) != 0) { /* the key is set up now: errors surface here, not at the first window */
+        slot_release(&rl->slot[0]);
+        memset(rl->key, 0, sizeof(rl->key));
+        free(rl);
+        return NULL;
+    }
     return rl;
 }
 
@@ -172,20 +256,14 @@ void ptls_mi355x_record_layer_free(ptls_mi355x_record_layer_t *rl)
         return;
     while (rl->nreg != 0)
         (void)ptls_mi355x_record_layer_unregister(rl, rl->reg[rl->nreg - 1].base);
-    if (rl->stream != NULL) {
-        (void)hipStreamSynchronize(rl->stream);
-        (void)hipStreamDestroy(rl->stream);
+    for (int i = 0; i < RL_SLOTS; ++i) {
+        rl_op_t *op = &rl->slot[i].op;
+        if (op->busy) { /* never waited: completes here, its results dropped */
+            free(op->layers);
+            memset(op, 0, sizeof(*op));
+        }
+        slot_release(&rl->slot[i]);
     }
-    if (rl->h_buf != NULL) {
-        memset(rl->h_buf, 0, rl->cap); /* plaintexts passed through the staging */
-        (void)hipHostFree(rl->h_buf);
-    }
-    if (rl->d_buf != NULL) {
-        (void)hipMemset(rl->d_buf, 0, rl->d_cap);
-        (void)hipFree(rl->d_buf);
-    }
-    free(rl->recs);
-    ptls_mi355x_aesgcm_free(rl->ctx);
     memset(rl->key, 0, sizeof(rl->key));
     memset(rl->iv, 0, sizeof(rl->iv));
     free(rl);
@@ -193,7 +271,40 @@ void ptls_mi355x_record_layer_free(ptls_mi355x_record_layer_t *rl)
 
 uint64_t ptls_mi355x_record_layer_get_seq(const ptls_mi355x_record_layer_t *rl) { return rl->seq; }
 
-void ptls_mi355x_record_layer_set_seq(ptls_mi355x_record_layer_t *rl, uint64_t seq) { rl->seq = seq; }
+void ptls_mi355x_record_layer_set_seq(ptls_mi355x_record_layer_t *rl, uint64_t seq) { rl->seq = rl->spec_seq = seq; }
+
+size_t ptls_mi355x_record_layer_pending(const ptls_mi355x_record_layer_t *rl) { return (size_t)(rl->next_ticket - rl->oldest); }
+
+int ptls_mi355x_record_layer_rekey(ptls_mi355x_record_layer_t *rl, const void *key, size_t key_size, const void *iv12)
+{
+    if (key_size != 16 && key_size != 32)
+        return rl_msg("key size must be 16 or 32");
+    if (rl->next_ticket != rl->oldest)
+        return rl_msg("rekey with windows outstanding (wait for them first)");
+    uint8_t k[32];
+    memcpy(k, key, key_size);
+    ptls_mi355x_aesgcm_context_t *ctx = ptls_mi355x_aesgcm_new(k, key_size, 0);
+    if (ctx == NULL) {
+        memset(k, 0, sizeof(k));
+        return rl_msg(ptls_mi355x_last_error());
+    }
+    for (int i = 0; i < RL_SLOTS; ++i) { /* every slot's context holds the old key: the first gets the new one */
+        rl_slot_t *s = &rl->slot[i];
+        if (s->ctx != NULL) {
+            if (s->stream != NULL)
+                (void)hipStreamSynchronize(s->stream);
+            ptls_mi355x_aesgcm_free(s->ctx);
+            s->ctx = NULL;
+        }
+    }
+    rl->slot[0].ctx = ctx;
+    memcpy(rl->key, k, key_size);
+    memset(k, 0, sizeof(k));
+    rl->key_size = key_size;
+    memcpy(rl->iv, iv12, 12);
+    rl->seq = rl->spec_seq = 0; /* a new traffic key starts at record 0 (setup_traffic_protection, lib/picotls.c:1217) */
+    return 0;
+}
 
 size_t ptls_mi355x_record_layer_set_zero_copy_bytes(ptls_mi355x_record_layer_t *rl, size_t n)
 {
@@ -204,10 +315,8 @@ size_t ptls_mi355x_record_layer_set_zero_copy_bytes(ptls_mi355x_record_layer_t *
 
 int ptls_mi355x_record_layer_register(ptls_mi355x_record_layer_t *rl, void *base, size_t len)
 {
-    if (rl->nreg == RL_MAX_REGIONS || base == NULL || len == 0) {
-        snprintf(rl_err, sizeof(rl_err), "record layer: %s", base == NULL || len == 0 ? "empty range" : "too many ranges");
-        return -1;
-    }
+    if (rl->nreg == RL_MAX_REGIONS || base == NULL || len == 0)
+        return rl_msg(base == NULL || len == 0 ? "empty range" : "too many ranges");
     hipError_t e;
     uint8_t *dev = NULL;
     int owned = 1;
@@ -230,7 +339,9 @@ int ptls_mi355x_record_layer_unregister(ptls_mi355x_record_layer_t *rl, void *ba
 {
     for (size_t i = 0; i < rl->nreg; ++i) {
         if (rl->reg[i].base == base) {
-            (void)hipStreamSynchronize(rl->stream); /* no launch of this layer still reads the range */
+            for (int k = 0; k < RL_SLOTS; ++k) /* no window of this layer still reads the range */
+                if (rl->slot[k].stream != NULL)
+                    (void)hipStreamSynchronize(rl->slot[k].stream);
             hipError_t e = rl->reg[i].owned ? hipHostUnregister(base) : hipSuccess;
             if (e == hipErrorHostMemoryNotRegistered) { /* registered twice, already released by the other owner */
                 (void)hipGetLastError();
@@ -240,8 +351,7 @@ int ptls_mi355x_record_layer_unregister(ptls_mi355x_record_layer_t *rl, void *ba
             return e == hipSuccess ? 0 : rl_fail("hipHostUnregister", e);
         }
     }
-    snprintf(rl_err, sizeof(rl_err), "record layer: range not registered");
-    return -1;
+    return rl_msg("range not registered");
 }
 
 /* device address of [p, p+len) inside a range registered with any of the layers, else NULL */
@@ -255,162 +365,13 @@ static uint8_t *dev_addr_any(ptls_mi355x_record_layer_t *const *layers, size_t n
     return NULL;
 }
 
+static int overlaps(const void *a, size_t alen, const void *b, size_t blen)
+{
+    const uint8_t *x = a, *y = b;
+    return alen != 0 && blen != 0 && x < y + blen && y < x + alen;
+}
+
 static uint32_t be32(const uint8_t *b) { return (uint32_t)b[0] << 24 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 8 | b[3]; }
-
-int ptls_mi355x_record_layer_seal_multi(ptls_mi355x_record_layer_t *const *layers, size_t nlayers,
-                                        const ptls_mi355x_iovec_t *const *frags, const size_t *nfrags, uint8_t type,
-                                        void *const *out, const size_t *capacity, size_t *outlen, size_t *nrecords)
-{
-    if (nlayers == 0)
-        return 0;
-    ptls_mi355x_record_layer_t *rl = layers[0];
-    size_t nrec = 0, srcbytes = 0, wire = 0;
-    for (size_t l = 0; l < nlayers; ++l) {
-        const ptls_mi355x_record_layer_t *x = layers[l];
-        outlen[l] = 0;
-        if (nrecords != NULL)
-            nrecords[l] = 0;
-        /* one launch, one key image: the connections of one session (rapido: the session key, the IV differing in
-         * bytes 0..3 only, derive_connection_aead_iv lib/rapido.c:123-133) */
-        if (x->key_size != rl->key_size || memcmp(x->key, rl->key, rl->key_size) != 0 ||
-            memcmp(x->iv + 4, rl->iv + 4, 8) != 0) {
-            snprintf(rl_err, sizeof(rl_err), "record layer: layer %zu has another key or IV bytes 4..11", l);
-            return -1;
-        }
-        size_t wl = 0;
-        for (size_t f = 0; f < nfrags[l]; ++f) {
-            uint64_t sq = 0;
-            size_t w = 0;
-            nrec += ptls_mi355x_tls_plan_send(frags[l][f].len, type, &sq, 0, 0, NULL, 0, &w);
-            srcbytes += frags[l][f].len;
-            wl += w;
-        }
-        if (wl > capacity[l]) {
-            snprintf(rl_err, sizeof(rl_err), "record layer: %zu wire bytes exceed the output capacity %zu (layer %zu)",
-                     wl, capacity[l], l);
-            return -1;
-        }
-        outlen[l] = wl; /* provisional: reset below unless the call succeeds */
-        wire += wl;
-    }
-    if (nrec == 0) {
-        for (size_t l = 0; l < nlayers; ++l)
-            outlen[l] = 0;
-        return 0;
-    }
-    if (reserve_recs(rl, nrec) != 0)
-        goto Fail;
-    /* direct: every non-empty fragment and every output in registered ranges; addressed from the lowest of each */
-    uint8_t *src_base = NULL, *dst_base = NULL;
-    int direct = 1;
-    for (size_t l = 0; direct && l < nlayers; ++l) {
-        uint8_t *d = outlen[l] != 0 ? dev_addr_any(layers, nlayers, out[l], outlen[l]) : NULL;
-        if (outlen[l] != 0 && d == NULL)
-            direct = 0;
-        else if (d != NULL && (dst_base == NULL || d < dst_base))
-            dst_base = d;
-        for (size_t f = 0; direct && f < nfrags[l]; ++f) {
-            if (frags[l][f].len == 0)
-                continue;
-            if ((d = dev_addr_any(layers, nlayers, frags[l][f].base, frags[l][f].len)) == NULL)
-                direct = 0;
-            else if (src_base == NULL || d < src_base)
-                src_base = d;
-        }
-    }
-    const size_t off_conn = up16(nrec * sizeof(ptls_mi355x_tls_record_t));
-    const size_t off_src = off_conn + (nlayers > 1 ? up16(nrec * 4) : 0);
-    const size_t off_dst = off_src + (direct ? 0 : up16(srcbytes)), total = off_dst + (direct ? 0 : up16(wire));
-    const int zero_copy = direct || total <= rl->zero_copy_bytes;
-    if (reserve_stage(rl, total) != 0 || (!zero_copy && reserve_device(rl, total) != 0))
-        goto Fail;
-    /* descriptors (offsets relative to the src / dst bases), the per-record IV differences and, unless direct, the
-     * fragments back to back */
-    uint32_t *conn = (uint32_t *)(rl->h_buf + off_conn);
-    uint64_t *seqs = (uint64_t *)malloc(nlayers * sizeof(uint64_t));
-    if (seqs == NULL) {
-        snprintf(rl_err, sizeof(rl_err), "record layer: out of memory");
-        goto Fail;
-    }
-    size_t k = 0, src_off = 0, dst_off = 0;
-    for (size_t l = 0; l < nlayers; ++l) {
-        seqs[l] = layers[l]->seq;
-        if (direct && outlen[l] != 0)
-            dst_off = (size_t)(dev_addr_any(layers, nlayers, out[l], outlen[l]) - dst_base);
-        const uint32_t cid = be32(layers[l]->iv) ^ be32(rl->iv); /* BE32(cid) ^ IV[0..3] of layer 0 = layer l's */
-        const size_t k0 = k;
-        for (size_t f = 0; f < nfrags[l]; ++f) {
-            const ptls_mi355x_iovec_t *fr = &frags[l][f];
-            size_t w = 0;
-            if (direct && fr->len != 0)
-                src_off = (size_t)(dev_addr_any(layers, nlayers, fr->base, fr->len) - src_base);
-            k += ptls_mi355x_tls_plan_send(fr->len, type, &seqs[l], src_off, dst_off, rl->recs + k, nrec - k, &w);
-            if (!direct) {
-                if (fr->len != 0)
-                    memcpy(rl->h_buf + off_src + src_off, fr->base, fr->len);
-                src_off += fr->len;
-            }
-            dst_off += w;
-        }
-        if (nlayers > 1)
-            for (size_t i = k0; i < k; ++i)
-                conn[i] = cid;
-    }
-    memcpy(rl->h_buf, rl->recs, nrec * sizeof(ptls_mi355x_tls_record_t));
-    uint8_t *base = zero_copy ? rl->h_dev : rl->d_buf;
-    hipError_t e;
-    int rc;
-    if (!zero_copy &&
-        (e = hipMemcpyAsync(rl->d_buf, rl->h_buf, off_src + srcbytes, hipMemcpyHostToDevice, rl->stream)) != hipSuccess) {
-        free(seqs);
-        rl_fail("H2D", e);
-        goto Fail;
-    }
-    if (nlayers == 1)
-        rc = ptls_mi355x_tls_seal_records(rl->ctx, rl->iv, (const ptls_mi355x_tls_record_t *)base, nrec,
-                                          direct ? src_base : base + off_src, direct ? dst_base : base + off_dst,
-                                          rl->stream);
-    else
-        rc = ptls_mi355x_tls_seal_records_multi(rl->ctx, rl->iv, (const ptls_mi355x_tls_record_t *)base,
-                                                (const uint32_t *)(base + off_conn), nrec,
-                                                direct ? src_base : base + off_src, direct ? dst_base : base + off_dst,
-                                                rl->stream);
-    if (rc != 0) {
-        free(seqs);
-        snprintf(rl_err, sizeof(rl_err), "record layer: %s", ptls_mi355x_last_error());
-        goto Fail;
-    }
-    if ((!zero_copy && (e = hipMemcpyAsync(rl->h_buf + off_dst, rl->d_buf + off_dst, wire, hipMemcpyDeviceToHost,
-                                           rl->stream)) != hipSuccess) ||
-        (e = hipStreamSynchronize(rl->stream)) != hipSuccess) {
-        free(seqs);
-        rl_fail("synchronize", e);
-        goto Fail;
-    }
-    for (size_t l = 0, off = 0; l < nlayers; ++l) {
-        if (!direct) {
-            memcpy(out[l], rl->h_buf + off_dst + off, outlen[l]);
-            off += outlen[l];
-        }
-        if (nrecords != NULL)
-            nrecords[l] = (size_t)(seqs[l] - layers[l]->seq);
-        layers[l]->seq = seqs[l];
-    }
-    free(seqs);
-    if (!direct)
-        memset(rl->h_buf + off_src, 0, srcbytes); /* no plaintext left in the staging */
-    return 0;
-Fail:
-    for (size_t l = 0; l < nlayers; ++l)
-        outlen[l] = 0;
-    return -1;
-}
-
-int ptls_mi355x_record_layer_seal(ptls_mi355x_record_layer_t *rl, const ptls_mi355x_iovec_t *frags, size_t nfrags,
-                                  uint8_t type, void *out, size_t capacity, size_t *outlen, size_t *nrecords)
-{
-    return ptls_mi355x_record_layer_seal_multi(&rl, 1, &frags, &nfrags, type, &out, &capacity, outlen, nrecords);
-}
 
 /* the layers of one launch share the key and IV bytes 4..11 (the connections of a session) */
 static int same_session(ptls_mi355x_record_layer_t *const *layers, size_t nlayers)
@@ -427,11 +388,517 @@ static int same_session(ptls_mi355x_record_layer_t *const *layers, size_t nlayer
     return 1;
 }
 
-typedef struct {
-    size_t k0, n, cons, ptbytes; /* its descriptors rl->recs[k0 .. k0 + n), wire bytes parsed, plaintext slot bytes */
-    uint64_t src_add, dst_add;   /* added to its descriptors' offsets (its position in the launch's src / dst) */
-    int perr;
-} rl_open_part_t;
+/* a new op on layers[0]'s next slot: its arrays allocated, NULL when the queue is full or on error */
+static rl_slot_t *op_begin(ptls_mi355x_record_layer_t *const *layers, size_t nlayers, int is_seal)
+{
+    ptls_mi355x_record_layer_t *rl = layers[0];
+    if (rl->next_ticket - rl->oldest >= RL_SLOTS) {
+        rl_msg("all window slots are in flight (wait for the oldest first)");
+        return NULL;
+    }
+    rl_slot_t *s = &rl->slot[rl->next_ticket % RL_SLOTS];
+    if (slot_ready(rl, s) != 0)
+        return NULL;
+    rl_op_t *op = &s->op;
+    memset(op, 0, sizeof(*op));
+    /* one allocation: layers | out | capacity | parts */
+    const size_t bytes = nlayers * (2 * sizeof(void *) + sizeof(size_t) + sizeof(rl_part_t));
+    uint8_t *mem = calloc(1, bytes);
+    if (mem == NULL) {
+        rl_msg("out of memory");
+        return NULL;
+    }
+    op->layers = (ptls_mi355x_record_layer_t **)mem;
+    op->out = (void **)(mem + nlayers * sizeof(void *));
+    op->capacity = (size_t *)(mem + 2 * nlayers * sizeof(void *));
+    op->part = (rl_part_t *)(mem + nlayers * (2 * sizeof(void *) + sizeof(size_t)));
+    memcpy(op->layers, layers, nlayers * sizeof(void *));
+    op->nlayers = nlayers;
+    op->is_seal = is_seal;
+    return s;
+}
+
+static void op_discard(rl_op_t *op)
+{
+    free(op->layers);
+    memset(op, 0, sizeof(*op));
+}
+
+/* launched: the op joins the queue */
+static void op_commit(rl_slot_t *s, uint64_t *ticket)
+{
+    ptls_mi355x_record_layer_t *rl = s->op.layers[0];
+    s->op.busy = 1;
+    s->op.ticket = rl->next_ticket++;
+    if (ticket != NULL)
+        *ticket = s->op.ticket;
+}
+
+/* H2D (copy windows), the launch, D2H: everything on the slot's stream */
+static int op_launch(rl_slot_t *s, const uint8_t *src_base, uint8_t *dst_base)
+{
+    rl_op_t *op = &s->op;
+    ptls_mi355x_record_layer_t *rl = op->layers[0];
+    uint8_t *base = op->zero_copy ? s->h_dev : s->d_buf;
+    const uint8_t *src = op->direct ? src_base : base + op->off_src;
+    uint8_t *dst = op->direct ? dst_base : base + op->off_dst;
+    const uint32_t *conn = op->nlayers > 1 ? (const uint32_t *)(base + up16(op->nrec * sizeof(ptls_mi355x_tls_record_t))) : NULL;
+    hipError_t e;
+    int rc;
+    if (!op->zero_copy &&
+        (e = hipMemcpyAsync(s->d_buf, s->h_buf, op->off_src + op->srcbytes, hipMemcpyHostToDevice, s->stream)) != hipSuccess)
+        return rl_fail("H2D", e);
+    (void)rl;
+    if (op->is_seal)
+        rc = ptls_mi355x_tls_seal_records_multi(s->ctx, op->layers[0]->iv, (const ptls_mi355x_tls_record_t *)base, conn,
+                                                op->nrec, src, dst, s->stream);
+    else /* every record verified independently; the stop at a connection's first failure is the host loop in wait */
+        rc = ptls_mi355x_tls_open_records_multi(s->ctx, op->layers[0]->iv, (const ptls_mi355x_tls_record_t *)base, conn,
+                                                op->nrec, src, dst, (uint32_t *)(base + op->off_st), base + op->off_ty,
+                                                s->stream);
+    if (rc != 0)
+        return rl_msg(ptls_mi355x_last_error());
+    if (!op->zero_copy) {
+        const size_t from = op->off_dst, to = op->is_seal ? op->off_dst + op->dstbytes : op->off_ty + op->nrec;
+        if ((e = hipMemcpyAsync(s->h_buf + from, s->d_buf + from, to - from, hipMemcpyDeviceToHost, s->stream)) != hipSuccess)
+            return rl_fail("D2H", e);
+    }
+    return 0;
+}
+
+/* after a failed launch or wait: nothing of the window's plaintext stays in the staging */
+static void op_scrub(rl_slot_t *s)
+{
+    rl_op_t *op = &s->op;
+    if (s->stream != NULL)
+        (void)hipStreamSynchronize(s->stream);
+    if (!op->direct && s->h_buf != NULL) {
+        const size_t end = op->is_seal ? op->off_dst + op->dstbytes : op->off_st;
+        if (end > op->off_src && end <= s->cap)
+            memset(s->h_buf + op->off_src, 0, end - op->off_src);
+    }
+}
+
+/* ---------------------------------------------------------------------------------------------------- seal ---- */
+
+int ptls_mi355x_record_layer_seal_submit(ptls_mi355x_record_layer_t *const *layers, size_t nlayers,
+                                         const ptls_mi355x_iovec_t *const *frags, const size_t *nfrags, uint8_t type,
+                                         void *const *out, const size_t *capacity, uint64_t *ticket)
+{
+    if (nlayers == 0)
+        return rl_msg("no layers");
+    if (!same_session(layers, nlayers))
+        return -1;
+    rl_slot_t *s = op_begin(layers, nlayers, 1);
+    if (s == NULL)
+        return -1;
+    rl_op_t *op = &s->op;
+    const int limited = type == 23; /* ptls_send's key-update check; handshake messages are pushed past it */
+    size_t nrec = 0, srcbytes = 0, wire = 0;
+    for (size_t l = 0; l < nlayers; ++l) {
+        rl_part_t *p = &op->part[l];
+        uint64_t sq = layers[l]->seq;
+        p->seq0 = sq;
+        op->out[l] = out[l];
+        op->capacity[l] = capacity[l];
+        for (size_t f = 0; f < nfrags[l]; ++f) {
+            if (limited && sq >= PTLS_MI355X_RECORD_LAYER_SEQ_LIMIT) {
+                p->stopped = 1;
+                break;
+            }
+            size_t w = 0;
+            const size_t n = ptls_mi355x_tls_plan_send(frags[l][f].len, type, &sq, 0, 0, NULL, 0, &w);
+            sq += n;
+            p->nrec += n;
+            p->wire += w;
+            ++p->nfrags;
+            srcbytes += frags[l][f].len;
+        }
+        if (p->wire > capacity[l]) {
+            snprintf(rl_err, sizeof(rl_err), "record layer: %zu wire bytes exceed the output capacity %zu (layer %zu)",
+                     p->wire, capacity[l], l);
+            op_discard(op);
+            return -1;
+        }
+        nrec += p->nrec;
+        wire += p->wire;
+    }
+    op->nrec = nrec;
+    if (nrec == 0) { /* nothing to launch (empty or all at the limit): completes at its wait */
+        op_commit(s, ticket);
+        return 0;
+    }
+    if (reserve_recs(s, nrec) != 0)
+        goto Fail;
+    /* direct: every sealed fragment and every output in registered ranges, no fragment overlapping an output;
+     * addressed from the lowest of each */
+    uint8_t *src_base = NULL, *dst_base = NULL;
+    int direct = 1;
+    for (size_t l = 0; direct && l < nlayers; ++l) {
+        uint8_t *d = op->part[l].wire != 0 ? dev_addr_any(layers, nlayers, out[l], op->part[l].wire) : NULL;
+        if (op->part[l].wire != 0 && d == NULL)
+            direct = 0;
+        else if (d != NULL && (dst_base == NULL || d < dst_base))
+            dst_base = d;
+        for (size_t f = 0; direct && f < op->part[l].nfrags; ++f) {
+            if (frags[l][f].len == 0)
+                continue;
+            if ((d = dev_addr_any(layers, nlayers, frags[l][f].base, frags[l][f].len)) == NULL)
+                direct = 0;
+            else if (src_base == NULL || d < src_base)
+                src_base = d;
+            for (size_t m = 0; direct && m < nlayers; ++m)
+                if (overlaps(frags[l][f].base, frags[l][f].len, out[m], op->part[m].wire))
+                    direct = 0; /* the kernel would overwrite fragment bytes another workgroup still reads */
+        }
+    }
+    op->direct = direct;
+    const size_t off_conn = up16(nrec * sizeof(ptls_mi355x_tls_record_t));
+    op->off_src = off_conn + (nlayers > 1 ? up16(nrec * 4) : 0);
+    op->srcbytes = direct ? 0 : srcbytes;
+    op->off_dst = op->off_src + up16(op->srcbytes);
+    op->dstbytes = direct ? 0 : wire;
+    const size_t total = op->off_dst + up16(op->dstbytes);
+    op->zero_copy = direct || total <= layers[0]->zero_copy_bytes;
+    if (reserve_stage(s, total) != 0 || (!op->zero_copy && reserve_device(s) != 0))
+        goto Fail;
+    /* descriptors (offsets relative to the src / dst bases), the per-record IV differences and, unless direct, the
+     * fragments back to back */
+    uint32_t *conn = (uint32_t *)(s->h_buf + off_conn);
+    size_t k = 0, src_off = 0, dst_off = 0;
+    for (size_t l = 0; l < nlayers; ++l) {
+        rl_part_t *p = &op->part[l];
+        uint64_t sq = p->seq0;
+        if (direct && p->wire != 0)
+            dst_off = (size_t)(dev_addr_any(layers, nlayers, out[l], p->wire) - dst_base);
+        const uint32_t cid = be32(layers[l]->iv) ^ be32(layers[0]->iv); /* BE32(cid) ^ IV[0..3] of layer 0 = layer l's */
+        const size_t k0 = k;
+        for (size_t f = 0; f < p->nfrags; ++f) {
+            const ptls_mi355x_iovec_t *fr = &frags[l][f];
+            size_t w = 0;
+            if (direct && fr->len != 0)
+                src_off = (size_t)(dev_addr_any(layers, nlayers, fr->base, fr->len) - src_base);
+            k += ptls_mi355x_tls_plan_send(fr->len, type, &sq, src_off, dst_off, s->recs + k, nrec - k, &w);
+            if (!direct) {
+                if (fr->len != 0)
+                    memcpy(s->h_buf + op->off_src + src_off, fr->base, fr->len);
+                src_off += fr->len;
+            }
+            dst_off += w;
+        }
+        if (nlayers > 1)
+            for (size_t i = k0; i < k; ++i)
+                conn[i] = cid;
+    }
+    memcpy(s->h_buf, s->recs, nrec * sizeof(ptls_mi355x_tls_record_t));
+    if (op_launch(s, src_base, dst_base) != 0) {
+        op_scrub(s);
+        goto Fail;
+    }
+    for (size_t l = 0; l < nlayers; ++l) /* the records have their seq: the next window continues behind them */
+        layers[l]->seq = op->part[l].seq0 + op->part[l].nrec;
+    op_commit(s, ticket);
+    return 0;
+Fail:
+    op_discard(op);
+    return -1;
+}
+
+/* --------------------------------------------------------------------------------------------------- open ---- */
+
+static int open_submit(ptls_mi355x_record_layer_t *const *layers, size_t nlayers, const void *const *in,
+                       const size_t *inlen, void *const *out, const size_t *capacity, size_t *parsed, int any_type,
+                       uint64_t *ticket)
+{
+    if (nlayers == 0)
+        return rl_msg("no layers");
+    if (!same_session(layers, nlayers))
+        return -1;
+    rl_slot_t *s = op_begin(layers, nlayers, 0);
+    if (s == NULL)
+        return -1;
+    rl_op_t *op = &s->op;
+    op->any_type = any_type;
+    size_t max = 0, nrec = 0, srcbytes = 0, ptbytes = 0;
+    for (size_t l = 0; l < nlayers; ++l) /* a record takes at least 5 wire bytes */
+        max += any_type ? 1 : inlen[l] / PTLS_MI355X_TLS_HEADER_SIZE + 1;
+    if (reserve_recs(s, max) != 0)
+        goto Fail;
+    /* the complete application_data records at the start of every input, offsets local to it for now */
+    for (size_t l = 0; l < nlayers; ++l) {
+        rl_part_t *p = &op->part[l];
+        const size_t lmax = any_type ? 1 : inlen[l] / PTLS_MI355X_TLS_HEADER_SIZE + 1; /* its own budget */
+        uint64_t seq = layers[l]->spec_seq;
+        p->seq0 = seq;
+        p->k0 = nrec;
+        op->out[l] = out[l];
+        op->capacity[l] = capacity[l];
+        p->perr = ptls_mi355x_tls_parse_records((const uint8_t *)in[l], inlen[l], 0, &seq, 0, s->recs + nrec, lmax, &p->n,
+                                                &p->cons);
+        if (p->n != 0) {
+            const ptls_mi355x_tls_record_t *last = s->recs + nrec + p->n - 1;
+            p->ptbytes = last->dst + (last->len >= 16u ? last->len - 16u : 0u);
+        }
+        p->nrec = p->n;
+        nrec += p->n;
+        srcbytes += up16(p->cons);
+        ptbytes += up16(p->ptbytes);
+        if (parsed != NULL)
+            parsed[l] = p->cons;
+    }
+    op->nrec = nrec;
+    if (nrec == 0) {
+        op_commit(s, ticket);
+        return 0;
+    }
+    /* direct: every input and every plaintext buffer (at least as large as its slots) in registered ranges, and no
+     * input overlapping a plaintext buffer (slots are packed tighter than records: an in-place open would overwrite
+     * ciphertext another workgroup still reads) */
+    uint8_t *src_base = NULL, *dst_base = NULL;
+    int direct = 1;
+    for (size_t l = 0; direct && l < nlayers; ++l) {
+        const rl_part_t *p = &op->part[l];
+        if (p->n == 0)
+            continue;
+        uint8_t *di = dev_addr_any(layers, nlayers, in[l], p->cons);
+        uint8_t *dout = capacity[l] >= p->ptbytes ? dev_addr_any(layers, nlayers, out[l], p->ptbytes) : NULL;
+        if (di == NULL || dout == NULL) {
+            direct = 0;
+            break;
+        }
+        for (size_t m = 0; m < nlayers; ++m)
+            if (overlaps(in[l], p->cons, out[m], op->part[m].ptbytes))
+                direct = 0;
+        if (src_base == NULL || di < src_base)
+            src_base = di;
+        if (dst_base == NULL || dout < dst_base)
+            dst_base = dout;
+    }
+    op->direct = direct;
+    const size_t off_conn = up16(nrec * sizeof(ptls_mi355x_tls_record_t));
+    op->off_src = off_conn + (nlayers > 1 ? up16(nrec * 4) : 0);
+    op->srcbytes = direct ? 0 : srcbytes;
+    op->off_dst = op->off_src + op->srcbytes;
+    op->dstbytes = direct ? 0 : ptbytes;
+    op->off_st = op->off_dst + op->dstbytes;
+    op->off_ty = op->off_st + up16(nrec * 4);
+    const size_t total = op->off_ty + up16(nrec);
+    op->zero_copy = direct || total <= layers[0]->zero_copy_bytes;
+    if (reserve_stage(s, total) != 0 || (!op->zero_copy && reserve_device(s) != 0))
+        goto Fail;
+    uint32_t *conn = (uint32_t *)(s->h_buf + off_conn);
+    for (size_t l = 0, so = 0, dso = 0; l < nlayers; ++l) {
+        rl_part_t *p = &op->part[l];
+        if (p->n == 0)
+            continue;
+        if (direct) {
+            p->src_add = (uint64_t)(dev_addr_any(layers, nlayers, in[l], p->cons) - src_base);
+            p->dst_add = (uint64_t)(dev_addr_any(layers, nlayers, out[l], p->ptbytes) - dst_base);
+        } else {
+            p->src_add = so;
+            p->dst_add = dso;
+            memcpy(s->h_buf + op->off_src + so, in[l], p->cons);
+            so += up16(p->cons);
+            dso += up16(p->ptbytes);
+        }
+        const uint32_t cid = be32(layers[l]->iv) ^ be32(layers[0]->iv);
+        for (size_t i = p->k0; i < p->k0 + p->n; ++i) {
+            s->recs[i].src += p->src_add;
+            s->recs[i].dst += p->dst_add;
+            if (nlayers > 1)
+                conn[i] = cid;
+        }
+    }
+    memcpy(s->h_buf, s->recs, nrec * sizeof(ptls_mi355x_tls_record_t));
+    if (op_launch(s, src_base, dst_base) != 0) {
+        op_scrub(s);
+        goto Fail;
+    }
+    for (size_t l = 0; l < nlayers; ++l) /* speculative: the next window's records follow these */
+        layers[l]->spec_seq = op->part[l].seq0 + op->part[l].n;
+    op_commit(s, ticket);
+    return 0;
+Fail:
+    op_discard(op);
+    return -1;
+}
+
+int ptls_mi355x_record_layer_open_submit(ptls_mi355x_record_layer_t *const *layers, size_t nlayers, const void *const *in,
+                                         const size_t *inlen, void *const *out, const size_t *capacity, size_t *parsed,
+                                         uint64_t *ticket)
+{
+    return open_submit(layers, nlayers, in, inlen, out, capacity, parsed, 0, ticket);
+}
+
+/* ---------------------------------------------------------------------------------------------------- wait ---- */
+
+static void finish_seal(rl_slot_t *s, size_t *outlen, size_t *nrecords, size_t *consumed, int *alerts)
+{
+    rl_op_t *op = &s->op;
+    for (size_t l = 0, off = 0; l < op->nlayers; ++l) {
+        const rl_part_t *p = &op->part[l];
+        if (!op->direct && p->wire != 0) {
+            memcpy(op->out[l], s->h_buf + op->off_dst + off, p->wire);
+            off += p->wire;
+        }
+        outlen[l] = p->wire;
+        if (nrecords != NULL)
+            nrecords[l] = p->nrec;
+        if (consumed != NULL)
+            consumed[l] = p->nfrags;
+        alerts[l] = p->stopped ? PTLS_MI355X_RECORD_LAYER_KEY_UPDATE : 0;
+    }
+    if (!op->direct && op->srcbytes != 0)
+        memset(s->h_buf + op->off_src, 0, op->srcbytes); /* no plaintext left in the staging */
+}
+
+static void finish_open(rl_slot_t *s, size_t *outlen, size_t *nrecords, size_t *consumed, int *alerts, uint8_t *type)
+{
+    rl_op_t *op = &s->op;
+    const uint32_t *status = (const uint32_t *)(s->h_buf + op->off_st);
+    const uint8_t *types = s->h_buf + op->off_ty;
+    for (size_t l = 0; l < op->nlayers; ++l) {
+        const rl_part_t *p = &op->part[l];
+        ptls_mi355x_record_layer_t *x = op->layers[l];
+        uint8_t *slots = op->direct ? (uint8_t *)op->out[l] : s->h_buf + op->off_dst + p->dst_add;
+        size_t done = 0, wire_done = 0, olen = 0;
+        int a = 0;
+        if (p->seq0 != x->seq) {
+            a = PTLS_MI355X_RECORD_LAYER_STALE; /* a window before this one stopped early */
+        } else if (p->n != 0) {
+            /* slot i of this layer at its local plaintext offset: in out[l] (direct) or in the staging */
+            for (size_t i = p->k0; i < p->k0 + p->n; ++i) {
+                if (status[i] == PTLS_MI355X_TLS_BAD_RECORD_MAC) {
+                    a = 20; /* PTLS_ALERT_BAD_RECORD_MAC */
+                    break;
+                }
+                if (status[i] == PTLS_MI355X_TLS_UNEXPECTED_MESSAGE) {
+                    a = 10; /* PTLS_ALERT_UNEXPECTED_MESSAGE: no content type */
+                    break;
+                }
+                if (types[i] != 23 && !op->any_type) /* a handshake / alert record: open_record delivers it */
+                    break;
+                if (olen + status[i] > op->capacity[l]) {
+                    if (done == 0) {
+                        snprintf(rl_err, sizeof(rl_err), "record layer: %u plaintext bytes exceed the output capacity %zu",
+                                 status[i], op->capacity[l]);
+                        a = -1;
+                    }
+                    break;
+                }
+                /* direct: slot i starts at or after olen, so the delivered plaintexts close up in place */
+                memmove((uint8_t *)op->out[l] + olen, slots + (s->recs[i].dst - p->dst_add), status[i]);
+                olen += status[i];
+                wire_done += PTLS_MI355X_TLS_HEADER_SIZE + s->recs[i].len;
+                if (type != NULL)
+                    *type = types[i];
+                ++done;
+            }
+            x->seq += done;
+        }
+        if (p->n != 0) {
+            if (op->direct)
+                memset((uint8_t *)op->out[l] + olen, 0, p->ptbytes - olen); /* padding, types, records not delivered */
+            else
+                memset(slots, 0, p->ptbytes); /* no plaintext left in the staging */
+        }
+        if (a == 0 && done == p->n)
+            a = p->perr; /* a DECODE_ERROR behind the parsed records */
+        if (a != PTLS_MI355X_RECORD_LAYER_STALE && done < p->n)
+            x->spec_seq = x->seq; /* stopped early: the windows behind this one are stale, new ones follow it */
+        consumed[l] = wire_done;
+        outlen[l] = olen;
+        if (nrecords != NULL)
+            nrecords[l] = done;
+        alerts[l] = a;
+    }
+}
+
+static int op_wait(ptls_mi355x_record_layer_t *rl, uint64_t ticket, size_t *outlen, size_t *nrecords, size_t *consumed,
+                   int *alerts, uint8_t *type)
+{
+    if (ticket != rl->oldest || rl->oldest == rl->next_ticket)
+        return rl_msg(rl->oldest == rl->next_ticket ? "no window outstanding" : "windows are completed in submission order");
+    rl_slot_t *s = &rl->slot[ticket % RL_SLOTS];
+    rl_op_t *op = &s->op;
+    int ret = 0;
+    hipError_t e;
+    if (op->nrec != 0 && (e = hipStreamSynchronize(s->stream)) != hipSuccess) {
+        rl_fail("synchronize", e);
+        op_scrub(s);
+        for (size_t l = 0; l < op->nlayers; ++l) {
+            outlen[l] = 0;
+            if (nrecords != NULL)
+                nrecords[l] = 0;
+            if (consumed != NULL)
+                consumed[l] = 0;
+            alerts[l] = 0;
+        }
+        ret = -1;
+    } else if (op->is_seal) {
+        finish_seal(s, outlen, nrecords, consumed, alerts);
+    } else {
+        size_t dummy[1];
+        finish_open(s, outlen, nrecords, consumed != NULL ? consumed : dummy, alerts, type);
+    }
+    ++rl->oldest;
+    op_discard(op);
+    return ret;
+}
+
+int ptls_mi355x_record_layer_wait(ptls_mi355x_record_layer_t *rl, uint64_t ticket, size_t *outlen, size_t *nrecords,
+                                  size_t *consumed, int *alerts)
+{
+    return op_wait(rl, ticket, outlen, nrecords, consumed, alerts, NULL);
+}
+
+/* ------------------------------------------------------------------------------------- synchronous calls ---- */
+
+/* 1 when no layer has an asynchronous window outstanding (a synchronous call is a submit and its wait) */
+static int no_pending(ptls_mi355x_record_layer_t *const *layers, size_t nlayers)
+{
+    for (size_t l = 0; l < nlayers; ++l) {
+        if (layers[l]->next_ticket != layers[l]->oldest) {
+            rl_msg("asynchronous windows outstanding (wait for them first)");
+            return 0;
+        }
+    }
+    return 1;
+}
+
+int ptls_mi355x_record_layer_seal_multi(ptls_mi355x_record_layer_t *const *layers, size_t nlayers,
+                                        const ptls_mi355x_iovec_t *const *frags, const size_t *nfrags, uint8_t type,
+                                        void *const *out, const size_t *capacity, size_t *outlen, size_t *nrecords)
+{
+    for (size_t l = 0; l < nlayers; ++l) {
+        outlen[l] = 0;
+        if (nrecords != NULL)
+            nrecords[l] = 0;
+    }
+    if (nlayers == 0)
+        return 0;
+    if (!no_pending(layers, nlayers))
+        return -1;
+    int stack_alerts[8], *alerts = nlayers <= 8 ? stack_alerts : malloc(nlayers * sizeof(int));
+    if (alerts == NULL)
+        return rl_msg("out of memory");
+    uint64_t t;
+    int ret = ptls_mi355x_record_layer_seal_submit(layers, nlayers, frags, nfrags, type, out, capacity, &t);
+    if (ret == 0)
+        ret = op_wait(layers[0], t, outlen, nrecords, NULL, alerts, NULL);
+    for (size_t l = 0; ret == 0 && l < nlayers; ++l)
+        if (alerts[l] == PTLS_MI355X_RECORD_LAYER_KEY_UPDATE)
+            ret = PTLS_MI355X_RECORD_LAYER_KEY_UPDATE;
+    if (alerts != stack_alerts)
+        free(alerts);
+    return ret;
+}
+
+int ptls_mi355x_record_layer_seal(ptls_mi355x_record_layer_t *rl, const ptls_mi355x_iovec_t *frags, size_t nfrags,
+                                  uint8_t type, void *out, size_t capacity, size_t *outlen, size_t *nrecords)
+{
+    return ptls_mi355x_record_layer_seal_multi(&rl, 1, &frags, &nfrags, type, &out, &capacity, outlen, nrecords);
+}
 
 int ptls_mi355x_record_layer_open_multi(ptls_mi355x_record_layer_t *const *layers, size_t nlayers, const void *const *in,
                                         const size_t *inlen, size_t *consumed, void *const *out, const size_t *capacity,
@@ -445,166 +912,12 @@ int ptls_mi355x_record_layer_open_multi(ptls_mi355x_record_layer_t *const *layer
     }
     if (nlayers == 0)
         return 0;
-    ptls_mi355x_record_layer_t *rl = layers[0];
-    if (!same_session(layers, nlayers))
+    if (!no_pending(layers, nlayers))
         return -1;
-    rl_open_part_t *part = (rl_open_part_t *)calloc(nlayers, sizeof(*part));
-    if (part == NULL) {
-        snprintf(rl_err, sizeof(rl_err), "record layer: out of memory");
+    uint64_t t;
+    if (open_submit(layers, nlayers, in, inlen, out, capacity, NULL, 0, &t) != 0)
         return -1;
-    }
-    int ret = -1;
-    size_t max = 0, nrec = 0, srcbytes = 0, ptbytes = 0;
-    for (size_t l = 0; l < nlayers; ++l)
-        max += inlen[l] / (PTLS_MI355X_TLS_HEADER_SIZE + 16) + 1;
-    if (reserve_recs(rl, max) != 0)
-        goto Exit;
-    /* the complete application_data records at the start of every input, offsets local to it for now */
-    for (size_t l = 0; l < nlayers; ++l) {
-        uint64_t seq = layers[l]->seq;
-        part[l].k0 = nrec;
-        part[l].perr = ptls_mi355x_tls_parse_records((const uint8_t *)in[l], inlen[l], 0, &seq, 0, rl->recs + nrec,
-                                                     max - nrec, &part[l].n, &part[l].cons);
-        if (part[l].n != 0) {
-            const ptls_mi355x_tls_record_t *last = rl->recs + nrec + part[l].n - 1;
-            part[l].ptbytes = last->dst + (last->len >= 16u ? last->len - 16u : 0u);
-        }
-        nrec += part[l].n;
-        srcbytes += up16(part[l].cons);
-        ptbytes += up16(part[l].ptbytes);
-    }
-    if (nrec == 0) {
-        for (size_t l = 0; l < nlayers; ++l)
-            alerts[l] = part[l].perr;
-        ret = 0;
-        goto Exit;
-    }
-    /* direct: every input and every plaintext buffer (at least as large as its slots) in registered ranges */
-    uint8_t *src_base = NULL, *dst_base = NULL;
-    int direct = 1;
-    for (size_t l = 0; direct && l < nlayers; ++l) {
-        if (part[l].n == 0)
-            continue;
-        uint8_t *di = dev_addr_any(layers, nlayers, in[l], part[l].cons);
-        uint8_t *dout = capacity[l] >= part[l].ptbytes ? dev_addr_any(layers, nlayers, out[l], part[l].ptbytes) : NULL;
-        if (di == NULL || dout == NULL) {
-            direct = 0;
-            break;
-        }
-        if (src_base == NULL || di < src_base)
-            src_base = di;
-        if (dst_base == NULL || dout < dst_base)
-            dst_base = dout;
-    }
-    const size_t off_conn = up16(nrec * sizeof(ptls_mi355x_tls_record_t));
-    const size_t off_src = off_conn + (nlayers > 1 ? up16(nrec * 4) : 0);
-    const size_t off_dst = off_src + (direct ? 0 : srcbytes), off_st = off_dst + (direct ? 0 : ptbytes);
-    const size_t off_ty = off_st + up16(nrec * 4), total = off_ty + up16(nrec);
-    const int zero_copy = direct || total <= rl->zero_copy_bytes;
-    if (reserve_stage(rl, total) != 0 || (!zero_copy && reserve_device(rl, total) != 0))
-        goto Exit;
-    uint32_t *conn = (uint32_t *)(rl->h_buf + off_conn);
-    for (size_t l = 0, so = 0, dso = 0; l < nlayers; ++l) {
-        if (part[l].n == 0)
-            continue;
-        if (direct) {
-            part[l].src_add = (uint64_t)(dev_addr_any(layers, nlayers, in[l], part[l].cons) - src_base);
-            part[l].dst_add = (uint64_t)(dev_addr_any(layers, nlayers, out[l], part[l].ptbytes) - dst_base);
-        } else {
-            part[l].src_add = so;
-            part[l].dst_add = dso;
-            memcpy(rl->h_buf + off_src + so, in[l], part[l].cons);
-            so += up16(part[l].cons);
-            dso += up16(part[l].ptbytes);
-        }
-        const uint32_t cid = be32(layers[l]->iv) ^ be32(rl->iv);
-        for (size_t i = part[l].k0; i < part[l].k0 + part[l].n; ++i) {
-            rl->recs[i].src += part[l].src_add;
-            rl->recs[i].dst += part[l].dst_add;
-            if (nlayers > 1)
-                conn[i] = cid;
-        }
-    }
-    memcpy(rl->h_buf, rl->recs, nrec * sizeof(ptls_mi355x_tls_record_t));
-    uint8_t *base = zero_copy ? rl->h_dev : rl->d_buf;
-    hipError_t e;
-    int rc;
-    if (!zero_copy && (e = hipMemcpyAsync(rl->d_buf, rl->h_buf, off_src + srcbytes, hipMemcpyHostToDevice,
-                                          rl->stream)) != hipSuccess) {
-        rl_fail("H2D", e);
-        goto Exit;
-    }
-    /* every record verified independently; the stop at a connection's first failure is the host loop below */
-    if (nlayers == 1)
-        rc = ptls_mi355x_tls_open_records(rl->ctx, rl->iv, (const ptls_mi355x_tls_record_t *)base, nrec,
-                                          direct ? src_base : base + off_src, direct ? dst_base : base + off_dst,
-                                          (uint32_t *)(base + off_st), base + off_ty, rl->stream);
-    else
-        rc = ptls_mi355x_tls_open_records_multi(rl->ctx, rl->iv, (const ptls_mi355x_tls_record_t *)base,
-                                                (const uint32_t *)(base + off_conn), nrec,
-                                                direct ? src_base : base + off_src, direct ? dst_base : base + off_dst,
-                                                (uint32_t *)(base + off_st), base + off_ty, rl->stream);
-    if (rc != 0) {
-        snprintf(rl_err, sizeof(rl_err), "record layer: %s", ptls_mi355x_last_error());
-        goto Exit;
-    }
-    if ((!zero_copy && (e = hipMemcpyAsync(rl->h_buf + off_dst, rl->d_buf + off_dst, off_ty + nrec - off_dst,
-                                           hipMemcpyDeviceToHost, rl->stream)) != hipSuccess) ||
-        (e = hipStreamSynchronize(rl->stream)) != hipSuccess) {
-        rl_fail("synchronize", e);
-        goto Exit;
-    }
-    const uint32_t *status = (const uint32_t *)(rl->h_buf + off_st);
-    const uint8_t *types = rl->h_buf + off_ty;
-    for (size_t l = 0; l < nlayers; ++l) {
-        if (part[l].n == 0) {
-            alerts[l] = part[l].perr;
-            continue;
-        }
-        /* slot i of this layer at its local plaintext offset: in out[l] (direct) or in the staging */
-        uint8_t *slots = direct ? (uint8_t *)out[l] : rl->h_buf + off_dst + part[l].dst_add;
-        size_t done = 0, wire_done = 0, olen = 0;
-        int a = 0;
-        for (size_t i = part[l].k0; i < part[l].k0 + part[l].n; ++i) {
-            if (status[i] == PTLS_MI355X_TLS_BAD_RECORD_MAC) {
-                a = 20; /* PTLS_ALERT_BAD_RECORD_MAC */
-                break;
-            }
-            if (status[i] == PTLS_MI355X_TLS_UNEXPECTED_MESSAGE) {
-                a = 10; /* PTLS_ALERT_UNEXPECTED_MESSAGE: no content type */
-                break;
-            }
-            if (types[i] != 23) /* a handshake / alert record inside: the caller's picotls path re-opens it */
-                break;
-            if (olen + status[i] > capacity[l]) {
-                if (done == 0) {
-                    snprintf(rl_err, sizeof(rl_err), "record layer: %u plaintext bytes exceed the output capacity %zu",
-                             status[i], capacity[l]);
-                    a = -1;
-                }
-                break;
-            }
-            /* direct: slot i starts at or after olen, so the delivered plaintexts close up in place */
-            memmove((uint8_t *)out[l] + olen, slots + (rl->recs[i].dst - part[l].dst_add), status[i]);
-            olen += status[i];
-            wire_done += PTLS_MI355X_TLS_HEADER_SIZE + (rl->recs[i].len);
-            ++done;
-        }
-        if (direct)
-            memset((uint8_t *)out[l] + olen, 0, part[l].ptbytes - olen); /* padding, types, records not delivered */
-        else
-            memset(slots, 0, part[l].ptbytes); /* no plaintext left in the staging */
-        layers[l]->seq += done;
-        consumed[l] = wire_done;
-        outlen[l] = olen;
-        if (nrecords != NULL)
-            nrecords[l] = done;
-        alerts[l] = a == 0 && done == part[l].n ? part[l].perr : a; /* a DECODE_ERROR behind the parsed records */
-    }
-    ret = 0;
-Exit:
-    free(part);
-    return ret;
+    return op_wait(layers[0], t, outlen, nrecords, consumed, alerts, NULL);
 }
 
 int ptls_mi355x_record_layer_open(ptls_mi355x_record_layer_t *rl, const void *in, size_t inlen, size_t *consumed,
@@ -613,5 +926,23 @@ int ptls_mi355x_record_layer_open(ptls_mi355x_record_layer_t *rl, const void *in
     int alert = 0;
     if (ptls_mi355x_record_layer_open_multi(&rl, 1, &in, &inlen, consumed, &out, &capacity, outlen, nrecords, &alert) != 0)
         return -1;
+    return alert;
+}
+
+int ptls_mi355x_record_layer_open_record(ptls_mi355x_record_layer_t *rl, const void *in, size_t inlen, size_t *consumed,
+                                         void *out, size_t capacity, size_t *outlen, uint8_t *content_type)
+{
+    *consumed = *outlen = 0;
+    *content_type = 0;
+    if (!no_pending(&rl, 1))
+        return -1;
+    uint64_t t;
+    int alert = 0;
+    if (open_submit(&rl, 1, &in, &inlen, &out, &capacity, NULL, 1, &t) != 0)
+        return -1;
+    if (op_wait(rl, t, outlen, NULL, consumed, &alert, content_type) != 0)
+        return -1;
+    if (*consumed == 0)
+        *content_type = 0;
     return alert;
 }

@@ -1,0 +1,167 @@
+/*
+ * scripts/rl_stream.c -- measurement driver (not part of the product library): the host-to-host rate of the
+ * asynchronous record layer (include/ptls_mi355x.h section 5) on a stream of rapido windows, driven from C as rapido
+ * itself would drive it (its send loop, lib/rapido.c:2176-2301, keeps many windows moving; a window is 16 records of
+ * 16 KiB, :2115-2126).
+ *
+ *   rl_stream [nwin] [depth] [key_bytes] [transport: direct|zero_copy|copy]
+ *
+ * nwin windows are sealed from one host buffer into another with `depth` windows in flight (seal_submit, and the wait
+ * of the oldest once `depth` are outstanding), then opened back the same way; the clock is CLOCK_MONOTONIC from the
+ * first submit to the last wait, after one untimed pass.  Every opened window is compared with its fragments.  Prints
+ * one JSON object.  Built by rapido_amd/build.py into scripts/_build/rl_stream; run by bench.py's record_layer_stream.
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include "../include/ptls_mi355x.h"
+
+#define WIN 16
+#define FRAG 16384
+#define WIRE_WIN (WIN * (FRAG + PTLS_MI355X_TLS_OVERHEAD))
+#define PT_WIN (WIN * (FRAG + 1))
+
+static double now(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+static void *page_alloc(size_t n)
+{
+    void *p = NULL;
+    if (posix_memalign(&p, 4096, n) != 0)
+        return NULL;
+    memset(p, 0, n);
+    return p;
+}
+
+static void die(const char *what)
+{
+    fprintf(stderr, "rl_stream: %s: %s\n", what, ptls_mi355x_record_layer_last_error());
+    exit(1);
+}
+
+typedef struct {
+    ptls_mi355x_record_layer_t *tx, *rx;
+    uint8_t *send, *wire, *pt;
+    ptls_mi355x_iovec_t (*frags)[WIN];
+    size_t nwin;
+} stream_t;
+
+/* one pass: seal every window (depth in flight), or open every window */
+static double pass(stream_t *st, int seal, size_t depth, size_t max_inflight_seen[1])
+{
+    ptls_mi355x_record_layer_t *rl = seal ? st->tx : st->rx;
+    uint64_t tickets[64], head = 0, tail = 0;
+    ptls_mi355x_record_layer_set_seq(rl, 0);
+    const double t0 = now();
+    for (size_t w = 0; w < st->nwin + depth; ++w) {
+        if (tail - head == depth || (w >= st->nwin && tail != head)) {
+            size_t outlen, nrec, cons;
+            int alert;
+            if (ptls_mi355x_record_layer_wait(rl, tickets[head % 64], &outlen, &nrec, &cons, &alert) != 0)
+                die("wait");
+            if (nrec != WIN || alert != 0 || outlen != (seal ? (size_t)WIRE_WIN : (size_t)WIN * FRAG)) {
+                fprintf(stderr, "rl_stream: window %zu: %zu records, %zu bytes, alert %d\n", (size_t)head, nrec, outlen, alert);
+                exit(1);
+            }
+            ++head;
+        }
+        if (w >= st->nwin)
+            continue;
+        if (seal) {
+            const ptls_mi355x_iovec_t *f = st->frags[w];
+            const size_t nf = WIN, cap = WIRE_WIN;
+            void *out = st->wire + w * WIRE_WIN;
+            if (ptls_mi355x_record_layer_seal_submit(&st->tx, 1, &f, &nf, 23, &out, &cap, &tickets[tail % 64]) != 0)
+                die("seal_submit");
+        } else {
+            const void *in = st->wire + w * WIRE_WIN;
+            const size_t inlen = WIRE_WIN, cap = PT_WIN;
+            void *out = st->pt + w * PT_WIN;
+            size_t parsed;
+            if (ptls_mi355x_record_layer_open_submit(&st->rx, 1, &in, &inlen, &out, &cap, &parsed, &tickets[tail % 64]) != 0)
+                die("open_submit");
+        }
+        ++tail;
+        if (tail - head > max_inflight_seen[0])
+            max_inflight_seen[0] = tail - head;
+    }
+    return now() - t0;
+}
+
+int main(int argc, char **argv)
+{
+    const size_t nwin = argc > 1 ? (size_t)atoi(argv[1]) : 64, depth = argc > 2 ? (size_t)atoi(argv[2]) : 4;
+    const size_t key_bytes = argc > 3 ? (size_t)atoi(argv[3]) : 16;
+    const char *transport = argc > 4 ? argv[4] : "direct";
+    if (depth < 1 || depth > 4 || nwin < 1 || (key_bytes != 16 && key_bytes != 32)) {
+        fprintf(stderr, "usage: rl_stream [nwin] [depth 1..4] [16|32] [direct|zero_copy|copy]\n");
+        return 2;
+    }
+    stream_t st = {0};
+    st.nwin = nwin;
+    uint8_t key[32], iv[12];
+    uint64_t x = 0x9e3779b97f4a7c15ull;
+    for (size_t i = 0; i < 32; ++i)
+        key[i] = (uint8_t)((x = x * 6364136223846793005ull + 1442695040888963407ull) >> 56);
+    for (size_t i = 0; i < 12; ++i)
+        iv[i] = (uint8_t)((x = x * 6364136223846793005ull + 1442695040888963407ull) >> 56);
+    st.send = page_alloc(nwin * WIN * FRAG);
+    st.wire = page_alloc(nwin * WIRE_WIN);
+    st.pt = page_alloc(nwin * PT_WIN);
+    st.frags = malloc(nwin * sizeof(*st.frags));
+    if (st.send == NULL || st.wire == NULL || st.pt == NULL || st.frags == NULL)
+        return 1;
+    for (size_t i = 0; i < nwin * WIN * FRAG; i += 8) {
+        x = x * 6364136223846793005ull + 1442695040888963407ull;
+        memcpy(st.send + i, &x, 8);
+    }
+    for (size_t w = 0; w < nwin; ++w)
+        for (size_t i = 0; i < WIN; ++i)
+            st.frags[w][i] = (ptls_mi355x_iovec_t){st.send + (w * WIN + i) * FRAG, FRAG};
+    if ((st.tx = ptls_mi355x_record_layer_new(key, key_bytes, iv, 0)) == NULL ||
+        (st.rx = ptls_mi355x_record_layer_new(key, key_bytes, iv, 0)) == NULL)
+        die("record_layer_new");
+    if (strcmp(transport, "direct") == 0) {
+        if (ptls_mi355x_record_layer_register(st.tx, st.send, nwin * WIN * FRAG) != 0 ||
+            ptls_mi355x_record_layer_register(st.tx, st.wire, nwin * WIRE_WIN) != 0 ||
+            ptls_mi355x_record_layer_register(st.rx, st.wire, nwin * WIRE_WIN) != 0 ||
+            ptls_mi355x_record_layer_register(st.rx, st.pt, nwin * PT_WIN) != 0)
+            die("register");
+    } else if (strcmp(transport, "copy") == 0) {
+        ptls_mi355x_record_layer_set_zero_copy_bytes(st.tx, 0);
+        ptls_mi355x_record_layer_set_zero_copy_bytes(st.rx, 0);
+    }
+    size_t inflight = 0;
+    double t_seal = 0, t_open = 0, t_seal1 = 0, t_open1 = 0;
+    pass(&st, 1, depth, &inflight); /* untimed: every slot's stream, context and staging created */
+    pass(&st, 0, depth, &inflight);
+    t_seal = pass(&st, 1, depth, &inflight);
+    t_open = pass(&st, 0, depth, &inflight);
+    t_seal1 = pass(&st, 1, 1, &inflight);
+    t_open1 = pass(&st, 0, 1, &inflight);
+    for (size_t w = 0; w < nwin; ++w) {
+        if (memcmp(st.pt + w * PT_WIN, st.send + w * WIN * FRAG, (size_t)WIN * FRAG) != 0) {
+            fprintf(stderr, "rl_stream: window %zu opened to other bytes than its fragments\n", w);
+            return 1;
+        }
+    }
+    const double bytes = (double)nwin * WIN * FRAG, gib = (double)(1u << 30);
+    printf("{\"seal_gibps\": %.2f, \"open_gibps\": %.2f, \"seal_us_per_window\": %.2f, \"open_us_per_window\": %.2f, "
+           "\"seal_gibps_sync\": %.2f, \"open_gibps_sync\": %.2f, \"windows\": %zu, \"depth\": %zu, \"max_in_flight\": %zu, "
+           "\"transport\": \"%s\", \"key_bits\": %zu}\n",
+           bytes / t_seal / gib, bytes / t_open / gib, t_seal / nwin * 1e6, t_open / nwin * 1e6, bytes / t_seal1 / gib,
+           bytes / t_open1 / gib, nwin, depth, inflight, transport, 8 * key_bytes);
+    ptls_mi355x_record_layer_free(st.tx);
+    ptls_mi355x_record_layer_free(st.rx);
+    free(st.send);
+    free(st.wire);
+    free(st.pt);
+    free(st.frags);
+    return 0;
+}

@@ -1,0 +1,243 @@
+"""The record layer's asynchronous windows, the 2^24-record key-update limit, open_record and rekey
+(include/ptls_mi355x.h section 5, rapido_amd/csrc/record_layer.c), on every transport: direct (registered host
+buffers, the kernels work on them in place), zero-copy (pinned staging) and copy (DMA).
+
+Every wire byte is checked against the oracle's TLS 1.3 record functions, which reproduce the reference ptls_send /
+ptls_receive (tests/test_tls_records.py, tests/golden/tls_records.json).  The limit follows ptls_send
+(lib/picotls.c:4969-4988): a call starting at seq >= 2^24 first sends a KeyUpdate (update_send_key, :4949-4962,
+sealed under the old key at that seq) and continues under the next key from seq 0; the check is at the start of a
+call, so a fragment that starts below the limit is sealed whole."""
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+import oracle
+import rapido_amd as ra
+from conftest import kernel_family
+from test_gpu_record_layer import conn_iv, oracle_window, page_buffer
+
+pytestmark = pytest.mark.gpu
+
+TRANSPORTS = ["direct", "zero_copy", "copy"]
+LIMIT = ra.RECORD_LAYER_SEQ_LIMIT
+KEY_UPDATE_MSG = bytes([24, 0, 0, 1, 0])  # handshake KeyUpdate, update_not_requested (RFC 8446 sec. 4.6.3)
+
+
+class Host:
+    """Host buffers for one transport: registered page-aligned ranges (direct) or plain arrays (staging)."""
+
+    def __init__(self, transport, layers, nbytes):
+        self.transport, self.layers = transport, layers
+        self.buf = page_buffer(nbytes)
+        self.pos = 0
+        if transport == "direct":
+            for rl in layers:
+                rl.register(self.buf)
+        for rl in layers:
+            if transport == "copy":
+                rl.set_zero_copy_bytes(0)
+
+    def take(self, n, fill=None):
+        """n bytes of the buffer (64-B aligned pieces, so windows do not share lines by accident)"""
+        v = self.buf[self.pos:self.pos + n]
+        self.pos += (n + 63) & ~63
+        assert self.pos <= self.buf.size
+        if fill is not None:
+            v[:] = np.frombuffer(fill, np.uint8) if isinstance(fill, (bytes, bytearray)) else fill
+        return v
+
+
+def oracle_windows_parallel(key, iv, seq, windows):
+    """oracle_window over many windows on 8 threads (the C oracle releases the GIL): wire bytes per window"""
+    seqs, s = [], seq
+    for w in windows:
+        seqs.append(s)
+        s += sum(max(1, -(-len(f) // 16384)) if f else 0 for f in w)
+    with ThreadPoolExecutor(8) as ex:
+        return list(ex.map(lambda a: oracle_window(key, iv, a[0], a[1])[0], zip(seqs, windows)))
+
+
+@pytest.mark.parametrize("transport", TRANSPORTS)
+def test_key_update_limit(gpu, transport):
+    rng = np.random.default_rng(2024)
+    key, key2 = rng.integers(0, 256, 16, dtype=np.uint8).tobytes(), rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+    iv, iv2 = conn_iv(rng.integers(0, 256, 12, dtype=np.uint8).tobytes(), 5), rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    frags_b = [rng.integers(0, 256, 1000 + 37 * i, dtype=np.uint8).tobytes() for i in range(16)]
+    tx, rx = ra.RecordLayer(key, iv, seq=LIMIT - 3), ra.RecordLayer(key, iv, seq=LIMIT - 3)
+    h = Host(transport, [tx, rx], 1 << 21)
+    frags = [h.take(len(f), f) for f in frags_b]
+    # a 16-record window at 2^24 - 3: three fragments sealed, the window stops at the limit
+    out = h.take(1 << 17)
+    olen, nrec = tx.seal_into(frags, out)
+    want3, _ = oracle_window(key, iv, LIMIT - 3, frags_b[:3])
+    assert tx.key_update and nrec == 3 and out[:olen].tobytes() == want3 and tx.seq == LIMIT
+    # nothing more of type 23 under this key
+    out0 = h.take(1 << 12)
+    assert tx.seal_into(frags[3:4], out0) == (0, 0) and tx.key_update and tx.seq == LIMIT
+    # the KeyUpdate message itself goes out at 2^24 under the old key (update_send_key)
+    ku = h.take(len(KEY_UPDATE_MSG), KEY_UPDATE_MSG)
+    out_ku = h.take(64)
+    olen_ku, n_ku = tx.seal_into([ku], out_ku, content_type=22)
+    assert not tx.key_update and n_ku == 1 and tx.seq == LIMIT + 1
+    assert out_ku[:olen_ku].tobytes() == oracle.tls_seal_record(key, iv, LIMIT, 22, KEY_UPDATE_MSG)
+    # the next traffic key: seq restarts at 0, the rest of the window follows
+    tx.rekey(key2, iv2)
+    assert tx.seq == 0
+    out2 = h.take(1 << 17)
+    olen2, nrec2 = tx.seal_into(frags[3:], out2)
+    want13, _ = oracle_window(key2, iv2, 0, frags_b[3:])
+    assert not tx.key_update and nrec2 == 13 and out2[:olen2].tobytes() == want13 and tx.seq == 13
+    # the receiver: three records, stop at the handshake record, open_record hands it over, rekey, the rest
+    wire_b = out[:olen].tobytes() + out_ku[:olen_ku].tobytes() + out2[:olen2].tobytes()
+    wire = h.take(len(wire_b), wire_b)
+    pt = h.take(len(wire_b))
+    rc, plen, cons, n = rx.open_into(wire, pt)
+    assert (rc, n, cons) == (0, 3, olen) and pt[:plen].tobytes() == b"".join(frags_b[:3]) and rx.seq == LIMIT
+    rc, msg, cons_ku, ctype = rx.open_record(wire_b[cons:])
+    assert (rc, msg, cons_ku, ctype) == (0, KEY_UPDATE_MSG, olen_ku, 22) and rx.seq == LIMIT + 1
+    rx.rekey(key2, iv2)
+    rc, plen, cons2, n = rx.open_into(wire[cons + cons_ku:], pt)
+    assert (rc, n, cons2) == (0, 13, olen2) and pt[:plen].tobytes() == b"".join(frags_b[3:]) and rx.seq == 13
+    # ptls_send checks the limit at its start: a 40000-byte fragment starting at 2^24 - 1 is sealed whole
+    tx.seq = LIMIT - 1
+    tx.rekey(key, iv)
+    tx.seq = LIMIT - 1
+    big_b = rng.integers(0, 256, 40000, dtype=np.uint8).tobytes()
+    big = h.take(len(big_b), big_b)
+    out3 = h.take(1 << 16)
+    olen3, nrec3 = tx.seal_into([big, frags[0]], out3)
+    want_big, _ = oracle_window(key, iv, LIMIT - 1, [big_b])
+    assert tx.key_update and nrec3 == 3 and out3[:olen3].tobytes() == want_big and tx.seq == LIMIT + 2
+    for rl in (tx, rx):
+        rl.close()
+
+
+def test_key_update_limit_multi(gpu):
+    """seal_multi: each connection stops at its own limit; the others seal their whole windows."""
+    rng = np.random.default_rng(2025)
+    key = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+    iv = rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    ivs = [conn_iv(iv, c) for c in range(3)]
+    seqs = [LIMIT - 2, 7, LIMIT]
+    layers = [ra.RecordLayer(key, ivs[c], seq=seqs[c]) for c in range(3)]
+    windows = [[rng.integers(0, 256, 500 + 100 * i, dtype=np.uint8).tobytes() for i in range(4)] for _ in range(3)]
+    got = ra.record_layer_seal_multi(layers, windows)
+    assert got[0] == (oracle_window(key, ivs[0], LIMIT - 2, windows[0][:2])[0], 2) and layers[0].seq == LIMIT
+    assert got[1] == (oracle_window(key, ivs[1], 7, windows[1])[0], 4) and layers[1].seq == 11
+    assert got[2] == (b"", 0) and layers[2].seq == LIMIT
+    for rl in layers:
+        rl.close()
+
+
+def _stream(transport, nwin, depth, key, iv, rng):
+    """nwin windows of 16 x 16 KiB through seal_submit / wait and open_submit / wait, `depth` in flight"""
+    WIN, FRAG = 16, 16384
+    tx, rx = ra.RecordLayer(key, iv), ra.RecordLayer(key, iv)
+    h = Host(transport, [tx, rx], nwin * WIN * (3 * FRAG + 192) + (1 << 20))
+    frags_b = [[rng.integers(0, 256, FRAG, dtype=np.uint8).tobytes() for _ in range(WIN)] for _ in range(nwin)]
+    frags = [[h.take(FRAG, f) for f in w] for w in frags_b]
+    wire_win = WIN * (FRAG + ra.TLS_OVERHEAD)
+    wires = [h.take(wire_win) for _ in range(nwin)]
+    pts = [h.take(WIN * (FRAG + 1)) for _ in range(nwin)]
+    tickets, done = [], []
+    for w in range(nwin):
+        if len(tickets) == depth:
+            done.append(tx.wait(tickets.pop(0)))
+        tickets.append(tx.seal_submit(frags[w], wires[w]))
+        assert tx.seq == WIN * (w + 1) and tx.pending == len(tickets)
+    done += [tx.wait(t) for t in tickets]
+    assert done == [(wire_win, WIN, WIN, 0)] * nwin and tx.pending == 0
+    want = oracle_windows_parallel(key, iv, 0, frags_b)
+    for w in range(nwin):
+        assert wires[w].tobytes() == want[w], f"window {w}"
+    tickets, done = [], []
+    for w in range(nwin):
+        if len(tickets) == depth:
+            done.append(rx.wait(tickets.pop(0)))
+        t, parsed = rx.open_submit(wires[w], pts[w])
+        assert parsed == wire_win
+        tickets.append(t)
+    done += [rx.wait(t) for t in tickets]
+    assert done == [(WIN * FRAG, WIN, wire_win, 0)] * nwin and rx.seq == nwin * WIN
+    for w in range(nwin):
+        assert pts[w][:WIN * FRAG].tobytes() == b"".join(frags_b[w]), f"window {w}"
+    tx.close()
+    rx.close()
+
+
+@pytest.mark.parametrize("transport", TRANSPORTS)
+def test_async_stream_matches_oracle(gpu, transport):
+    """64 back-to-back rapido send windows, 4 in flight, then their receive windows: every wire byte is
+    ptls_send's, every plaintext comes back."""
+    rng = np.random.default_rng(64)
+    _stream(transport, 64, 4, rng.integers(0, 256, 16, dtype=np.uint8).tobytes(),
+            rng.integers(0, 256, 12, dtype=np.uint8).tobytes(), rng)
+
+
+@pytest.mark.parametrize("family", ["split", "window16", "batch"])
+def test_async_stream_families(gpu, family):
+    rng = np.random.default_rng(65)
+    with kernel_family(family, framing=True):
+        _stream("direct", 6, 3, rng.integers(0, 256, 32, dtype=np.uint8).tobytes(),
+                rng.integers(0, 256, 12, dtype=np.uint8).tobytes(), rng)
+
+
+@pytest.mark.parametrize("transport", TRANSPORTS)
+def test_async_open_stale_after_failure(gpu, transport):
+    """Windows in flight behind a window that stops early (a bad record) complete STALE with nothing delivered;
+    resubmitted from the stop they open normally."""
+    rng = np.random.default_rng(99)
+    key, iv = rng.integers(0, 256, 16, dtype=np.uint8).tobytes(), rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    rx = ra.RecordLayer(key, iv, seq=100)
+    h = Host(transport, [rx], 1 << 21)
+    frags = [[rng.integers(0, 256, 700 + 13 * i, dtype=np.uint8).tobytes() for i in range(8)] for _ in range(4)]
+    wires_b = oracle_windows_parallel(key, iv, 100, frags)
+    rec_bounds = []  # wire offsets of window 1's records
+    off = 0
+    for f in frags[1]:
+        rec_bounds.append(off)
+        off += len(f) + ra.TLS_OVERHEAD
+    bad = bytearray(wires_b[1])
+    bad[rec_bounds[2] + 9] ^= 1  # ciphertext of record 2 of window 1
+    wires = [h.take(len(w), w) for w in (wires_b[0], bytes(bad), wires_b[2], wires_b[3])]
+    pts = [h.take(len(w)) for w in wires_b]
+    tickets = [rx.open_submit(wires[w], pts[w])[0] for w in range(4)]
+    with pytest.raises(RuntimeError):
+        rx.open_submit(wires[0], pts[0])  # all four slots in flight
+    with pytest.raises(RuntimeError):
+        rx.wait(tickets[1])  # completion is in submission order
+    with pytest.raises(RuntimeError):
+        rx.open(wires_b[0])  # a synchronous window behind asynchronous ones
+    r0 = rx.wait(tickets[0])
+    assert r0 == (sum(map(len, frags[0])), 8, len(wires_b[0]), 0) and pts[0][:r0[0]].tobytes() == b"".join(frags[0])
+    r1 = rx.wait(tickets[1])
+    assert r1 == (sum(map(len, frags[1][:2])), 2, rec_bounds[2], 20) and rx.seq == 110
+    assert pts[1][:r1[0]].tobytes() == b"".join(frags[1][:2])
+    for w in (2, 3):
+        assert rx.wait(tickets[w]) == (0, 0, 0, ra.RECORD_LAYER_STALE)
+    assert rx.seq == 110 and rx.pending == 0
+    # resubmitted from the stop (the intact bytes of window 1 from record 2, then windows 2 and 3)
+    tail = h.take(len(wires_b[1]) - rec_bounds[2], wires_b[1][rec_bounds[2]:])
+    outs = [h.take(len(wires_b[1])) for _ in range(3)]
+    tickets = [rx.open_submit(x, o)[0] for x, o in zip((tail, wires[2], wires[3]), outs)]
+    res = [rx.wait(t) for t in tickets]
+    assert [r[1] for r in res] == [6, 8, 8] and all(r[3] == 0 for r in res) and rx.seq == 132
+    assert outs[0][:res[0][0]].tobytes() == b"".join(frags[1][2:])
+    assert outs[2][:res[2][0]].tobytes() == b"".join(frags[3])
+    rx.close()
+
+
+def test_async_rekey_and_free_with_pending(gpu):
+    rng = np.random.default_rng(7)
+    key, iv = rng.integers(0, 256, 16, dtype=np.uint8).tobytes(), rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    tx = ra.RecordLayer(key, iv)
+    h = Host("zero_copy", [tx], 1 << 20)
+    f = h.take(5000, rng.integers(0, 256, 5000, dtype=np.uint8))
+    t = tx.seal_submit([f], h.take(8192))
+    with pytest.raises(RuntimeError):
+        tx.rekey(key, iv)  # a window outstanding
+    assert tx.wait(t)[:2] == (5000 + ra.TLS_OVERHEAD, 1)
+    tx.rekey(key, iv)
+    tx.seal_submit([f], h.take(8192))
+    tx.close()  # frees with a window never waited for
