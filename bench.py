@@ -179,6 +179,15 @@ def cpu_baseline(main_key: int, main_length: int) -> dict:
            "sample": f"lib/fusion.c (unmodified), t/ptlsbench.c methodology: 1000-record batches sealed then opened, "
                      f"32-B AAD = h[4] with seq, CLOCK_PROCESS_CPUTIME_ID; {len(workers)} pinned processes x "
                      f"~1-1.5 GB each per config; value = AES-{8 * main_key} {main_length} B seal+open, all workers"}
+    # what the whole host would do (an extrapolation, not a measurement): every physical core at the measured 1-core
+    # rate times the scaling efficiency measured on the cores this process may use (cgroup quota)
+    eff = main["scaling_cputime"] / max(1, min(len(workers), physical))
+    out["extrapolated_all_physical_cores"] = {
+        "value": round(physical * main["seal_open_gibps_1core"] * eff, 1), "unit": "GiB/s", "cores": physical,
+        "value_1core": main["seal_open_gibps_1core"], "scaling_efficiency_measured": round(eff, 3),
+        "label": f"EXTRAPOLATION, not measured: {physical} physical cores x {main['seal_open_gibps_1core']} GiB/s x "
+                 f"{eff:.3f} (the {len(workers)}-worker efficiency); all-core clocks under sustained VAES/VPCLMUL "
+                 f"load may lower it further"}
     if os.path.exists(PTLSBENCH):  # configs[0]-style unmodified run (L = 1500, the reference's own CSV)
         try:
             r = subprocess.run([PTLSBENCH], capture_output=True, text=True, timeout=120)
@@ -264,8 +273,9 @@ def measure(ra, wl_key, args, dev, rank, world, check):
         dist.barrier()
         elapsed = max_over_ranks(elapsed, dev)
 
-    seal_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
-    open_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in events]))
+    seal_all = [e[0].elapsed_time(e[1]) for e in events]
+    open_all = [e[1].elapsed_time(e[2]) for e in events]
+    seal_ms, open_ms = float(np.mean(seal_all)), float(np.mean(open_all))
 
     # correctness after timing: every status verifies and sampled records open back to their plaintext (parity with
     # the reference engine is the test suite's job: tests/test_gpu_*.py against oracle/ and its pinned fixtures)
@@ -313,7 +323,9 @@ def measure(ra, wl_key, args, dev, rank, world, check):
         "open_gibps": round(payload / (open_ms * 1e-3) / GIB, 2),
         "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                     "algorithmic_bytes_per_launch": dom_bytes, "launch_ms": round(dom_ms, 4)},
+                     "algorithmic_bytes_per_launch": dom_bytes, "launch_ms": round(dom_ms, 4),
+                     "launch_ms_median": round(float(np.median(seal_all if dom_is_seal else open_all)), 4),
+                     "launches": "the timed steps' launches only (HIP events on the launch stream), warmups excluded"},
         "lds_roofline": {"bound": "lds", "kernel": kname, "achieved": round(dom_payload, 1),
                          "peak": round(lds_ceiling, 1), "unit": "GB/s payload",
                          "frac": round(dom_payload / lds_ceiling, 4),
@@ -321,6 +333,18 @@ def measure(ra, wl_key, args, dev, rank, world, check):
                                   f"{lds_cycles_per_block:.2f} LDS clk/block/CU, {ncu} CU x {LDS_CLOCK_GHZ} GHz",
                          "note": "this read mix alone sustains 0.78 of the nominal rate (profiles/r01c_lds_ceiling.json)"},
     }
+    # the clock the chip holds under this kernel (DVFS at the board power limit): GRBM_GUI_ACTIVE / 8 over the
+    # launch time in the PMC pass (scripts/collect_profiles.py -> profiles/held_clock.json)
+    hpath = os.path.join(ROOT, "profiles", "held_clock.json")
+    if os.path.exists(hpath):
+        try:
+            held = json.load(open(hpath)).get(wl_key, {}).get(kname)
+        except ValueError:
+            held = None
+        if held:
+            peak_held = lds_ceiling * held["ghz"] / LDS_CLOCK_GHZ
+            res["lds_roofline"].update({"held_clock_ghz": held["ghz"], "peak_held": round(peak_held, 1),
+                                        "frac_held": round(dom_payload / peak_held, 4), "held_clock_source": held["source"]})
     extra = dict(eng=eng, iv=iv, d_src=d_src, d_ct=d_ct, d_recs=d_recs, d_aad=d_aad, recs=recs, n=n,
                  src_bytes=src_bytes, payload=payload, stream=stream, key=wl["key"])
     return res, extra
@@ -411,21 +435,28 @@ def e2e_pcie(ra, extra, dev, steps):
                     "around one launch; pipelined = 16 chunks over 3 streams"}
 
 
-def record_layer_stream(key_bytes: int = 16, nwin: int = 64, depth: int = 4, transport: str = "direct"):
+def record_layer_stream(key_bytes: int = 16, nwin: int = 64, depth: int = 4, transport: str = "direct",
+                        per_launch=(8, 1)):
     """Host-to-host side figure (never `value`): rapido send and receive windows (16 x 16 KiB records, lib/rapido.c
     :2115-2126) through the asynchronous record layer (include/ptls_mi355x.h section 5) on registered host buffers
-    (direct: the kernels read and write the socket buffers in place over PCIe), `depth` windows in flight.  Driven
-    from C (scripts/rl_stream.c), as rapido would drive it; timed on the host clock from the first submit to the last
-    wait; every opened window is compared with its fragments.  *_sync: one window at a time."""
+    (direct: the kernels read the socket buffers in place over PCIe, the delivery kernel writes the plaintexts),
+    `depth` launches in flight, each launch carrying the windows of `per_launch` connections of a session
+    (record_layer_seal_submit / open_submit over that many layers, as rapido's loop keeps many connections' windows
+    moving, lib/rapido.c:2176-2301).  Driven from C (scripts/rl_stream.c); timed on the host clock from the first
+    submit to the last wait; every opened window is compared with its fragments.  *_sync: one launch at a time."""
     exe = os.path.join(ROOT, "scripts", "_build", "rl_stream")
-    r = subprocess.run([exe, str(nwin), str(depth), str(key_bytes), transport], capture_output=True, text=True,
-                       timeout=120)
-    if r.returncode != 0:
-        raise SystemExit("bench: record-layer stream failed -- " + r.stderr.strip())
-    res = json.loads(r.stdout.strip().splitlines()[-1])
+    res = {}
+    for m in per_launch:
+        r = subprocess.run([exe, str(nwin), str(depth), str(key_bytes), transport, str(m)], capture_output=True,
+                           text=True, timeout=120)
+        if r.returncode != 0:
+            raise SystemExit("bench: record-layer stream failed -- " + r.stderr.strip())
+        one = json.loads(r.stdout.strip().splitlines()[-1])
+        res.update(one) if m == per_launch[0] else res.setdefault("one_window_per_launch", one)
     res["note"] = (f"{nwin} back-to-back windows of 16 x 16384 B records, AES-{8 * key_bytes}, host memory to host "
-                   f"memory ({transport}), {depth} windows in flight (record_layer_seal_submit / open_submit + wait), "
-                   "C driver scripts/rl_stream.c; *_sync: one window at a time")
+                   f"memory ({transport}: registered buffers), {per_launch[0]} connections' windows per launch, {depth} "
+                   "launches in flight (record_layer_seal_submit / open_submit + wait), C driver scripts/rl_stream.c; "
+                   "*_sync: one launch at a time; one_window_per_launch: a single connection's windows")
     return res
 
 

@@ -268,6 +268,27 @@ int ptls_mi355x_tls_open_records_ex(ptls_mi355x_aesgcm_context_t *ctx, const voi
                                     const uint8_t *src, uint8_t *dst, uint32_t *status, uint8_t *types, int flags,
                                     void *stream);
 
+/*
+ * Delivery of opened records: the receive loop of handle_input (lib/picotls.c:4757-4842) over a batch the open kernels
+ * verified, on the device.  For each part (one connection's records recs[k0 .. k0 + n) of that launch), the records
+ * are taken in order up to the first one whose status is a failure (BAD_RECORD_MAC, UNEXPECTED_MESSAGE,
+ * NOT_PROCESSED), whose type is not application_data (23) -- unless any_type, which takes exactly one record of any
+ * type -- or whose plaintext would overflow `capacity`; their plaintexts (status[i] bytes at slots + recs[i].dst)
+ * are copied back to back to out.  The host reproduces the counts from status / types (the same walk).  Device
+ * pointers (out may be a registered host range's device address); asynchronous on stream.  A part may hold at most
+ * 4096 records (max_records: the largest n of the parts).  0 or -1.
+ */
+#define PTLS_MI355X_DELIVER_MAX 4096
+typedef struct st_ptls_mi355x_tls_deliver_t {
+    const uint8_t *slots;
+    uint8_t *out;
+    uint64_t capacity;
+    uint32_t k0, n, any_type, reserved;
+} ptls_mi355x_tls_deliver_t;
+int ptls_mi355x_tls_deliver_records(ptls_mi355x_aesgcm_context_t *ctx, const ptls_mi355x_tls_record_t *recs,
+                                    const uint32_t *status, const uint8_t *types, const ptls_mi355x_tls_deliver_t *parts,
+                                    size_t nparts, size_t max_records, void *stream);
+
 /* Host-side planning (no device access), the loops of the reference record layer:
  *  plan_send: splits len bytes at src_off into <= 16384-byte fragments with consecutive seq
  *    from *seq, records laid out back to back from dst_off (buffer_push_encrypted_records,
@@ -387,8 +408,9 @@ int ptls_mi355x_record_layer_wait(ptls_mi355x_record_layer_t *rl, uint64_t ticke
 size_t ptls_mi355x_record_layer_pending(const ptls_mi355x_record_layer_t *rl);
 const char *ptls_mi355x_record_layer_last_error(void);
 /* How the bytes travel (record_layer.c): a call whose fragments and output (seal), or input and output (open; out
- * at least as large as the records' ciphertexts), all lie in ranges registered below runs DIRECT: the kernel reads
- * and writes them in place, no copy.  Otherwise a window of at most `zero copy bytes` (descriptors, input and
+ * at least as large as the records' ciphertexts), all lie in ranges registered below runs DIRECT: read and written in
+ * place by the kernels (default; an open's plaintexts are written once, back to back, by the delivery kernel), or by
+ * DMA to and from device memory (ptls_mi355x_record_layer_set_direct_dma), no staging copy either way.  Otherwise a window of at most `zero copy bytes` (descriptors, input and
  * output) is copied into the layer's pinned, mapped staging, which the kernel reads and writes over PCIe (one
  * launch, one synchronisation); larger windows move by one H2D and one D2H DMA copy.  Results are identical. */
 /* registers host memory [base, base+len) that stays allocated (a connection's socket buffers) for direct calls
@@ -399,6 +421,11 @@ int ptls_mi355x_record_layer_register(ptls_mi355x_record_layer_t *rl, void *base
 /* unregisters a range given to ptls_mi355x_record_layer_register (by its base); 0 or -1.  The layer unregisters
  * its ranges when freed. */
 int ptls_mi355x_record_layer_unregister(ptls_mi355x_record_layer_t *rl, void *base);
+/* windows whose buffers are all registered: 0 (default) has the kernels read the inputs in place over PCIe and write
+ * the outputs into the registered ranges (a sealed window whose fragments overlap its output goes through the
+ * staging instead); 1 moves them by DMA copies between the registered ranges and device memory around a
+ * device-resident launch (measured slower: DESIGN.md section 2).  Results are identical.  Returns the previous value. */
+int ptls_mi355x_record_layer_set_direct_dma(ptls_mi355x_record_layer_t *rl, int on);
 /* zero-copy limit in bytes (default 4 MiB; 0 = always DMA copies); returns the previous value */
 size_t ptls_mi355x_record_layer_set_zero_copy_bytes(ptls_mi355x_record_layer_t *rl, size_t n);
 

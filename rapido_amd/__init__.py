@@ -69,6 +69,7 @@ EXPORTED_FUNCTIONS = (
     "ptls_mi355x_record_layer_seal_multi", "ptls_mi355x_record_layer_open_multi",
     "ptls_mi355x_record_layer_open_record", "ptls_mi355x_record_layer_rekey", "ptls_mi355x_record_layer_seal_submit",
     "ptls_mi355x_record_layer_open_submit", "ptls_mi355x_record_layer_wait", "ptls_mi355x_record_layer_pending",
+    "ptls_mi355x_record_layer_set_direct_dma", "ptls_mi355x_tls_deliver_records",
 )
 EXPORTED_OBJECTS = ("ptls_mi355x_aes128gcm", "ptls_mi355x_aes256gcm", "ptls_mi355x_aes128ctr",
                     "ptls_mi355x_aes256ctr", "ptls_mi355x_aes128ecb", "ptls_mi355x_aes256ecb")
@@ -182,6 +183,7 @@ def lib() -> C.CDLL:
             L.ptls_mi355x_record_layer_wait.argtypes = [vp, u64, vp, vp, vp, vp]
             L.ptls_mi355x_record_layer_pending.argtypes = [vp]
             L.ptls_mi355x_record_layer_pending.restype = sz
+            L.ptls_mi355x_record_layer_set_direct_dma.argtypes = [vp, C.c_int]
         for name in ("ptls_mi355x_set_win16_records", "ptls_mi355x_set_split_records"):
             if hasattr(L, name):  # (absent from older builds used in A/B timing runs)
                 getattr(L, name).argtypes = [sz]
@@ -518,6 +520,10 @@ class RecordLayer:
         if rc < 0:
             raise RuntimeError("record_layer_open failed: " + lib().ptls_mi355x_record_layer_last_error().decode())
         return rc, out.raw[:olen.value], cons.value, nrec.value
+
+    def set_direct_dma(self, on: bool) -> bool:
+        """Registered windows by DMA to and from device memory (True) or read in place by the kernels (False, default)."""
+        return bool(lib().ptls_mi355x_record_layer_set_direct_dma(self.handle, 1 if on else 0))
 
     def set_zero_copy_bytes(self, n: int) -> int:
         """Windows of at most n staged bytes run zero-copy on the pinned staging (0: DMA copies); -> previous."""

@@ -64,7 +64,7 @@ def build_engine(verbose: bool = False, force: bool = False) -> str:
              verbose)
     for c_src, c_obj in zip(C_SRCS, C_OBJS):
         if force or _newer(c_obj, [c_src] + HEADERS):
-            _run([CC, "-std=gnu99", "-O2", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter", "-D__HIP_PLATFORM_AMD__",
+            _run([CC, "-std=gnu99", "-O2", "-g", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter", "-D__HIP_PLATFORM_AMD__",
                   "-I" + ROCM_INCLUDE, "-c", c_src, "-o", c_obj], verbose)
     if force or _newer(LIB, [hip_obj] + C_OBJS):
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, hip_obj] + C_OBJS, verbose)
@@ -87,7 +87,7 @@ def build_rl_stream(verbose: bool = False, force: bool = False) -> str:
     """The C driver of bench.py's record_layer_stream (measurement, not part of the product)."""
     os.makedirs(os.path.dirname(RL_STREAM), exist_ok=True)
     if force or _newer(RL_STREAM, [RL_STREAM_SRC, LIB] + HEADERS):
-        _run([CC, "-std=gnu99", "-O2", "-Wall", "-o", RL_STREAM, RL_STREAM_SRC, "-L" + LIBDIR, "-lptls_mi355x",
+        _run([CC, "-std=gnu99", "-O2", "-g", "-rdynamic", "-Wall", "-o", RL_STREAM, RL_STREAM_SRC, "-L" + LIBDIR, "-lptls_mi355x",
               "-Wl,-rpath,$ORIGIN/../../rapido_amd/_lib"], verbose)
     return RL_STREAM
 

@@ -1170,6 +1170,90 @@ extern "C" __global__ void mi355x_tls_truncate(const TlsRecord *__restrict__ rec
     }
 }
 
+/*
+ * Delivery of opened records (ptls_mi355x_tls_deliver_records): picotls' receive loop on the device.  Workgroup
+ * (part, g) of a part's records [k0, k0 + n): thread 0 walks them in order as handle_input does -- stop at the first
+ * failed record, at the first record of another inner content type (unless any_type: then one record of any type),
+ * or at the first one that would overflow the capacity -- and the delivered records' plaintexts are copied back to
+ * back into out, record i by the groups with i % gridDim.y == g.  The slots (plaintext, type, padding, as the open
+ * kernels leave them) are read from `slots`; out is written once, at the compact offsets (no host memmove).  Parts
+ * of more than DELIVER_MAX records are not handled here (the host falls back to its own loop).
+ */
+constexpr uint32_t DELIVER_MAX = PTLS_MI355X_DELIVER_MAX;
+
+struct DeliverPart {
+    const uint8_t *slots; /* record i's slot at slots + recs[i].dst */
+    uint8_t *out;
+    uint64_t capacity;
+    uint32_t k0, n, any_type, pad_;
+};
+static_assert(sizeof(DeliverPart) == sizeof(ptls_mi355x_tls_deliver_t), "delivery layout");
+
+/* dst[0, len) <- src[0, len) by one workgroup: 16-byte accesses when src and dst share their alignment mod 16 (slots
+ * 16-aligned, plaintexts of whole 16-B blocks), else 4-byte stores from aligned source dwords (v_alignbyte) */
+__device__ __forceinline__ void copy_bytes(uint8_t *dst, const uint8_t *src, uint32_t len, uint32_t tid, uint32_t nthr)
+{
+    const uint32_t a = (uint32_t)((uintptr_t)dst & 15u);
+    if (a == (uint32_t)((uintptr_t)src & 15u)) {
+        const uint32_t head = ((16u - a) & 15u) < len ? ((16u - a) & 15u) : len;
+        if (tid < head)
+            dst[tid] = src[tid];
+        const uint32_t body = (len - head) / 16u, tail0 = head + 16u * body;
+        const u32x4 *s4 = (const u32x4 *)(src + head);
+        u32x4 *d4 = (u32x4 *)(dst + head);
+        for (uint32_t w = tid; w < body; w += nthr)
+            d4[w] = s4[w];
+        if (tid < len - tail0)
+            dst[tail0 + tid] = src[tail0 + tid];
+        return;
+    }
+    const uint32_t head = ((4u - (a & 3u)) & 3u) < len ? ((4u - (a & 3u)) & 3u) : len;
+    if (tid < head)
+        dst[tid] = src[tid];
+    const uint32_t body = (len - head) / 4u, tail0 = head + 4u * body;
+    const uint8_t *s = src + head;
+    const uint32_t sh = (uint32_t)((uintptr_t)s & 3u);
+    const uint32_t *sa = (const uint32_t *)(s - sh);
+    uint32_t *d = (uint32_t *)(dst + head);
+    for (uint32_t w = tid; w < body; w += nthr) {
+        const uint32_t lo = sa[w];
+        const uint32_t hi = sh ? sa[w + 1] : 0u; /* (inside the slot: the type byte follows the plaintext) */
+        d[w] = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
+    }
+    if (tid < len - tail0)
+        dst[tail0 + tid] = src[tail0 + tid];
+}
+
+extern "C" __global__ __launch_bounds__(256) void mi355x_tls_deliver(const TlsRecord *__restrict__ recs,
+                                                                      const uint32_t *__restrict__ status,
+                                                                      const uint8_t *__restrict__ types,
+                                                                      const DeliverPart *__restrict__ parts)
+{
+    __shared__ uint32_t off[DELIVER_MAX + 1];
+    __shared__ uint32_t ndone;
+    const DeliverPart p = parts[blockIdx.x];
+    if (threadIdx.x == 0) {
+        uint32_t o = 0u, i = 0u;
+        for (; i < p.n && i < DELIVER_MAX; ++i) {
+            const uint32_t st = status[p.k0 + i];
+            if (st >= PTLS_MI355X_TLS_NOT_PROCESSED || (!p.any_type && types[p.k0 + i] != 23u) ||
+                (uint64_t)o + st > p.capacity)
+                break;
+            off[i] = o;
+            o += st;
+            if (p.any_type) {
+                ++i;
+                break;
+            }
+        }
+        off[i] = o;
+        ndone = i;
+    }
+    __syncthreads();
+    for (uint32_t i = blockIdx.y; i < ndone; i += gridDim.y)
+        copy_bytes(p.out + off[i], p.slots + recs[p.k0 + i].dst, off[i + 1] - off[i], threadIdx.x, blockDim.x);
+}
+
 /* keys = GHASH steps of each record (its work), values = record index */
 extern "C" __global__ void mi355x_sort_keys(const Record *__restrict__ recs, uint32_t n, uint32_t *keys, uint32_t *vals)
 {
@@ -1866,6 +1950,24 @@ int ptls_mi355x_tls_open_records_ex(ptls_mi355x_aesgcm_context_t *ctx, const voi
                                                       hipcub::Equality(), stream));
     hipLaunchKernelGGL(mi355x_tls_truncate, dim3(g), dim3(256), 0, stream, (const TlsRecord *)recs, (uint32_t)n, first,
                        dst, status, types);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int ptls_mi355x_tls_deliver_records(ptls_mi355x_aesgcm_context_t *ctx, const ptls_mi355x_tls_record_t *recs,
+                                    const uint32_t *status, const uint8_t *types, const ptls_mi355x_tls_deliver_t *parts,
+                                    size_t nparts, size_t max_records, void *stream_)
+{
+    if (nparts == 0)
+        return 0;
+    if (max_records > DELIVER_MAX || nparts > 65535) {
+        snprintf(g_err, sizeof(g_err), "deliver: more than %u records in a part, or too many parts", DELIVER_MAX);
+        return -1;
+    }
+    DeviceGuard guard(ctx->device);
+    unsigned groups = (unsigned)(max_records < 64 ? (max_records ? max_records : 1) : 64); /* a record per group */
+    hipLaunchKernelGGL(mi355x_tls_deliver, dim3((unsigned)nparts, groups), dim3(256), 0, (hipStream_t)stream_,
+                       (const TlsRecord *)recs, status, types, (const DeliverPart *)parts);
     HIPCHK(hipGetLastError());
     return 0;
 }

@@ -32,9 +32,13 @@
  *
  * Where the bytes travel, per window (the first that applies):
  *   direct     -- the fragments and the output (seal), or the input and the output (open), all lie in host ranges
- *                 the caller registered (ptls_mi355x_record_layer_register: long-lived socket buffers) and the
- *                 inputs do not overlap the outputs: the kernel reads and writes them in place over PCIe.  Only the
- *                 descriptors (and statuses) pass through the slot's staging.  No copy at all.
+ *                 the caller registered (ptls_mi355x_record_layer_register: long-lived socket buffers): the kernel
+ *                 reads the input in place over PCIe.  Seal writes the wire records in place (inputs overlapping the
+ *                 outputs go through the staging instead); open leaves the plaintext slots in device memory and the
+ *                 delivery kernel (ptls_mi355x_tls_deliver_records) writes the delivered plaintexts once, back to
+ *                 back, into the caller's buffer.  Only descriptors and statuses pass through the slot's staging.
+ *                 ptls_mi355x_record_layer_set_direct_dma(rl, 1) moves registered windows by DMA copies to and from
+ *                 device memory instead (measured slower).
  *   zero-copy  -- the window fits the zero-copy limit: fragments / input are copied into the slot's pinned,
  *                 mapped, coherent staging and the kernel works on it over PCIe.
  *   copy       -- larger windows: staging -> one H2D copy -> launch -> one D2H copy (DMA at the link rate).
@@ -64,12 +68,19 @@ typedef struct {
     int stopped;         /* stopped at the limit */
     /* open */
     size_t k0, n, cons, ptbytes; /* descriptors recs[k0 .. k0 + n), wire bytes parsed, plaintext slot bytes */
+    size_t slots16;              /* the slot bytes with every slot 16-aligned (delivery kernel) */
     uint64_t src_add, dst_add;   /* added to its descriptors' offsets (its position in the launch's src / dst) */
     int perr;
     /* both */
     uint64_t seq0; /* seq of its first record */
     size_t nrec;   /* records in the launch */
 } rl_part_t;
+
+typedef struct {
+    void *dst;
+    const void *src;
+    size_t n;
+} rl_copy_t;
 
 typedef struct {
     int busy, is_seal, any_type; /* any_type: open_record (one record of any inner content type) */
@@ -79,8 +90,11 @@ typedef struct {
     void **out;
     size_t *capacity;
     rl_part_t *part;
-    int direct, zero_copy;
-    size_t nrec, off_src, srcbytes, off_dst, dstbytes, off_st, off_ty;
+    int direct, zero_copy, dma; /* direct: the results land in the caller's buffers (mapped or dma) */
+    int deliver;                /* mapped open: slots in device memory, the delivery kernel writes the plaintexts */
+    size_t nrec, off_src, srcbytes, off_dst, dstbytes, off_st, off_ty, off_dp, max_part;
+    rl_copy_t *h2d, *d2h; /* dma: registered host ranges <-> the slot's device buffer */
+    size_t nh2d, nd2h;
 } rl_op_t;
 
 typedef struct {
@@ -103,6 +117,7 @@ struct st_ptls_mi355x_record_layer_t {
     uint64_t seq;      /* seal: the next record's seq; open: the seq of the next record to deliver */
     uint64_t spec_seq; /* open: the seq of the next record to submit (ahead of seq while windows are in flight) */
     size_t zero_copy_bytes;
+    int direct_dma; /* registered windows move by DMA to and from device memory (1) or are read in place (0, default) */
     rl_region_t reg[RL_MAX_REGIONS];
     size_t nreg;
     rl_slot_t slot[RL_SLOTS];
@@ -110,6 +125,8 @@ struct st_ptls_mi355x_record_layer_t {
 };
 
 static char rl_err[160];
+
+static void op_discard(rl_op_t *op);
 
 static size_t up16(size_t x) { return (x + 15) & ~(size_t)15; }
 
@@ -241,6 +258,7 @@ ptls_mi355x_record_layer_t *ptls_mi355x_record_layer_new(const void *key, size_t
     memcpy(rl->iv, iv12, 12);
     rl->seq = rl->spec_seq = seq;
     rl->zero_copy_bytes = RL_ZERO_COPY_DEFAULT;
+    rl->direct_dma = 0;
     if (slot_ready(rl, &rl->slot[0]) != 0) { /* the key is set up now: errors surface here, not at the first window */
         slot_release(&rl->slot[0]);
         memset(rl->key, 0, sizeof(rl->key));
@@ -258,10 +276,8 @@ void ptls_mi355x_record_layer_free(ptls_mi355x_record_layer_t *rl)
         (void)ptls_mi355x_record_layer_unregister(rl, rl->reg[rl->nreg - 1].base);
     for (int i = 0; i < RL_SLOTS; ++i) {
         rl_op_t *op = &rl->slot[i].op;
-        if (op->busy) { /* never waited: completes here, its results dropped */
-            free(op->layers);
-            memset(op, 0, sizeof(*op));
-        }
+        if (op->busy) /* never waited: completes here, its results dropped */
+            op_discard(op);
         slot_release(&rl->slot[i]);
     }
     memset(rl->key, 0, sizeof(rl->key));
@@ -304,6 +320,13 @@ int ptls_mi355x_record_layer_rekey(ptls_mi355x_record_layer_t *rl, const void *k
     memcpy(rl->iv, iv12, 12);
     rl->seq = rl->spec_seq = 0; /* a new traffic key starts at record 0 (setup_traffic_protection, lib/picotls.c:1217) */
     return 0;
+}
+
+int ptls_mi355x_record_layer_set_direct_dma(ptls_mi355x_record_layer_t *rl, int on)
+{
+    const int prev = rl->direct_dma;
+    rl->direct_dma = on != 0;
+    return prev;
 }
 
 size_t ptls_mi355x_record_layer_set_zero_copy_bytes(ptls_mi355x_record_layer_t *rl, size_t n)
@@ -420,6 +443,7 @@ static rl_slot_t *op_begin(ptls_mi355x_record_layer_t *const *layers, size_t nla
 
 static void op_discard(rl_op_t *op)
 {
+    free(op->h2d);
     free(op->layers);
     memset(op, 0, sizeof(*op));
 }
@@ -434,21 +458,48 @@ static void op_commit(rl_slot_t *s, uint64_t *ticket)
         *ticket = s->op.ticket;
 }
 
-/* H2D (copy windows), the launch, D2H: everything on the slot's stream */
+/* a copy list of up to n entries (dma windows: one allocation for both directions) */
+static int op_copies(rl_op_t *op, size_t n)
+{
+    if ((op->h2d = calloc(2 * n, sizeof(rl_copy_t))) == NULL)
+        return rl_msg("out of memory");
+    op->d2h = op->h2d + n;
+    return 0;
+}
+
+/* host -> device copy of [src, src + n) to dst, merged with the previous one when both are contiguous */
+static void op_h2d(rl_op_t *op, void *dst, const void *src, size_t n)
+{
+    rl_copy_t *c = op->nh2d != 0 ? &op->h2d[op->nh2d - 1] : NULL;
+    if (c != NULL && (const uint8_t *)c->src + c->n == (const uint8_t *)src && (uint8_t *)c->dst + c->n == (uint8_t *)dst)
+        c->n += n;
+    else if (n != 0)
+        op->h2d[op->nh2d++] = (rl_copy_t){dst, src, n};
+}
+
+/*
+ * H2D, the launch, D2H, everything on the slot's stream.  zero-copy: the kernel works on the pinned staging; copy: the
+ * staging moves to the device buffer and back; mapped: descriptors from the staging, data in place in registered host
+ * memory; dma: descriptors and the registered inputs to the device buffer, the outputs back into the registered
+ * ranges (statuses and types of an open into the staging).
+ */
 static int op_launch(rl_slot_t *s, const uint8_t *src_base, uint8_t *dst_base)
 {
     rl_op_t *op = &s->op;
-    ptls_mi355x_record_layer_t *rl = op->layers[0];
     uint8_t *base = op->zero_copy ? s->h_dev : s->d_buf;
-    const uint8_t *src = op->direct ? src_base : base + op->off_src;
-    uint8_t *dst = op->direct ? dst_base : base + op->off_dst;
+    const int mapped = op->direct && !op->dma;
+    const uint8_t *src = mapped ? src_base : base + op->off_src;
+    uint8_t *dst = op->deliver ? s->d_buf + op->off_dst : mapped ? dst_base : base + op->off_dst;
     const uint32_t *conn = op->nlayers > 1 ? (const uint32_t *)(base + up16(op->nrec * sizeof(ptls_mi355x_tls_record_t))) : NULL;
     hipError_t e;
     int rc;
     if (!op->zero_copy &&
-        (e = hipMemcpyAsync(s->d_buf, s->h_buf, op->off_src + op->srcbytes, hipMemcpyHostToDevice, s->stream)) != hipSuccess)
+        (e = hipMemcpyAsync(s->d_buf, s->h_buf, op->dma ? op->off_src : op->off_src + op->srcbytes, hipMemcpyHostToDevice,
+                            s->stream)) != hipSuccess)
         return rl_fail("H2D", e);
-    (void)rl;
+    for (size_t i = 0; i < op->nh2d; ++i)
+        if ((e = hipMemcpyAsync(op->h2d[i].dst, op->h2d[i].src, op->h2d[i].n, hipMemcpyHostToDevice, s->stream)) != hipSuccess)
+            return rl_fail("H2D", e);
     if (op->is_seal)
         rc = ptls_mi355x_tls_seal_records_multi(s->ctx, op->layers[0]->iv, (const ptls_mi355x_tls_record_t *)base, conn,
                                                 op->nrec, src, dst, s->stream);
@@ -456,11 +507,20 @@ static int op_launch(rl_slot_t *s, const uint8_t *src_base, uint8_t *dst_base)
         rc = ptls_mi355x_tls_open_records_multi(s->ctx, op->layers[0]->iv, (const ptls_mi355x_tls_record_t *)base, conn,
                                                 op->nrec, src, dst, (uint32_t *)(base + op->off_st), base + op->off_ty,
                                                 s->stream);
+    if (rc == 0 && op->deliver)
+        rc = ptls_mi355x_tls_deliver_records(s->ctx, (const ptls_mi355x_tls_record_t *)base, (uint32_t *)(base + op->off_st),
+                                             base + op->off_ty, (const ptls_mi355x_tls_deliver_t *)(base + op->off_dp),
+                                             op->nlayers, op->max_part, s->stream);
     if (rc != 0)
         return rl_msg(ptls_mi355x_last_error());
-    if (!op->zero_copy) {
-        const size_t from = op->off_dst, to = op->is_seal ? op->off_dst + op->dstbytes : op->off_ty + op->nrec;
-        if ((e = hipMemcpyAsync(s->h_buf + from, s->d_buf + from, to - from, hipMemcpyDeviceToHost, s->stream)) != hipSuccess)
+    for (size_t i = 0; i < op->nd2h; ++i)
+        if ((e = hipMemcpyAsync(op->d2h[i].dst, op->d2h[i].src, op->d2h[i].n, hipMemcpyDeviceToHost, s->stream)) != hipSuccess)
+            return rl_fail("D2H", e);
+    if (!op->zero_copy && !(op->dma && op->is_seal)) {
+        const size_t from = op->dma ? op->off_st : op->off_dst;
+        const size_t to = op->is_seal ? op->off_dst + op->dstbytes : op->off_ty + op->nrec;
+        if (to > from &&
+            (e = hipMemcpyAsync(s->h_buf + from, s->d_buf + from, to - from, hipMemcpyDeviceToHost, s->stream)) != hipSuccess)
             return rl_fail("D2H", e);
     }
     return 0;
@@ -530,10 +590,12 @@ int ptls_mi355x_record_layer_seal_submit(ptls_mi355x_record_layer_t *const *laye
     }
     if (reserve_recs(s, nrec) != 0)
         goto Fail;
-    /* direct: every sealed fragment and every output in registered ranges, no fragment overlapping an output;
-     * addressed from the lowest of each */
+    /* direct: every sealed fragment and every output in registered ranges; addressed from the lowest of each.  In
+     * place (mapped) only when no fragment overlaps an output: the kernel would overwrite fragment bytes another
+     * workgroup still reads.  dma windows copy the fragments to the device first, so overlap is harmless there. */
     uint8_t *src_base = NULL, *dst_base = NULL;
-    int direct = 1;
+    int direct = 1, overlap = 0;
+    size_t nfr = 0;
     for (size_t l = 0; direct && l < nlayers; ++l) {
         uint8_t *d = op->part[l].wire != 0 ? dev_addr_any(layers, nlayers, out[l], op->part[l].wire) : NULL;
         if (op->part[l].wire != 0 && d == NULL)
@@ -541,26 +603,31 @@ int ptls_mi355x_record_layer_seal_submit(ptls_mi355x_record_layer_t *const *laye
         else if (d != NULL && (dst_base == NULL || d < dst_base))
             dst_base = d;
         for (size_t f = 0; direct && f < op->part[l].nfrags; ++f) {
+            ++nfr;
             if (frags[l][f].len == 0)
                 continue;
             if ((d = dev_addr_any(layers, nlayers, frags[l][f].base, frags[l][f].len)) == NULL)
                 direct = 0;
             else if (src_base == NULL || d < src_base)
                 src_base = d;
-            for (size_t m = 0; direct && m < nlayers; ++m)
-                if (overlaps(frags[l][f].base, frags[l][f].len, out[m], op->part[m].wire))
-                    direct = 0; /* the kernel would overwrite fragment bytes another workgroup still reads */
+            for (size_t m = 0; m < nlayers; ++m)
+                overlap |= overlaps(frags[l][f].base, frags[l][f].len, out[m], op->part[m].wire);
         }
     }
+    const int dma = direct && layers[0]->direct_dma;
+    if (direct && !dma && overlap)
+        direct = 0;
+    const int packed = !direct || dma; /* fragments and records back to back in the staging / device layout */
     op->direct = direct;
+    op->dma = dma;
     const size_t off_conn = up16(nrec * sizeof(ptls_mi355x_tls_record_t));
     op->off_src = off_conn + (nlayers > 1 ? up16(nrec * 4) : 0);
-    op->srcbytes = direct ? 0 : srcbytes;
+    op->srcbytes = packed ? srcbytes : 0;
     op->off_dst = op->off_src + up16(op->srcbytes);
-    op->dstbytes = direct ? 0 : wire;
+    op->dstbytes = packed ? wire : 0;
     const size_t total = op->off_dst + up16(op->dstbytes);
-    op->zero_copy = direct || total <= layers[0]->zero_copy_bytes;
-    if (reserve_stage(s, total) != 0 || (!op->zero_copy && reserve_device(s) != 0))
+    op->zero_copy = (direct && !dma) || (!direct && total <= layers[0]->zero_copy_bytes);
+    if (reserve_stage(s, total) != 0 || (!op->zero_copy && reserve_device(s) != 0) || (dma && op_copies(op, nfr + nlayers) != 0))
         goto Fail;
     /* descriptors (offsets relative to the src / dst bases), the per-record IV differences and, unless direct, the
      * fragments back to back */
@@ -569,18 +636,22 @@ int ptls_mi355x_record_layer_seal_submit(ptls_mi355x_record_layer_t *const *laye
     for (size_t l = 0; l < nlayers; ++l) {
         rl_part_t *p = &op->part[l];
         uint64_t sq = p->seq0;
-        if (direct && p->wire != 0)
+        if (!packed && p->wire != 0)
             dst_off = (size_t)(dev_addr_any(layers, nlayers, out[l], p->wire) - dst_base);
+        if (dma && p->wire != 0) /* the layer's wire records, back to the caller's output in one copy */
+            op->d2h[op->nd2h++] = (rl_copy_t){out[l], s->d_buf + op->off_dst + dst_off, p->wire};
         const uint32_t cid = be32(layers[l]->iv) ^ be32(layers[0]->iv); /* BE32(cid) ^ IV[0..3] of layer 0 = layer l's */
         const size_t k0 = k;
         for (size_t f = 0; f < p->nfrags; ++f) {
             const ptls_mi355x_iovec_t *fr = &frags[l][f];
             size_t w = 0;
-            if (direct && fr->len != 0)
+            if (!packed && fr->len != 0)
                 src_off = (size_t)(dev_addr_any(layers, nlayers, fr->base, fr->len) - src_base);
             k += ptls_mi355x_tls_plan_send(fr->len, type, &sq, src_off, dst_off, s->recs + k, nrec - k, &w);
-            if (!direct) {
-                if (fr->len != 0)
+            if (packed) {
+                if (dma)
+                    op_h2d(op, s->d_buf + op->off_src + src_off, fr->base, fr->len);
+                else if (fr->len != 0)
                     memcpy(s->h_buf + op->off_src + src_off, fr->base, fr->len);
                 src_off += fr->len;
             }
@@ -619,7 +690,7 @@ static int open_submit(ptls_mi355x_record_layer_t *const *layers, size_t nlayers
         return -1;
     rl_op_t *op = &s->op;
     op->any_type = any_type;
-    size_t max = 0, nrec = 0, srcbytes = 0, ptbytes = 0;
+    size_t max = 0, nrec = 0, srcbytes = 0, ptbytes = 0, slots16 = 0;
     for (size_t l = 0; l < nlayers; ++l) /* a record takes at least 5 wire bytes */
         max += any_type ? 1 : inlen[l] / PTLS_MI355X_TLS_HEADER_SIZE + 1;
     if (reserve_recs(s, max) != 0)
@@ -639,6 +710,9 @@ static int open_submit(ptls_mi355x_record_layer_t *const *layers, size_t nlayers
             const ptls_mi355x_tls_record_t *last = s->recs + nrec + p->n - 1;
             p->ptbytes = last->dst + (last->len >= 16u ? last->len - 16u : 0u);
         }
+        for (size_t i = nrec; i < nrec + p->n; ++i)
+            p->slots16 += up16(s->recs[i].len >= 16u ? s->recs[i].len - 16u : 0u);
+        slots16 += p->slots16;
         p->nrec = p->n;
         nrec += p->n;
         srcbytes += up16(p->cons);
@@ -655,7 +729,7 @@ static int open_submit(ptls_mi355x_record_layer_t *const *layers, size_t nlayers
      * input overlapping a plaintext buffer (slots are packed tighter than records: an in-place open would overwrite
      * ciphertext another workgroup still reads) */
     uint8_t *src_base = NULL, *dst_base = NULL;
-    int direct = 1;
+    int direct = 1, overlap = 0;
     for (size_t l = 0; direct && l < nlayers; ++l) {
         const rl_part_t *p = &op->part[l];
         if (p->n == 0)
@@ -667,37 +741,72 @@ static int open_submit(ptls_mi355x_record_layer_t *const *layers, size_t nlayers
             break;
         }
         for (size_t m = 0; m < nlayers; ++m)
-            if (overlaps(in[l], p->cons, out[m], op->part[m].ptbytes))
-                direct = 0;
+            overlap |= overlaps(in[l], p->cons, out[m], op->part[m].ptbytes);
         if (src_base == NULL || di < src_base)
             src_base = di;
         if (dst_base == NULL || dout < dst_base)
             dst_base = dout;
     }
+    const int dma = direct && layers[0]->direct_dma; /* (the input reaches the device before any output is written) */
+    size_t max_part = 0;
+    for (size_t l = 0; l < nlayers; ++l)
+        max_part = op->part[l].n > max_part ? op->part[l].n : max_part;
+    /* mapped: the records read in place, their slots in device memory, the delivery kernel writes each plaintext once
+     * to its final place in the caller's buffer; overlapping buffers are harmless then */
+    const int deliver = direct && !dma && max_part <= PTLS_MI355X_DELIVER_MAX;
+    if (direct && !dma && !deliver && overlap)
+        direct = 0;
+    const int packed = !direct || dma;
     op->direct = direct;
+    op->dma = dma;
+    op->deliver = deliver;
+    op->max_part = max_part;
     const size_t off_conn = up16(nrec * sizeof(ptls_mi355x_tls_record_t));
     op->off_src = off_conn + (nlayers > 1 ? up16(nrec * 4) : 0);
-    op->srcbytes = direct ? 0 : srcbytes;
+    op->srcbytes = packed ? srcbytes : 0;
     op->off_dst = op->off_src + op->srcbytes;
-    op->dstbytes = direct ? 0 : ptbytes;
+    op->dstbytes = packed ? ptbytes : deliver ? slots16 : 0;
     op->off_st = op->off_dst + op->dstbytes;
     op->off_ty = op->off_st + up16(nrec * 4);
-    const size_t total = op->off_ty + up16(nrec);
-    op->zero_copy = direct || total <= layers[0]->zero_copy_bytes;
-    if (reserve_stage(s, total) != 0 || (!op->zero_copy && reserve_device(s) != 0))
+    op->off_dp = op->off_ty + up16(nrec);
+    const size_t total = op->off_dp + (deliver ? nlayers * sizeof(ptls_mi355x_tls_deliver_t) : 0);
+    op->zero_copy = (direct && !dma) || (!direct && total <= layers[0]->zero_copy_bytes);
+    if (reserve_stage(s, total) != 0 || ((!op->zero_copy || deliver) && reserve_device(s) != 0) ||
+        (dma && op_copies(op, nlayers) != 0))
         goto Fail;
+    ptls_mi355x_tls_deliver_t *dp = (ptls_mi355x_tls_deliver_t *)(s->h_buf + op->off_dp);
     uint32_t *conn = (uint32_t *)(s->h_buf + off_conn);
     for (size_t l = 0, so = 0, dso = 0; l < nlayers; ++l) {
         rl_part_t *p = &op->part[l];
+        if (deliver)
+            dp[l] = (ptls_mi355x_tls_deliver_t){s->d_buf + op->off_dst, NULL, 0u, (uint32_t)p->k0, 0u, 0u, 0u};
         if (p->n == 0)
             continue;
-        if (direct) {
+        if (deliver) {
+            p->src_add = (uint64_t)(dev_addr_any(layers, nlayers, in[l], p->cons) - src_base);
+            p->dst_add = dso;
+            /* every slot 16-aligned in the device buffer (parse_records packed them): the delivery kernel's copies
+             * of whole-block plaintexts then run on 16-byte accesses */
+            uint64_t at = 0;
+            for (size_t i = p->k0; i < p->k0 + p->n; ++i) {
+                s->recs[i].dst = at;
+                at += up16(s->recs[i].len >= 16u ? s->recs[i].len - 16u : 0u);
+            }
+            dp[l] = (ptls_mi355x_tls_deliver_t){s->d_buf + op->off_dst, dev_addr_any(layers, nlayers, out[l], p->ptbytes),
+                                                 capacity[l], (uint32_t)p->k0, (uint32_t)p->n, (uint32_t)any_type, 0u};
+            dso += p->slots16;
+        } else if (!packed) {
             p->src_add = (uint64_t)(dev_addr_any(layers, nlayers, in[l], p->cons) - src_base);
             p->dst_add = (uint64_t)(dev_addr_any(layers, nlayers, out[l], p->ptbytes) - dst_base);
         } else {
             p->src_add = so;
             p->dst_add = dso;
-            memcpy(s->h_buf + op->off_src + so, in[l], p->cons);
+            if (dma) { /* the records in, the plaintext slots straight back into the caller's buffer */
+                op_h2d(op, s->d_buf + op->off_src + so, in[l], p->cons);
+                op->d2h[op->nd2h++] = (rl_copy_t){out[l], s->d_buf + op->off_dst + dso, p->ptbytes};
+            } else {
+                memcpy(s->h_buf + op->off_src + so, in[l], p->cons);
+            }
             so += up16(p->cons);
             dso += up16(p->ptbytes);
         }
@@ -786,8 +895,9 @@ static void finish_open(rl_slot_t *s, size_t *outlen, size_t *nrecords, size_t *
                     }
                     break;
                 }
-                /* direct: slot i starts at or after olen, so the delivered plaintexts close up in place */
-                memmove((uint8_t *)op->out[l] + olen, slots + (s->recs[i].dst - p->dst_add), status[i]);
+                /* delivered by the kernel; direct: slot i starts at or after olen, so the plaintexts close up in place */
+                if (!op->deliver)
+                    memmove((uint8_t *)op->out[l] + olen, slots + (s->recs[i].dst - p->dst_add), status[i]);
                 olen += status[i];
                 wire_done += PTLS_MI355X_TLS_HEADER_SIZE + s->recs[i].len;
                 if (type != NULL)
@@ -796,7 +906,7 @@ static void finish_open(rl_slot_t *s, size_t *outlen, size_t *nrecords, size_t *
             }
             x->seq += done;
         }
-        if (p->n != 0) {
+        if (p->n != 0 && !op->deliver) {
             if (op->direct)
                 memset((uint8_t *)op->out[l] + olen, 0, p->ptbytes - olen); /* padding, types, records not delivered */
             else

@@ -7,6 +7,11 @@ Writes
   profiles/<label>_bench.jsonl        the bench lines of that run (all workloads)
   profiles/<label>_pmc.json           PMC per kernel: FETCH_SIZE / WRITE_SIZE (separate passes) and SQ counters
   profiles/pmc_traffic.json           HBM bytes per launch for bench.py's roofline.traffic
+  profiles/<label>_launches.json      per-dispatch durations of the engine kernels in every kernel-trace run, the
+                                      warmup launches dropped: mean / median / min of the timed launches, and
+                                      roofline.frac recomputed from them against the bench line's
+  profiles/held_clock.json            the clock held under each kernel: GRBM_GUI_ACTIVE / 8 over the dispatch time
+                                      of the PMC pass (bench.py's lds_roofline.peak_held)
 
 HBM bytes = 2 x FETCH_SIZE x 1024 + WRITE_SIZE x 1024: on gfx950 FETCH_SIZE reports half the bytes of
 a wide (16 B/lane) streaming read and WRITE_SIZE is exact for 16 B/lane stores
@@ -20,6 +25,8 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from bench import WORKLOADS  # noqa: E402  (bench.py imports nothing heavy at module level)
 
 
 def counters(path):
@@ -28,6 +35,36 @@ def counters(path):
         if "mi355x_" in r["Kernel_Name"]:
             agg[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in agg.items()}
+
+
+def launches(trace_csv, warmup):
+    """kernel -> durations (ms) of its dispatches in order, from a rocprofv3 --kernel-trace CSV"""
+    d = collections.defaultdict(list)
+    for r in csv.DictReader(open(trace_csv)):
+        if r["Kernel_Name"].startswith("mi355x_"):
+            d[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6)
+    out = {}
+    for k, v in d.items():
+        t = sorted(v[warmup:]) if len(v) > warmup else sorted(v)
+        out[k] = {"dispatches": len(v), "warmup_dropped": len(v) - len(t), "timed_mean_ms": round(sum(t) / len(t), 4),
+                  "timed_median_ms": round(t[len(t) // 2], 4), "timed_min_ms": round(t[0], 4),
+                  "all_ms": [round(x, 4) for x in v]}
+    return out
+
+
+def held_cycles(counter_csv, warmup):
+    """kernel -> (median GRBM_GUI_ACTIVE / 8 = GPU-busy cycles of one XCD per dispatch, median clock over the
+    profiled dispatch time in GHz), timed dispatches"""
+    d = collections.defaultdict(list)
+    for r in csv.DictReader(open(counter_csv)):
+        if r["Kernel_Name"].startswith("mi355x_") and r["Counter_Name"] == "GRBM_GUI_ACTIVE":
+            dt = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            d[r["Kernel_Name"]].append((float(r["Counter_Value"]) / 8.0, float(r["Counter_Value"]) / 8.0 / dt))
+    out = {}
+    for k, v in d.items():
+        t = v[warmup:] or v
+        out[k] = (sorted(x[0] for x in t)[len(t) // 2], sorted(x[1] for x in t)[len(t) // 2])
+    return out
 
 
 def main(tag, label):
@@ -88,6 +125,56 @@ def main(tag, label):
                    "kernels": pmc, "other_workloads": others, "sq_16k-aes128": sq16}, f, indent=1)
     with open(tpath, "w") as f:
         json.dump(allt, f, indent=1)
+    # per-launch durations (warmups dropped) and roofline.frac recomputed against the bench lines
+    lines = {}
+    for name in ("bench_1400.json", "bench_other.jsonl"):
+        p = os.path.join(src, name)
+        if os.path.exists(p):
+            for line in open(p):
+                if line.strip().startswith("{"):
+                    b = json.loads(line)
+                    lines[b["config"]["workload"]] = b
+    name_of = {"1400": "trace", "16k": "trace_16k", "16k-aes128": "trace_16k-aes128", "ragged": "trace_ragged"}
+    la = {}
+    for w, d in name_of.items():
+        p = os.path.join(src, d, "run_kernel_trace.csv")
+        if not os.path.exists(p):
+            continue
+        ent = {"launches": launches(p, 3 if w == "1400" else 2), "trace": f"gpurun_out/{tag}/{d}"}
+        line = lines.get(WORKLOADS[w]["name"])
+        if line is not None:
+            rf = line["roofline"]
+            k = ent["launches"].get(rf["kernel"])
+            if k is not None:
+                ent["roofline_from_profile"] = {
+                    "kernel": rf["kernel"], "algorithmic_bytes_per_launch": rf["algorithmic_bytes_per_launch"],
+                    "frac_timed_mean": round(rf["algorithmic_bytes_per_launch"] / (k["timed_mean_ms"] * 1e-3) / 1e9 / rf["peak"], 4),
+                    "frac_timed_median": round(rf["algorithmic_bytes_per_launch"] / (k["timed_median_ms"] * 1e-3) / 1e9 / rf["peak"], 4),
+                    "bench_line_frac": rf["frac"], "bench_line_launch_ms": rf["launch_ms"]}
+        la[w] = ent
+    with open(os.path.join(dst, f"{label}_launches.json"), "w") as f:
+        json.dump(la, f, indent=1)
+    hc = {}
+    for w, d in (("1400", "pmc_sq"), ("16k-aes128", "pmc_sq_16k-aes128")):
+        p = os.path.join(src, d, "run_counter_collection.csv")
+        line = lines.get(WORKLOADS[w]["name"])
+        if os.path.exists(p):
+            hc[w] = {}
+            for k, (cyc, ghz_prof) in held_cycles(p, 1).items():
+                # the kernel's busy cycles over its UN-profiled launch time (the bench line's HIP events): the clock
+                # the chip holds in the benchmark itself; the profiled dispatches run slower (counter collection)
+                if line is not None and line["roofline"]["kernel"] == k:
+                    ghz, how = cyc / (line["roofline"]["launch_ms"] * 1e6), "GRBM_GUI_ACTIVE / 8 / bench launch_ms"
+                else:
+                    ghz, how = ghz_prof, "GRBM_GUI_ACTIVE / 8 / profiled dispatch time"
+                hc[w][k] = {"ghz": round(ghz, 3), "ghz_profiled_dispatch": round(ghz_prof, 3),
+                            "source": f"profiles/{label}_pmc.json ({how})"}
+    if hc:
+        hpath = os.path.join(dst, "held_clock.json")
+        allh = json.load(open(hpath)) if os.path.exists(hpath) else {}
+        allh.update(hc)
+        with open(hpath, "w") as f:
+            json.dump(allh, f, indent=1)
     print(json.dumps(pmc, indent=1))
 
 

@@ -17,7 +17,7 @@ typedef float v16f __attribute__((ext_vector_type(16)));
 typedef float v4f __attribute__((ext_vector_type(4)));
 
 extern "C" __global__ __launch_bounds__(64) void isa_layout(const uint32_t *a, const uint32_t *b, const uint32_t *sa,
-                                                          const uint32_t *sb, float *c32, float *c16)
+                                                          const uint32_t *sb, float *c32, float *c16, float *c32u)
 {
     const int l = threadIdx.x;
     v8i A = {(int)a[4 * l], (int)a[4 * l + 1], (int)a[4 * l + 2], (int)a[4 * l + 3], 0, 0, 0, 0};
@@ -26,6 +26,11 @@ extern "C" __global__ __launch_bounds__(64) void isa_layout(const uint32_t *a, c
     acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(A, B, acc, 4, 4, 0, (int)sa[l], 0, (int)sb[l]);
     for (int i = 0; i < 16; ++i)
         c32[16 * l + i] = acc[i];
+    /* immediate zero scales: hipcc selects the unscaled v_mfma_f32_32x32x64_f8f6f4 */
+    v16f accu = {};
+    accu = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(A, B, accu, 4, 4, 0, 0, 0, 0);
+    for (int i = 0; i < 16; ++i)
+        c32u[16 * l + i] = accu[i];
     v4f acc2 = {};
     acc2 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(A, B, acc2, 4, 4, 0, (int)sa[l], 0, (int)sb[l]);
     for (int i = 0; i < 4; ++i)
@@ -40,7 +45,7 @@ __device__ __forceinline__ void fill(uint32_t (&x)[8])
         asm volatile("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "+v"(x[i & 7]) : "v"(x[(i + 1) & 7]), "v"(x[(i + 2) & 7]));
 }
 
-template <int NV, bool M16>
+template <int NV, bool M16, int SC = 127>
 __device__ void rate_body(const uint32_t *in, uint64_t *out, int iters)
 {
     const int l = threadIdx.x & 63;
@@ -64,13 +69,13 @@ __device__ void rate_body(const uint32_t *in, uint64_t *out, int iters)
             b3 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(A, B, b3, 4, 4, 0, 127, 0, 127);
             fill<NV>(x);
         } else {
-            a0 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(A, B, a0, 4, 4, 0, 127, 0, 127);
+            a0 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(A, B, a0, 4, 4, 0, SC, 0, SC);
             fill<NV>(x);
-            a1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(A, B, a1, 4, 4, 0, 127, 0, 127);
+            a1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(A, B, a1, 4, 4, 0, SC, 0, SC);
             fill<NV>(x);
-            a2 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(A, B, a2, 4, 4, 0, 127, 0, 127);
+            a2 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(A, B, a2, 4, 4, 0, SC, 0, SC);
             fill<NV>(x);
-            a3 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(A, B, a3, 4, 4, 0, 127, 0, 127);
+            a3 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(A, B, a3, 4, 4, 0, SC, 0, SC);
             fill<NV>(x);
         }
     }
@@ -114,6 +119,16 @@ RATE(8, 1)
     {                                                                                                                  \
         rate_body<NV, false>(in, out, iters);                                                                          \
     }
+/* the unscaled form (v_mfma_f32_32x32x64_f8f6f4: immediate zero scales) */
+#define RATE4U(NV)                                                                                                     \
+    extern "C" __global__ __launch_bounds__(1024) void isa_rate4u_##NV(const uint32_t *in, uint64_t *out, int iters)  \
+    {                                                                                                                  \
+        rate_body<NV, false, 0>(in, out, iters);                                                                       \
+    }
+RATE4U(0)
+RATE4U(8)
+RATE4U(16)
+RATE4U(32)
 RATE4(0)
 RATE4(4)
 RATE4(8)
@@ -145,10 +160,10 @@ extern "C" __global__ __launch_bounds__(1024) void isa_valu_only(const uint32_t 
 }
 
 /* ------------------------------------------------------------------ host entry points ---- */
-extern "C" int run_layout(const void *a, const void *b, const void *sa, const void *sb, void *c32, void *c16)
+extern "C" int run_layout(const void *a, const void *b, const void *sa, const void *sb, void *c32, void *c16, void *c32u)
 {
     hipLaunchKernelGGL(isa_layout, dim3(1), dim3(64), 0, 0, (const uint32_t *)a, (const uint32_t *)b,
-                       (const uint32_t *)sa, (const uint32_t *)sb, (float *)c32, (float *)c16);
+                       (const uint32_t *)sa, (const uint32_t *)sb, (float *)c32, (float *)c16, (float *)c32u);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess)
         e = hipDeviceSynchronize();
@@ -160,7 +175,8 @@ extern "C" const char *err_str(int e) { return hipGetErrorString((hipError_t)e);
 extern "C" int run_rate4(int nv, const void *in, void *out, int iters, int blocks)
 {
     typedef void (*kern_t)(const uint32_t *, uint64_t *, int);
-    kern_t k = nv < 0 ? isa_valu_only : nv == 0 ? isa_rate4_0 : nv == 4 ? isa_rate4_4 : nv == 8 ? isa_rate4_8 :
+    kern_t k = nv == 1000 ? isa_rate4u_0 : nv == 1008 ? isa_rate4u_8 : nv == 1016 ? isa_rate4u_16 : nv == 1032 ? isa_rate4u_32 :
+               nv < 0 ? isa_valu_only : nv == 0 ? isa_rate4_0 : nv == 4 ? isa_rate4_4 : nv == 8 ? isa_rate4_8 :
                nv == 12 ? isa_rate4_12 : nv == 16 ? isa_rate4_16 : nv == 24 ? isa_rate4_24 : nv == 32 ? isa_rate4_32 : nullptr;
     if (k == nullptr)
         return -2;

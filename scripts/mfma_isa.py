@@ -71,7 +71,7 @@ def run():
     import torch  # first: the process then uses torch's HIP runtime for this library too
     lib = C.CDLL(SO)
     vp = C.c_void_p
-    lib.run_layout.argtypes = [vp] * 6
+    lib.run_layout.argtypes = [vp] * 7
     lib.run_rate.argtypes = [C.c_int, C.c_int, vp, vp, C.c_int, C.c_int]
     lib.err_str.restype = C.c_char_p
     dev = torch.device("cuda:0")
@@ -86,7 +86,8 @@ def run():
         t = [torch.from_numpy(x.view(np.int32)).to(dev) for x in (a.ravel(), b.ravel(), sa, sb)]
         c32 = torch.zeros(64 * 16, dtype=torch.float32, device=dev)
         c16 = torch.zeros(64 * 4, dtype=torch.float32, device=dev)
-        rc = lib.run_layout(*(x.data_ptr() for x in t), c32.data_ptr(), c16.data_ptr())
+        c32u = torch.zeros(64 * 16, dtype=torch.float32, device=dev)
+        rc = lib.run_layout(*(x.data_ptr() for x in t), c32.data_ptr(), c16.data_ptr(), c32u.data_ptr())
         assert rc == 0, lib.err_str(rc).decode()
         for shape, cc in ((32, c32), (16, c16)):
             got = c_layout(cc.cpu().numpy().reshape(64, -1), shape)
@@ -105,6 +106,13 @@ def run():
                     ok.append(name)
             report["layout"].setdefault(f"{shape}x{shape}", []).append(ok)
             print(f"trial {trial} {shape}x{shape}: matching maps {ok}", flush=True)
+        # the unscaled instruction (immediate zero scales): the plain product, no E8M0 factor
+        km = cmaps(32)["32g+j"]
+        gu = c_layout(c32u.cpu().numpy().reshape(64, -1), 32)
+        one = np.full(64, 127, np.uint32)
+        unscaled_ok = bool(np.array_equal(expand(a, one, 32, 64, km) @ expand(b, one, 32, 64, km).T, gu))
+        report["layout"].setdefault("32x32_unscaled_is_plain_product", []).append(unscaled_ok)
+        print(f"trial {trial} unscaled v_mfma_f32_32x32x64_f8f6f4 = plain product: {unscaled_ok}", flush=True)
         np.savez(os.path.join(ROOT, "gpurun_out", f"mfma_layout_{trial}.npz"), a=a, b=b, sa=sa, sb=sb,
                  c32=c32.cpu().numpy(), c16=c16.cpu().numpy())
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
@@ -124,13 +132,14 @@ def run():
                 print(f"{key}: {per:.2f} cycles per {'MFMA (+ fillers)' if nv >= 0 else 'v_bitop3'}", flush=True)
     lib.run_rate4.argtypes = [C.c_int, vp, vp, C.c_int, C.c_int]
     out = torch.zeros(ncu * 16, dtype=torch.int64, device=dev)
-    for nv in (-1, 0, 4, 8, 12, 16, 24, 32):
+    for nv in (-1, 0, 4, 8, 12, 16, 24, 32, 1000, 1008, 1016, 1032):
         for n in (10, iters):
             rc = lib.run_rate4(nv, inp.data_ptr(), out.data_ptr(), n, ncu)
             assert rc == 0, lib.err_str(rc).decode()
         cyc = float(np.median(out.cpu().numpy()))
         per = cyc / (iters * (4 if nv >= 0 else 32))
-        key = f"4waves_per_simd_{'valu_only' if nv < 0 else '32x32x64'}_nv{nv}"
+        key = (f"4waves_per_simd_{'valu_only' if nv < 0 else '32x32x64'}_nv{nv}" if nv < 1000 else
+               f"4waves_per_simd_32x32x64_unscaled_nv{nv - 1000}")
         report["rate"][key] = round(per, 2)
         print(f"{key}: {per:.2f} wave-cycles per {'MFMA (+ fillers)' if nv >= 0 else 'v_bitop3'}", flush=True)
     print(json.dumps(report))

@@ -4,7 +4,7 @@
  * itself would drive it (its send loop, lib/rapido.c:2176-2301, keeps many windows moving; a window is 16 records of
  * 16 KiB, :2115-2126).
  *
- *   rl_stream [nwin] [depth] [key_bytes] [transport: direct|zero_copy|copy]
+ *   rl_stream [nwin] [depth] [key_bytes] [transport: direct|dma|zero_copy|copy] [windows per launch]
  *
  * nwin windows are sealed from one host buffer into another with `depth` windows in flight (seal_submit, and the wait
  * of the oldest once `depth` are outstanding), then opened back the same way; the clock is CLOCK_MONOTONIC from the
@@ -16,7 +16,19 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <signal.h>
+#include <execinfo.h>
+#include <unistd.h>
 #include "../include/ptls_mi355x.h"
+
+static void on_fault(int sig)
+{
+    void *bt[32];
+    const int n = backtrace(bt, 32);
+    fprintf(stderr, "rl_stream: signal %d\n", sig);
+    backtrace_symbols_fd(bt, n, 2);
+    _exit(128 + sig);
+}
 
 #define WIN 16
 #define FRAG 16384
@@ -47,6 +59,8 @@ static void die(const char *what)
 
 typedef struct {
     ptls_mi355x_record_layer_t *tx, *rx;
+    ptls_mi355x_record_layer_t *txs[8], *rxs[8]; /* multi: the windows of `multi` connections per launch */
+    size_t multi;
     uint8_t *send, *wire, *pt;
     ptls_mi355x_iovec_t (*frags)[WIN];
     size_t nwin;
@@ -58,22 +72,47 @@ static double pass(stream_t *st, int seal, size_t depth, size_t max_inflight_see
     ptls_mi355x_record_layer_t *rl = seal ? st->tx : st->rx;
     uint64_t tickets[64], head = 0, tail = 0;
     ptls_mi355x_record_layer_set_seq(rl, 0);
+    for (size_t c = 0; st->multi > 1 && c < st->multi; ++c) { /* each connection's windows: its own seq from 0 */
+        ptls_mi355x_record_layer_set_seq(st->txs[c], 0);
+        ptls_mi355x_record_layer_set_seq(st->rxs[c], 0);
+    }
     const double t0 = now();
     for (size_t w = 0; w < st->nwin + depth; ++w) {
         if (tail - head == depth || (w >= st->nwin && tail != head)) {
-            size_t outlen, nrec, cons;
-            int alert;
-            if (ptls_mi355x_record_layer_wait(rl, tickets[head % 64], &outlen, &nrec, &cons, &alert) != 0)
+            size_t outlen[8], nrec[8], cons[8];
+            int alert[8];
+            if (ptls_mi355x_record_layer_wait(st->multi > 1 ? (seal ? st->txs[0] : st->rxs[0]) : rl, tickets[head % 64], outlen,
+                                              nrec, cons, alert) != 0)
                 die("wait");
-            if (nrec != WIN || alert != 0 || outlen != (seal ? (size_t)WIRE_WIN : (size_t)WIN * FRAG)) {
-                fprintf(stderr, "rl_stream: window %zu: %zu records, %zu bytes, alert %d\n", (size_t)head, nrec, outlen, alert);
-                exit(1);
-            }
+            for (size_t c = 0; c < (st->multi > 1 ? st->multi : 1); ++c)
+                if (nrec[c] != WIN || alert[c] != 0 || outlen[c] != (seal ? (size_t)WIRE_WIN : (size_t)WIN * FRAG)) {
+                    fprintf(stderr, "rl_stream: window %zu: %zu records, %zu bytes, alert %d\n", (size_t)head, nrec[c],
+                            outlen[c], alert[c]);
+                    exit(1);
+                }
             ++head;
         }
         if (w >= st->nwin)
             continue;
-        if (seal) {
+        if (st->multi > 1) { /* windows w .. w + multi - 1 as `multi` connections of one launch (_multi) */
+            const ptls_mi355x_iovec_t *f[8];
+            size_t nf[8], cap[8], inlen[8], parsed[8];
+            void *out[8];
+            const void *in[8];
+            for (size_t c = 0; c < st->multi; ++c) {
+                f[c] = st->frags[w + c];
+                nf[c] = WIN;
+                cap[c] = seal ? WIRE_WIN : PT_WIN;
+                out[c] = seal ? st->wire + (w + c) * WIRE_WIN : st->pt + (w + c) * PT_WIN;
+                in[c] = st->wire + (w + c) * WIRE_WIN;
+                inlen[c] = WIRE_WIN;
+            }
+            if ((seal ? ptls_mi355x_record_layer_seal_submit(st->txs, st->multi, f, nf, 23, out, cap, &tickets[tail % 64])
+                      : ptls_mi355x_record_layer_open_submit(st->rxs, st->multi, in, inlen, out, cap, parsed,
+                                                             &tickets[tail % 64])) != 0)
+                die("multi submit");
+            w += st->multi - 1;
+        } else if (seal) {
             const ptls_mi355x_iovec_t *f = st->frags[w];
             const size_t nf = WIN, cap = WIRE_WIN;
             void *out = st->wire + w * WIRE_WIN;
@@ -99,12 +138,16 @@ int main(int argc, char **argv)
     const size_t nwin = argc > 1 ? (size_t)atoi(argv[1]) : 64, depth = argc > 2 ? (size_t)atoi(argv[2]) : 4;
     const size_t key_bytes = argc > 3 ? (size_t)atoi(argv[3]) : 16;
     const char *transport = argc > 4 ? argv[4] : "direct";
-    if (depth < 1 || depth > 4 || nwin < 1 || (key_bytes != 16 && key_bytes != 32)) {
-        fprintf(stderr, "usage: rl_stream [nwin] [depth 1..4] [16|32] [direct|zero_copy|copy]\n");
+    const size_t multi = argc > 5 ? (size_t)atoi(argv[5]) : 1; /* windows per launch (_multi, distinct connections) */
+    if (depth < 1 || depth > 4 || nwin < 1 || (key_bytes != 16 && key_bytes != 32) || multi < 1 || multi > 8 ||
+        nwin % multi != 0) {
+        fprintf(stderr, "usage: rl_stream [nwin] [depth 1..4] [16|32] [direct|dma|zero_copy|copy]\n");
         return 2;
     }
+    signal(SIGSEGV, on_fault);
     stream_t st = {0};
     st.nwin = nwin;
+    st.multi = multi;
     uint8_t key[32], iv[12];
     uint64_t x = 0x9e3779b97f4a7c15ull;
     for (size_t i = 0; i < 32; ++i)
@@ -127,15 +170,30 @@ int main(int argc, char **argv)
     if ((st.tx = ptls_mi355x_record_layer_new(key, key_bytes, iv, 0)) == NULL ||
         (st.rx = ptls_mi355x_record_layer_new(key, key_bytes, iv, 0)) == NULL)
         die("record_layer_new");
-    if (strcmp(transport, "direct") == 0) {
-        if (ptls_mi355x_record_layer_register(st.tx, st.send, nwin * WIN * FRAG) != 0 ||
-            ptls_mi355x_record_layer_register(st.tx, st.wire, nwin * WIRE_WIN) != 0 ||
-            ptls_mi355x_record_layer_register(st.rx, st.wire, nwin * WIRE_WIN) != 0 ||
-            ptls_mi355x_record_layer_register(st.rx, st.pt, nwin * PT_WIN) != 0)
-            die("register");
-    } else if (strcmp(transport, "copy") == 0) {
-        ptls_mi355x_record_layer_set_zero_copy_bytes(st.tx, 0);
-        ptls_mi355x_record_layer_set_zero_copy_bytes(st.rx, 0);
+    for (size_t c = 0; multi > 1 && c < multi; ++c) { /* connection c: IV bytes 0..3 ^ BE32(c) (lib/rapido.c:123-133) */
+        uint8_t civ[12];
+        memcpy(civ, iv, 12);
+        civ[3] ^= (uint8_t)c;
+        if ((st.txs[c] = ptls_mi355x_record_layer_new(key, key_bytes, civ, 0)) == NULL ||
+            (st.rxs[c] = ptls_mi355x_record_layer_new(key, key_bytes, civ, 0)) == NULL)
+            die("record_layer_new");
+    }
+    ptls_mi355x_record_layer_t *all[18] = {st.tx, st.rx};
+    size_t nall = 2;
+    for (size_t c = 0; multi > 1 && c < multi; ++c) {
+        all[nall++] = st.txs[c];
+        all[nall++] = st.rxs[c];
+    }
+    for (size_t i = 0; i < nall; ++i) {
+        if (strcmp(transport, "direct") == 0 || strcmp(transport, "dma") == 0) {
+            if (ptls_mi355x_record_layer_register(all[i], st.send, nwin * WIN * FRAG) != 0 ||
+                ptls_mi355x_record_layer_register(all[i], st.wire, nwin * WIRE_WIN) != 0 ||
+                ptls_mi355x_record_layer_register(all[i], st.pt, nwin * PT_WIN) != 0)
+                die("register");
+            ptls_mi355x_record_layer_set_direct_dma(all[i], strcmp(transport, "dma") == 0);
+        } else if (strcmp(transport, "copy") == 0) {
+            ptls_mi355x_record_layer_set_zero_copy_bytes(all[i], 0);
+        }
     }
     size_t inflight = 0;
     double t_seal = 0, t_open = 0, t_seal1 = 0, t_open1 = 0;
@@ -154,11 +212,11 @@ int main(int argc, char **argv)
     const double bytes = (double)nwin * WIN * FRAG, gib = (double)(1u << 30);
     printf("{\"seal_gibps\": %.2f, \"open_gibps\": %.2f, \"seal_us_per_window\": %.2f, \"open_us_per_window\": %.2f, "
            "\"seal_gibps_sync\": %.2f, \"open_gibps_sync\": %.2f, \"windows\": %zu, \"depth\": %zu, \"max_in_flight\": %zu, "
-           "\"transport\": \"%s\", \"key_bits\": %zu}\n",
+           "\"transport\": \"%s\", \"key_bits\": %zu, \"windows_per_launch\": %zu}\n",
            bytes / t_seal / gib, bytes / t_open / gib, t_seal / nwin * 1e6, t_open / nwin * 1e6, bytes / t_seal1 / gib,
-           bytes / t_open1 / gib, nwin, depth, inflight, transport, 8 * key_bytes);
-    ptls_mi355x_record_layer_free(st.tx);
-    ptls_mi355x_record_layer_free(st.rx);
+           bytes / t_open1 / gib, nwin, depth, inflight, transport, 8 * key_bytes, multi);
+    for (size_t i = 0; i < nall; ++i)
+        ptls_mi355x_record_layer_free(all[i]);
     free(st.send);
     free(st.wire);
     free(st.pt);

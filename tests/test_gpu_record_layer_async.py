@@ -1,6 +1,7 @@
 """The record layer's asynchronous windows, the 2^24-record key-update limit, open_record and rekey
 (include/ptls_mi355x.h section 5, rapido_amd/csrc/record_layer.c), on every transport: direct (registered host
-buffers, the kernels work on them in place), zero-copy (pinned staging) and copy (DMA).
+buffers read and written in place by the kernels), direct_dma (moved by DMA to and from device memory), zero-copy
+(pinned staging) and copy (staging + DMA).
 
 Every wire byte is checked against the oracle's TLS 1.3 record functions, which reproduce the reference ptls_send /
 ptls_receive (tests/test_tls_records.py, tests/golden/tls_records.json).  The limit follows ptls_send
@@ -19,7 +20,9 @@ from test_gpu_record_layer import conn_iv, oracle_window, page_buffer
 
 pytestmark = pytest.mark.gpu
 
-TRANSPORTS = ["direct", "zero_copy", "copy"]
+# direct: registered buffers read in place by the kernels, plaintexts written by the delivery kernel (the default);
+# direct_dma: registered buffers moved by DMA around a device-resident launch; zero_copy / copy: the layer's staging
+TRANSPORTS = ["direct", "direct_dma", "zero_copy", "copy"]
 LIMIT = ra.RECORD_LAYER_SEQ_LIMIT
 KEY_UPDATE_MSG = bytes([24, 0, 0, 1, 0])  # handshake KeyUpdate, update_not_requested (RFC 8446 sec. 4.6.3)
 
@@ -31,9 +34,10 @@ class Host:
         self.transport, self.layers = transport, layers
         self.buf = page_buffer(nbytes)
         self.pos = 0
-        if transport == "direct":
+        if transport.startswith("direct"):
             for rl in layers:
                 rl.register(self.buf)
+                rl.set_direct_dma(transport == "direct_dma")
         for rl in layers:
             if transport == "copy":
                 rl.set_zero_copy_bytes(0)
