@@ -17,8 +17,9 @@
  *     dwords cross to the lower half (Y is folded into block 0 there).
  *
  *   probe_gf2_run<MODE>  persistent 1024-thread groups, work in units of 16 wave steps of 128 blocks:
- *                        MODE 0 AES-CTR only (2 blocks per lane and step), 1 AES + MFMA GHASH, 2 AES + nibble-table
- *                        GHASH (the batch kernels' fused rounds, aes_ghash_fused_h, H^4 Horner per lane)
+ *                        MODE 0 AES-CTR only (2 blocks per lane and step), 1 AES + MFMA GHASH (v_perm gather pack),
+ *                        2 AES + nibble-table GHASH (the batch kernels' fused rounds, aes_ghash_fused_h, H^4 Horner per
+ *                        lane), 3 AES + MFMA GHASH with the v_alignbit pack (W rows in its bit order)
  *   probe_gf2_check      one wave: the MFMA GHASH of given data (S chunks of 32 records x 4 blocks) -> Y per record
  *
  * Driven by scripts/probe_gf2.py.
@@ -109,6 +110,7 @@ __device__ __forceinline__ uint32_t gather4(float a, float b, float c, float d)
  * Value i of M tile mt in lane half h is W row 32 mt + (i & 3) + 8 (i >> 2) + 4 h and Y' bit
  * 64 h + 32 (mt >> 1) + 4 (mt & 1) + 8 (i & 3) + (i >> 2) (scripts/probe_gf2.py builds W to that map).
  */
+template <int PACK>
 __device__ __forceinline__ void gf2_chunk(const uint8_t *lds, uint32_t lane, const u32x4 &b0, const u32x4 &b1,
                                           uint32_t &y0, uint32_t &y1)
 {
@@ -130,13 +132,22 @@ __device__ __forceinline__ void gf2_chunk(const uint8_t *lds, uint32_t lane, con
         for (int t = 0; t < 8; ++t) {
             const u32x4 a = lds_u32x4(lds, W_BASE + (uint32_t)(mt * 8 + t) * 1024u + lane * 16u);
             const v8i A = {(int)a[0], (int)a[1], (int)a[2], (int)a[3], 0, 0, 0, 0};
-            acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(A, B[t], acc, 4, 4, 0, 127, 0, 127);
+            /* immediate zero scales: the unscaled v_mfma_f32_32x32x64_f8f6f4 (holds the SIMD's issue ~17 cycles
+             * instead of ~19, profiles/r03a_mfma_isa.json) */
+            acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(A, B[t], acc, 4, 4, 0, 0, 0, 0);
         }
-        uint32_t bits = 0u;
+        if (PACK == 0) {
+            uint32_t bits = 0u;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) /* values 4g .. 4g + 3 -> bits 8k + g (k = value & 3) */
-            bits |= (gather4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]) & 0x01010101u) << g;
-        y[mt >> 1] |= bits << (4 * (mt & 1));
+            for (int g = 0; g < 4; ++g) /* values 4g .. 4g + 3 -> bits 8k + g (k = value & 3) */
+                bits |= (gather4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]) & 0x01010101u) << g;
+            y[mt >> 1] |= bits << (4 * (mt & 1));
+        } else {
+            /* v_alignbit: y = (y >> 1) | (parity << 31), one VALU per bit, no masking (W rows ordered to match) */
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                y[mt >> 1] = alignbit(__float_as_uint(acc[i]), y[mt >> 1], 1u);
+        }
     }
     y0 = y[0];
     y1 = y[1];
@@ -188,7 +199,7 @@ __device__ void run_body(const KeyImage *ki, const u32x4 *w, uint32_t nunits, ui
                 } else {
                     x0 ^= Y;
                     uint32_t y0, y1;
-                    gf2_chunk(lds, lane, x0, x1, y0, y1);
+                    gf2_chunk<MODE == 3>(lds, lane, x0, x1, y0, y1);
                     Y = gf2_fold(lane, y0, y1);
                 }
             }
@@ -210,12 +221,15 @@ __device__ void run_body(const KeyImage *ki, const u32x4 *w, uint32_t nunits, ui
 RUN(10, 0)
 RUN(10, 1)
 RUN(10, 2)
+RUN(10, 3)
+RUN(14, 3)
 RUN(14, 0)
 RUN(14, 1)
 RUN(14, 2)
 
 /* one wave: Y of each of 32 records after S chunks (data[((s * 32 + n) * 4 + j) * 16], block j of record n) */
-extern "C" __global__ __launch_bounds__(64) void probe_gf2_check(const u32x4 *w, const u32x4 *data, uint32_t S, u32x4 *y_out)
+extern "C" __global__ __launch_bounds__(64) void probe_gf2_check(const u32x4 *w, const u32x4 *data, uint32_t S, u32x4 *y_out,
+                                                                 uint32_t pack)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
     for (uint32_t i = threadIdx.x; i < 0x8000u / 16u; i += blockDim.x)
@@ -227,7 +241,10 @@ extern "C" __global__ __launch_bounds__(64) void probe_gf2_check(const u32x4 *w,
         u32x4 x0 = data[(s * 32u + n) * 4u + 2u * h], x1 = data[(s * 32u + n) * 4u + 2u * h + 1u];
         x0 ^= Y;
         uint32_t y0, y1;
-        gf2_chunk(lds, lane, x0, x1, y0, y1);
+        if (pack)
+            gf2_chunk<1>(lds, lane, x0, x1, y0, y1);
+        else
+            gf2_chunk<0>(lds, lane, x0, x1, y0, y1);
         Y = gf2_fold(lane, y0, y1);
     }
     if (lane < 32u)
@@ -254,17 +271,17 @@ extern "C" int probe_run(int nr, int mode, const void *d_ki, const void *d_w, ui
                          void *d_work, void *d_out, void *stream)
 {
     typedef void (*kern_t)(const KeyImage *, const u32x4 *, uint32_t, uint32_t *, uint32_t *);
-    kern_t k = nr == 10 ? (mode == 0 ? probe_gf2_run_10_0 : mode == 1 ? probe_gf2_run_10_1 : probe_gf2_run_10_2)
-                        : (mode == 0 ? probe_gf2_run_14_0 : mode == 1 ? probe_gf2_run_14_1 : probe_gf2_run_14_2);
+    kern_t k = nr == 10 ? (mode == 0 ? probe_gf2_run_10_0 : mode == 1 ? probe_gf2_run_10_1 : mode == 2 ? probe_gf2_run_10_2 : probe_gf2_run_10_3)
+                        : (mode == 0 ? probe_gf2_run_14_0 : mode == 1 ? probe_gf2_run_14_1 : mode == 2 ? probe_gf2_run_14_2 : probe_gf2_run_14_3);
     hipLaunchKernelGGL(k, dim3(nblocks), dim3(1024), 0, (hipStream_t)stream, (const KeyImage *)d_ki, (const u32x4 *)d_w,
                        nunits, (uint32_t *)d_work, (uint32_t *)d_out);
     return (int)hipGetLastError();
 }
 
-extern "C" int probe_check(const void *d_w, const void *d_data, uint32_t S, void *d_y, void *stream)
+extern "C" int probe_check(const void *d_w, const void *d_data, uint32_t S, void *d_y, void *stream, uint32_t pack)
 {
     hipLaunchKernelGGL(probe_gf2_check, dim3(1), dim3(64), 0, (hipStream_t)stream, (const u32x4 *)d_w,
-                       (const u32x4 *)d_data, S, (u32x4 *)d_y);
+                       (const u32x4 *)d_data, S, (u32x4 *)d_y, pack);
     return (int)hipGetLastError();
 }
 

@@ -55,7 +55,10 @@ def mul_matrix(c: bytes) -> np.ndarray:
     return M
 
 
-def build_w(H: bytes) -> np.ndarray:
+def build_w(H: bytes, pack: int = 0) -> np.ndarray:
+    """pack 0: value i of M tile mt, lane half h -> Y' bit 64 h + 32 (mt >> 1) + 4 (mt & 1) + 8 (i & 3) + (i >> 2)
+    (the v_perm gather); pack 1: -> bit 64 h + 32 (mt >> 1) + 16 (mt & 1) + i (the v_alignbit chain: the first of the
+    32 values alignbit'ed into a dword ends at bit 0)"""
     powers = [H]
     for _ in range(3):
         powers.append(gf_mul(powers[-1], H))
@@ -67,7 +70,10 @@ def build_w(H: bytes) -> np.ndarray:
             hh, r = lane // 32, lane % 32
             # row 32 mt + r is value i of lane half h' with r = (i & 3) + 8 (i >> 2) + 4 h'
             h_out, i = (r >> 2) & 1, (r & 3) + 4 * (r >> 3)
-            ybit = 64 * h_out + 32 * (mt >> 1) + 4 * (mt & 1) + 8 * (i & 3) + (i >> 2)
+            if pack == 0:
+                ybit = 64 * h_out + 32 * (mt >> 1) + 4 * (mt & 1) + 8 * (i & 3) + (i >> 2)
+            else:
+                ybit = 64 * h_out + 32 * (mt >> 1) + 16 * (mt & 1) + i
             for t in range(8):
                 blk, dd = 2 * hh + (t >> 2), t & 3
                 M = Ms[4 - blk]
@@ -93,7 +99,7 @@ def run():
     lib.probe_key.argtypes = [vp, u32, vp, vp, vp]
     lib.probe_key_image_size.restype = C.c_size_t
     lib.probe_run.argtypes = [C.c_int, C.c_int, vp, vp, u32, u32, vp, vp, vp]
-    lib.probe_check.argtypes = [vp, vp, u32, vp, vp]
+    lib.probe_check.argtypes = [vp, vp, u32, vp, vp, u32]
     lib.probe_err.restype = C.c_char_p
     dev = torch.device("cuda:0")
     stream = torch.cuda.current_stream(dev).cuda_stream
@@ -103,24 +109,26 @@ def run():
         if rc != 0:
             raise SystemExit(lib.probe_err(rc).decode())
 
-    # correctness: 3 chunks of 32 records x 4 blocks against Algorithm-1 GHASH
+    # correctness: 3 chunks of 32 records x 4 blocks against Algorithm-1 GHASH, both packs
     rng = np.random.default_rng(17)
     H = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
-    w = build_w(H)
     S = 3
     data = rng.integers(0, 256, S * 32 * 4 * 16, dtype=np.uint8)
-    d_w = torch.from_numpy(w.view(np.int32)).to(dev)
     d_data = torch.from_numpy(data).to(dev)
-    d_y = torch.zeros(32 * 16, dtype=torch.uint8, device=dev)
-    ok(lib.probe_check(d_w.data_ptr(), d_data.data_ptr(), S, d_y.data_ptr(), stream))
-    torch.cuda.synchronize()
-    got = d_y.cpu().numpy().tobytes()
-    for n in range(32):
-        blocks = [data[((s * 32 + n) * 4 + j) * 16:((s * 32 + n) * 4 + j + 1) * 16].tobytes() for s in range(S)
-                  for j in range(4)]
-        if got[16 * n:16 * n + 16] != ghash_ref(H, blocks):
-            raise SystemExit(f"MFMA GHASH differs from the reference GHASH for record {n}")
-    print("MFMA GHASH bit-exact against Algorithm-1 GHASH: 32 records x 12 blocks", flush=True)
+    d_ws = {}
+    for pack in (0, 1):
+        w = build_w(H, pack)
+        d_ws[pack] = d_w = torch.from_numpy(w.view(np.int32)).to(dev)
+        d_y = torch.zeros(32 * 16, dtype=torch.uint8, device=dev)
+        ok(lib.probe_check(d_w.data_ptr(), d_data.data_ptr(), S, d_y.data_ptr(), stream, pack))
+        torch.cuda.synchronize()
+        got = d_y.cpu().numpy().tobytes()
+        for n in range(32):
+            blocks = [data[((s * 32 + n) * 4 + j) * 16:((s * 32 + n) * 4 + j + 1) * 16].tobytes() for s in range(S)
+                      for j in range(4)]
+            if got[16 * n:16 * n + 16] != ghash_ref(H, blocks):
+                raise SystemExit(f"MFMA GHASH (pack {pack}) differs from the reference GHASH for record {n}")
+        print(f"MFMA GHASH (pack {pack}) bit-exact against Algorithm-1 GHASH: 32 records x 12 blocks", flush=True)
 
     results = {}
     for keylen in [int(x) for x in os.environ.get("PROBE_KEYS", "16,32").split(",")]:
@@ -135,7 +143,8 @@ def run():
         d_out = torch.zeros(ncu * 1024, dtype=torch.int32, device=dev)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         res = {}
-        for mode, name in ((0, "aes_only"), (1, "aes+mfma_ghash"), (2, "aes+nibble_ghash")):
+        for mode, name in ((0, "aes_only"), (1, "aes+mfma_ghash"), (3, "aes+mfma_ghash_alignbit"), (2, "aes+nibble_ghash")):
+            d_w = d_ws[1 if mode == 3 else 0]
             ts = []
             for rep in range(int(os.environ.get("PROBE_REPS", "4"))):
                 d_work.zero_()
