@@ -445,18 +445,22 @@ def record_layer_stream(key_bytes: int = 16, nwin: int = 64, depth: int = 4, tra
     moving, lib/rapido.c:2176-2301).  Driven from C (scripts/rl_stream.c); timed on the host clock from the first
     submit to the last wait; every opened window is compared with its fragments.  *_sync: one launch at a time."""
     exe = os.path.join(ROOT, "scripts", "_build", "rl_stream")
-    res = {}
-    for m in per_launch:
-        r = subprocess.run([exe, str(nwin), str(depth), str(key_bytes), transport, str(m)], capture_output=True,
-                           text=True, timeout=120)
+    def run(*extra):
+        r = subprocess.run([exe, str(nwin), str(depth), str(key_bytes), transport, *map(str, extra)],
+                           capture_output=True, text=True, timeout=120)
         if r.returncode != 0:
             raise SystemExit("bench: record-layer stream failed -- " + r.stderr.strip())
-        one = json.loads(r.stdout.strip().splitlines()[-1])
-        res.update(one) if m == per_launch[0] else res.setdefault("one_window_per_launch", one)
+        return json.loads(r.stdout.strip().splitlines()[-1])
+
+    res = run(per_launch[0])
+    # one connection: its consecutive windows, `per_launch[0]` of them per launch (the layer given that many times)
+    res["one_connection"] = run(per_launch[0], "one")
+    res["one_window_per_launch"] = run(per_launch[1])
     res["note"] = (f"{nwin} back-to-back windows of 16 x 16384 B records, AES-{8 * key_bytes}, host memory to host "
                    f"memory ({transport}: registered buffers), {per_launch[0]} connections' windows per launch, {depth} "
                    "launches in flight (record_layer_seal_submit / open_submit + wait), C driver scripts/rl_stream.c; "
-                   "*_sync: one launch at a time; one_window_per_launch: a single connection's windows")
+                   f"*_sync: one launch at a time; one_connection: {per_launch[0]} consecutive windows of a single "
+                   "connection per launch; one_window_per_launch: a single connection's windows, one per launch")
     return res
 
 

@@ -385,6 +385,8 @@ int ptls_mi355x_record_layer_rekey(ptls_mi355x_record_layer_t *rl, const void *k
  * most 4 windows per layer are outstanding (a fifth submit returns -1).  A synchronous call on a layer with windows
  * outstanding returns -1.  Buffers (fragments, inputs, outputs) must stay untouched until the window's wait.
  *
+ * A layer may appear several times in one submit: its windows in that order, each behind the one before (one
+ * connection's consecutive windows in one launch).
  *  seal_submit: the records take their seq at submit (get_seq includes them).  Its wait gives per layer outlen[l],
  *               nrecords[l], consumed[l] = fragments sealed, alerts[l] = 0 or PTLS_MI355X_RECORD_LAYER_KEY_UPDATE.
  *  open_submit: parsed[l] = the wire bytes of the complete records taken from in[l] (the next window starts behind

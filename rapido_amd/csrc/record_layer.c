@@ -558,6 +558,9 @@ int ptls_mi355x_record_layer_seal_submit(ptls_mi355x_record_layer_t *const *laye
     for (size_t l = 0; l < nlayers; ++l) {
         rl_part_t *p = &op->part[l];
         uint64_t sq = layers[l]->seq;
+        for (size_t m = 0; m < l; ++m) /* a layer given again: its next window, behind the earlier one */
+            if (layers[m] == layers[l])
+                sq = op->part[m].seq0 + op->part[m].nrec;
         p->seq0 = sq;
         op->out[l] = out[l];
         op->capacity[l] = capacity[l];
@@ -700,6 +703,9 @@ static int open_submit(ptls_mi355x_record_layer_t *const *layers, size_t nlayers
         rl_part_t *p = &op->part[l];
         const size_t lmax = any_type ? 1 : inlen[l] / PTLS_MI355X_TLS_HEADER_SIZE + 1; /* its own budget */
         uint64_t seq = layers[l]->spec_seq;
+        for (size_t m = 0; m < l; ++m) /* a layer given again: its next window, behind the earlier one */
+            if (layers[m] == layers[l])
+                seq = op->part[m].seq0 + op->part[m].n;
         p->seq0 = seq;
         p->k0 = nrec;
         op->out[l] = out[l];

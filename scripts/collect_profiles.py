@@ -161,6 +161,8 @@ def main(tag, label):
         if os.path.exists(p):
             hc[w] = {}
             for k, (cyc, ghz_prof) in held_cycles(p, 1).items():
+                if not k.startswith(("mi355x_gcm_seal_", "mi355x_gcm_open_")):
+                    continue  # microsecond kernels: GRBM_GUI_ACTIVE spans more than the dispatch, no clock to read
                 # the kernel's busy cycles over its UN-profiled launch time (the bench line's HIP events): the clock
                 # the chip holds in the benchmark itself; the profiled dispatches run slower (counter collection)
                 if line is not None and line["roofline"]["kernel"] == k:

@@ -4,7 +4,9 @@
  * itself would drive it (its send loop, lib/rapido.c:2176-2301, keeps many windows moving; a window is 16 records of
  * 16 KiB, :2115-2126).
  *
- *   rl_stream [nwin] [depth] [key_bytes] [transport: direct|dma|zero_copy|copy] [windows per launch]
+ *   rl_stream [nwin] [depth] [key_bytes] [transport: direct|dma|zero_copy|copy] [windows per launch] [one]
+ *   (windows per launch > 1: windows of that many connections per launch, or with "one" consecutive windows of one
+ *   connection)
  *
  * nwin windows are sealed from one host buffer into another with `depth` windows in flight (seal_submit, and the wait
  * of the oldest once `depth` are outstanding), then opened back the same way; the clock is CLOCK_MONOTONIC from the
@@ -138,7 +140,8 @@ int main(int argc, char **argv)
     const size_t nwin = argc > 1 ? (size_t)atoi(argv[1]) : 64, depth = argc > 2 ? (size_t)atoi(argv[2]) : 4;
     const size_t key_bytes = argc > 3 ? (size_t)atoi(argv[3]) : 16;
     const char *transport = argc > 4 ? argv[4] : "direct";
-    const size_t multi = argc > 5 ? (size_t)atoi(argv[5]) : 1; /* windows per launch (_multi, distinct connections) */
+    const size_t multi = argc > 5 ? (size_t)atoi(argv[5]) : 1; /* windows per launch (_multi) */
+    const int one_conn = argc > 6 && strcmp(argv[6], "one") == 0; /* ... of one connection instead of `multi` */
     if (depth < 1 || depth > 4 || nwin < 1 || (key_bytes != 16 && key_bytes != 32) || multi < 1 || multi > 8 ||
         nwin % multi != 0) {
         fprintf(stderr, "usage: rl_stream [nwin] [depth 1..4] [16|32] [direct|dma|zero_copy|copy]\n");
@@ -174,13 +177,18 @@ int main(int argc, char **argv)
         uint8_t civ[12];
         memcpy(civ, iv, 12);
         civ[3] ^= (uint8_t)c;
+        if (one_conn && c > 0) { /* the same connection again: its next window in the same launch */
+            st.txs[c] = st.txs[0];
+            st.rxs[c] = st.rxs[0];
+            continue;
+        }
         if ((st.txs[c] = ptls_mi355x_record_layer_new(key, key_bytes, civ, 0)) == NULL ||
             (st.rxs[c] = ptls_mi355x_record_layer_new(key, key_bytes, civ, 0)) == NULL)
             die("record_layer_new");
     }
     ptls_mi355x_record_layer_t *all[18] = {st.tx, st.rx};
     size_t nall = 2;
-    for (size_t c = 0; multi > 1 && c < multi; ++c) {
+    for (size_t c = 0; multi > 1 && c < (one_conn ? 1 : multi); ++c) {
         all[nall++] = st.txs[c];
         all[nall++] = st.rxs[c];
     }
@@ -212,9 +220,9 @@ int main(int argc, char **argv)
     const double bytes = (double)nwin * WIN * FRAG, gib = (double)(1u << 30);
     printf("{\"seal_gibps\": %.2f, \"open_gibps\": %.2f, \"seal_us_per_window\": %.2f, \"open_us_per_window\": %.2f, "
            "\"seal_gibps_sync\": %.2f, \"open_gibps_sync\": %.2f, \"windows\": %zu, \"depth\": %zu, \"max_in_flight\": %zu, "
-           "\"transport\": \"%s\", \"key_bits\": %zu, \"windows_per_launch\": %zu}\n",
+           "\"transport\": \"%s\", \"key_bits\": %zu, \"windows_per_launch\": %zu, \"connections_per_launch\": %zu}\n",
            bytes / t_seal / gib, bytes / t_open / gib, t_seal / nwin * 1e6, t_open / nwin * 1e6, bytes / t_seal1 / gib,
-           bytes / t_open1 / gib, nwin, depth, inflight, transport, 8 * key_bytes, multi);
+           bytes / t_open1 / gib, nwin, depth, inflight, transport, 8 * key_bytes, multi, one_conn ? (size_t)1 : multi);
     for (size_t i = 0; i < nall; ++i)
         ptls_mi355x_record_layer_free(all[i]);
     free(st.send);

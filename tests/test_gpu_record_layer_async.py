@@ -245,3 +245,44 @@ def test_async_rekey_and_free_with_pending(gpu):
     tx.rekey(key, iv)
     tx.seal_submit([f], h.take(8192))
     tx.close()  # frees with a window never waited for
+
+
+@pytest.mark.parametrize("transport", ["direct", "zero_copy"])
+def test_one_connection_windows_in_one_launch(gpu, transport):
+    """A layer given several times in one _multi call: its consecutive windows in one launch, each behind the one
+    before (the same bytes as one seal after another); a receive window that stops early leaves the same
+    connection's windows behind it STALE, the other connection's window unaffected."""
+    rng = np.random.default_rng(31)
+    key, iv = rng.integers(0, 256, 16, dtype=np.uint8).tobytes(), rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    iv0, iv1 = conn_iv(iv, 0), conn_iv(iv, 1)
+    tx, other = ra.RecordLayer(key, iv0, seq=5), ra.RecordLayer(key, iv1, seq=70)
+    h = Host(transport, [tx, other], 1 << 22)
+    wins_b = [[rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in rng.integers(1, 16385, k)]
+              for k in (16, 3, 9, 5)]
+    wins = [[h.take(len(f), f) for f in w] for w in wins_b]
+    outs = [h.take(sum(len(f) + ra.TLS_OVERHEAD for f in w)) for w in wins_b]
+    layers = [tx, other, tx, tx]
+    got = ra.record_layer_seal_multi(layers, wins, outs=outs)
+    want0, s = oracle_window(key, iv0, 5, wins_b[0])
+    want2, s = oracle_window(key, iv0, s, wins_b[2])
+    want3, s = oracle_window(key, iv0, s, wins_b[3])
+    want1, s1 = oracle_window(key, iv1, 70, wins_b[1])
+    for o, (wlen, n), want, k in zip(outs, got, (want0, want1, want2, want3), (16, 3, 9, 5)):
+        assert o[:wlen].tobytes() == want and n == k
+    assert tx.seq == s == 5 + 30 and other.seq == s1
+    # the receiver: window 0 of connection 0 has a bad record 4, so its windows 2 and 3 come back STALE
+    rx, rx1 = ra.RecordLayer(key, iv0, seq=5), ra.RecordLayer(key, iv1, seq=70)
+    bad = bytearray(want0)
+    r4 = sum(len(f) + ra.TLS_OVERHEAD for f in wins_b[0][:4])
+    bad[r4 + 7] ^= 2
+    res = ra.record_layer_open_multi([rx, rx1, rx, rx], [bytes(bad), want1, want2, want3])
+    assert res[0] == (20, b"".join(wins_b[0][:4]), r4, 4)
+    assert res[1] == (0, b"".join(wins_b[1]), len(want1), 3) and rx1.seq == s1
+    assert [r[0] for r in res[2:]] == [ra.RECORD_LAYER_STALE] * 2 and [r[3] for r in res[2:]] == [0, 0]
+    assert rx.seq == 9
+    # resent intact, the three windows of connection 0 in one launch
+    rx.seq = 5
+    res = ra.record_layer_open_multi([rx, rx, rx], [want0, want2, want3])
+    assert [r[:2] for r in res] == [(0, b"".join(wins_b[k])) for k in (0, 2, 3)] and rx.seq == 35
+    for rl in (tx, other, rx, rx1):
+        rl.close()
