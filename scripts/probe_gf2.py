@@ -5,6 +5,10 @@ cores against the nibble tables, inside the batch kernels' AES-CTR, compute-only
     python scripts/probe_gf2.py run       # GPU: MFMA GHASH bit-exact against the host GHASH, then the throughput
                                           # of AES only / AES + MFMA GHASH / AES + nibble GHASH (GB/s of blocks)
 
+    PROBE_MODES (0 AES only, 1 MFMA v_perm pack, 3 MFMA v_alignbit pack, 2 nibble tables), PROBE_KEYS (16,32),
+    PROBE_REPS: one mode under rocprofv3 --pmc, or many repetitions for amd-smi power samples
+    (scripts/gpu_probe_gf2_pmc.sh).
+
 W (128 x 512 bits of M(H^4) | M(H^3) | M(H^2) | M(H)) is laid out as the kernel's fragments: 32 KiB, fragment
 (mt, t) = 1 KiB, lane l's 16 bytes = row 32 mt + l % 32, the 32 elements of K tile t of lane half l // 32.
 """
@@ -143,7 +147,10 @@ def run():
         d_out = torch.zeros(ncu * 1024, dtype=torch.int32, device=dev)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         res = {}
+        modes = [int(m) for m in os.environ.get("PROBE_MODES", "0,1,3,2").split(",")]
         for mode, name in ((0, "aes_only"), (1, "aes+mfma_ghash"), (3, "aes+mfma_ghash_alignbit"), (2, "aes+nibble_ghash")):
+            if mode not in modes:
+                continue
             d_w = d_ws[1 if mode == 3 else 0]
             ts = []
             for rep in range(int(os.environ.get("PROBE_REPS", "4"))):
