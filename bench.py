@@ -435,32 +435,36 @@ def e2e_pcie(ra, extra, dev, steps):
                     "around one launch; pipelined = 16 chunks over 3 streams"}
 
 
-def record_layer_stream(key_bytes: int = 16, nwin: int = 64, depth: int = 4, transport: str = "direct",
+def record_layer_stream(key_bytes: int = 16, nwin: int = 64, depth: int = 4, transport: str = "dma_in",
                         per_launch=(8, 1)):
     """Host-to-host side figure (never `value`): rapido send and receive windows (16 x 16 KiB records, lib/rapido.c
-    :2115-2126) through the asynchronous record layer (include/ptls_mi355x.h section 5) on registered host buffers
-    (direct: the kernels read the socket buffers in place over PCIe, the delivery kernel writes the plaintexts),
+    :2115-2126) through the asynchronous record layer (include/ptls_mi355x.h section 5) on registered host buffers,
     `depth` launches in flight, each launch carrying the windows of `per_launch` connections of a session
     (record_layer_seal_submit / open_submit over that many layers, as rapido's loop keeps many connections' windows
-    moving, lib/rapido.c:2176-2301).  Driven from C (scripts/rl_stream.c); timed on the host clock from the first
+    moving, lib/rapido.c:2176-2301).  dma_in (PTLS_MI355X_RECORD_LAYER_DMA_IN): the inputs reach device memory by
+    DMA, the kernels write the wire records / the delivery kernel the plaintexts in place; direct: the kernels also
+    read the inputs in place over PCIe.  Driven from C (scripts/rl_stream.c); timed on the host clock from the first
     submit to the last wait; every opened window is compared with its fragments.  *_sync: one launch at a time."""
     exe = os.path.join(ROOT, "scripts", "_build", "rl_stream")
-    def run(*extra):
-        r = subprocess.run([exe, str(nwin), str(depth), str(key_bytes), transport, *map(str, extra)],
+
+    def run(tr, *extra):
+        r = subprocess.run([exe, str(nwin), str(depth), str(key_bytes), tr, *map(str, extra)],
                            capture_output=True, text=True, timeout=120)
         if r.returncode != 0:
             raise SystemExit("bench: record-layer stream failed -- " + r.stderr.strip())
         return json.loads(r.stdout.strip().splitlines()[-1])
 
-    res = run(per_launch[0])
+    res = run(transport, per_launch[0])
     # one connection: its consecutive windows, `per_launch[0]` of them per launch (the layer given that many times)
-    res["one_connection"] = run(per_launch[0], "one")
-    res["one_window_per_launch"] = run(per_launch[1])
+    res["one_connection"] = run(transport, per_launch[0], "one")
+    res["one_window_per_launch"] = run(transport, per_launch[1])
+    res["inputs_read_in_place"] = run("direct", per_launch[0])
     res["note"] = (f"{nwin} back-to-back windows of 16 x 16384 B records, AES-{8 * key_bytes}, host memory to host "
-                   f"memory ({transport}: registered buffers), {per_launch[0]} connections' windows per launch, {depth} "
+                   f"memory (registered buffers, {transport}), {per_launch[0]} connections' windows per launch, {depth} "
                    "launches in flight (record_layer_seal_submit / open_submit + wait), C driver scripts/rl_stream.c; "
                    f"*_sync: one launch at a time; one_connection: {per_launch[0]} consecutive windows of a single "
-                   "connection per launch; one_window_per_launch: a single connection's windows, one per launch")
+                   "connection per launch; one_window_per_launch: a single connection's windows, one per launch; "
+                   "inputs_read_in_place: transport direct (kernels read the inputs over PCIe)")
     return res
 
 

@@ -426,7 +426,10 @@ int ptls_mi355x_record_layer_unregister(ptls_mi355x_record_layer_t *rl, void *ba
 /* windows whose buffers are all registered: 0 (default) has the kernels read the inputs in place over PCIe and write
  * the outputs into the registered ranges (a sealed window whose fragments overlap its output goes through the
  * staging instead); 1 moves them by DMA copies between the registered ranges and device memory around a
- * device-resident launch (measured slower: DESIGN.md section 2).  Results are identical.  Returns the previous value. */
+ * device-resident launch (measured slower: DESIGN.md section 2); PTLS_MI355X_RECORD_LAYER_DMA_IN (2) moves only the
+ * inputs (fragments, wire records) to device memory by DMA and writes the outputs in place as 0 does (the fastest
+ * open: DESIGN.md section 2).  Results are identical.  Returns the previous value. */
+#define PTLS_MI355X_RECORD_LAYER_DMA_IN 2
 int ptls_mi355x_record_layer_set_direct_dma(ptls_mi355x_record_layer_t *rl, int on);
 /* zero-copy limit in bytes (default 4 MiB; 0 = always DMA copies); returns the previous value */
 size_t ptls_mi355x_record_layer_set_zero_copy_bytes(ptls_mi355x_record_layer_t *rl, size_t n);

@@ -59,7 +59,7 @@ struct gpu_record_layer_cb {
     void *ranges[4];
     size_t range_len[4], nranges;
     int zero_copy_off;
-    int dma; /* registered ranges moved by DMA copies instead of read in place by the kernels */
+    int dma; /* registered ranges moved by DMA copies (1) or an open's input by DMA (2) instead of read in place */
     unsigned calls;
 };
 
@@ -88,7 +88,7 @@ static int gpu_update_traffic_key(ptls_update_traffic_key_t *self, ptls_t *tls, 
         if (ret == 0 && cb->zero_copy_off)
             ptls_mi355x_record_layer_set_zero_copy_bytes(*l, 0);
         if (ret == 0 && cb->dma)
-            ptls_mi355x_record_layer_set_direct_dma(*l, 1);
+            ptls_mi355x_record_layer_set_direct_dma(*l, cb->dma);
     } else if (ptls_mi355x_record_layer_rekey(*l, key, cs->aead->key_size, iv) != 0) { /* a KeyUpdate epoch change */
         ret = PTLS_ERROR_LIBRARY;
     }
@@ -192,8 +192,8 @@ int main(int argc, char **argv)
     memset(arena, 0, arena_cap);
 
     struct gpu_record_layer_cb cb = {{gpu_update_traffic_key}};
-    cb.direct_ranges = strcmp(transport, "direct") == 0 || strcmp(transport, "dma") == 0;
-    cb.dma = strcmp(transport, "dma") == 0;
+    cb.direct_ranges = strcmp(transport, "direct") == 0 || strcmp(transport, "dma") == 0 || strcmp(transport, "dma_in") == 0;
+    cb.dma = strcmp(transport, "dma") == 0 ? 1 : strcmp(transport, "dma_in") == 0 ? PTLS_MI355X_RECORD_LAYER_DMA_IN : 0;
     cb.zero_copy_off = strcmp(transport, "copy") == 0;
     cb.ranges[0] = arena;
     cb.range_len[0] = arena_cap;

@@ -469,6 +469,7 @@ class _IoVec(C.Structure):
 RECORD_LAYER_SEQ_LIMIT = 1 << 24  # ptls_send's key-update threshold (lib/picotls.c:4976-4977)
 RECORD_LAYER_KEY_UPDATE = 1
 RECORD_LAYER_STALE = -2
+RECORD_LAYER_DMA_IN = 2  # set_direct_dma: the inputs by DMA, the outputs written in place
 
 
 class RecordLayer:
@@ -521,9 +522,12 @@ class RecordLayer:
             raise RuntimeError("record_layer_open failed: " + lib().ptls_mi355x_record_layer_last_error().decode())
         return rc, out.raw[:olen.value], cons.value, nrec.value
 
-    def set_direct_dma(self, on: bool) -> bool:
-        """Registered windows by DMA to and from device memory (True) or read in place by the kernels (False, default)."""
-        return bool(lib().ptls_mi355x_record_layer_set_direct_dma(self.handle, 1 if on else 0))
+    def set_direct_dma(self, on) -> int:
+        """Registered windows by DMA to and from device memory (True / 1), read in place by the kernels (False / 0,
+        default), or the inputs by DMA with the outputs written in place (RECORD_LAYER_DMA_IN).  Returns the previous
+        mode."""
+        mode = on if on == RECORD_LAYER_DMA_IN else (1 if on else 0)
+        return lib().ptls_mi355x_record_layer_set_direct_dma(self.handle, mode)
 
     def set_zero_copy_bytes(self, n: int) -> int:
         """Windows of at most n staged bytes run zero-copy on the pinned staging (0: DMA copies); -> previous."""

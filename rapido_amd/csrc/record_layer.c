@@ -38,7 +38,9 @@
  *                 delivery kernel (ptls_mi355x_tls_deliver_records) writes the delivered plaintexts once, back to
  *                 back, into the caller's buffer.  Only descriptors and statuses pass through the slot's staging.
  *                 ptls_mi355x_record_layer_set_direct_dma(rl, 1) moves registered windows by DMA copies to and from
- *                 device memory instead (measured slower).
+ *                 device memory instead (measured slower); (rl, 2) moves only the inputs by DMA (the copy
+ *                 engine reads host memory faster than kernel loads do) and keeps the in-place writes: seal's wire
+ *                 records, an open's delivery kernel.
  *   zero-copy  -- the window fits the zero-copy limit: fragments / input are copied into the slot's pinned,
  *                 mapped, coherent staging and the kernel works on it over PCIe.
  *   copy       -- larger windows: staging -> one H2D copy -> launch -> one D2H copy (DMA at the link rate).
@@ -92,6 +94,7 @@ typedef struct {
     rl_part_t *part;
     int direct, zero_copy, dma; /* direct: the results land in the caller's buffers (mapped or dma) */
     int deliver;                /* mapped open: slots in device memory, the delivery kernel writes the plaintexts */
+    int dma_in;                 /* direct, the inputs moved to device memory by DMA first (set_direct_dma 2) */
     size_t nrec, off_src, srcbytes, off_dst, dstbytes, off_st, off_ty, off_dp, max_part;
     rl_copy_t *h2d, *d2h; /* dma: registered host ranges <-> the slot's device buffer */
     size_t nh2d, nd2h;
@@ -117,7 +120,8 @@ struct st_ptls_mi355x_record_layer_t {
     uint64_t seq;      /* seal: the next record's seq; open: the seq of the next record to deliver */
     uint64_t spec_seq; /* open: the seq of the next record to submit (ahead of seq while windows are in flight) */
     size_t zero_copy_bytes;
-    int direct_dma; /* registered windows move by DMA to and from device memory (1) or are read in place (0, default) */
+    int direct_dma; /* registered windows move by DMA to and from device memory (1), are read in place (0, default), or
+                     * the inputs move by DMA and the outputs are written in place (2) */
     rl_region_t reg[RL_MAX_REGIONS];
     size_t nreg;
     rl_slot_t slot[RL_SLOTS];
@@ -325,7 +329,7 @@ int ptls_mi355x_record_layer_rekey(ptls_mi355x_record_layer_t *rl, const void *k
 int ptls_mi355x_record_layer_set_direct_dma(ptls_mi355x_record_layer_t *rl, int on)
 {
     const int prev = rl->direct_dma;
-    rl->direct_dma = on != 0;
+    rl->direct_dma = on == PTLS_MI355X_RECORD_LAYER_DMA_IN ? on : on != 0;
     return prev;
 }
 
@@ -488,7 +492,7 @@ static int op_launch(rl_slot_t *s, const uint8_t *src_base, uint8_t *dst_base)
     rl_op_t *op = &s->op;
     uint8_t *base = op->zero_copy ? s->h_dev : s->d_buf;
     const int mapped = op->direct && !op->dma;
-    const uint8_t *src = mapped ? src_base : base + op->off_src;
+    const uint8_t *src = op->dma_in ? s->d_buf + op->off_src : mapped ? src_base : base + op->off_src;
     uint8_t *dst = op->deliver ? s->d_buf + op->off_dst : mapped ? dst_base : base + op->off_dst;
     const uint32_t *conn = op->nlayers > 1 ? (const uint32_t *)(base + up16(op->nrec * sizeof(ptls_mi355x_tls_record_t))) : NULL;
     hipError_t e;
@@ -617,20 +621,24 @@ int ptls_mi355x_record_layer_seal_submit(ptls_mi355x_record_layer_t *const *laye
                 overlap |= overlaps(frags[l][f].base, frags[l][f].len, out[m], op->part[m].wire);
         }
     }
-    const int dma = direct && layers[0]->direct_dma;
-    if (direct && !dma && overlap)
+    const int dma = direct && layers[0]->direct_dma == 1;
+    /* DMA in: the fragments copied into device memory (one copy per contiguous run) first, the wire written in place */
+    const int dma_in = direct && layers[0]->direct_dma == PTLS_MI355X_RECORD_LAYER_DMA_IN;
+    if (direct && !dma && !dma_in && overlap)
         direct = 0;
     const int packed = !direct || dma; /* fragments and records back to back in the staging / device layout */
     op->direct = direct;
     op->dma = dma;
+    op->dma_in = dma_in;
     const size_t off_conn = up16(nrec * sizeof(ptls_mi355x_tls_record_t));
     op->off_src = off_conn + (nlayers > 1 ? up16(nrec * 4) : 0);
-    op->srcbytes = packed ? srcbytes : 0;
+    op->srcbytes = packed || dma_in ? srcbytes : 0;
     op->off_dst = op->off_src + up16(op->srcbytes);
     op->dstbytes = packed ? wire : 0;
     const size_t total = op->off_dst + up16(op->dstbytes);
     op->zero_copy = (direct && !dma) || (!direct && total <= layers[0]->zero_copy_bytes);
-    if (reserve_stage(s, total) != 0 || (!op->zero_copy && reserve_device(s) != 0) || (dma && op_copies(op, nfr + nlayers) != 0))
+    if (reserve_stage(s, total) != 0 || ((!op->zero_copy || dma_in) && reserve_device(s) != 0) ||
+        ((dma || dma_in) && op_copies(op, nfr + nlayers) != 0))
         goto Fail;
     /* descriptors (offsets relative to the src / dst bases), the per-record IV differences and, unless direct, the
      * fragments back to back */
@@ -648,11 +656,11 @@ int ptls_mi355x_record_layer_seal_submit(ptls_mi355x_record_layer_t *const *laye
         for (size_t f = 0; f < p->nfrags; ++f) {
             const ptls_mi355x_iovec_t *fr = &frags[l][f];
             size_t w = 0;
-            if (!packed && fr->len != 0)
+            if (!packed && !dma_in && fr->len != 0)
                 src_off = (size_t)(dev_addr_any(layers, nlayers, fr->base, fr->len) - src_base);
             k += ptls_mi355x_tls_plan_send(fr->len, type, &sq, src_off, dst_off, s->recs + k, nrec - k, &w);
-            if (packed) {
-                if (dma)
+            if (packed || dma_in) {
+                if (dma || dma_in)
                     op_h2d(op, s->d_buf + op->off_src + src_off, fr->base, fr->len);
                 else if (fr->len != 0)
                     memcpy(s->h_buf + op->off_src + src_off, fr->base, fr->len);
@@ -753,7 +761,7 @@ static int open_submit(ptls_mi355x_record_layer_t *const *layers, size_t nlayers
         if (dst_base == NULL || dout < dst_base)
             dst_base = dout;
     }
-    const int dma = direct && layers[0]->direct_dma; /* (the input reaches the device before any output is written) */
+    const int dma = direct && layers[0]->direct_dma == 1; /* (the input reaches the device before any output is written) */
     size_t max_part = 0;
     for (size_t l = 0; l < nlayers; ++l)
         max_part = op->part[l].n > max_part ? op->part[l].n : max_part;
@@ -762,14 +770,17 @@ static int open_submit(ptls_mi355x_record_layer_t *const *layers, size_t nlayers
     const int deliver = direct && !dma && max_part <= PTLS_MI355X_DELIVER_MAX;
     if (direct && !dma && !deliver && overlap)
         direct = 0;
+    /* DMA in: the records copied into device memory (one copy per contiguous run of inputs) before the launch */
+    const int dma_in = deliver && layers[0]->direct_dma == PTLS_MI355X_RECORD_LAYER_DMA_IN;
     const int packed = !direct || dma;
     op->direct = direct;
     op->dma = dma;
     op->deliver = deliver;
+    op->dma_in = dma_in;
     op->max_part = max_part;
     const size_t off_conn = up16(nrec * sizeof(ptls_mi355x_tls_record_t));
     op->off_src = off_conn + (nlayers > 1 ? up16(nrec * 4) : 0);
-    op->srcbytes = packed ? srcbytes : 0;
+    op->srcbytes = packed || dma_in ? srcbytes : 0;
     op->off_dst = op->off_src + op->srcbytes;
     op->dstbytes = packed ? ptbytes : deliver ? slots16 : 0;
     op->off_st = op->off_dst + op->dstbytes;
@@ -778,7 +789,7 @@ static int open_submit(ptls_mi355x_record_layer_t *const *layers, size_t nlayers
     const size_t total = op->off_dp + (deliver ? nlayers * sizeof(ptls_mi355x_tls_deliver_t) : 0);
     op->zero_copy = (direct && !dma) || (!direct && total <= layers[0]->zero_copy_bytes);
     if (reserve_stage(s, total) != 0 || ((!op->zero_copy || deliver) && reserve_device(s) != 0) ||
-        (dma && op_copies(op, nlayers) != 0))
+        ((dma || dma_in) && op_copies(op, nlayers) != 0))
         goto Fail;
     ptls_mi355x_tls_deliver_t *dp = (ptls_mi355x_tls_deliver_t *)(s->h_buf + op->off_dp);
     uint32_t *conn = (uint32_t *)(s->h_buf + off_conn);
@@ -789,7 +800,13 @@ static int open_submit(ptls_mi355x_record_layer_t *const *layers, size_t nlayers
         if (p->n == 0)
             continue;
         if (deliver) {
-            p->src_add = (uint64_t)(dev_addr_any(layers, nlayers, in[l], p->cons) - src_base);
+            if (dma_in) { /* the input's packed place in device memory */
+                p->src_add = so;
+                op_h2d(op, s->d_buf + op->off_src + so, in[l], p->cons);
+                so += up16(p->cons);
+            } else {
+                p->src_add = (uint64_t)(dev_addr_any(layers, nlayers, in[l], p->cons) - src_base);
+            }
             p->dst_add = dso;
             /* every slot 16-aligned in the device buffer (parse_records packed them): the delivery kernel's copies
              * of whole-block plaintexts then run on 16-byte accesses */

@@ -4,7 +4,7 @@
  * itself would drive it (its send loop, lib/rapido.c:2176-2301, keeps many windows moving; a window is 16 records of
  * 16 KiB, :2115-2126).
  *
- *   rl_stream [nwin] [depth] [key_bytes] [transport: direct|dma|zero_copy|copy] [windows per launch] [one]
+ *   rl_stream [nwin] [depth] [key_bytes] [transport: direct|dma|dma_in|zero_copy|copy] [windows per launch] [one]
  *   (windows per launch > 1: windows of that many connections per launch, or with "one" consecutive windows of one
  *   connection)
  *
@@ -36,6 +36,7 @@ static void on_fault(int sig)
 #define FRAG 16384
 #define WIRE_WIN (WIN * (FRAG + PTLS_MI355X_TLS_OVERHEAD))
 #define PT_WIN (WIN * (FRAG + 1))
+#define MAXM 16 /* windows per launch */
 
 static double now(void)
 {
@@ -61,7 +62,7 @@ static void die(const char *what)
 
 typedef struct {
     ptls_mi355x_record_layer_t *tx, *rx;
-    ptls_mi355x_record_layer_t *txs[8], *rxs[8]; /* multi: the windows of `multi` connections per launch */
+    ptls_mi355x_record_layer_t *txs[MAXM], *rxs[MAXM]; /* multi: the windows of `multi` connections per launch */
     size_t multi;
     uint8_t *send, *wire, *pt;
     ptls_mi355x_iovec_t (*frags)[WIN];
@@ -81,8 +82,8 @@ static double pass(stream_t *st, int seal, size_t depth, size_t max_inflight_see
     const double t0 = now();
     for (size_t w = 0; w < st->nwin + depth; ++w) {
         if (tail - head == depth || (w >= st->nwin && tail != head)) {
-            size_t outlen[8], nrec[8], cons[8];
-            int alert[8];
+            size_t outlen[MAXM], nrec[MAXM], cons[MAXM];
+            int alert[MAXM];
             if (ptls_mi355x_record_layer_wait(st->multi > 1 ? (seal ? st->txs[0] : st->rxs[0]) : rl, tickets[head % 64], outlen,
                                               nrec, cons, alert) != 0)
                 die("wait");
@@ -97,10 +98,10 @@ static double pass(stream_t *st, int seal, size_t depth, size_t max_inflight_see
         if (w >= st->nwin)
             continue;
         if (st->multi > 1) { /* windows w .. w + multi - 1 as `multi` connections of one launch (_multi) */
-            const ptls_mi355x_iovec_t *f[8];
-            size_t nf[8], cap[8], inlen[8], parsed[8];
-            void *out[8];
-            const void *in[8];
+            const ptls_mi355x_iovec_t *f[MAXM];
+            size_t nf[MAXM], cap[MAXM], inlen[MAXM], parsed[MAXM];
+            void *out[MAXM];
+            const void *in[MAXM];
             for (size_t c = 0; c < st->multi; ++c) {
                 f[c] = st->frags[w + c];
                 nf[c] = WIN;
@@ -142,9 +143,9 @@ int main(int argc, char **argv)
     const char *transport = argc > 4 ? argv[4] : "direct";
     const size_t multi = argc > 5 ? (size_t)atoi(argv[5]) : 1; /* windows per launch (_multi) */
     const int one_conn = argc > 6 && strcmp(argv[6], "one") == 0; /* ... of one connection instead of `multi` */
-    if (depth < 1 || depth > 4 || nwin < 1 || (key_bytes != 16 && key_bytes != 32) || multi < 1 || multi > 8 ||
+    if (depth < 1 || depth > 4 || nwin < 1 || (key_bytes != 16 && key_bytes != 32) || multi < 1 || multi > MAXM ||
         nwin % multi != 0) {
-        fprintf(stderr, "usage: rl_stream [nwin] [depth 1..4] [16|32] [direct|dma|zero_copy|copy]\n");
+        fprintf(stderr, "usage: rl_stream [nwin] [depth 1..4] [16|32] [direct|dma|dma_in|zero_copy|copy] [windows per launch 1..16] [one]\n");
         return 2;
     }
     signal(SIGSEGV, on_fault);
@@ -186,19 +187,21 @@ int main(int argc, char **argv)
             (st.rxs[c] = ptls_mi355x_record_layer_new(key, key_bytes, civ, 0)) == NULL)
             die("record_layer_new");
     }
-    ptls_mi355x_record_layer_t *all[18] = {st.tx, st.rx};
+    ptls_mi355x_record_layer_t *all[2 + 2 * MAXM] = {st.tx, st.rx};
     size_t nall = 2;
     for (size_t c = 0; multi > 1 && c < (one_conn ? 1 : multi); ++c) {
         all[nall++] = st.txs[c];
         all[nall++] = st.rxs[c];
     }
     for (size_t i = 0; i < nall; ++i) {
-        if (strcmp(transport, "direct") == 0 || strcmp(transport, "dma") == 0) {
+        if (strcmp(transport, "direct") == 0 || strcmp(transport, "dma") == 0 || strcmp(transport, "dma_in") == 0) {
             if (ptls_mi355x_record_layer_register(all[i], st.send, nwin * WIN * FRAG) != 0 ||
                 ptls_mi355x_record_layer_register(all[i], st.wire, nwin * WIRE_WIN) != 0 ||
                 ptls_mi355x_record_layer_register(all[i], st.pt, nwin * PT_WIN) != 0)
                 die("register");
-            ptls_mi355x_record_layer_set_direct_dma(all[i], strcmp(transport, "dma") == 0);
+            ptls_mi355x_record_layer_set_direct_dma(all[i], strcmp(transport, "dma") == 0      ? 1
+                                                            : strcmp(transport, "dma_in") == 0 ? PTLS_MI355X_RECORD_LAYER_DMA_IN
+                                                                                                : 0);
         } else if (strcmp(transport, "copy") == 0) {
             ptls_mi355x_record_layer_set_zero_copy_bytes(all[i], 0);
         }

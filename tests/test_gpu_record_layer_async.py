@@ -21,8 +21,9 @@ from test_gpu_record_layer import conn_iv, oracle_window, page_buffer
 pytestmark = pytest.mark.gpu
 
 # direct: registered buffers read in place by the kernels, plaintexts written by the delivery kernel (the default);
-# direct_dma: registered buffers moved by DMA around a device-resident launch; zero_copy / copy: the layer's staging
-TRANSPORTS = ["direct", "direct_dma", "zero_copy", "copy"]
+# direct_dma: registered buffers moved by DMA around a device-resident launch; direct_dma_in: the inputs moved by DMA,
+# the outputs written in place (seal's wire records, an open's delivery kernel); zero_copy / copy: the layer's staging
+TRANSPORTS = ["direct", "direct_dma", "direct_dma_in", "zero_copy", "copy"]
 LIMIT = ra.RECORD_LAYER_SEQ_LIMIT
 KEY_UPDATE_MSG = bytes([24, 0, 0, 1, 0])  # handshake KeyUpdate, update_not_requested (RFC 8446 sec. 4.6.3)
 
@@ -37,7 +38,7 @@ class Host:
         if transport.startswith("direct"):
             for rl in layers:
                 rl.register(self.buf)
-                rl.set_direct_dma(transport == "direct_dma")
+                rl.set_direct_dma(ra.RECORD_LAYER_DMA_IN if transport == "direct_dma_in" else transport == "direct_dma")
         for rl in layers:
             if transport == "copy":
                 rl.set_zero_copy_bytes(0)
@@ -247,7 +248,7 @@ def test_async_rekey_and_free_with_pending(gpu):
     tx.close()  # frees with a window never waited for
 
 
-@pytest.mark.parametrize("transport", ["direct", "zero_copy"])
+@pytest.mark.parametrize("transport", ["direct", "direct_dma_in", "zero_copy"])
 def test_one_connection_windows_in_one_launch(gpu, transport):
     """A layer given several times in one _multi call: its consecutive windows in one launch, each behind the one
     before (the same bytes as one seal after another); a receive window that stops early leaves the same
@@ -286,3 +287,24 @@ def test_one_connection_windows_in_one_launch(gpu, transport):
     assert [r[:2] for r in res] == [(0, b"".join(wins_b[k])) for k in (0, 2, 3)] and rx.seq == 35
     for rl in (tx, other, rx, rx1):
         rl.close()
+
+
+@pytest.mark.parametrize("transport", ["direct", "direct_dma_in"])
+def test_seal_output_over_its_fragments(gpu, transport):
+    """A window sealed over its own fragments (the output range starts at the first fragment): direct mode takes the
+    staging for it, DMA-in copies the fragments to the device first; both give ptls_send's bytes."""
+    rng = np.random.default_rng(77)
+    key, iv = rng.integers(0, 256, 16, dtype=np.uint8).tobytes(), rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    tx = ra.RecordLayer(key, iv, seq=11)
+    h = Host(transport, [tx], 1 << 20)
+    frags_b = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in (16384, 3000, 1, 16384)]
+    region = h.take(sum(len(f) + ra.TLS_OVERHEAD for f in frags_b))
+    frags, pos = [], 0
+    for f in frags_b:
+        region[pos:pos + len(f)] = np.frombuffer(f, np.uint8)
+        frags.append(region[pos:pos + len(f)])
+        pos += len(f)
+    olen, nrec = tx.seal_into(frags, region)
+    want, seq = oracle_window(key, iv, 11, frags_b)
+    assert region[:olen].tobytes() == want and nrec == 4 and tx.seq == seq
+    tx.close()

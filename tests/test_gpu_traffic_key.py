@@ -20,7 +20,7 @@ HARNESS = os.path.join(ROOT, "oracle", "_ref", "ref_traffic_key_harness")
 
 
 @pytest.mark.parametrize("keylen", [16, 32])
-@pytest.mark.parametrize("transport", ["direct", "dma", "zero_copy", "copy"])
+@pytest.mark.parametrize("transport", ["direct", "dma", "dma_in", "zero_copy", "copy"])
 def test_update_traffic_key_against_picotls(gpu, transport, keylen):
     assert os.path.exists(HARNESS), "oracle/_ref/ref_traffic_key_harness not built (oracle/Makefile, needs /root/reference)"
     r = subprocess.run([HARNESS, transport, str(keylen)], capture_output=True, text=True, timeout=100)
