@@ -397,3 +397,52 @@ def test_open_stop_at_first_failure(gpu, multi):
                     assert st[i] == n and ty[i] == 23, (flags, i, st[i])
                     assert pt[a:a + n].tobytes() == frags[i], (flags, i)
     eng.close()
+
+
+def test_open_stop_at_failure_two_streams(gpu):
+    """Two STOP_AT_FAILURE opens from one context on two streams, the second launched while the first still runs: each
+    stops at its own first failure (the per-context scratch of the stop pass is ordered across streams)."""
+    import torch
+    key, iv = bytes(range(16)), bytes(range(12))
+    eng = ra.Engine(key)
+
+    def batch(n, ln, bad, seed):
+        trecs = np.zeros(n, ra.TLS_RECORD_DTYPE)
+        trecs["src"] = np.arange(n, dtype=np.uint64) * ln
+        trecs["dst"] = np.arange(n, dtype=np.uint64) * (ln + 22)
+        trecs["seq"] = np.arange(n, dtype=np.uint64) + seed
+        trecs["len"] = ln
+        trecs["type"] = 23
+        src = xorshift64star(seed, n * ln)
+        d_wire = torch.zeros(n * (ln + 22), dtype=torch.uint8, device="cuda")
+        eng.tls_seal_records(iv, dev(trecs.view(np.uint8)).data_ptr(), n, dev(src).data_ptr(), d_wire.data_ptr())
+        torch.cuda.synchronize()
+        wire = d_wire.cpu().numpy().copy()
+        wire[bad * (ln + 22) + 9] ^= 0x10
+        orecs = trecs.copy()
+        orecs["src"], orecs["dst"], orecs["len"] = trecs["dst"], np.arange(n, dtype=np.uint64) * (ln + 1), ln + 17
+        return orecs, dev(wire), src
+
+    jobs = [batch(60000, 1400, 41000, 1), batch(500, 1400, 37, 900000)]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = []
+    for (orecs, d_w, _), s in zip(jobs, streams):
+        n = len(orecs)
+        d_o = dev(orecs.view(np.uint8))
+        d_pt = torch.full((n * 1401,), 0xAA, dtype=torch.uint8, device="cuda")
+        d_st = torch.zeros(n, dtype=torch.int32, device="cuda")
+        d_ty = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        outs.append((d_o, d_pt, d_st, d_ty))
+    for (orecs, d_w, _), (d_o, d_pt, d_st, d_ty), s in zip(jobs, outs, streams):  # back to back, no sync between
+        eng.tls_open_records(iv, d_o.data_ptr(), len(orecs), d_w.data_ptr(), d_pt.data_ptr(), d_st.data_ptr(),
+                             d_ty.data_ptr(), stream=s.cuda_stream, flags=ra.OPEN_STOP_AT_FAILURE)
+    torch.cuda.synchronize()
+    for (orecs, _, src), (_, d_pt, d_st, _), bad in zip(jobs, outs, (41000, 37)):
+        st = d_st.cpu().numpy().view(np.uint32)
+        assert (st[:bad] == 1400).all() and st[bad] == ra.TLS_BAD_RECORD_MAC
+        assert (st[bad + 1:] == ra.TLS_NOT_PROCESSED).all()
+        pt = d_pt.cpu().numpy().reshape(-1, 1401)
+        assert pt[:bad, :1400].tobytes() == src[:bad * 1400].tobytes()
+        assert not pt[bad + 1:].any()
+    eng.close()
