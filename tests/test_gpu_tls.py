@@ -415,7 +415,8 @@ def test_open_stop_at_failure_two_streams(gpu):
         trecs["type"] = 23
         src = xorshift64star(seed, n * ln)
         d_wire = torch.zeros(n * (ln + 22), dtype=torch.uint8, device="cuda")
-        eng.tls_seal_records(iv, dev(trecs.view(np.uint8)).data_ptr(), n, dev(src).data_ptr(), d_wire.data_ptr())
+        d_recs, d_src = dev(trecs.view(np.uint8)), dev(src)  # alive until the seal has run
+        eng.tls_seal_records(iv, d_recs.data_ptr(), n, d_src.data_ptr(), d_wire.data_ptr())
         torch.cuda.synchronize()
         wire = d_wire.cpu().numpy().copy()
         wire[bad * (ln + 22) + 9] ^= 0x10
