@@ -80,6 +80,7 @@ enum : uint32_t {
     MAX_KERNEL_K = 8,
     GH5_CHUNKS = 26u,                 /* 5-bit tables: chunk c = bits [5c, 5c + 5) of the 128-bit X */
     GH5_BYTES = GH5_CHUNKS * 512u,    /* per chunk a 256-B row of low halves, then one of high halves */
+    GH8_BYTES = 256u * 256u,          /* 8-bit latin tables: 256 rows (byte value) x 16 slots (byte position) */
 };
 
 #ifndef GCM_GH5
@@ -95,13 +96,29 @@ enum : uint32_t {
  * ds_read_b64 does not broadcast lanes that read the same address, and random 5-bit indices put 2-4 lanes
  * on each entry.
  */
+#ifndef GCM_GH8
+#define GCM_GH8 1
+#endif
+#ifndef GCM_GH8_KR_SALU
+#define GCM_GH8_KR_SALU 1 /* GH8 rounds: rotl16 of the round keys by two SALU per key, in the round */
+#endif
+/*
+ * GCM_GH8: K = 4 with the Horner factor H^4 as 8-bit "latin" tables (gh8_* below): 16 conflict-free ds_read_b128 per
+ * multiply instead of the nibble tables' 32.  The 64 KiB table takes [0, 64K); the AES runs on the two-table image
+ * (T0 | T1) at [64K, 128K), addressed through byte 2 of the lane selector (aes_b2); the nibble tables of H^4..H^1
+ * for the closing lane scaling stay at [128K, 160K).
+ */
 template <int K>
 struct Layout {
-    static constexpr bool four_tables = K <= 4;
-    static constexpr bool gh5 = GCM_GH5 && K == 4;
+    static constexpr bool gh8 = GCM_GH8 && K == 4;
+    static constexpr bool four_tables = K <= 4 && !gh8;
+    static constexpr bool gh5 = GCM_GH5 && K == 4 && !gh8;
     static constexpr uint32_t aes_base = gh5 ? (uint32_t)GH5_BYTES : 0u;
+    /* v_perm selector of an AES address's byte 2: 0x0c = zero (image at aes_base), 0x02 = lanesel byte 2 (+64K) */
+    static constexpr uint32_t aes_b2 = gh8 ? 0x02u : 0x0cu;
     static constexpr uint32_t aes_bytes = four_tables ? 0x20000u : 0x10000u;
-    static constexpr uint32_t gh_base = aes_base + aes_bytes; /* nibble tables: slot s = H^(n_nibble - s) */
+    /* nibble tables: slot s = H^(n_nibble - s) */
+    static constexpr uint32_t gh_base = gh8 ? 0x20000u : aes_base + aes_bytes;
     static constexpr uint32_t n_nibble = gh5 ? 2u : (uint32_t)K;
     static constexpr uint32_t total = gh_base + n_nibble * GH_TABLE_BYTES;
     static constexpr bool split_scale = false; /* lane scaling by one table H^(K - slot) (lane_walk) */
@@ -693,7 +710,154 @@ __device__ __forceinline__ void aes_round_tt2_asm_x2(uint32_t ls, const uint32_t
         : "memory");
 }
 
+/*
+ * A middle round on the two-table image for the GH8 layout: the image is reached through byte 2 of the lane selector
+ * (selectors 0x0c02....), and the round key enters before the rotation, kr = rotl16(k) (wave-uniform):
+ *     column = T0[a] ^ T1[b] ^ rotl16(T0[c] ^ T1[d] ^ kr)
+ * three VALU per column (xor3, rotate, xor3) instead of aes_round_tt2_asm's four.
+ */
+__device__ __forceinline__ void aes_round_tt2k_asm(uint32_t ls, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3,
+                                                   const uint32_t *kr, uint32_t &n0, uint32_t &n1, uint32_t &n2,
+                                                   uint32_t &n3)
+{
+    uint32_t t1, t2, t3, t5, t6, t7, t9, t10, t11, t13, t14, t15;
+    asm volatile(
+        "v_perm_b32 %[n0], %[s0], %[ls], %[a0]\n\t"
+        "v_perm_b32 %[t1], %[s1], %[ls], %[a1]\n\t"
+        "v_perm_b32 %[t2], %[s2], %[ls], %[a2]\n\t"
+        "v_perm_b32 %[t3], %[s3], %[ls], %[a3]\n\t"
+        "ds_read_b32 %[n0], %[n0]\n\t"
+        "ds_read_b32 %[t1], %[t1] offset:128\n\t"
+        "ds_read_b32 %[t2], %[t2]\n\t"
+        "ds_read_b32 %[t3], %[t3] offset:128\n\t"
+        "v_perm_b32 %[n1], %[s1], %[ls], %[a0]\n\t"
+        "v_perm_b32 %[t5], %[s2], %[ls], %[a1]\n\t"
+        "v_perm_b32 %[t6], %[s3], %[ls], %[a2]\n\t"
+        "v_perm_b32 %[t7], %[s0], %[ls], %[a3]\n\t"
+        "ds_read_b32 %[n1], %[n1]\n\t"
+        "ds_read_b32 %[t5], %[t5] offset:128\n\t"
+        "ds_read_b32 %[t6], %[t6]\n\t"
+        "ds_read_b32 %[t7], %[t7] offset:128\n\t"
+        "v_perm_b32 %[n2], %[s2], %[ls], %[a0]\n\t"
+        "v_perm_b32 %[t9], %[s3], %[ls], %[a1]\n\t"
+        "v_perm_b32 %[t10], %[s0], %[ls], %[a2]\n\t"
+        "v_perm_b32 %[t11], %[s1], %[ls], %[a3]\n\t"
+        "ds_read_b32 %[n2], %[n2]\n\t"
+        "ds_read_b32 %[t9], %[t9] offset:128\n\t"
+        "ds_read_b32 %[t10], %[t10]\n\t"
+        "ds_read_b32 %[t11], %[t11] offset:128\n\t"
+        "v_perm_b32 %[n3], %[s3], %[ls], %[a0]\n\t"
+        "v_perm_b32 %[t13], %[s0], %[ls], %[a1]\n\t"
+        "v_perm_b32 %[t14], %[s1], %[ls], %[a2]\n\t"
+        "v_perm_b32 %[t15], %[s2], %[ls], %[a3]\n\t"
+        "ds_read_b32 %[n3], %[n3]\n\t"
+        "ds_read_b32 %[t13], %[t13] offset:128\n\t"
+        "ds_read_b32 %[t14], %[t14]\n\t"
+        "ds_read_b32 %[t15], %[t15] offset:128\n\t"
+        "s_waitcnt lgkmcnt(12)\n\t"
+        "v_bitop3_b32 %[t2], %[t2], %[t3], %[r0] bitop3:0x96\n\t"
+        "v_alignbit_b32 %[t2], %[t2], %[t2], 16\n\t"
+        "v_bitop3_b32 %[n0], %[n0], %[t1], %[t2] bitop3:0x96\n\t"
+        "s_waitcnt lgkmcnt(8)\n\t"
+        "v_bitop3_b32 %[t6], %[t6], %[t7], %[r1] bitop3:0x96\n\t"
+        "v_alignbit_b32 %[t6], %[t6], %[t6], 16\n\t"
+        "v_bitop3_b32 %[n1], %[n1], %[t5], %[t6] bitop3:0x96\n\t"
+        "s_waitcnt lgkmcnt(4)\n\t"
+        "v_bitop3_b32 %[t10], %[t10], %[t11], %[r2] bitop3:0x96\n\t"
+        "v_alignbit_b32 %[t10], %[t10], %[t10], 16\n\t"
+        "v_bitop3_b32 %[n2], %[n2], %[t9], %[t10] bitop3:0x96\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_bitop3_b32 %[t14], %[t14], %[t15], %[r3] bitop3:0x96\n\t"
+        "v_alignbit_b32 %[t14], %[t14], %[t14], 16\n\t"
+        "v_bitop3_b32 %[n3], %[n3], %[t13], %[t14] bitop3:0x96"
+        : [n0] "=&v"(n0), [n1] "=&v"(n1), [n2] "=&v"(n2), [n3] "=&v"(n3), [t1] "=&v"(t1), [t2] "=&v"(t2),
+          [t3] "=&v"(t3), [t5] "=&v"(t5), [t6] "=&v"(t6), [t7] "=&v"(t7), [t9] "=&v"(t9), [t10] "=&v"(t10),
+          [t11] "=&v"(t11), [t13] "=&v"(t13), [t14] "=&v"(t14), [t15] "=&v"(t15)
+        : [s0] "v"(s0), [s1] "v"(s1), [s2] "v"(s2), [s3] "v"(s3), [ls] "v"(ls), [r0] "s"(kr[0]), [r1] "s"(kr[1]),
+          [r2] "s"(kr[2]), [r3] "s"(kr[3]), [a0] "s"(0x0c020400u), [a1] "s"(0x0c020500u), [a2] "s"(0x0c020600u),
+          [a3] "s"(0x0c020700u)
+        : "memory");
+}
+
 #endif
+
+/*
+ * 8-bit latin GHASH tables (Layout<4>::gh8).  Multiplication by a constant c is GF(2)-linear, so
+ * X * c = XOR over the 16 byte positions p of T_p[X_p], T_p[e] = (e at byte p of X) * c.  The 64 KiB table at LDS 0 has
+ * T_p[e] at row e (256 B, one full bank row of the 64 banks), slot p: bank group p.  A ds_read_b128 is served 16
+ * consecutive lanes at a time; lane i (= lane & 15) takes, at read r (0..15), byte position r ^ i of its X, so the 16
+ * lanes of a pass always hit 16 distinct bank groups, whatever their bytes: conflict-free, 16 reads per multiply
+ * against the nibble tables' 32 (whose rows are per nibble position, so 16 lanes on one row conflict only through
+ * equal entries, which broadcast).  The lane multiplies X with its bytes permuted by i (gh8_rotate: byte r of Xr =
+ * byte r ^ i of X; 8 v_cndmask swap the dwords, 4 v_perm with a lane selector swap the bytes); read r's address is one
+ * v_perm of byte r & 3 of dword r >> 2 and of byte r & 3 of C_q = Ci ^ K_q (q = r >> 2, one v_xor per four reads),
+ * ((r ^ i) << 4).  The product is the same for every i (measured bit-exact against the nibble tables by
+ * scripts/probe_gh8.py, and through every batch-kernel suite).
+ */
+struct Gh8Lane {
+    uint32_t selL; /* v_perm selector: byte b <- byte b ^ (i & 3) */
+    uint32_t Ci;   /* (i << 4) in every byte */
+    bool q1, q2;   /* bits 2 and 3 of i: the dword swaps */
+};
+
+GCM_HD Gh8Lane gh8_lane(uint32_t i)
+{
+    Gh8Lane L;
+    i &= 15u;
+    L.selL = 0x03020100u ^ ((i & 3u) * 0x01010101u);
+    L.Ci = (i << 4) * 0x01010101u;
+    L.q1 = (i & 4u) != 0u;
+    L.q2 = (i & 8u) != 0u;
+    return L;
+}
+
+/* byte r of the result = byte r ^ i of X */
+GCM_HD u32x4 gh8_rotate(const u32x4 &X, const Gh8Lane &L)
+{
+    const uint32_t v0 = L.q1 ? X[1] : X[0], v1 = L.q1 ? X[0] : X[1], v2 = L.q1 ? X[3] : X[2], v3 = L.q1 ? X[2] : X[3];
+    const uint32_t w0 = L.q2 ? v2 : v0, w1 = L.q2 ? v3 : v1, w2 = L.q2 ? v0 : v2, w3 = L.q2 ? v1 : v3;
+    return u32x4{perm(w0, w0, L.selL), perm(w1, w1, L.selL), perm(w2, w2, L.selL), perm(w3, w3, L.selL)};
+}
+
+/* byte s of K_q = (4q + s) << 4 */
+GCM_HDC uint32_t gh8_kq(int q)
+{
+    return ((uint32_t)(4 * q) << 4) * 0x01010101u + 0x30201000u;
+}
+
+/* reads r, r + 1 of the multiply of the rotated Xr */
+GCM_HD void gh8_issue2(const uint8_t *lds, const u32x4 &Xr, const Gh8Lane &L, int r, u32x4 g[2])
+{
+    const uint32_t C = L.Ci ^ gh8_kq(r >> 2); /* r even: both reads in dword r >> 2 */
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int rr = r + t;
+        const uint32_t sel = 0x0c0c0000u | ((uint32_t)(rr & 3) << 8) | (4u + (uint32_t)(rr & 3));
+        g[t] = lds_u32x4(lds, perm(C, Xr[rr >> 2], sel));
+    }
+}
+
+GCM_HD void gh8_acc2(const u32x4 g[2], u32x4 &P)
+{
+    P[0] = xor3_pinned(P[0], g[0][0], g[1][0]);
+    P[1] = xor3_pinned(P[1], g[0][1], g[1][1]);
+    P[2] = xor3_pinned(P[2], g[0][2], g[1][2]);
+    P[3] = xor3_pinned(P[3], g[0][3], g[1][3]);
+}
+
+/* X * H^4 from the GH8 table, not fused */
+GCM_HD u32x4 gh8_mul_lds(const uint8_t *lds, const u32x4 &X, const Gh8Lane &L)
+{
+    const u32x4 Xr = gh8_rotate(X, L);
+    u32x4 P = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {
+        u32x4 g[2];
+        gh8_issue2(lds, Xr, L, r, g);
+        gh8_acc2(g, P);
+    }
+    return P;
+}
 
 /*
  * AES of w (in place) fused with P = A * c (nibble tables of c at basereg): the GHASH reads are
@@ -739,11 +903,11 @@ GCM_HD u32x4 aes_ghash_fused(const uint8_t *lds, uint32_t lanesel, const uint32_
 #undef GCM_TB
 }
 
-/* T_t[byte kk of x] from the 4-table or the 2-table image */
-template <bool FOUR>
+/* T_t[byte kk of x] from the 4-table or the 2-table image; B2: selector of the address's byte 2 (Layout::aes_b2) */
+template <bool FOUR, uint32_t B2 = 0x0cu>
 GCM_HD uint32_t tlook(const uint8_t *lds, uint32_t lanesel, uint32_t x, uint32_t kk, int t)
 {
-    const uint32_t a = perm(x, lanesel, 0x0c0c0400u | ((4u + kk) << 8));
+    const uint32_t a = perm(x, lanesel, 0x0c000400u | (B2 << 16) | ((4u + kk) << 8));
     if (t == 0)
         return lds_u32(lds, a);
     if (t == 1)
@@ -788,33 +952,27 @@ GCM_HD void aes_round1_consts(const uint8_t *lds, uint32_t lanesel, const uint32
  * its three other terms plus the round key are constants c[4..7].  Per block: 1 + 4 table reads for
  * rounds 1-2 instead of 2 + 16.  c[0..7] are recomputed when ctr & 0xffffff00 changes.
  */
-template <bool FOUR>
+template <bool FOUR, uint32_t B2 = 0x0cu>
 GCM_HD void aes_round12_consts(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk, uint32_t iv0, uint32_t iv1,
                                uint32_t iv2, uint32_t ctr_hi, uint32_t c[8])
 {
+#define GCM_TL(x, kk, t) tlook<FOUR, B2>(lds, lanesel, (x), (kk), (t))
     /* ctr_hi = ctr & 0xffffff00 */
     const uint32_t s0 = iv0 ^ rk[0], s1 = iv1 ^ rk[1], s2 = iv2 ^ rk[2], s3 = bswap32(ctr_hi) ^ rk[3];
     const uint32_t *k = rk + 4;
-    c[0] = xor3(tlook<FOUR>(lds, lanesel, s0, 0, 0), tlook<FOUR>(lds, lanesel, s1, 1, 1),
-                tlook<FOUR>(lds, lanesel, s2, 2, 2) ^ k[0]); /* + T3[s3.b3] per block */
-    const uint32_t n1 = xor3(xor3(tlook<FOUR>(lds, lanesel, s1, 0, 0), tlook<FOUR>(lds, lanesel, s2, 1, 1), k[1]),
-                             tlook<FOUR>(lds, lanesel, s3, 2, 2), tlook<FOUR>(lds, lanesel, s0, 3, 3));
-    const uint32_t n2 = xor3(xor3(tlook<FOUR>(lds, lanesel, s2, 0, 0), tlook<FOUR>(lds, lanesel, s3, 1, 1), k[2]),
-                             tlook<FOUR>(lds, lanesel, s0, 2, 2), tlook<FOUR>(lds, lanesel, s1, 3, 3));
-    const uint32_t n3 = xor3(xor3(tlook<FOUR>(lds, lanesel, s3, 0, 0), tlook<FOUR>(lds, lanesel, s0, 1, 1), k[3]),
-                             tlook<FOUR>(lds, lanesel, s1, 2, 2), tlook<FOUR>(lds, lanesel, s2, 3, 3));
+    c[0] = xor3(GCM_TL(s0, 0, 0), GCM_TL(s1, 1, 1), GCM_TL(s2, 2, 2) ^ k[0]); /* + T3[s3.b3] per block */
+    const uint32_t n1 = xor3(xor3(GCM_TL(s1, 0, 0), GCM_TL(s2, 1, 1), k[1]), GCM_TL(s3, 2, 2), GCM_TL(s0, 3, 3));
+    const uint32_t n2 = xor3(xor3(GCM_TL(s2, 0, 0), GCM_TL(s3, 1, 1), k[2]), GCM_TL(s0, 2, 2), GCM_TL(s1, 3, 3));
+    const uint32_t n3 = xor3(xor3(GCM_TL(s3, 0, 0), GCM_TL(s0, 1, 1), k[3]), GCM_TL(s1, 2, 2), GCM_TL(s2, 3, 3));
     c[1] = n1;
     c[2] = n2;
     c[3] = n3;
     const uint32_t *k2 = rk + 8;
-    c[4] = xor3(tlook<FOUR>(lds, lanesel, n1, 1, 1), tlook<FOUR>(lds, lanesel, n2, 2, 2),
-                tlook<FOUR>(lds, lanesel, n3, 3, 3) ^ k2[0]); /* + T0[n0.b0] */
-    c[5] = xor3(tlook<FOUR>(lds, lanesel, n1, 0, 0), tlook<FOUR>(lds, lanesel, n2, 1, 1),
-                tlook<FOUR>(lds, lanesel, n3, 2, 2) ^ k2[1]); /* + T3[n0.b3] */
-    c[6] = xor3(tlook<FOUR>(lds, lanesel, n2, 0, 0), tlook<FOUR>(lds, lanesel, n3, 1, 1),
-                tlook<FOUR>(lds, lanesel, n1, 3, 3) ^ k2[2]); /* + T2[n0.b2] */
-    c[7] = xor3(tlook<FOUR>(lds, lanesel, n3, 0, 0), tlook<FOUR>(lds, lanesel, n1, 2, 2),
-                tlook<FOUR>(lds, lanesel, n2, 3, 3) ^ k2[3]); /* + T1[n0.b1] */
+    c[4] = xor3(GCM_TL(n1, 1, 1), GCM_TL(n2, 2, 2), GCM_TL(n3, 3, 3) ^ k2[0]); /* + T0[n0.b0] */
+    c[5] = xor3(GCM_TL(n1, 0, 0), GCM_TL(n2, 1, 1), GCM_TL(n3, 2, 2) ^ k2[1]); /* + T3[n0.b3] */
+    c[6] = xor3(GCM_TL(n2, 0, 0), GCM_TL(n3, 1, 1), GCM_TL(n1, 3, 3) ^ k2[2]); /* + T2[n0.b2] */
+    c[7] = xor3(GCM_TL(n3, 0, 0), GCM_TL(n1, 2, 2), GCM_TL(n2, 3, 3) ^ k2[3]); /* + T1[n0.b1] */
+#undef GCM_TL
 }
 
 /*
@@ -912,6 +1070,82 @@ GCM_HD u32x4 aes_ghash_fused_h(const uint8_t *lds, uint32_t lanesel, const uint3
     }
     return P;
 #undef GCM_TA
+}
+
+/*
+ * aes_ghash_fused_h for the GH8 layout (Layout<4>::gh8): the AES on the two-table image at 64K (selectors take byte 2
+ * of lanesel; middle rounds aes_round_tt2k_asm with kr = rotl16 of the round keys), P = A * H^4 from the GH8 table:
+ * A rotated once (gh8_rotate), its 16 reads issued two per slot -- rounds 1-2, then rounds 3..9 -- ahead of the
+ * round's asm block and accumulated after it.  Writes the keystream to w[4].
+ */
+template <int NR>
+GCM_HD u32x4 aes_gh8_fused_h(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk, const uint32_t *kr, const uint32_t *c,
+                             uint32_t ctr, uint32_t w[4], const u32x4 &A, const Gh8Lane &L)
+{
+#define GCM_TL(x, kk, t) tlook<false, 0x02u>(lds, lanesel, (x), (kk), (t))
+    const u32x4 Ar = gh8_rotate(A, L);
+    u32x4 P = {0u, 0u, 0u, 0u};
+    const uint32_t s3 = bswap32(ctr) ^ rk[3];
+    /* rounds 1 and 2 from the window constants c[0..7] (aes_round12_consts): 5 reads */
+    const uint32_t n0 = c[0] ^ GCM_TL(s3, 3, 3);
+    uint32_t s0 = c[4] ^ GCM_TL(n0, 0, 0), s1 = c[5] ^ GCM_TL(n0, 3, 3);
+    uint32_t s2 = c[6] ^ GCM_TL(n0, 2, 2), s3r = c[7] ^ GCM_TL(n0, 1, 1);
+    {
+        u32x4 g[2];
+        gh8_issue2(lds, Ar, L, 0, g);
+        gh8_acc2(g, P);
+    }
+    GCM_SCHED_FENCE();
+#pragma unroll
+    for (int r = 3; r < NR; ++r) {
+        uint32_t n[4];
+        u32x4 g[2];
+        if (r <= 9)
+            gh8_issue2(lds, Ar, L, 2 * (r - 2), g);
+#if defined(__HIP_DEVICE_COMPILE__) && GCM_ROUND_ASM
+#if GCM_GH8_KR_SALU
+        /* rotl16 of the round keys on the scalar unit, here, rather than 44-60 more live SGPRs */
+        uint32_t krr[4];
+        for (int col = 0; col < 4; ++col) {
+            uint32_t t;
+            asm("s_lshl_b32 %0, %2, 16\n\ts_pack_hh_b32_b16 %1, %2, %0" : "=&s"(t), "=s"(krr[col]) : "s"(rk[4 * r + col]));
+        }
+        aes_round_tt2k_asm(lanesel, s0, s1, s2, s3r, krr, n[0], n[1], n[2], n[3]);
+#else
+        aes_round_tt2k_asm(lanesel, s0, s1, s2, s3r, kr + 4 * r, n[0], n[1], n[2], n[3]);
+#endif
+#else
+        {
+            const uint32_t s[4] = {s0, s1, s2, s3r}, *k = rk + 4 * r;
+            for (int col = 0; col < 4; ++col)
+                n[col] = xor3(GCM_TL(s[col], 0, 0), GCM_TL(s[(col + 1) & 3], 1, 1), GCM_TL(s[(col + 2) & 3], 2, 2)) ^
+                         GCM_TL(s[(col + 3) & 3], 3, 3) ^ k[col];
+            (void)kr;
+        }
+#endif
+        if (r <= 9)
+            gh8_acc2(g, P);
+        GCM_SCHED_FENCE();
+        s0 = n[0];
+        s1 = n[1];
+        s2 = n[2];
+        s3r = n[3];
+    }
+    {
+        const uint32_t *k = rk + 4 * NR;
+        const uint32_t x[4] = {s0, s1, s2, s3r};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            /* S[x] is byte 1 (and 2) of T0[x]: all four reads from T0 */
+            const uint32_t ra = lds_u32(lds, perm(x[j], lanesel, 0x0c020400u));
+            const uint32_t rb = lds_u32(lds, perm(x[(j + 1) & 3], lanesel, 0x0c020500u));
+            const uint32_t rc = lds_u32(lds, perm(x[(j + 2) & 3], lanesel, 0x0c020600u));
+            const uint32_t rd = lds_u32(lds, perm(x[(j + 3) & 3], lanesel, 0x0c020700u));
+            w[j] = xor3(perm(rb, ra, 0x0c0c0501u), perm(rd, rc, 0x06020c0cu), k[j]);
+        }
+    }
+    return P;
+#undef GCM_TL
 }
 
 /*
@@ -1594,10 +1828,21 @@ GCM_HD u32x2 gh5_entry(const KeyImage *ki, uint32_t c, uint32_t half, uint32_t v
 GCM_HD void fill_lds(uint8_t *lds, const uint32_t *t0, const KeyImage *ki, uint32_t K, uint32_t tid, uint32_t nthr)
 {
     /* mirrors struct Layout<K> */
-    const bool gh5 = GCM_GH5 && K == 4u;
-    const uint32_t aes_base = gh5 ? (uint32_t)GH5_BYTES : 0u;
-    const uint32_t aes_bytes = K <= 4 ? 0x20000u : 0x10000u, gh_base = aes_base + aes_bytes;
+    const bool gh8 = GCM_GH8 && K == 4u;
+    const bool gh5 = GCM_GH5 && K == 4u && !gh8;
+    /* gh8: the two-table image at [64K, 128K), the GH8 table at [0, 64K) */
+    const uint32_t aes_base = gh5 ? (uint32_t)GH5_BYTES : gh8 ? 0x10000u : 0u;
+    const uint32_t aes_bytes = K <= 4 && !gh8 ? 0x20000u : 0x10000u, gh_base = gh8 ? 0x20000u : aes_base + aes_bytes;
     const uint32_t n_nibble = gh5 ? 2u : K;
+    if (gh8) {
+        /* row e, slot p: (e at byte p) * H^4 = nibble tables 2p (low nibble of e) ^ 2p + 1 (high nibble) */
+        for (uint32_t i = tid; i < GH8_BYTES / 16u; i += nthr) {
+            const uint32_t e = i >> 4, p = i & 15u;
+            const u32x4 lo = *(const u32x4 *)ki->gh[3][2u * p][e & 15u];
+            const u32x4 hi = *(const u32x4 *)ki->gh[3][2u * p + 1u][e >> 4];
+            *(u32x4 *)(lds + 16u * i) = lo ^ hi;
+        }
+    }
     for (uint32_t i = tid; i < aes_bytes / 16; i += nthr) {
         uint32_t off = i * 16, x = (off >> 8) & 0xffu;
         uint32_t v = t0[x];
@@ -1632,6 +1877,8 @@ template <int KW = 4, int SEG = 64>
 struct LayoutWin {
     static constexpr bool four_tables = false;
     static constexpr bool gh5 = false;
+    static constexpr bool gh8 = false;
+    static constexpr uint32_t aes_b2 = 0x0cu;
     static constexpr uint32_t aes_base = 0u;
     static constexpr uint32_t gh_base = 0x10000u;
     /* join tables: H^SEG (within groups of 4 segments), H^(4 SEG) (across groups); SEG = 32 adds H^256
@@ -1659,6 +1906,8 @@ struct LayoutWin {
 struct LayoutWin16 {
     static constexpr bool four_tables = false;
     static constexpr bool gh5 = false;
+    static constexpr bool gh8 = false;
+    static constexpr uint32_t aes_b2 = 0x0cu;
     static constexpr uint32_t aes_base = 0u;
     static constexpr uint32_t gh_pow1 = 0x10000u; /* H^1; H^e at gh_pow1 + (e - 1) GH_TABLE_BYTES */
     static constexpr uint32_t gh_base = 0x20000u; /* H^16 */
@@ -1732,6 +1981,8 @@ GCM_HD void fill_lds_window(uint8_t *lds, const uint32_t *t0, const KeyImage *ki
 struct LayoutSplit {
     static constexpr bool four_tables = false;
     static constexpr bool gh5 = false;
+    static constexpr bool gh8 = false;
+    static constexpr uint32_t aes_b2 = 0x0cu;
     static constexpr uint32_t aes_base = 0u;
     static constexpr uint32_t gh_pow1 = 0x10000u;
     static constexpr uint32_t gh_base = 0x20000u;  /* H^16 */
@@ -1983,8 +2234,10 @@ template <int NR, int K, bool SEAL, bool FRAME = false, class LY = Layout<K>, in
 GCM_HD u32x4 lane_walk_seg(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk, uint32_t j, const Record &rec,
                            bool valid, uint32_t Tmax, uint32_t iv0, uint32_t iv1, uint32_t iv2, const uint8_t *src,
                            uint8_t *dst, const uint8_t *aad, const uint8_t *dummy, uint32_t ctype, bool use_seg,
-                           Walk segw, uint32_t t0)
+                           Walk segw, uint32_t t0, const uint32_t *kr = nullptr)
 {
+    /* kr (LY::gh8): rotl16 of the round keys, wave-uniform (aes_round_tt2k_asm) */
+    const Gh8Lane L8 = gh8_lane(lanesel >> 2); /* lane & 15: the GH8 read order (LY::gh8) */
     /* use_seg: walk the segment segw (window kernels); otherwise the whole record (make_walk) */
     /*
      * FRAME (TLS 1.3 record framing, lib/picotls.c:621-684 and :4779-4791): the AAD is the 5-byte
@@ -2023,7 +2276,7 @@ GCM_HD u32x4 lane_walk_seg(const uint8_t *lds, uint32_t lanesel, const uint32_t 
 #if GCM_R2CACHE
     constexpr uint32_t WIN = 0xffffff00u; /* 2^8-block windows (aes_round12_consts) */
     uint32_t c1[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, c1_hi = 0u;
-    aes_round12_consts<LY::four_tables>(lds + LY::aes_base, lanesel, rk, iv0, iv1, iv2, 0u, c1);
+    aes_round12_consts<LY::four_tables, LY::aes_b2>(lds + LY::aes_base, lanesel, rk, iv0, iv1, iv2, 0u, c1);
 #else
     constexpr uint32_t WIN = 0xffff0000u; /* 2^16-block windows (aes_round1_consts) */
     uint32_t c1[4] = {0u, 0u, 0u, 0u}, c1_hi = 0u;
@@ -2182,13 +2435,16 @@ GCM_HD u32x4 lane_walk_seg(const uint8_t *lds, uint32_t lanesel, const uint32_t 
             GCM_OPAQUE(o2);
             GCM_OPAQUE(ol);
 #if GCM_R2CACHE
-            aes_round12_consts<LY::four_tables>(lds + LY::aes_base, ol, rk, o0, o1, o2, c1_hi, c1);
+            aes_round12_consts<LY::four_tables, LY::aes_b2>(lds + LY::aes_base, ol, rk, o0, o1, o2, c1_hi, c1);
 #else
             aes_round1_consts<LY::four_tables>(lds + LY::aes_base, ol, rk, o0, o1, o2, c1_hi, c1);
 #endif
         }
-        const u32x4 P =
-            aes_ghash_fused_h<NR, LY::four_tables, LY::gh5, LY::aes_base>(lds, lanesel, rk, c1, ctr, w, LY::gh_base, acc);
+        u32x4 P;
+        if constexpr (LY::gh8)
+            P = aes_gh8_fused_h<NR>(lds, lanesel, rk, kr, c1, ctr, w, acc, L8);
+        else
+            P = aes_ghash_fused_h<NR, LY::four_tables, LY::gh5, LY::aes_base>(lds, lanesel, rk, c1, ctr, w, LY::gh_base, acc);
 #endif
         const u32x4 ks = {w[0], w[1], w[2], w[3]};
 
@@ -2362,11 +2618,11 @@ template <int NR, int K, bool SEAL, bool FRAME = false, class LY = Layout<K>, in
 GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk, uint32_t j, const Record &rec, bool valid,
                        uint32_t Tmax, uint32_t iv0, uint32_t iv1, uint32_t iv2, const uint8_t *src, uint8_t *dst,
                        const uint8_t *aad, const uint8_t *dummy, uint32_t ctype = 0u, const Walk *seg = nullptr,
-                       uint32_t t0 = 0u)
+                       uint32_t t0 = 0u, const uint32_t *kr = nullptr)
 {
     return lane_walk_seg<NR, K, SEAL, FRAME, LY, PF>(lds, lanesel, rk, j, rec, valid, Tmax, iv0, iv1, iv2, src, dst, aad,
                                                      dummy, ctype, seg != nullptr, seg != nullptr ? *seg : Walk{0, 0, 0, 0},
-                                                     t0);
+                                                     t0, kr);
 }
 
 } // namespace mi355x

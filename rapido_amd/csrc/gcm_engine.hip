@@ -175,10 +175,12 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
 
     fill_lds(lds, c_tabs.t0, ki, K, threadIdx.x, blockDim.x);
 
-    uint32_t rk[4 * (NR + 1)];
+    uint32_t rk[4 * (NR + 1)], kr[4 * (NR + 1)];
 #pragma unroll
-    for (int i = 0; i < 4 * (NR + 1); ++i)
+    for (int i = 0; i < 4 * (NR + 1); ++i) {
         rk[i] = ki->rk[i];
+        kr[i] = rotl32(rk[i], 16); /* GH8 layout: the round keys of aes_round_tt2k_asm (wave-uniform) */
+    }
     __syncthreads();
 
     const uint32_t lane = threadIdx.x & 63u;
@@ -249,7 +251,7 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
         /* 16 always-readable bytes for idle prefetch slots: the first descriptor (>= 32 B, nrecs >= 1) */
         const uint8_t *dummy = (const uint8_t *)descs;
         u32x4 part = lane_walk<NR, K, SEAL, FRAME>(lds, lanesel, rk, j, rec, valid, Tmax, n0, n1, n2, src, dst, aad,
-                                                   dummy, ctype);
+                                                   dummy, ctype, nullptr, 0u, kr);
 #pragma unroll
         for (int o = GCM_LANE_MAJOR ? (int)R : 1; o < (GCM_LANE_MAJOR ? 64 : K); o <<= 1)
             part ^= shfl_xor_u32x4(part, o);

@@ -494,6 +494,39 @@ extern "C" int model_batch(int is_seal, int K, const uint8_t *key, size_t keylen
     return rc;
 }
 
+/*
+ * GH8 (gcm_core.h, Layout<4>::gh8): X * H^4 through the 8-bit latin table for every lane index i = 0..15 (the dword
+ * swaps and byte permutations of all sixteen read orders), out[16 * (16 * n + i)] for input n, against the nibble
+ * tables (out + 16 * 16 * nx).  Returns 0 when every i agrees with the nibble product, else 1 + the first bad i.
+ */
+extern "C" int model_gh8_mul(const uint8_t *key, size_t keylen, const uint8_t *x, size_t nx, uint8_t *out)
+{
+    KeyImage *ki = (KeyImage *)aligned_alloc(64, sizeof(KeyImage));
+    uint8_t *lds = (uint8_t *)aligned_alloc(256, 160u * 1024u);
+    if (build_key_image(kTabs.sbox, key, (uint32_t)keylen, ki) != 0) {
+        free(ki);
+        free(lds);
+        return -1;
+    }
+    fill_lds(lds, kTabs.t0, ki, 4u, 0, 1);
+    int rc = 0;
+    for (size_t n = 0; n < nx; ++n) {
+        u32x4 X;
+        memcpy(&X, x + 16 * n, 16);
+        const u32x4 want = ghash_mul_lds(lds, Layout<4>::gh_base, X); /* slot 0: H^4 */
+        memcpy(out + 16 * (16 * nx + n), &want, 16);
+        for (uint32_t i = 0; i < 16u; ++i) {
+            const u32x4 got = gh8_mul_lds(lds, X, gh8_lane(i));
+            memcpy(out + 16 * (16 * n + i), &got, 16);
+            if (rc == 0 && memcmp(&got, &want, 16) != 0)
+                rc = 1 + (int)i;
+        }
+    }
+    free(ki);
+    free(lds);
+    return rc;
+}
+
 /* exposes the key image (round keys, H, tables) for table-level tests */
 extern "C" int model_key_image(const uint8_t *key, size_t keylen, void *out, size_t outlen)
 {

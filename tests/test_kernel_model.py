@@ -510,3 +510,26 @@ def test_bitsliced_last_round_matches_sbox(model):
         ga, gb = a.copy(), b.copy()
         model.model_last_round_bs2(ga.ctypes.data, gb.ctypes.data, k.ctypes.data)
         assert (ga == want[0]).all() and (gb == want[1]).all()
+
+
+@pytest.mark.parametrize("keylen", [16, 32])
+def test_gh8_latin_tables_every_read_order(model, keylen):
+    """GH8 (the K = 4 batch kernels' Horner multiply, Layout<4>::gh8): X * H^4 through the 8-bit latin table for all 16
+    lane read orders (lane & 15: dword swaps and byte permutations) equals the nibble-table product and the oracle's
+    Algorithm-1 multiply by H^4."""
+    model.model_gh8_mul.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p]
+    key = bytes(range(7, 7 + keylen))
+    H = oracle.ecb(key, bytes(16))
+    h4 = oracle.gf128_mul(oracle.gf128_mul(H, H), oracle.gf128_mul(H, H))
+    rng = np.random.default_rng(keylen)
+    xs = rng.integers(0, 256, (12, 16), dtype=np.uint8)
+    xs[0] = 0
+    xs[1] = 0xFF
+    out = C.create_string_buffer(16 * 17 * len(xs))
+    assert model.model_gh8_mul(key, keylen, xs.tobytes(), len(xs), out) == 0
+    raw = out.raw
+    for n, x in enumerate(xs):
+        want = oracle.gf128_mul(x.tobytes(), h4)
+        assert raw[16 * (16 * len(xs) + n):16 * (16 * len(xs) + n + 1)] == want
+        for i in range(16):
+            assert raw[16 * (16 * n + i):16 * (16 * n + i + 1)] == want, (n, i)
