@@ -309,10 +309,12 @@ def measure(ra, wl_key, args, dev, rank, world, check):
         except (ValueError, KeyError):
             traffic = None
 
-    # the kernels' binding resource: LDS-array cycles of the T-table AES + nibble-table GHASH reads
+    # the kernels' binding resource: LDS-array cycles of the T-table AES + table GHASH reads (16 ds_read_b128 per
+    # block from the 8-bit latin tables at K = 4, 32 from the nibble tables)
     # (MI355X_MICROARCH.md LDS table: ds_read_b32 2 clk, ds_read_b128 4 clk per wave)
     b32_reads = 133 if wl["key"] == 16 else 197
-    lds_cycles_per_block = (2.0 * b32_reads + 4.0 * 32) / 64.0
+    b128_reads = ra.batch_ghash_reads()
+    lds_cycles_per_block = (2.0 * b32_reads + 4.0 * b128_reads) / 64.0
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     lds_ceiling = ncu * LDS_CLOCK_GHZ * 1e9 / lds_cycles_per_block * 16 / 1e9  # payload GB/s
     dom_payload = payload / (dom_ms * 1e-3) / 1e9
@@ -329,7 +331,7 @@ def measure(ra, wl_key, args, dev, rank, world, check):
         "lds_roofline": {"bound": "lds", "kernel": kname, "achieved": round(dom_payload, 1),
                          "peak": round(lds_ceiling, 1), "unit": "GB/s payload",
                          "frac": round(dom_payload / lds_ceiling, 4),
-                         "model": f"{b32_reads} ds_read_b32 + 32 ds_read_b128 per 16-B block = "
+                         "model": f"{b32_reads} ds_read_b32 + {b128_reads} ds_read_b128 per 16-B block = "
                                   f"{lds_cycles_per_block:.2f} LDS clk/block/CU, {ncu} CU x {LDS_CLOCK_GHZ} GHz",
                          "note": "this read mix alone sustains 0.78 of the nominal rate (profiles/r01c_lds_ceiling.json)"},
     }

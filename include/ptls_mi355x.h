@@ -485,6 +485,10 @@ uint32_t ptls_mi355x_set_work_ticket_origin(uint32_t origin);
 /* name of the kernel symbol a launch of n records with these parameters uses on the current device (framing:
  * the section-4 entry points) -- the same selection launch_batch makes (for profiling and reports) */
 const char *ptls_mi355x_kernel_name(int is_seal, size_t key_size, size_t n, int framing);
+/* LDS table reads (ds_read_b128) per 16-byte block of the batch kernels' GHASH Horner multiply at k lanes per record:
+ * 16 with the 8-bit latin tables (k = 4), 32 with the nibble tables; -1 for an invalid k
+ * (for the LDS roofline in reports) */
+int ptls_mi355x_batch_ghash_reads(int k);
 /* last HIP error string seen by the engine ("" if none) */
 const char *ptls_mi355x_last_error(void);
 

@@ -56,6 +56,7 @@ EXPORTED_FUNCTIONS = (
     "ptls_mi355x_seal_batch", "ptls_mi355x_open_batch", "ptls_mi355x_order_by_length",
     "ptls_mi355x_seal_batch_ordered", "ptls_mi355x_open_batch_ordered", "ptls_mi355x_set_lanes_per_record",
     "ptls_mi355x_get_lanes_per_record", "ptls_mi355x_kernel_name", "ptls_mi355x_last_error",
+    "ptls_mi355x_batch_ghash_reads",
     "ptls_mi355x_tls_seal_records", "ptls_mi355x_tls_open_records", "ptls_mi355x_tls_seal_records_multi",
     "ptls_mi355x_tls_open_records_multi", "ptls_mi355x_set_tls_window_records",
     "ptls_mi355x_set_aead_window_records", "ptls_mi355x_set_slot_zero_copy_bytes",
@@ -768,6 +769,11 @@ def set_split_records(n: int) -> int:
 def set_work_ticket_origin(origin: int) -> int:
     """Contexts created afterwards start their batch work counters at `origin` (diagnostics: the 2^32 wrap)."""
     return lib().ptls_mi355x_set_work_ticket_origin(origin & 0xFFFFFFFF)
+
+
+def batch_ghash_reads(k: int = 0) -> int:
+    """ds_read_b128 per block of the batch kernels' Horner multiply at k lanes per record (0: the current setting)."""
+    return int(lib().ptls_mi355x_batch_ghash_reads(int(k or lib().ptls_mi355x_get_lanes_per_record())))
 
 
 def kernel_name(is_seal: bool, key_size: int, n: int, framing: bool = False) -> str:

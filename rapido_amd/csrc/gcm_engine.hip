@@ -1753,6 +1753,17 @@ size_t ptls_mi355x_set_slot_zero_copy_bytes(size_t n)
     return prev;
 }
 
+int ptls_mi355x_batch_ghash_reads(int k)
+{
+    switch (k) {
+    case 1: return Layout<1>::gh8 ? 16 : 32;
+    case 2: return Layout<2>::gh8 ? 16 : 32;
+    case 4: return Layout<4>::gh8 ? 16 : 32;
+    case 8: return Layout<8>::gh8 ? 16 : 32;
+    default: return -1;
+    }
+}
+
 const char *ptls_mi355x_kernel_name(int is_seal, size_t key_size, size_t n, int framing)
 {
     int dev = 0, ncu = 0;

@@ -35,7 +35,9 @@ VARIANTS = {
     "gh5": ["-DGCM_GH5=1", "-DGCM_GH8=0"],
     # r03: the nibble-table H^4 Horner (four T-table images) against the 8-bit latin tables (two T-table images)
     "nogh8": ["-DGCM_GH8=0"],
-    "gh8": ["-DGCM_GH8=1"],  # 5-bit ds_read_b64 GHASH tables for K = 4 (evaluated: 33% slower, bank conflicts)
+    "gh8": ["-DGCM_GH8=1"],
+    "gh8pair": ["-DGCM_GH8=1", "-DGCM_PAIR_STORES=1"],
+    "gh8nt": ["-DGCM_GH8=1", "-DGCM_NT_LOADS=1"],  # 5-bit ds_read_b64 GHASH tables for K = 4 (evaluated: 33% slower, bank conflicts)
     # "@src=DIR": compile gcm_engine.hip from DIR (e.g. a `git show` of an older revision) instead of csrc/
     "head": ["@src=" + os.path.join(VDIR, "src_head")],
     "no_ghash": ["-DGCM_ABLATE_GHASH=1"],
