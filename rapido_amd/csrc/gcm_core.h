@@ -794,10 +794,16 @@ __device__ __forceinline__ void aes_round_tt2k_asm(uint32_t ls, uint32_t s0, uin
  * ((r ^ i) << 4).  The product is the same for every i (measured bit-exact against the nibble tables by
  * scripts/probe_gh8.py, and through every batch-kernel suite).
  */
+#ifndef GCM_GH8_LANESEL
+#define GCM_GH8_LANESEL 0 /* 1: the byte part of the permutation in per-lane address selectors (4 VGPRs, 4 VALU less) */
+#endif
 struct Gh8Lane {
     uint32_t selL; /* v_perm selector: byte b <- byte b ^ (i & 3) */
     uint32_t Ci;   /* (i << 4) in every byte */
     bool q1, q2;   /* bits 2 and 3 of i: the dword swaps */
+#if GCM_GH8_LANESEL
+    uint32_t selv[4]; /* read 4q + s: address byte 1 <- byte s ^ (i & 3) of dword q, byte 0 <- byte s of C_q */
+#endif
 };
 
 GCM_HD Gh8Lane gh8_lane(uint32_t i)
@@ -808,15 +814,23 @@ GCM_HD Gh8Lane gh8_lane(uint32_t i)
     L.Ci = (i << 4) * 0x01010101u;
     L.q1 = (i & 4u) != 0u;
     L.q2 = (i & 8u) != 0u;
+#if GCM_GH8_LANESEL
+    for (uint32_t t = 0; t < 4u; ++t)
+        L.selv[t] = 0x0c0c0000u | ((t ^ (i & 3u)) << 8) | (4u + t);
+#endif
     return L;
 }
 
-/* byte r of the result = byte r ^ i of X */
+/* byte r of the result = byte r ^ i of X (GCM_GH8_LANESEL: only the dwords; the bytes by the address selectors) */
 GCM_HD u32x4 gh8_rotate(const u32x4 &X, const Gh8Lane &L)
 {
     const uint32_t v0 = L.q1 ? X[1] : X[0], v1 = L.q1 ? X[0] : X[1], v2 = L.q1 ? X[3] : X[2], v3 = L.q1 ? X[2] : X[3];
     const uint32_t w0 = L.q2 ? v2 : v0, w1 = L.q2 ? v3 : v1, w2 = L.q2 ? v0 : v2, w3 = L.q2 ? v1 : v3;
+#if GCM_GH8_LANESEL
+    return u32x4{w0, w1, w2, w3};
+#else
     return u32x4{perm(w0, w0, L.selL), perm(w1, w1, L.selL), perm(w2, w2, L.selL), perm(w3, w3, L.selL)};
+#endif
 }
 
 /* byte s of K_q = (4q + s) << 4 */
@@ -832,7 +846,11 @@ GCM_HD void gh8_issue2(const uint8_t *lds, const u32x4 &Xr, const Gh8Lane &L, in
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
         const int rr = r + t;
+#if GCM_GH8_LANESEL
+        const uint32_t sel = L.selv[rr & 3];
+#else
         const uint32_t sel = 0x0c0c0000u | ((uint32_t)(rr & 3) << 8) | (4u + (uint32_t)(rr & 3));
+#endif
         g[t] = lds_u32x4(lds, perm(C, Xr[rr >> 2], sel));
     }
 }

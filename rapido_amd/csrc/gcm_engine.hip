@@ -159,6 +159,9 @@ static_assert(sizeof(TlsRecord) == sizeof(ptls_mi355x_tls_record_t), "descriptor
  * type) || tag at dst (lib/picotls.c:630-643,658-684), open verifies header-framed records and
  * strips padding / pops the content type (lib/picotls.c:4779-4791) into status / types.
  */
+#ifndef GCM_BATCH_PF
+#define GCM_BATCH_PF 3 /* batch kernels: loads issued three steps ahead, four buffers (1: one step ahead, two buffers) */
+#endif
 template <int NR, int K, bool SEAL, bool FRAME>
 __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2,
                                                const void *__restrict__ descs, const uint32_t *__restrict__ order,
@@ -250,8 +253,8 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
         const uint32_t n0 = conn != nullptr && in_batch ? iv0 ^ bswap32(conn[r]) : iv0;
         /* 16 always-readable bytes for idle prefetch slots: the first descriptor (>= 32 B, nrecs >= 1) */
         const uint8_t *dummy = (const uint8_t *)descs;
-        u32x4 part = lane_walk<NR, K, SEAL, FRAME>(lds, lanesel, rk, j, rec, valid, Tmax, n0, n1, n2, src, dst, aad,
-                                                   dummy, ctype, nullptr, 0u, kr);
+        u32x4 part = lane_walk<NR, K, SEAL, FRAME, Layout<K>, GCM_BATCH_PF>(lds, lanesel, rk, j, rec, valid, Tmax, n0, n1,
+                                                                           n2, src, dst, aad, dummy, ctype, nullptr, 0u, kr);
 #pragma unroll
         for (int o = GCM_LANE_MAJOR ? (int)R : 1; o < (GCM_LANE_MAJOR ? 64 : K); o <<= 1)
             part ^= shfl_xor_u32x4(part, o);
