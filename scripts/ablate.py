@@ -38,6 +38,7 @@ VARIANTS = {
     "gh8": ["-DGCM_GH8=1"],
     "gh8pair": ["-DGCM_GH8=1", "-DGCM_PAIR_STORES=1"],
     "gh8nt": ["-DGCM_GH8=1", "-DGCM_NT_LOADS=1"],
+    "pf3nt": ["-DGCM_NT_LOADS=1"],  # the default build (GH8, three-step prefetch) with non-temporal input loads
     "gh8pf3": ["-DGCM_GH8=1", "-DGCM_BATCH_PF=3"],  # batch loads three steps ahead (four buffers; the default)
     "gh8pf1": ["-DGCM_GH8=1", "-DGCM_BATCH_PF=1"],  # batch loads one step ahead (two buffers; before r03s)
     "gh8sel": ["-DGCM_GH8=1", "-DGCM_GH8_LANESEL=1"],  # GH8 byte permutation folded into per-lane address selectors  # 5-bit ds_read_b64 GHASH tables for K = 4 (evaluated: 33% slower, bank conflicts)
