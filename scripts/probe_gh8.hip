@@ -8,9 +8,8 @@
  * 64 banks) has T_p[e] in slot p, i.e. in bank group p.  A ds_read_b128 is served 16 lanes at a time; lane i
  * (= lane & 15) reads, at read r (0..15), byte position (r + i) & 15 of its X, so the 16 lanes of a pass hit 16
  * distinct bank groups whatever their bytes are: conflict-free, 16 reads per multiply instead of the nibble tables' 32.
- * The lane works on X rotated by i bytes (byte r of Xr = byte (r + i) & 15 of X: 8 v_cndmask for the word rotation
- * and 4 v_alignbit for the bytes), so read r's address is one v_perm of byte r of Xr and the lane constant
- * ((r + i) & 15) << 4.
+ * (This probe first ran a rotate-by-i read order, lane i reading position (r + i) & 15 at read r; it now runs the
+ * product's XOR order, position r ^ i, from gcm_core.h.)
  *
  * 64 KiB does not fit beside the four bank-replicated T-table images (128 KiB), so the AES runs on two of them
  * (T2 = rotl16(T0), T3 = rotl16(T1), as the K = 8 and window kernels do).  The rotated column costs one VALU more than
@@ -173,69 +172,8 @@ __device__ __forceinline__ void round_tt2b(uint32_t ls, uint32_t s0, uint32_t s1
 #undef RB_INS
 }
 
-/* lane constants of the GH8 reads: lane i = lane & 15 */
-struct Gh8Lane {
-    uint32_t sh;   /* 8 (i & 3): the byte part of the rotation */
-    uint32_t C[4]; /* byte s of C[q] = ((4q + s + i) & 15) << 4: the bank group of read 4q + s */
-    bool q1, q2;   /* bits 0 and 1 of i >> 2: the word part */
-};
-
-__device__ __forceinline__ Gh8Lane gh8_lane(uint32_t lane)
-{
-    Gh8Lane L;
-    const uint32_t i = lane & 15u;
-    L.sh = 8u * (i & 3u);
-    for (uint32_t q = 0; q < 4u; ++q) {
-        uint32_t c = 0;
-        for (uint32_t s = 0; s < 4u; ++s)
-            c |= (((4u * q + s + i) & 15u) << 4) << (8u * s);
-        L.C[q] = c;
-    }
-    L.q1 = (i & 4u) != 0u;
-    L.q2 = (i & 8u) != 0u;
-    return L;
-}
-
-/* byte r of the result = byte (r + i) & 15 of X */
-__device__ __forceinline__ u32x4 gh8_rotate(const u32x4 &X, const Gh8Lane &L)
-{
-    const uint32_t v0 = L.q1 ? X[1] : X[0], v1 = L.q1 ? X[2] : X[1], v2 = L.q1 ? X[3] : X[2], v3 = L.q1 ? X[0] : X[3];
-    const uint32_t w0 = L.q2 ? v2 : v0, w1 = L.q2 ? v3 : v1, w2 = L.q2 ? v0 : v2, w3 = L.q2 ? v1 : v3;
-    return u32x4{alignbit(w1, w0, L.sh), alignbit(w2, w1, L.sh), alignbit(w3, w2, L.sh), alignbit(w0, w3, L.sh)};
-}
-
-/* reads r, r + 1 of a GH8 multiply of the rotated Xr */
-__device__ __forceinline__ void gh8_issue2(const uint8_t *lds, const u32x4 &Xr, const Gh8Lane &L, int r, u32x4 g[2])
-{
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        const int rr = r + t;
-        const uint32_t sel = 0x0c0c0000u | ((uint32_t)(rr & 3) << 8) | (4u + (uint32_t)(rr & 3));
-        g[t] = lds_u32x4(lds, GH8_BASE + perm(L.C[rr >> 2], Xr[rr >> 2], sel));
-    }
-}
-
-__device__ __forceinline__ void acc2(const u32x4 g[2], u32x4 &P)
-{
-    P[0] = xor3_pinned(P[0], g[0][0], g[1][0]);
-    P[1] = xor3_pinned(P[1], g[0][1], g[1][1]);
-    P[2] = xor3_pinned(P[2], g[0][2], g[1][2]);
-    P[3] = xor3_pinned(P[3], g[0][3], g[1][3]);
-}
-
-/* X * H^4 from the GH8 table (not fused) */
-__device__ u32x4 gh8_mul(const uint8_t *lds, const u32x4 &X, const Gh8Lane &L)
-{
-    const u32x4 Xr = gh8_rotate(X, L);
-    u32x4 P = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int r = 0; r < 16; r += 2) {
-        u32x4 g[2];
-        gh8_issue2(lds, Xr, L, r, g);
-        acc2(g, P);
-    }
-    return P;
-}
+/* the GH8 read order, rotation and reads are the product's own (gcm_core.h: Gh8Lane, gh8_lane, gh8_rotate,
+ * gh8_issue2, gh8_acc2, gh8_mul_lds; round 3's first probe used a rotate-by-i variant with 4 lane constants) */
 
 /*
  * AES-CTR on the two-table image B fused with P = A * H^4 (GH: 0 none, 1 nibble tables at NIB_BASE, 2 GH8):
@@ -259,7 +197,7 @@ __device__ __forceinline__ u32x4 fused_b(const uint8_t *lds, uint32_t lanesel, c
     if (GH == 2) {
         u32x4 g[2];
         gh8_issue2(lds, Ar, L, 0, g);
-        acc2(g, P);
+        gh8_acc2(g, P);
     }
     GCM_SCHED_FENCE();
 #pragma unroll
@@ -279,7 +217,7 @@ __device__ __forceinline__ u32x4 fused_b(const uint8_t *lds, uint32_t lanesel, c
         if (GH == 1 && gh)
             ghash_quarter_acc(g, P);
         if (GH == 2 && gh)
-            acc2(g, P);
+            gh8_acc2(g, P);
         GCM_SCHED_FENCE();
         s0 = m0;
         s1 = m1;
@@ -352,7 +290,7 @@ __device__ void run_body(const KeyImage *ki, uint32_t nunits, uint32_t *work, ui
     const uint32_t lane = threadIdx.x & 63u;
     const bool four = MODE == 0 || MODE == 2;
     const uint32_t lanesel = (lane & 31u) * 4u | 0x10000u;
-    const Gh8Lane L = gh8_lane(lane);
+    const Gh8Lane L = gh8_lane(lane & 15u);
     const uint32_t iv0 = 0x03020100u ^ lane, iv1 = 0x07060504u ^ blockIdx.x, iv2 = 0x0b0a0908u ^ (threadIdx.x >> 6);
     uint32_t c1[8];
     if (four)
@@ -421,11 +359,11 @@ extern "C" __global__ __launch_bounds__(64) void probe_gh8_check(const KeyImage 
     fill(lds, ki, 3);
     __syncthreads();
     const uint32_t lane = threadIdx.x;
-    const Gh8Lane L = gh8_lane(lane);
+    const Gh8Lane L = gh8_lane(lane & 15u);
     u32x4 A = {0u, 0u, 0u, 0u}, B = {0u, 0u, 0u, 0u};
     for (uint32_t s = 0; s < S; ++s) {
         const u32x4 d = data[s * 64u + lane];
-        A = gh8_mul(lds, A ^ d, L);
+        A = gh8_mul_lds(lds, A ^ d, L);
         B = ghash_mul_lds(lds, (NIB_BASE >> 8) << 8, B ^ d);
     }
     out[lane] = A;
