@@ -246,6 +246,15 @@ GCM_HD uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
 #else
 #define GCM_OPAQUE(x) ((void)0)
 #endif
+/* x as a wave-uniform (scalar) value: lane 0's copy; the host kernel model runs one lane at a time */
+GCM_HD uint32_t wave_uniform(uint32_t x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_readfirstlane(x);
+#else
+    return x;
+#endif
+}
 
 GCM_HD uint32_t lds_u32(const uint8_t *lds, uint32_t addr) { return *(const uint32_t *)(lds + addr); }
 GCM_HD u32x4 lds_u32x4(const uint8_t *lds, uint32_t addr) { return *(const u32x4 *)(lds + addr); }
@@ -1493,6 +1502,21 @@ GCM_HD uint32_t walk_scale_slot(const Walk &w, uint32_t j, uint32_t K, uint32_t 
     return K - (uint32_t)(end - q_last);
 }
 
+/*
+ * Interior steps of lane j's walk: [lo, hi), the steps t whose position holds a whole payload block read from the
+ * input, 0 <= c < len / 16 with c = j + K t - pad - A (len: the payload bytes taken from the input; a FRAME seal's
+ * content-type byte is not one).  In those steps lane_walk's step is: counter c + 2, load at in + 16 c, store at
+ * out + 16 c, chain ^= ciphertext -- nothing else.  The batch kernels intersect the lanes' ranges over the wave
+ * (gcm_batch_body) and pass it to lane_walk, which then takes that path by a scalar branch.
+ */
+GCM_HD void walk_interior(const Walk &w, uint32_t j, uint32_t K, uint32_t len, uint32_t &lo, uint32_t &hi)
+{
+    const int32_t cb = (int32_t)j - (int32_t)w.pad - (int32_t)w.A; /* c(t) = cb + K t */
+    const int32_t nfull = (int32_t)(len >> 4), k = (int32_t)K;
+    lo = cb >= 0 ? 0u : (uint32_t)((k - 1 - cb) / k);          /* ceil(-cb / K): c >= 0 */
+    hi = nfull > cb ? (uint32_t)((nfull - cb + k - 1) / k) : 0u; /* K t < nfull - cb: c < nfull */
+}
+
 /* the walk's output alignment key: the payload output address in 16-byte units */
 GCM_HD uint32_t walk_out16(const uint8_t *out) { return (uint32_t)((uintptr_t)out >> 4); }
 
@@ -2252,9 +2276,10 @@ template <int NR, int K, bool SEAL, bool FRAME = false, class LY = Layout<K>, in
 GCM_HD u32x4 lane_walk_seg(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk, uint32_t j, const Record &rec,
                            bool valid, uint32_t Tmax, uint32_t iv0, uint32_t iv1, uint32_t iv2, const uint8_t *src,
                            uint8_t *dst, const uint8_t *aad, const uint8_t *dummy, uint32_t ctype, bool use_seg,
-                           Walk segw, uint32_t t0, const uint32_t *kr = nullptr)
+                           Walk segw, uint32_t t0, const uint32_t *kr = nullptr, uint32_t f_lo = 0u, uint32_t f_hi = 0u)
 {
     /* kr (LY::gh8): rotl16 of the round keys, wave-uniform (aes_round_tt2k_asm) */
+    /* [f_lo, f_hi): interior steps of every lane of the wave (walk_interior; none by default), taken on a fast path */
     const Gh8Lane L8 = gh8_lane(lanesel >> 2); /* lane & 15: the GH8 read order (LY::gh8) */
     /* use_seg: walk the segment segw (window kernels); otherwise the whole record (make_walk) */
     /*
@@ -2306,8 +2331,12 @@ GCM_HD u32x4 lane_walk_seg(const uint8_t *lds, uint32_t lanesel, const uint32_t 
      * nothing to read load 16 harmless bytes at `dummy`): with a load in every step the compiler can wait with
      * vmcnt(1) for the current block while the next one is in flight, instead of vmcnt(0).
      */
+    const uint32_t cb = j - wk.pad - wk.A; /* payload block of step t: c = cb + K t (two's complement) */
     auto fetch_ptr = [&](uint32_t t) -> const uint8_t * {
         GCM_OPAQUE(t); /* recompute from t: no strength-reduced induction variables (VGPRs) */
+        const uint32_t tu = wave_uniform(t);
+        if (tu >= f_lo && tu < f_hi) /* interior step: every lane reads its whole payload block */
+            return in + 16u * (cb + (uint32_t)K * tu);
         return walk_fetch_ptr<K, SEAL, FRAME>(t, j, wk, rec, valid, plen, in, ad, dummy);
     };
 
@@ -2424,17 +2453,31 @@ GCM_HD u32x4 lane_walk_seg(const uint8_t *lds, uint32_t lanesel, const uint32_t 
     };
     auto step = [&](uint32_t t, u32x4 cur) {
         GCM_OPAQUE(t);
-        const int32_t p = (int32_t)(j + K * t) - (int32_t)wk.pad;
-        const bool active = valid && t < wk.T && p < (int32_t)gend;
-        const bool is_aad = active && p >= 0 && (uint32_t)p < wk.A;
-        const bool is_pay = active && (uint32_t)p >= wk.A && (uint32_t)p < wk.A + wk.C && p >= 0;
-        const bool is_len = active && (uint32_t)p == wk.A + wk.C;
-        const uint32_t c = (uint32_t)p - wk.A;
+        /*
+         * Interior step (f_lo <= t < f_hi, wave-uniform: a scalar branch): every lane seals / opens a whole payload
+         * block c, so the flags below are not evaluated; the rare cases stay on the general path.
+         */
+        const uint32_t tu = wave_uniform(t);
+        const bool fast = tu >= f_lo && tu < f_hi;
+        int32_t p = 0;
+        bool active = false, is_aad = false, is_pay = false, is_len = false;
+        uint32_t c, ctr;
+        if (fast) {
+            c = cb + (uint32_t)K * tu;
+            ctr = c + 2u;
+        } else {
+            p = (int32_t)(j + K * t) - (int32_t)wk.pad;
+            active = valid && t < wk.T && p < (int32_t)gend;
+            is_aad = active && p >= 0 && (uint32_t)p < wk.A;
+            is_pay = active && (uint32_t)p >= wk.A && (uint32_t)p < wk.A + wk.C && p >= 0;
+            is_len = active && (uint32_t)p == wk.A + wk.C;
+            c = (uint32_t)p - wk.A;
+            /* one AES per lane per step: payload counter c + 2, otherwise J0 (counter 1) */
+            ctr = is_pay ? c + 2u : 1u;
+        }
         const uint32_t clen = plen - 16u * c;    /* bytes of this payload block if < 16 */
         const uint32_t flen = rec.len - 16u * c; /* of them from the input (FRAME seal: all but the type byte) */
 
-        /* one AES per lane per step: payload counter c + 2, otherwise J0 (counter 1) */
-        uint32_t ctr = is_pay ? c + 2u : 1u;
         uint32_t w[4] = {iv0, iv1, iv2, bswap32(ctr)};
 #if GCM_ABLATE_AES && GCM_ABLATE_GHASH
         const u32x4 P = acc;
@@ -2465,6 +2508,12 @@ GCM_HD u32x4 lane_walk_seg(const uint8_t *lds, uint32_t lanesel, const uint32_t 
             P = aes_ghash_fused_h<NR, LY::four_tables, LY::gh5, LY::aes_base>(lds, lanesel, rk, c1, ctr, w, LY::gh_base, acc);
 #endif
         const u32x4 ks = {w[0], w[1], w[2], w[3]};
+        if (fast) {
+            const u32x4 o = cur ^ ks;
+            put(t, c, o);
+            acc = P ^ (SEAL ? o : cur);
+            return;
+        }
 
         u32x4 X = {0u, 0u, 0u, 0u};
         if (is_pay) {
@@ -2636,11 +2685,11 @@ template <int NR, int K, bool SEAL, bool FRAME = false, class LY = Layout<K>, in
 GCM_HD u32x4 lane_walk(const uint8_t *lds, uint32_t lanesel, const uint32_t *rk, uint32_t j, const Record &rec, bool valid,
                        uint32_t Tmax, uint32_t iv0, uint32_t iv1, uint32_t iv2, const uint8_t *src, uint8_t *dst,
                        const uint8_t *aad, const uint8_t *dummy, uint32_t ctype = 0u, const Walk *seg = nullptr,
-                       uint32_t t0 = 0u, const uint32_t *kr = nullptr)
+                       uint32_t t0 = 0u, const uint32_t *kr = nullptr, uint32_t f_lo = 0u, uint32_t f_hi = 0u)
 {
     return lane_walk_seg<NR, K, SEAL, FRAME, LY, PF>(lds, lanesel, rk, j, rec, valid, Tmax, iv0, iv1, iv2, src, dst, aad,
                                                      dummy, ctype, seg != nullptr, seg != nullptr ? *seg : Walk{0, 0, 0, 0},
-                                                     t0, kr);
+                                                     t0, kr, f_lo, f_hi);
 }
 
 } // namespace mi355x

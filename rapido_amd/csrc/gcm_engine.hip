@@ -162,6 +162,9 @@ static_assert(sizeof(TlsRecord) == sizeof(ptls_mi355x_tls_record_t), "descriptor
 #ifndef GCM_BATCH_PF
 #define GCM_BATCH_PF 3 /* batch kernels: loads issued three steps ahead, four buffers (1: one step ahead, two buffers) */
 #endif
+#ifndef GCM_FAST_STEP
+#define GCM_FAST_STEP 1 /* batch kernels: interior steps on lane_walk's fast path (scalar branch, no per-lane flags) */
+#endif
 template <int NR, int K, bool SEAL, bool FRAME>
 __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2,
                                                const void *__restrict__ descs, const uint32_t *__restrict__ order,
@@ -242,11 +245,20 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
             rec = recs[r];
         }
         const uint32_t plen = FRAME && SEAL ? rec.len + 1u : rec.len;
-        uint32_t T = valid ? make_walk(plen, rec.aadlen, K, walk_out16(dst + rec.dst)).T : 0u;
-        uint32_t Tmax = T;
+        const Walk wk = make_walk(plen, rec.aadlen, K, walk_out16(dst + rec.dst));
+        uint32_t Tmax = valid ? wk.T : 0u;
+        /* the steps in which every lane of the wave holds a whole payload block (walk_interior): lane_walk's fast path */
+        uint32_t f_lo = 0xffffffffu, f_hi = 0u;
+        if (GCM_FAST_STEP && valid)
+            walk_interior(wk, j, K, rec.len, f_lo, f_hi);
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1)
+        for (int o = 32; o >= 1; o >>= 1) {
             Tmax = max(Tmax, shfl_xor_u32(Tmax, o));
+            f_lo = max(f_lo, shfl_xor_u32(f_lo, o));
+            f_hi = min(f_hi, shfl_xor_u32(f_hi, o));
+        }
+        f_lo = __builtin_amdgcn_readfirstlane(f_lo);
+        f_hi = __builtin_amdgcn_readfirstlane(f_hi);
 
         const uint32_t n1 = iv1 ^ bswap32((uint32_t)(rec.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)rec.seq);
         /* per-connection IV (rapido derive_connection_aead_iv, lib/rapido.c:127-133): IV bytes 0..3 ^= BE32(id) */
@@ -254,7 +266,8 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
         /* 16 always-readable bytes for idle prefetch slots: the first descriptor (>= 32 B, nrecs >= 1) */
         const uint8_t *dummy = (const uint8_t *)descs;
         u32x4 part = lane_walk<NR, K, SEAL, FRAME, Layout<K>, GCM_BATCH_PF>(lds, lanesel, rk, j, rec, valid, Tmax, n0, n1,
-                                                                           n2, src, dst, aad, dummy, ctype, nullptr, 0u, kr);
+                                                                           n2, src, dst, aad, dummy, ctype, nullptr, 0u, kr,
+                                                                           f_lo, f_hi);
 #pragma unroll
         for (int o = GCM_LANE_MAJOR ? (int)R : 1; o < (GCM_LANE_MAJOR ? 64 : K); o <<= 1)
             part ^= shfl_xor_u32x4(part, o);

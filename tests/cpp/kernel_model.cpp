@@ -52,9 +52,12 @@ static void run(const KeyImage *ki, const uint8_t *lds, const uint8_t *static_iv
         Walk wk = make_walk(r.len, r.aadlen, K, walk_out16(dst + r.dst));
         uint32_t n1 = iv1 ^ bswap32((uint32_t)(r.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)r.seq);
         u32x4 tag = {0, 0, 0, 0};
-        for (uint32_t j = 0; j < (uint32_t)K; ++j)
+        for (uint32_t j = 0; j < (uint32_t)K; ++j) {
+            uint32_t f_lo, f_hi; /* the lane's own interior steps: the fast path wherever a wave could take it */
+            walk_interior(wk, j, K, r.len, f_lo, f_hi);
             tag ^= lane_walk<NR, K, SEAL>(lds, 4u * (j & 31u) | 0x10000u, ki->rk, j, r, true, wk.T, iv0, n1, n2, src, dst,
-                                          aad, (const uint8_t *)recs);
+                                          aad, (const uint8_t *)recs, 0u, nullptr, 0u, nullptr, f_lo, f_hi);
+        }
         if (SEAL) {
             memcpy(dst + r.dst + r.len, &tag, 16);
         } else {
@@ -133,9 +136,13 @@ static void run_tls(const KeyImage *ki, const uint8_t *lds, const uint8_t *stati
         uint32_t n1 = iv1 ^ bswap32((uint32_t)(r.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)r.seq);
         const uint32_t n0 = conn ? iv0 ^ bswap32(conn[i]) : iv0; /* rapido's per-connection IV */
         u32x4 tag = {0, 0, 0, 0};
-        for (uint32_t j = 0; j < (uint32_t)K; ++j)
+        for (uint32_t j = 0; j < (uint32_t)K; ++j) {
+            uint32_t f_lo, f_hi;
+            walk_interior(wk, j, K, r.len, f_lo, f_hi);
             tag ^= lane_walk<NR, K, SEAL, true>(lds, 4u * (j & 31u) | 0x10000u, ki->rk, j, r, true, wk.T, n0, n1, n2, src,
-                                                dst, nullptr, (const uint8_t *)trecs, t.type);
+                                                dst, nullptr, (const uint8_t *)trecs, t.type, nullptr, 0u, nullptr, f_lo,
+                                                f_hi);
+        }
         if (SEAL) {
             memcpy(dst + r.dst + plen, &tag, 16);
             const uint32_t reclen = plen + 16;
