@@ -57,6 +57,12 @@
 #ifndef GCM_ABLATE_GHASH
 #define GCM_ABLATE_GHASH 0
 #endif
+#ifndef GCM_SCALE_W
+#define GCM_SCALE_W 0 /* the closing scaling multiply (lane_walk): 0 compiler-paired reads, 1 two batches of 16, 2 all 32 */
+#endif
+#ifndef GCM_ABLATE_SCALE
+#define GCM_ABLATE_SCALE 0 /* measurement builds: no closing scaling multiply (wrong tags) */
+#endif
 #ifndef GCM_ABLATE_AES
 #define GCM_ABLATE_AES 0
 #endif
@@ -2674,8 +2680,9 @@ Scale:
             e -= 8u;
         }
         acc = ghash_mul_scale<LY::wide_scale>(lds, e == 16u ? LY::gh_base : LY::gh_pow1 + (e - 1u) * GH_TABLE_BYTES, acc);
-    } else {
-        acc = ghash_mul_lds(lds, LY::gh_base + walk_scale_slot(wk, j, K, end_cap) * GH_TABLE_BYTES, acc);
+    } else if (!GCM_ABLATE_SCALE) {
+        /* GCM_SCALE_W: the reads issued in two batches of 16 (1) or all 32 (2) rather than as the compiler pairs them */
+        acc = ghash_mul_join<GCM_SCALE_W>(lds, LY::gh_base + walk_scale_slot(wk, j, K, end_cap) * GH_TABLE_BYTES, acc);
     }
     GCM_WALK_STAMP(13);
     return acc ^ ek0;

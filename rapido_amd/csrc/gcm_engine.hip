@@ -162,6 +162,9 @@ static_assert(sizeof(TlsRecord) == sizeof(ptls_mi355x_tls_record_t), "descriptor
 #ifndef GCM_BATCH_PF
 #define GCM_BATCH_PF 3 /* batch kernels: loads issued three steps ahead, four buffers (1: one step ahead, two buffers) */
 #endif
+#ifndef GCM_STATIC_GROUPS
+#define GCM_STATIC_GROUPS 0
+#endif
 #ifndef GCM_FAST_STEP
 #define GCM_FAST_STEP 1 /* batch kernels: interior steps on lane_walk's fast path (scalar branch, no per-lane flags) */
 #endif
@@ -210,11 +213,19 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
      * With `order` sorted by length (ptls_mi355x_order_by_length) this is longest-first
      * scheduling, and each group holds records of similar length.
      */
+#if GCM_STATIC_GROUPS /* measurement builds: group k of wave w is w + k * (waves in the grid), no atomic */
+    const uint32_t wave_id = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), nwaves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t gs = wave_id;; gs += nwaves) {
+        const uint32_t g = __builtin_amdgcn_readfirstlane(gs);
+        (void)work;
+        (void)work_base;
+#else
     for (;;) {
         uint32_t g = 0;
         if (lane == 0)
             g = atomicAdd(work, 1u) - work_base; /* tickets of this launch start at work_base (mod 2^32) */
         g = (uint32_t)__shfl((int)g, 0, 64);
+#endif
         if (g >= ngroups)
             break;
         const uint32_t idx = g * R + slot;

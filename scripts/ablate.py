@@ -41,7 +41,11 @@ VARIANTS = {
     "pf3nt": ["-DGCM_NT_LOADS=1"],  # the default build (GH8, three-step prefetch) with non-temporal input loads
     "gh8pf3": ["-DGCM_GH8=1", "-DGCM_BATCH_PF=3"],  # batch loads three steps ahead (four buffers; the default)
     "gh8pf1": ["-DGCM_GH8=1", "-DGCM_BATCH_PF=1"],  # batch loads one step ahead (two buffers; before r03s)
-    "nofast": ["-DGCM_FAST_STEP=0"],  # r03: every step through the per-lane flags (no interior fast path)
+    "nofast": ["-DGCM_FAST_STEP=0"],
+    "scale0": ["-DGCM_SCALE_W=0"],  # closing multiply with compiler-paired reads (16 round trips; before r03)
+    "scale2": ["-DGCM_SCALE_W=2"],  # closing multiply with all 32 reads in flight
+    "static": ["-DGCM_STATIC_GROUPS=1"],  # groups assigned round-robin to waves (no atomic; uniform batches only)
+    "noscale": ["-DGCM_ABLATE_SCALE=1"],  # no closing H^(K-j) multiply (wrong tags: timing only)  # r03: every step through the per-lane flags (no interior fast path)
     "gh8sel": ["-DGCM_GH8=1", "-DGCM_GH8_LANESEL=1"],  # GH8 byte permutation folded into per-lane address selectors  # 5-bit ds_read_b64 GHASH tables for K = 4 (evaluated: 33% slower, bank conflicts)
     # "@src=DIR": compile gcm_engine.hip from DIR (e.g. a `git show` of an older revision) instead of csrc/
     "head": ["@src=" + os.path.join(VDIR, "src_head")],
