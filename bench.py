@@ -257,6 +257,13 @@ def measure(ra, wl_key, args, dev, rank, world, check):
         if ev is not None:
             ev[2].record(stream)
 
+    # untimed pre-warm: the power manager takes ~10-20 ms of load to raise the clock (the first launches of a run are
+    # up to 35% slower, profiles/r03zc_launches.json), so steps run for prewarm_ms before the W warmup steps
+    t_pre, n_pre = time.perf_counter(), 0
+    while (time.perf_counter() - t_pre) * 1e3 < args.prewarm_ms:
+        step()
+        torch.cuda.synchronize(dev)
+        n_pre += 1
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -320,6 +327,7 @@ def measure(ra, wl_key, args, dev, rank, world, check):
     dom_payload = payload / (dom_ms * 1e-3) / 1e9
     res = {
         "workload": wl["name"], "records_per_gpu": n, "steps": args.steps, "warmup": args.warmup,
+        "prewarm": {"ms": args.prewarm_ms, "steps": n_pre},
         "value": round(value, 2), "unit": "GiB/s", "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "seal_gibps": round(payload / (seal_ms * 1e-3) / GIB, 2),
         "open_gibps": round(payload / (open_ms * 1e-3) / GIB, 2),
@@ -475,6 +483,8 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--prewarm-ms", type=float, default=300.0,
+                    help="untimed steps run for this long before the warmup steps (clock ramp)")
     ap.add_argument("--workload", default="1400", choices=sorted(WORKLOADS))
     ap.add_argument("--workloads", default=SIDE_WORKLOADS,
                     help="comma-separated side workloads measured at N=1 after the main one")
@@ -526,6 +536,7 @@ def main() -> None:
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "prewarm": res["prewarm"],
         "ms_per_step": res["ms_per_step"],
         "higher_is_better": True,
         "scaling": "weak",
