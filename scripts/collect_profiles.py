@@ -37,15 +37,16 @@ def counters(path):
     return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in agg.items()}
 
 
-def launches(trace_csv, warmup):
-    """kernel -> durations (ms) of its dispatches in order, from a rocprofv3 --kernel-trace CSV"""
+def launches(trace_csv, timed):
+    """kernel -> durations (ms) of its dispatches in order, from a rocprofv3 --kernel-trace CSV; the last `timed`
+    dispatches of each kernel are the timed steps' (bench.py's pre-warm and warmup steps come first)"""
     d = collections.defaultdict(list)
     for r in csv.DictReader(open(trace_csv)):
         if r["Kernel_Name"].startswith("mi355x_"):
             d[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6)
     out = {}
     for k, v in d.items():
-        t = sorted(v[warmup:]) if len(v) > warmup else sorted(v)
+        t = sorted(v[-timed:]) if len(v) > timed else sorted(v)
         out[k] = {"dispatches": len(v), "warmup_dropped": len(v) - len(t), "timed_mean_ms": round(sum(t) / len(t), 4),
                   "timed_median_ms": round(t[len(t) // 2], 4), "timed_min_ms": round(t[0], 4),
                   "all_ms": [round(x, 4) for x in v]}
@@ -140,7 +141,7 @@ def main(tag, label):
         p = os.path.join(src, d, "run_kernel_trace.csv")
         if not os.path.exists(p):
             continue
-        ent = {"launches": launches(p, 3 if w == "1400" else 2), "trace": f"gpurun_out/{tag}/{d}"}
+        ent = {"launches": launches(p, 20 if w == "1400" else 10), "trace": f"gpurun_out/{tag}/{d}"}
         line = lines.get(WORKLOADS[w]["name"])
         if line is not None:
             rf = line["roofline"]
