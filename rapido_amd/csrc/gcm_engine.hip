@@ -162,6 +162,9 @@ static_assert(sizeof(TlsRecord) == sizeof(ptls_mi355x_tls_record_t), "descriptor
 #ifndef GCM_BATCH_PF
 #define GCM_BATCH_PF 3 /* batch kernels: loads issued three steps ahead, four buffers (1: one step ahead, two buffers) */
 #endif
+#ifndef GCM_UNIFORM_TMAX
+#define GCM_UNIFORM_TMAX 1
+#endif
 #ifndef GCM_STATIC_GROUPS
 #define GCM_STATIC_GROUPS 0
 #endif
@@ -270,6 +273,9 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
         }
         f_lo = __builtin_amdgcn_readfirstlane(f_lo);
         f_hi = __builtin_amdgcn_readfirstlane(f_hi);
+#if GCM_UNIFORM_TMAX
+        Tmax = __builtin_amdgcn_readfirstlane(Tmax); /* the walk's trip tests on the scalar unit */
+#endif
 
         const uint32_t n1 = iv1 ^ bswap32((uint32_t)(rec.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)rec.seq);
         /* per-connection IV (rapido derive_connection_aead_iv, lib/rapido.c:127-133): IV bytes 0..3 ^= BE32(id) */
