@@ -643,3 +643,18 @@ extern "C" int model_aes_ecb(const uint8_t *key, size_t keylen, int is_enc, uint
 
 /* aes_last_round_bs2 on the host: two blocks' round-NR inputs a, b (LE words) -> outputs, with round key k */
 extern "C" void model_last_round_bs2(uint32_t *a, uint32_t *b, const uint32_t *k) { aes_last_round_bs2(a, b, k); }
+
+/* make_walk + walk_interior for one lane: out = {A, C, T, pad, lo, hi} (tests/test_kernel_model.py) */
+extern "C" void model_walk_interior(uint32_t len, uint32_t aadlen, uint32_t K, uint32_t out16, uint32_t j, uint32_t in_len,
+                                    uint32_t *out)
+{
+    const Walk w = make_walk(len, aadlen, K, out16);
+    uint32_t lo, hi;
+    walk_interior(w, j, K, in_len, lo, hi);
+    out[0] = w.A;
+    out[1] = w.C;
+    out[2] = w.T;
+    out[3] = w.pad;
+    out[4] = lo;
+    out[5] = hi;
+}

@@ -533,3 +533,27 @@ def test_gh8_latin_tables_every_read_order(model, keylen):
         assert raw[16 * (16 * len(xs) + n):16 * (16 * len(xs) + n + 1)] == want
         for i in range(16):
             assert raw[16 * (16 * n + i):16 * (16 * n + i + 1)] == want, (n, i)
+
+
+@pytest.mark.parametrize("K", [1, 2, 4, 8])
+def test_walk_interior_is_exactly_the_whole_payload_steps(model, K):
+    """walk_interior (the batch kernels' fast-path range, gcm_core.h) against the walk's own position map: step t of lane j
+    is interior iff its position holds a whole payload block taken from the input (c = j + K t - pad - A, 0 <= c < len/16);
+    every length, AAD length, output alignment and lane, plus the TLS seal case (GCM payload = fragment + type byte)."""
+    fn = model.model_walk_interior
+    fn.argtypes = [C.c_uint32] * 6 + [C.c_void_p]
+    out = (C.c_uint32 * 6)()
+    for frame in (False, True):
+        for length in list(range(0, 70)) + [1399, 1400, 1401, 16383, 16384, 16385]:
+            plen = length + 1 if frame else length
+            for aadlen in ((5,) if frame else (0, 5, 13, 16, 17, 40, 64)):
+                for out16 in range(K):
+                    for j in range(K):
+                        fn(plen, aadlen, K, out16, j, length, out)
+                        A, Cn, T, pad, lo, hi = (int(v) for v in out)
+                        pad = pad - (1 << 32) if pad >= 1 << 31 else pad
+                        assert Cn == (plen + 15) // 16
+                        for t in range(T + 2):
+                            c = j + K * t - pad - A
+                            whole = 0 <= c < length // 16 and t < T
+                            assert whole == (lo <= t < hi), (frame, length, aadlen, out16, j, t, lo, hi)
