@@ -2214,6 +2214,9 @@ GCM_HD u32x4 shr_bytes(u32x4 v, uint32_t n)
 #ifndef GCM_NT_LOADS
 #define GCM_NT_LOADS 0
 #endif
+#ifndef GCM_NT_STORES
+#define GCM_NT_STORES 1 /* the walk's whole-block stores marked non-temporal (measured: scripts/ablate.py ntstore) */
+#endif
 /* a record block's 16-byte load (GCM_NT_LOADS: marked non-temporal, so the streamed input does not displace the
  * half-written output lines from L2) */
 GCM_HD u32x4 walk_load(const uint8_t *p)
@@ -2379,7 +2382,11 @@ GCM_HD u32x4 lane_walk_seg(const uint8_t *lds, uint32_t lanesel, const uint32_t 
                 pend_c = 0xffffffffu;
             }
         }
+#if defined(__HIP_DEVICE_COMPILE__) && GCM_NT_STORES
+        __builtin_nontemporal_store(o, (u32x4_u *)(out + 16u * c));
+#else
         *(u32x4_u *)(out + 16u * c) = o;
+#endif
     };
     /*
      * step_ctr and finish: step() below cut at its keystream, for the split kernels' two-step trip (x2 walk).  step()
