@@ -39,6 +39,7 @@
 #pragma once
 #include <stdint.h>
 #include <stddef.h>
+#include <type_traits>
 
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
@@ -2361,6 +2362,9 @@ GCM_HD u32x4 lane_walk_seg(const uint8_t *lds, uint32_t lanesel, const uint32_t 
      * first half of a line and stores it together with the next step's block, the second half (its address + 64).
      */
     constexpr bool PAIRST = GCM_PAIR_STORES && K == 4;
+    /* batch kernels (LY = Layout<K>): streamed output stores non-temporal; the window kernels keep plain stores (their
+     * last arrival reads a record's stored bytes back) */
+    constexpr bool NTST = GCM_NT_STORES && std::is_same<LY, Layout<K>>::value;
     u32x4 pend_v = {0u, 0u, 0u, 0u};
     uint32_t pend_c = 0xffffffffu; /* payload block of the held store (none: ~0) */
     /*
@@ -2382,11 +2386,12 @@ GCM_HD u32x4 lane_walk_seg(const uint8_t *lds, uint32_t lanesel, const uint32_t 
                 pend_c = 0xffffffffu;
             }
         }
-#if defined(__HIP_DEVICE_COMPILE__) && GCM_NT_STORES
-        __builtin_nontemporal_store(o, (u32x4_u *)(out + 16u * c));
-#else
-        *(u32x4_u *)(out + 16u * c) = o;
+#if defined(__HIP_DEVICE_COMPILE__)
+        if constexpr (NTST)
+            __builtin_nontemporal_store(o, (u32x4_u *)(out + 16u * c));
+        else
 #endif
+            *(u32x4_u *)(out + 16u * c) = o;
     };
     /*
      * step_ctr and finish: step() below cut at its keystream, for the split kernels' two-step trip (x2 walk).  step()
