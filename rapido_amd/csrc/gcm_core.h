@@ -445,6 +445,24 @@ GCM_HD u32x4 ghash5_mul_lds(const uint8_t *lds, u32x4 X)
     return P;
 }
 
+#ifndef GCM_ROUND_PRIO
+#define GCM_ROUND_PRIO 1 /* GH8 middle rounds: wave priority raised while a round issues its 16 LDS reads (measured) */
+#endif
+#ifndef GCM_PRIO_LEVEL
+#define GCM_PRIO_LEVEL 2
+#endif
+#ifndef GCM_PRIO_GH8
+#define GCM_PRIO_GH8 0 /* 1: raised already before the round's two GH8 reads */
+#endif
+#define GCM_STR2(x) #x
+#define GCM_STR(x) GCM_STR2(x)
+#if GCM_ROUND_PRIO
+#define GCM_PRIO_HI "s_setprio " GCM_STR(GCM_PRIO_LEVEL) "\n\t"
+#define GCM_PRIO_LO "s_setprio 0\n\t"
+#else
+#define GCM_PRIO_HI ""
+#define GCM_PRIO_LO ""
+#endif
 #ifndef GCM_ROUND_ASM
 #define GCM_ROUND_ASM 1
 #endif
@@ -738,6 +756,7 @@ __device__ __forceinline__ void aes_round_tt2k_asm(uint32_t ls, uint32_t s0, uin
 {
     uint32_t t1, t2, t3, t5, t6, t7, t9, t10, t11, t13, t14, t15;
     asm volatile(
+        GCM_PRIO_HI
         "v_perm_b32 %[n0], %[s0], %[ls], %[a0]\n\t"
         "v_perm_b32 %[t1], %[s1], %[ls], %[a1]\n\t"
         "v_perm_b32 %[t2], %[s2], %[ls], %[a2]\n\t"
@@ -770,6 +789,7 @@ __device__ __forceinline__ void aes_round_tt2k_asm(uint32_t ls, uint32_t s0, uin
         "ds_read_b32 %[t13], %[t13] offset:128\n\t"
         "ds_read_b32 %[t14], %[t14]\n\t"
         "ds_read_b32 %[t15], %[t15] offset:128\n\t"
+        GCM_PRIO_LO
         "s_waitcnt lgkmcnt(12)\n\t"
         "v_bitop3_b32 %[t2], %[t2], %[t3], %[r0] bitop3:0x96\n\t"
         "v_alignbit_b32 %[t2], %[t2], %[t2], 16\n\t"
@@ -1134,6 +1154,10 @@ GCM_HD u32x4 aes_gh8_fused_h(const uint8_t *lds, uint32_t lanesel, const uint32_
     for (int r = 3; r < NR; ++r) {
         uint32_t n[4];
         u32x4 g[2];
+#if defined(__HIP_DEVICE_COMPILE__) && GCM_ROUND_PRIO && GCM_PRIO_GH8
+        asm volatile(GCM_PRIO_HI ::: "memory");
+        GCM_SCHED_FENCE();
+#endif
         if (r <= 9)
             gh8_issue2(lds, Ar, L, 2 * (r - 2), g);
 #if defined(__HIP_DEVICE_COMPILE__) && GCM_ROUND_ASM

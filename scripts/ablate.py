@@ -48,6 +48,11 @@ VARIANTS = {
     "ntstore": ["-DGCM_NT_STORES=1"],  # the walk's output stores non-temporal (the default since r03zg)
     "tstore": ["-DGCM_NT_STORES=0"],  # the walk's output stores as plain (temporal) stores (before r03zg)
     "quarters": ["-DGCM_PASS_LANES=0"],  # K = 4: lane j = the wave quarter (two j per ds_read_b128 pass; before r03)
+    "prio": ["-DGCM_ROUND_PRIO=1"],  # s_setprio 2 while a GH8 middle round issues its LDS reads (the default since r03zm)
+    "noprio": ["-DGCM_ROUND_PRIO=0"],  # no wave-priority changes (before r03zm)
+    "prio3": ["-DGCM_PRIO_LEVEL=3"],  # s_setprio 3 instead of 2
+    "prio1": ["-DGCM_PRIO_LEVEL=1"],  # s_setprio 1 instead of 2
+    "priogh8": ["-DGCM_PRIO_GH8=1"],  # raised already before the round's two GH8 reads
     "static": ["-DGCM_STATIC_GROUPS=1"],  # groups assigned round-robin to waves (no atomic; uniform batches only)
     "noscale": ["-DGCM_ABLATE_SCALE=1"],  # no closing H^(K-j) multiply (wrong tags: timing only)  # r03: every step through the per-lane flags (no interior fast path)
     "gh8sel": ["-DGCM_GH8=1", "-DGCM_GH8_LANESEL=1"],  # GH8 byte permutation folded into per-lane address selectors  # 5-bit ds_read_b64 GHASH tables for K = 4 (evaluated: 33% slower, bank conflicts)
