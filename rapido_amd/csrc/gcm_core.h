@@ -452,7 +452,7 @@ GCM_HD u32x4 ghash5_mul_lds(const uint8_t *lds, u32x4 X)
 #define GCM_PRIO_LEVEL 2
 #endif
 #ifndef GCM_PRIO_GH8
-#define GCM_PRIO_GH8 0 /* 1: raised already before the round's two GH8 reads */
+#define GCM_PRIO_GH8 1 /* 1: raised already before the round's two GH8 reads */
 #endif
 #define GCM_STR2(x) #x
 #define GCM_STR(x) GCM_STR2(x)
