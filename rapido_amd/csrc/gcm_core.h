@@ -451,6 +451,9 @@ GCM_HD u32x4 ghash5_mul_lds(const uint8_t *lds, u32x4 X)
 #ifndef GCM_PRIO_LEVEL
 #define GCM_PRIO_LEVEL 2
 #endif
+#ifndef GCM_PRIO_LAST
+#define GCM_PRIO_LAST 0 /* 1: raised through the last round's 16 S-box reads too */
+#endif
 #ifndef GCM_PRIO_GH8
 #define GCM_PRIO_GH8 1 /* 1: raised already before the round's two GH8 reads */
 #endif
@@ -1190,6 +1193,10 @@ GCM_HD u32x4 aes_gh8_fused_h(const uint8_t *lds, uint32_t lanesel, const uint32_
         s3r = n[3];
     }
     {
+#if defined(__HIP_DEVICE_COMPILE__) && GCM_ROUND_PRIO && GCM_PRIO_LAST
+        asm volatile(GCM_PRIO_HI ::: "memory");
+        GCM_SCHED_FENCE();
+#endif
         const uint32_t *k = rk + 4 * NR;
         const uint32_t x[4] = {s0, s1, s2, s3r};
 #pragma unroll
@@ -1201,6 +1208,10 @@ GCM_HD u32x4 aes_gh8_fused_h(const uint8_t *lds, uint32_t lanesel, const uint32_
             const uint32_t rd = lds_u32(lds, perm(x[(j + 3) & 3], lanesel, 0x0c020700u));
             w[j] = xor3(perm(rb, ra, 0x0c0c0501u), perm(rd, rc, 0x06020c0cu), k[j]);
         }
+#if defined(__HIP_DEVICE_COMPILE__) && GCM_ROUND_PRIO && GCM_PRIO_LAST
+        GCM_SCHED_FENCE();
+        asm volatile(GCM_PRIO_LO ::: "memory");
+#endif
     }
     return P;
 #undef GCM_TL

@@ -52,6 +52,7 @@ VARIANTS = {
     "noprio": ["-DGCM_ROUND_PRIO=0"],  # no wave-priority changes (before r03zm)
     "prio3": ["-DGCM_PRIO_LEVEL=3"],  # s_setprio 3 instead of 2
     "prio1": ["-DGCM_PRIO_LEVEL=1"],  # s_setprio 1 instead of 2
+    "priolast": ["-DGCM_PRIO_LAST=1"],  # raised through the last round's S-box reads too
     "priogh8": ["-DGCM_PRIO_GH8=1"],  # raised already before the round's two GH8 reads
     "static": ["-DGCM_STATIC_GROUPS=1"],  # groups assigned round-robin to waves (no atomic; uniform batches only)
     "noscale": ["-DGCM_ABLATE_SCALE=1"],  # no closing H^(K-j) multiply (wrong tags: timing only)  # r03: every step through the per-lane flags (no interior fast path)
