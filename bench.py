@@ -236,26 +236,50 @@ def measure(ra, wl_key, args, dev, rank, world, check):
     ragged = wl["length"] is None
     d_order = torch.zeros(n, dtype=torch.int32, device=dev)
 
-    def step(ev=None):
-        if ev is not None:
-            ev[0].record(stream)
+    # The step's pipeline: the batch in `chunks` contiguous record ranges, chunk c sealed and then
+    # opened on stream c % 2, each stream with its own engine context (work counters, sort scratch).  A persistent batch
+    # kernel leaves CUs idle while its last record groups finish; the other stream's launch fills them.  Chunk c's bytes
+    # are touched only by its stream, so consecutive steps need no synchronisation either.
+    nchunk = max(1, int(args.pipeline))
+    nstream = 1 if nchunk == 1 else 2
+    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(nstream - 1)]
+    engs = [eng] + [ra.Engine(key) for _ in range(nstream - 1)]
+    bounds = [min(n, (n * c // nchunk + 63) // 64 * 64) for c in range(nchunk)] + [n]
+    chunks = [(c % nstream, bounds[c], bounds[c + 1]) for c in range(nchunk) if bounds[c + 1] > bounds[c]]
+
+    def seal_chunk(e, s, r0, cnt):
+        rp = d_recs.data_ptr() + r0 * DESC_BYTES
         if ragged:
             # length-binned, longest-first schedule; the device sort is inside the timed step
-            eng.order_by_length(d_recs.data_ptr(), n, d_order.data_ptr(), sh)
-            eng.seal_batch_ordered(iv, d_recs.data_ptr(), d_order.data_ptr(), n, d_src.data_ptr(), d_ct.data_ptr(),
-                                   d_aad.data_ptr(), sh)
+            e.order_by_length(rp, cnt, d_order.data_ptr() + 4 * r0, s)
+            e.seal_batch_ordered(iv, rp, d_order.data_ptr() + 4 * r0, cnt, d_src.data_ptr(), d_ct.data_ptr(),
+                                 d_aad.data_ptr(), s)
         else:
-            eng.seal_batch(iv, d_recs.data_ptr(), n, d_src.data_ptr(), d_ct.data_ptr(), d_aad.data_ptr(), sh)
-        if ev is not None:
-            ev[1].record(stream)
+            e.seal_batch(iv, rp, cnt, d_src.data_ptr(), d_ct.data_ptr(), d_aad.data_ptr(), s)
+
+    def open_chunk(e, s, r0, cnt):
+        rp = d_recs.data_ptr() + r0 * DESC_BYTES
         if ragged:
-            eng.open_batch_ordered(iv, d_recs.data_ptr(), d_order.data_ptr(), n, d_ct.data_ptr(), d_pt.data_ptr(),
-                                   d_aad.data_ptr(), d_st.data_ptr(), sh)
+            e.open_batch_ordered(iv, rp, d_order.data_ptr() + 4 * r0, cnt, d_ct.data_ptr(), d_pt.data_ptr(),
+                                 d_aad.data_ptr(), d_st.data_ptr() + 4 * r0, s)
         else:
-            eng.open_batch(iv, d_recs.data_ptr(), n, d_ct.data_ptr(), d_pt.data_ptr(), d_aad.data_ptr(),
-                           d_st.data_ptr(), sh)
-        if ev is not None:
-            ev[2].record(stream)
+            e.open_batch(iv, rp, cnt, d_ct.data_ptr(), d_pt.data_ptr(), d_aad.data_ptr(), d_st.data_ptr() + 4 * r0, s)
+
+    def step():
+        for si, r0, r1 in chunks:
+            seal_chunk(engs[si], streams[si].cuda_stream, r0, r1 - r0)
+        for si, r0, r1 in chunks:
+            open_chunk(engs[si], streams[si].cuda_stream, r0, r1 - r0)
+
+    def fork(ev):
+        ev.record(streams[0])
+        for s in streams[1:]:
+            s.wait_event(ev)
+
+    def join(ev_list):
+        for s, ev in zip(streams[1:], ev_list):
+            ev.record(s)
+            streams[0].wait_event(ev)
 
     # untimed pre-warm: the power manager takes ~10-20 ms of load to raise the clock (the first launches of a run are
     # up to 35% slower, profiles/r03zc_launches.json), so steps run for prewarm_ms before the W warmup steps
@@ -267,21 +291,38 @@ def measure(ra, wl_key, args, dev, rank, world, check):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    ev_t0 = torch.cuda.Event(enable_timing=True)
+    ev_t1 = torch.cuda.Event(enable_timing=True)
+    ev_join = [torch.cuda.Event() for _ in streams[1:]]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    fork(ev_t0)
     for i in range(args.steps):
-        step(events[i])
+        step()
+    join(ev_join)
+    ev_t1.record(streams[0])
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
         elapsed = max_over_ranks(elapsed, dev)
+    region_ms = ev_t0.elapsed_time(ev_t1)  # the timed region on the GPU clock (HIP events)
 
-    seal_all = [e[0].elapsed_time(e[1]) for e in events]
-    open_all = [e[1].elapsed_time(e[2]) for e in events]
+    # the kernels one launch at a time, after the timed region: the whole batch sealed, then opened, on one stream with
+    # HIP events around each launch (per-kernel launch times for the roofline's serial_launch and lds_roofline)
+    serial_steps = max(3, min(args.steps, 10))
+    sev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(serial_steps)]
+    for ev in sev:
+        ev[0].record(stream)
+        seal_chunk(eng, sh, 0, n)
+        ev[1].record(stream)
+        open_chunk(eng, sh, 0, n)
+        ev[2].record(stream)
+    torch.cuda.synchronize(dev)
+    seal_all = [e[0].elapsed_time(e[1]) for e in sev]
+    open_all = [e[1].elapsed_time(e[2]) for e in sev]
     seal_ms, open_ms = float(np.mean(seal_all)), float(np.mean(open_all))
 
     # correctness after timing: every status verifies and sampled records open back to their plaintext (parity with
@@ -303,8 +344,12 @@ def measure(ra, wl_key, args, dev, rank, world, check):
     dom_is_seal = seal_ms >= open_ms
     dom_ms = seal_ms if dom_is_seal else open_ms
     dom_bytes = seal_b if dom_is_seal else open_b
-    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    achieved_serial = dom_bytes / (dom_ms * 1e-3) / 1e9
+    # the timed region: every launch's algorithmic bytes over the region's HIP-event time (launches overlap at their
+    # ends when chunks > 1, so the per-launch time of one kernel is not defined there)
+    achieved = (seal_b + open_b) * args.steps / (region_ms * 1e-3) / 1e9
     kname = ra.kernel_name(dom_is_seal, wl["key"], n)
+    chunk_kernels = sorted({ra.kernel_name(s, wl["key"], r1 - r0) for s in (True, False) for _, r0, r1 in chunks})
 
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -331,11 +376,22 @@ def measure(ra, wl_key, args, dev, rank, world, check):
         "value": round(value, 2), "unit": "GiB/s", "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "seal_gibps": round(payload / (seal_ms * 1e-3) / GIB, 2),
         "open_gibps": round(payload / (open_ms * 1e-3) / GIB, 2),
-        "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+        "pipeline": {"chunks": len(chunks), "streams": nstream, "kernels": chunk_kernels,
+                     "region_ms": round(region_ms, 4), "wall_ms": round(elapsed * 1e3, 4)},
+        "roofline": {"bound": "hbm", "kernel": kname if nchunk == 1 else "+".join(chunk_kernels),
+                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                     "algorithmic_bytes_per_launch": dom_bytes, "launch_ms": round(dom_ms, 4),
-                     "launch_ms_median": round(float(np.median(seal_all if dom_is_seal else open_all)), 4),
-                     "launches": "the timed steps' launches only (HIP events on the launch stream), warmups excluded"},
+                     "algorithmic_bytes_per_step": seal_b + open_b,
+                     "launches": f"the timed region: {args.steps} steps x {2 * len(chunks)} launches (seal and open of "
+                                 f"{len(chunks)} chunk(s) on {nstream} stream(s)), algorithmic bytes / HIP-event time "
+                                 f"of the region; warmups excluded",
+                     "serial_launch": {"kernel": kname, "algorithmic_bytes_per_launch": dom_bytes,
+                                       "launch_ms": round(dom_ms, 4),
+                                       "launch_ms_median": round(float(np.median(seal_all if dom_is_seal else open_all)), 4),
+                                       "achieved": round(achieved_serial, 1),
+                                       "frac": round(achieved_serial / HBM_PEAK_GBPS, 4),
+                                       "launches": f"{serial_steps} launches of the whole batch one at a time after the "
+                                                   f"timed region (HIP events on the launch stream)"}},
         "lds_roofline": {"bound": "lds", "kernel": kname, "achieved": round(dom_payload, 1),
                          "peak": round(lds_ceiling, 1), "unit": "GB/s payload",
                          "frac": round(dom_payload / lds_ceiling, 4),
@@ -355,6 +411,8 @@ def measure(ra, wl_key, args, dev, rank, world, check):
             peak_held = lds_ceiling * held["ghz"] / LDS_CLOCK_GHZ
             res["lds_roofline"].update({"held_clock_ghz": held["ghz"], "peak_held": round(peak_held, 1),
                                         "frac_held": round(dom_payload / peak_held, 4), "held_clock_source": held["source"]})
+    for e in engs[1:]:
+        e.close()
     extra = dict(eng=eng, iv=iv, d_src=d_src, d_ct=d_ct, d_recs=d_recs, d_aad=d_aad, recs=recs, n=n,
                  src_bytes=src_bytes, payload=payload, stream=stream, key=wl["key"])
     return res, extra
@@ -490,6 +548,8 @@ def main() -> None:
                     help="comma-separated side workloads measured at N=1 after the main one")
     ap.add_argument("--no-workloads", action="store_true", help="measure the main workload only")
     ap.add_argument("--side-steps", type=int, default=10, help="timed steps of each side workload")
+    ap.add_argument("--pipeline", type=int, default=2,
+                    help="chunks of the batch per step, alternating over two streams (1: one stream, one launch each)")
     ap.add_argument("--lanes", type=int, default=0, help="lanes per record (1/2/4/8); 0 = engine default")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e", action="store_true", help="time the PCIe-inclusive path (pinned host in/out); default at N=1")
@@ -551,6 +611,9 @@ def main() -> None:
         "open_gibps": res["open_gibps"],
         "roofline": res["roofline"],
         "lds_roofline": res["lds_roofline"],
+        "pipeline": res["pipeline"],
+        "build_id": ra.build_id(),
+        "build_id_matches_sources": ra.build_id() == ra.source_build_id(),
     }
     if world == 1 and not args.no_e2e:
         out["window_latency"] = window_latency(ra, extra, dev)

@@ -491,6 +491,12 @@ const char *ptls_mi355x_kernel_name(int is_seal, size_t key_size, size_t n, int 
 int ptls_mi355x_batch_ghash_reads(int k);
 /* last HIP error string seen by the engine ("" if none) */
 const char *ptls_mi355x_last_error(void);
+/*
+ * Build provenance: the first 16 hex digits of SHA-256 over the library's sources (rapido_amd/csrc/ and this header,
+ * in name order, each as "<name>\0<bytes>"), fixed when the library was built (rapido_amd/build.py).  Equal to
+ * rapido_amd.source_build_id() of the tree iff the library was built from that tree's sources.
+ */
+const char *ptls_mi355x_build_id(void);
 
 #ifdef __cplusplus
 }

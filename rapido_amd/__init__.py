@@ -56,7 +56,7 @@ EXPORTED_FUNCTIONS = (
     "ptls_mi355x_seal_batch", "ptls_mi355x_open_batch", "ptls_mi355x_order_by_length",
     "ptls_mi355x_seal_batch_ordered", "ptls_mi355x_open_batch_ordered", "ptls_mi355x_set_lanes_per_record",
     "ptls_mi355x_get_lanes_per_record", "ptls_mi355x_kernel_name", "ptls_mi355x_last_error",
-    "ptls_mi355x_batch_ghash_reads",
+    "ptls_mi355x_batch_ghash_reads", "ptls_mi355x_build_id",
     "ptls_mi355x_tls_seal_records", "ptls_mi355x_tls_open_records", "ptls_mi355x_tls_seal_records_multi",
     "ptls_mi355x_tls_open_records_multi", "ptls_mi355x_set_tls_window_records",
     "ptls_mi355x_set_aead_window_records", "ptls_mi355x_set_slot_zero_copy_bytes",
@@ -145,6 +145,7 @@ def lib() -> C.CDLL:
         L.ptls_mi355x_kernel_name.argtypes = [C.c_int, sz, sz, C.c_int]
         L.ptls_mi355x_kernel_name.restype = C.c_char_p
         L.ptls_mi355x_last_error.restype = C.c_char_p
+        L.ptls_mi355x_build_id.restype = C.c_char_p
         L.ptls_mi355x_tls_seal_records.argtypes = [vp, vp, vp, sz, vp, vp, vp]
         L.ptls_mi355x_tls_open_records.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]
         L.ptls_mi355x_tls_seal_records_multi.argtypes = [vp, vp, vp, vp, sz, vp, vp, vp]
@@ -207,6 +208,17 @@ def lib() -> C.CDLL:
 
 def last_error() -> str:
     return lib().ptls_mi355x_last_error().decode()
+
+
+def build_id() -> str:
+    """The source hash the loaded library was built from (ptls_mi355x_build_id, rapido_amd/build.py)."""
+    return lib().ptls_mi355x_build_id().decode()
+
+
+def source_build_id() -> str:
+    """The same hash over this tree's sources: equal to build_id() iff the library was built from them."""
+    from rapido_amd import build as _b
+    return _b.source_build_id()
 
 
 def is_supported() -> bool:

@@ -32,6 +32,16 @@ def test_library_exports_every_declared_symbol(engine_lib):
         assert hasattr(engine_lib, name), name
 
 
+def test_library_build_id_is_the_source_hash(engine_lib):
+    """Build provenance: the library in the tree was built from the tree's sources (rapido_amd/build.py stamps it
+    with their hash and rebuilds whenever the hash changes)."""
+    import rapido_amd as ra
+    from rapido_amd import build
+    bid = ra.build_id()
+    assert re.fullmatch(r"[0-9a-f]{16}", bid)
+    assert bid == ra.source_build_id() == build.stamped_build_id()
+
+
 def test_library_has_gfx950_code_object(engine_lib):
     """The fat binary embedded in the library carries a gfx950 code object (and only that target)."""
     import rapido_amd
