@@ -81,6 +81,39 @@ def max_over_ranks(value: float, device=None) -> float:
     return float(t.item())
 
 
+def check_device_map(dev_index: int, same_device_ok: bool, device_count: int):
+    """Fail fast on a rank-to-GPU map that would measure the wrong thing: a device ordinal the node does not have, or two
+    ranks of one host on one GPU (allowed only for the rehearsal, RAPIDO_BENCH_SAME_DEVICE=1).  Collective over the
+    process group (all_gather_object); returns every rank's (host, device ordinal)."""
+    import socket
+
+    import torch.distributed as dist
+    if not same_device_ok and not 0 <= dev_index < device_count:
+        raise SystemExit(f"bench: device ordinal {dev_index} but torch.cuda.device_count() is {device_count}")
+    world = dist.get_world_size()
+    where = [None] * world
+    dist.all_gather_object(where, (socket.gethostname(), dev_index))
+    if not same_device_ok and len(set(where)) != world:
+        raise SystemExit(f"bench: ranks share a GPU {where}; set RAPIDO_BENCH_SAME_DEVICE=1 for a same-device rehearsal")
+    return where
+
+
+RANK_KEYS = ("rank", "host", "device", "device_name", "rank_gibps", "rank_ms_per_step", "seal_gibps", "open_gibps",
+             "launch_ms")
+
+
+def gather_rank_stats(mine: dict):
+    """Every rank's own figures (RANK_KEYS) gathered to every rank, in rank order (all_gather_object), so rank 0's line
+    shows which rank lags.  `mine` must hold RANK_KEYS."""
+    import torch.distributed as dist
+    missing = [k for k in RANK_KEYS if k not in mine]
+    if missing:
+        raise ValueError(f"rank stats miss {missing}")
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, {k: mine[k] for k in RANK_KEYS})
+    return out
+
+
 def algorithmic_bytes(lengths_sum: int, n: int, aad_sum: int, seal: bool) -> int:
     """seal: read L + aad + descriptor, write L + 16; open: read L + 16 + aad + descriptor, write L + 4."""
     if seal:
@@ -305,6 +338,7 @@ def measure(ra, wl_key, args, dev, rank, world, check):
     ev_t1.record(streams[0])
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    elapsed_rank = elapsed
     if world > 1:
         dist.barrier()
         elapsed = max_over_ranks(elapsed, dev)
@@ -376,6 +410,8 @@ def measure(ra, wl_key, args, dev, rank, world, check):
         "value": round(value, 2), "unit": "GiB/s", "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "seal_gibps": round(payload / (seal_ms * 1e-3) / GIB, 2),
         "open_gibps": round(payload / (open_ms * 1e-3) / GIB, 2),
+        "rank_gibps": round(2.0 * payload * args.steps / elapsed_rank / GIB, 2),
+        "rank_ms_per_step": round(elapsed_rank / args.steps * 1e3, 4),
         "pipeline": {"chunks": len(chunks), "streams": nstream, "kernels": chunk_kernels,
                      "region_ms": round(region_ms, 4), "wall_ms": round(elapsed * 1e3, 4)},
         "roofline": {"bound": "hbm", "kernel": kname if nchunk == 1 else "+".join(chunk_kernels),
@@ -582,6 +618,10 @@ def main() -> None:
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
         else:
             dist.init_process_group(backend)
+    device_count = torch.cuda.device_count()
+    placement = None
+    if world > 1:
+        placement = check_device_map(dev_index, os.environ.get("RAPIDO_BENCH_SAME_DEVICE") == "1", device_count)
     dev = torch.device("cuda", dev_index if world > 1 else 0)
     torch.cuda.set_device(dev)
     ra.require_gpu()
@@ -615,6 +655,15 @@ def main() -> None:
         "build_id": ra.build_id(),
         "build_id_matches_sources": ra.build_id() == ra.source_build_id(),
     }
+    out["device_count"] = device_count
+    if world > 1:
+        import socket
+        out["ranks"] = gather_rank_stats({
+            "rank": rank, "host": socket.gethostname(), "device": dev_index,
+            "device_name": torch.cuda.get_device_name(dev), "rank_gibps": res["rank_gibps"],
+            "rank_ms_per_step": res["rank_ms_per_step"], "seal_gibps": res["seal_gibps"],
+            "open_gibps": res["open_gibps"], "launch_ms": res["roofline"]["serial_launch"]["launch_ms"]})
+        out["placement"] = [list(p) for p in placement]
     if world == 1 and not args.no_e2e:
         out["window_latency"] = window_latency(ra, extra, dev)
     if (args.e2e or world == 1) and not args.no_e2e:

@@ -334,8 +334,9 @@ void ptls_mi355x_record_layer_set_seq(ptls_mi355x_record_layer_t *rl, uint64_t s
  * fragment of n bytes is max(1, ceil(n / 16384)) records, none when empty), nothing after it.  The caller then sends
  * the KeyUpdate message (type 22, sealed past the limit under the old key, as update_send_key does, :4949-4962),
  * installs the next traffic key (ptls_mi355x_record_layer_rekey: seq restarts at 0) and seals the rest.
- * Returns 0, PTLS_MI355X_RECORD_LAYER_KEY_UPDATE, or -1 (capacity below the wire size, or an engine error; nothing
- * written, seq unchanged). */
+ * Returns 0, PTLS_MI355X_RECORD_LAYER_KEY_UPDATE, or -1: a capacity below the wire size (nothing written, seq
+ * unchanged), or an engine error (seq unchanged if the launch failed; if the launch was accepted and the wait failed,
+ * records may be partly written and seq stays past them, so no nonce is ever used twice). */
 #define PTLS_MI355X_RECORD_LAYER_SEQ_LIMIT (1ull << 24)
 #define PTLS_MI355X_RECORD_LAYER_KEY_UPDATE 1
 int ptls_mi355x_record_layer_seal(ptls_mi355x_record_layer_t *rl, const ptls_mi355x_iovec_t *frags, size_t nfrags,
@@ -345,8 +346,9 @@ int ptls_mi355x_record_layer_seal(ptls_mi355x_record_layer_t *rl, const ptls_mi3
  * layer's seq advanced.  The layers must share the key and IV bytes 4..11: rapido's connections of a session, whose
  * IVs differ by the connection id in bytes 0..3 (derive_connection_aead_iv, lib/rapido.c:123-133); the kernel applies
  * each record's difference (ptls_mi355x_tls_seal_records_multi).  Runs on layers[0]'s stream and staging; direct when
- * every fragment and output lies in a range registered with any of the layers.  0, or -1 (nothing written, no seq
- * advanced: a capacity, a layer with another key or IV, or an engine error). */
+ * every fragment and output lies in a range registered with any of the layers.  0, or -1: a capacity or a layer with
+ * another key or IV (nothing written, no seq advanced), or an engine error (as for ptls_mi355x_record_layer_seal: seq
+ * stays past records whose launch was accepted). */
 int ptls_mi355x_record_layer_seal_multi(ptls_mi355x_record_layer_t *const *layers, size_t nlayers,
                                         const ptls_mi355x_iovec_t *const *frags, const size_t *nfrags, uint8_t type,
                                         void *const *out, const size_t *capacity, size_t *outlen, size_t *nrecords);
@@ -382,8 +384,11 @@ int ptls_mi355x_record_layer_rekey(ptls_mi355x_record_layer_t *rl, const void *k
  * 4 slots -- each its own stream, staging and engine context -- and returns at once; so consecutive windows of one
  * connection, and windows of several connections, overlap their PCIe transfers and kernels.  Windows complete in
  * submission order: ptls_mi355x_record_layer_wait(rl, ticket, ...) for the oldest ticket of rl, then the next.  At
- * most 4 windows per layer are outstanding (a fifth submit returns -1).  A synchronous call on a layer with windows
- * outstanding returns -1.  Buffers (fragments, inputs, outputs) must stay untouched until the window's wait.
+ * most 4 windows per layer are outstanding (a fifth submit returns -1).  A synchronous call or a rekey on a layer
+ * with windows outstanding -- its own, or another layer's windows that name it -- returns -1.  Buffers (fragments,
+ * inputs, outputs) must stay untouched until the window's wait.  Freeing or unregistering a layer that another
+ * layer's outstanding window names first waits for the device; that window then completes with alerts[l] =
+ * PTLS_MI355X_RECORD_LAYER_STALE for it and delivers nothing to it.
  *
  * A layer may appear several times in one submit: its windows in that order, each behind the one before (one
  * connection's consecutive windows in one launch).

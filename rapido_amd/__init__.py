@@ -634,6 +634,13 @@ class RecordLayer:
         self._check(lib().ptls_mi355x_record_layer_wait(self.handle, ticket, olen, nrec, cons, al), "wait")
         return olen[0], nrec[0], cons[0], al[0]
 
+    def wait_multi(self, ticket: int, nlayers: int):
+        """Completes the oldest window of a submit over `nlayers` layers led by this one -> per layer (outlen, records,
+        consumed, alert)."""
+        olen, nrec, cons, al = (sz * nlayers)(), (sz * nlayers)(), (sz * nlayers)(), (C.c_int * nlayers)()
+        self._check(lib().ptls_mi355x_record_layer_wait(self.handle, ticket, olen, nrec, cons, al), "wait")
+        return [(olen[i], nrec[i], cons[i], al[i]) for i in range(nlayers)]
+
     def close(self) -> None:
         if self.handle:
             lib().ptls_mi355x_record_layer_free(self.handle)  # unregisters its ranges
@@ -675,14 +682,56 @@ def record_layer_seal_multi(layers, windows, content_type: int = 23, outs=None):
         caps = [o.nbytes for o in outs]
         out_ptrs = (C.c_void_p * n)(*[o.ctypes.data for o in outs])
     capv = (sz * n)(*caps)
-    olen, nrec = (sz * n)(), (sz * n)()
+    olen, nrec, cons, alerts = (sz * n)(), (sz * n)(), (sz * n)(), (C.c_int * n)()
     handles = (C.c_void_p * n)(*[lr.handle for lr in layers])
-    if lib().ptls_mi355x_record_layer_seal_multi(handles, n, frag_ptrs, nfr, content_type, out_ptrs, capv, olen,
-                                                 nrec) not in (0, RECORD_LAYER_KEY_UPDATE):
+    # the synchronous call as its submit + wait, for the wait's per-layer alerts: layers[l].key_update is set when its
+    # window stopped at the 2^24-record limit (send the KeyUpdate, rekey, seal the rest)
+    if any(lib().ptls_mi355x_record_layer_pending(lr.handle) for lr in layers):
+        raise RuntimeError("record_layer_seal_multi failed: asynchronous windows outstanding (wait for them first)")
+    ticket = C.c_uint64()
+    if lib().ptls_mi355x_record_layer_seal_submit(handles, n, frag_ptrs, nfr, content_type, out_ptrs, capv,
+                                                  C.byref(ticket)) or \
+            lib().ptls_mi355x_record_layer_wait(layers[0].handle, ticket.value, olen, nrec, cons, alerts):
         raise RuntimeError("record_layer_seal_multi failed: " + lib().ptls_mi355x_record_layer_last_error().decode())
+    for lr in layers:
+        lr.key_update = False
+    for i in range(n):
+        layers[i].key_update = layers[i].key_update or alerts[i] == RECORD_LAYER_KEY_UPDATE
     if outs is None:
         return [(bufs[i].raw[:olen[i]], nrec[i]) for i in range(n)]
     return [(olen[i], nrec[i]) for i in range(n)]
+
+
+def record_layer_seal_submit_multi(layers, windows, outs, content_type: int = 23) -> int:
+    """Asynchronous seal over several layers of a session (ptls_mi355x_record_layer_seal_submit): windows[l] lists
+    uint8 numpy fragments for layers[l], outs[l] its output -> ticket of layers[0] (layers[0].wait_multi)."""
+    n = len(layers)
+    iovs = []
+    for frags in windows:
+        iov = (_IoVec * max(len(frags), 1))()
+        for i, f in enumerate(frags):
+            iov[i].base = C.c_void_p(f.ctypes.data)
+            iov[i].len = f.nbytes
+        iovs.append(iov)
+    frag_ptrs = (C.c_void_p * n)(*[C.cast(a, C.c_void_p) for a in iovs])
+    nfr = (sz * n)(*[len(w) for w in windows])
+    out_ptrs, caps = (C.c_void_p * n)(*[o.ctypes.data for o in outs]), (sz * n)(*[o.nbytes for o in outs])
+    handles, t = (C.c_void_p * n)(*[lr.handle for lr in layers]), C.c_uint64()
+    if lib().ptls_mi355x_record_layer_seal_submit(handles, n, frag_ptrs, nfr, content_type, out_ptrs, caps, C.byref(t)):
+        raise RuntimeError("seal_submit failed: " + lib().ptls_mi355x_record_layer_last_error().decode())
+    return t.value
+
+
+def record_layer_open_submit_multi(layers, wires, outs):
+    """Asynchronous open over several layers of a session (ptls_mi355x_record_layer_open_submit): wires[l] / outs[l]
+    uint8 numpy arrays -> (ticket of layers[0], wire bytes parsed per layer)."""
+    n = len(layers)
+    in_ptrs, inl = (C.c_void_p * n)(*[w.ctypes.data for w in wires]), (sz * n)(*[w.nbytes for w in wires])
+    out_ptrs, caps = (C.c_void_p * n)(*[o.ctypes.data for o in outs]), (sz * n)(*[o.nbytes for o in outs])
+    handles, parsed, t = (C.c_void_p * n)(*[lr.handle for lr in layers]), (sz * n)(), C.c_uint64()
+    if lib().ptls_mi355x_record_layer_open_submit(handles, n, in_ptrs, inl, out_ptrs, caps, parsed, C.byref(t)):
+        raise RuntimeError("open_submit failed: " + lib().ptls_mi355x_record_layer_last_error().decode())
+    return t.value, list(parsed)
 
 
 def record_layer_open_multi(layers, wires):

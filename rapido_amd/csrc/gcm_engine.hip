@@ -1356,18 +1356,25 @@ struct st_ptls_mi355x_aesgcm_context {
     DeviceShared *shared;
     uint32_t *d_work;               /* WORK_SLOTS dynamic-scheduling ticket counters, set once at setup */
     uint32_t work_base[WORK_SLOTS]; /* each counter's value at the start of its next launch */
-    hipStream_t work_stream[WORK_SLOTS]; /* stream of the slot's last launch */
     uint32_t work_next;
-    hipEvent_t reuse_event;         /* orders a slot's reuse on another stream after its last launch */
     void *d_scratch;                /* order_by_length / stop-at-failure workspace */
     size_t scratch_cap;
-    hipStream_t scratch_stream;     /* stream of the last use of d_scratch (valid once scratch_used) */
-    bool scratch_used;
-    hipEvent_t scratch_event;       /* orders a use of d_scratch on another stream after it */
     u32x4 *d_split;                 /* split window kernels: SPLIT_MAXRUN partials per record, then the tickets */
     size_t split_cap;               /* records the buffer holds */
-    hipStream_t split_stream;       /* stream of the last split launch */
-    hipEvent_t split_event;         /* orders a split launch on another stream after it */
+    /*
+     * Stream ordering of the shared resources (work slots, split tickets, scratch).  A context launches on the first
+     * stream it is given ("home"); while every launch goes there, stream order alone keeps two launches from sharing a
+     * resource at once.  The first launch on another stream synchronises the device once (everything queued before it
+     * is done) and switches the context to multi-stream mode: from then on each use of a resource records that
+     * resource's event on the stream of the use, right after the use, and the next use on any stream first waits on
+     * it -- never an event recorded later on a stored stream handle, which may have been destroyed since.
+     */
+    hipStream_t home;
+    bool home_set, multi;
+    hipEvent_t work_ev[WORK_SLOTS]; /* multi-stream mode: the slot's last launch (created on first use) */
+    bool work_ev_valid[WORK_SLOTS];
+    hipEvent_t split_ev, scratch_ev;
+    bool split_ev_valid, scratch_ev_valid;
 };
 
 struct st_ptls_mi355x_aes_context {
@@ -1612,6 +1619,39 @@ static LaunchPlan plan_launch(bool seal, bool frame, uint32_t key_size, size_t n
 
 static inline uint32_t le32(const uint8_t *p) { return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24; }
 
+/* a launch of ctx on `stream` is about to use shared resources (see the context's stream-ordering note) */
+static int ctx_stream(ptls_mi355x_aesgcm_context_t *ctx, hipStream_t stream)
+{
+    if (!ctx->home_set) {
+        ctx->home = stream;
+        ctx->home_set = true;
+    } else if (!ctx->multi && stream != ctx->home) {
+        HIPCHK(hipDeviceSynchronize()); /* once: every launch queued so far, on any stream, is done */
+        ctx->multi = true;
+    }
+    return 0;
+}
+
+/* multi-stream mode: `stream` waits for the resource's last use (if one was recorded) */
+static int res_wait(ptls_mi355x_aesgcm_context_t *ctx, hipEvent_t ev, bool valid, hipStream_t stream)
+{
+    if (ctx->multi && valid)
+        HIPCHK(hipStreamWaitEvent(stream, ev, 0));
+    return 0;
+}
+
+/* multi-stream mode: the use just queued on `stream` is the resource's last (its event recorded there, now) */
+static int res_used(ptls_mi355x_aesgcm_context_t *ctx, hipEvent_t *ev, bool *valid, hipStream_t stream)
+{
+    if (!ctx->multi)
+        return 0;
+    if (*ev == nullptr)
+        HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(*ev, stream));
+    *valid = true;
+    return 0;
+}
+
 static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void *static_iv12, const void *recs,
                         const uint32_t *order, size_t n, const uint8_t *src, uint8_t *dst, const uint8_t *aad,
                         uint32_t *status, hipStream_t stream, bool frame = false, uint8_t *types = nullptr,
@@ -1628,35 +1668,29 @@ static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void
     DeviceGuard guard(ctx->device);
     if (p.split != nullptr) {
         /* partials and tickets for n records (tickets are zero between launches: each record's last run resets its) */
+        if (ctx_stream(ctx, stream) != 0)
+            return -1;
         if (ctx->split_cap < n) {
             if (ctx->d_split)
                 (void)hipFree(ctx->d_split); /* synchronises the device: no launch still uses it */
             ctx->d_split = nullptr;
             ctx->split_cap = 0;
+            ctx->split_ev_valid = false;
             const size_t cap = n < 64 ? 64 : n;
             HIPCHK(hipMalloc(&ctx->d_split, cap * (SPLIT_PSLOTS * sizeof(u32x4) + sizeof(uint32_t))));
             HIPCHK(hipMemsetAsync((uint8_t *)ctx->d_split + cap * SPLIT_PSLOTS * sizeof(u32x4), 0, cap * sizeof(uint32_t),
                                   stream));
             ctx->split_cap = cap;
-            ctx->split_stream = stream;
         }
-        if (ctx->split_stream != stream) { /* the tickets are shared: order after the previous split launch */
-            if (ctx->split_event == nullptr)
-                HIPCHK(hipEventCreateWithFlags(&ctx->split_event, hipEventDisableTiming));
-            if (hipEventRecord(ctx->split_event, ctx->split_stream) == hipSuccess) {
-                HIPCHK(hipStreamWaitEvent(stream, ctx->split_event, 0));
-            } else {
-                (void)hipGetLastError();
-                HIPCHK(hipDeviceSynchronize());
-            }
-        }
+        /* the tickets are shared: order after the previous split launch */
+        if (res_wait(ctx, ctx->split_ev, ctx->split_ev_valid, stream) != 0)
+            return -1;
         uint32_t *tickets = (uint32_t *)((uint8_t *)ctx->d_split + ctx->split_cap * SPLIT_PSLOTS * sizeof(u32x4));
         hipLaunchKernelGGL(p.split, dim3(p.blocks), dim3(p.threads), 0, stream, ctx->d_ki, le32(iv), le32(iv + 4),
                            le32(iv + 8), recs, (uint32_t)n, src, dst, aad, status, types, conn,
                            (const u32x4 *)ctx->shared->d_win_aes, ctx->d_split, tickets);
         HIPCHK(hipGetLastError());
-        ctx->split_stream = stream;
-        return 0;
+        return res_used(ctx, &ctx->split_ev, &ctx->split_ev_valid, stream);
     }
     if (p.win != nullptr) {
         hipLaunchKernelGGL(p.win, dim3(p.blocks), dim3(p.threads), 0, stream, ctx->d_ki, le32(iv), le32(iv + 4),
@@ -1668,54 +1702,37 @@ static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void
     /*
      * Work counters are never reset: every wave takes tickets until one is out of range, so a launch consumes
      * exactly ngroups + (its waves) tickets, and the next launch on the slot starts there.  A slot is reused
-     * every WORK_SLOTS launches; when its previous launch went to another stream, the new stream first waits
-     * for everything queued on that one (reuse_event), so two launches never share a counter at once.  The
-     * slot's base is committed only once the launch has been accepted.
+     * every WORK_SLOTS launches; in multi-stream mode the new launch first waits on the slot's event, recorded
+     * right after its previous launch, so two launches never share a counter at once.  The slot's base is
+     * committed only once the launch has been accepted.
      */
     const uint32_t k = frame ? 4u : (uint32_t)g_lanes;
     const uint32_t ngroups = (uint32_t)((n + (64 / k) - 1) / (64 / k));
     const uint32_t wslot = ctx->work_next % WORK_SLOTS;
     uint32_t *work = ctx->d_work + wslot;
     const uint32_t work_base = ctx->work_base[wslot];
-    if (ctx->work_stream[wslot] != stream && ctx->work_next >= WORK_SLOTS) {
-        if (hipEventRecord(ctx->reuse_event, ctx->work_stream[wslot]) == hipSuccess) {
-            HIPCHK(hipStreamWaitEvent(stream, ctx->reuse_event, 0));
-        } else { /* that stream is gone (its work with it) or unusable: wait for the device instead */
-            (void)hipGetLastError();
-            HIPCHK(hipDeviceSynchronize());
-        }
-    }
+    if (ctx_stream(ctx, stream) != 0 || res_wait(ctx, ctx->work_ev[wslot], ctx->work_ev_valid[wslot], stream) != 0)
+        return -1;
     hipLaunchKernelGGL(p.batch, dim3(p.blocks), dim3(p.threads), 0, stream, ctx->d_ki, le32(iv), le32(iv + 4),
                        le32(iv + 8), recs, order, (uint32_t)n, src, dst, aad, status, types, work, work_base, conn);
     HIPCHK(hipGetLastError());
     ctx->work_base[wslot] = work_base + ngroups + p.blocks * (uint32_t)(WG_THREADS / 64);
-    ctx->work_stream[wslot] = stream;
     ++ctx->work_next;
-    return 0;
+    return res_used(ctx, &ctx->work_ev[wslot], &ctx->work_ev_valid[wslot], stream);
 }
 
 static inline size_t up16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 /*
  * The workspace of order_by_length and the stop-at-failure scan, for a use on `stream`.  Launches of one context may
- * go to any streams, and they share this buffer: a use on another stream than the last one first waits for
- * everything queued on that one (scratch_event), as the split tickets and the work slots do.  Growing it waits for
- * the last use before the old buffer is freed.
+ * go to any streams, and they share this buffer: in multi-stream mode a use first waits on the event recorded right
+ * after the previous use (scratch_done), as the split tickets and the work slots do.  Growing it waits for the last
+ * use before the old buffer is freed.
  */
 static int ensure_scratch(ptls_mi355x_aesgcm_context_t *ctx, size_t need, hipStream_t stream)
 {
-    if (ctx->scratch_used && ctx->scratch_stream != stream) {
-        if (ctx->scratch_event == nullptr)
-            HIPCHK(hipEventCreateWithFlags(&ctx->scratch_event, hipEventDisableTiming));
-        if (hipEventRecord(ctx->scratch_event, ctx->scratch_stream) == hipSuccess) {
-            HIPCHK(hipStreamWaitEvent(stream, ctx->scratch_event, 0));
-        } else { /* that stream is gone (its work with it) or unusable: wait for the device instead */
-            (void)hipGetLastError();
-            HIPCHK(hipDeviceSynchronize());
-        }
-    }
-    ctx->scratch_stream = stream;
-    ctx->scratch_used = true;
+    if (ctx_stream(ctx, stream) != 0 || res_wait(ctx, ctx->scratch_ev, ctx->scratch_ev_valid, stream) != 0)
+        return -1;
     if (need <= ctx->scratch_cap)
         return 0;
     if (ctx->d_scratch) {
@@ -1727,6 +1744,12 @@ static int ensure_scratch(ptls_mi355x_aesgcm_context_t *ctx, size_t need, hipStr
     HIPCHK(hipMalloc(&ctx->d_scratch, need));
     ctx->scratch_cap = need;
     return 0;
+}
+
+/* the scratch use just queued on `stream` (after ensure_scratch and its launches) */
+static int scratch_done(ptls_mi355x_aesgcm_context_t *ctx, hipStream_t stream)
+{
+    return res_used(ctx, &ctx->scratch_ev, &ctx->scratch_ev_valid, stream);
 }
 
 extern "C" {
@@ -1844,15 +1867,12 @@ ptls_mi355x_aesgcm_context_t *ptls_mi355x_aesgcm_new(const void *key, size_t key
     ctx->shared = d;
     ctx->num_cu = prop.multiProcessorCount;
     if (hipMalloc(&ctx->d_ki, sizeof(KeyImage)) != hipSuccess ||
-        hipMalloc(&ctx->d_work, WORK_SLOTS * sizeof(uint32_t)) != hipSuccess ||
-        hipEventCreateWithFlags(&ctx->reuse_event, hipEventDisableTiming) != hipSuccess) {
+        hipMalloc(&ctx->d_work, WORK_SLOTS * sizeof(uint32_t)) != hipSuccess) {
         snprintf(g_err, sizeof(g_err), "context allocation: %s", hipGetErrorString(hipGetLastError()));
         goto Fail;
     }
-    for (uint32_t i = 0; i < WORK_SLOTS; ++i) {
+    for (uint32_t i = 0; i < WORK_SLOTS; ++i)
         ctx->work_base[i] = g_ticket_origin;
-        ctx->work_stream[i] = nullptr;
-    }
     {
         /* the key goes through the shared pinned staging (zero-copy read by the setup kernel), cleared after */
         std::lock_guard<std::mutex> lk(d->mu);
@@ -1898,14 +1918,15 @@ void ptls_mi355x_aesgcm_free(ptls_mi355x_aesgcm_context_t *ctx)
         (void)hipFree(ctx->d_work);
     if (ctx->d_scratch)
         (void)hipFree(ctx->d_scratch);
-    if (ctx->scratch_event)
-        (void)hipEventDestroy(ctx->scratch_event);
-    if (ctx->reuse_event)
-        (void)hipEventDestroy(ctx->reuse_event);
     if (ctx->d_split)
         (void)hipFree(ctx->d_split);
-    if (ctx->split_event)
-        (void)hipEventDestroy(ctx->split_event);
+    for (uint32_t i = 0; i < WORK_SLOTS; ++i)
+        if (ctx->work_ev[i])
+            (void)hipEventDestroy(ctx->work_ev[i]);
+    if (ctx->split_ev)
+        (void)hipEventDestroy(ctx->split_ev);
+    if (ctx->scratch_ev)
+        (void)hipEventDestroy(ctx->scratch_ev);
     free(ctx);
 }
 
@@ -2015,7 +2036,7 @@ int ptls_mi355x_tls_open_records_ex(ptls_mi355x_aesgcm_context_t *ctx, const voi
     hipLaunchKernelGGL(mi355x_tls_truncate, dim3(g), dim3(256), 0, stream, (const TlsRecord *)recs, (uint32_t)n, first,
                        dst, status, types);
     HIPCHK(hipGetLastError());
-    return 0;
+    return scratch_done(ctx, stream);
 }
 
 int ptls_mi355x_tls_deliver_records(ptls_mi355x_aesgcm_context_t *ctx, const ptls_mi355x_tls_record_t *recs,
@@ -2060,7 +2081,7 @@ int ptls_mi355x_order_by_length(ptls_mi355x_aesgcm_context_t *ctx, const ptls_mi
     HIPCHK(hipGetLastError());
     HIPCHK(hipcub::DeviceRadixSort::SortPairsDescending(base + 3 * arr, temp, keys_in, keys_out, vals_in, order, (int)n, 0,
                                                         24, stream));
-    return 0;
+    return scratch_done(ctx, stream);
 }
 
 /*

@@ -126,11 +126,16 @@ struct st_ptls_mi355x_record_layer_t {
     size_t nreg;
     rl_slot_t slot[RL_SLOTS];
     uint64_t next_ticket, oldest; /* tickets [oldest, next_ticket) are outstanding */
+    /* windows in flight that name this layer, on its own slots or on another layer's (a multi-layer submit): counted
+     * once per window at submit, dropped when the window completes (its wait, or its lead layer's free) */
+    size_t inflight;
+    int zombie; /* freed while windows of other layers still name it: its memory goes with the last of them */
 };
 
 static char rl_err[160];
 
 static void op_discard(rl_op_t *op);
+static void op_release_layers(rl_op_t *op);
 
 static size_t up16(size_t x) { return (x + 15) & ~(size_t)15; }
 
@@ -272,21 +277,36 @@ ptls_mi355x_record_layer_t *ptls_mi355x_record_layer_new(const void *key, size_t
     return rl;
 }
 
+static void layer_dispose(ptls_mi355x_record_layer_t *rl)
+{
+    memset(rl->key, 0, sizeof(rl->key));
+    memset(rl->iv, 0, sizeof(rl->iv));
+    free(rl);
+}
+
 void ptls_mi355x_record_layer_free(ptls_mi355x_record_layer_t *rl)
 {
     if (rl == NULL)
         return;
-    while (rl->nreg != 0)
-        (void)ptls_mi355x_record_layer_unregister(rl, rl->reg[rl->nreg - 1].base);
     for (int i = 0; i < RL_SLOTS; ++i) {
         rl_op_t *op = &rl->slot[i].op;
-        if (op->busy) /* never waited: completes here, its results dropped */
+        if (rl->slot[i].stream != NULL) /* its own windows finish before their buffers and ranges go */
+            (void)hipStreamSynchronize(rl->slot[i].stream);
+        if (op->busy) { /* never waited: completes here, its results dropped */
+            op_release_layers(op);
             op_discard(op);
-        slot_release(&rl->slot[i]);
+        }
     }
-    memset(rl->key, 0, sizeof(rl->key));
-    memset(rl->iv, 0, sizeof(rl->iv));
-    free(rl);
+    while (rl->nreg != 0) /* waits for other layers' windows that still read or write its ranges */
+        (void)ptls_mi355x_record_layer_unregister(rl, rl->reg[rl->nreg - 1].base);
+    for (int i = 0; i < RL_SLOTS; ++i)
+        slot_release(&rl->slot[i]);
+    rl->next_ticket = rl->oldest;
+    if (rl->inflight != 0) { /* named by windows of other layers: they drop it at their completion */
+        rl->zombie = 1;
+        return;
+    }
+    layer_dispose(rl);
 }
 
 uint64_t ptls_mi355x_record_layer_get_seq(const ptls_mi355x_record_layer_t *rl) { return rl->seq; }
@@ -299,7 +319,7 @@ int ptls_mi355x_record_layer_rekey(ptls_mi355x_record_layer_t *rl, const void *k
 {
     if (key_size != 16 && key_size != 32)
         return rl_msg("key size must be 16 or 32");
-    if (rl->next_ticket != rl->oldest)
+    if (rl->next_ticket != rl->oldest || rl->inflight != 0)
         return rl_msg("rekey with windows outstanding (wait for them first)");
     uint8_t k[32];
     memcpy(k, key, key_size);
@@ -369,6 +389,9 @@ int ptls_mi355x_record_layer_unregister(ptls_mi355x_record_layer_t *rl, void *ba
             for (int k = 0; k < RL_SLOTS; ++k) /* no window of this layer still reads the range */
                 if (rl->slot[k].stream != NULL)
                     (void)hipStreamSynchronize(rl->slot[k].stream);
+            /* nor a window of another layer that names this one (its kernels may address the range): the device */
+            if (rl->inflight != 0)
+                (void)hipDeviceSynchronize();
             hipError_t e = rl->reg[i].owned ? hipHostUnregister(base) : hipSuccess;
             if (e == hipErrorHostMemoryNotRegistered) { /* registered twice, already released by the other owner */
                 (void)hipGetLastError();
@@ -452,14 +475,45 @@ static void op_discard(rl_op_t *op)
     memset(op, 0, sizeof(*op));
 }
 
-/* launched: the op joins the queue */
+/* 1 when layers[l] appeared earlier in the op (a layer given several times counts once) */
+static int repeated(const rl_op_t *op, size_t l)
+{
+    for (size_t m = 0; m < l; ++m)
+        if (op->layers[m] == op->layers[l])
+            return 1;
+    return 0;
+}
+
+/* launched: the op joins the queue, and every layer it names counts it in flight */
 static void op_commit(rl_slot_t *s, uint64_t *ticket)
 {
     ptls_mi355x_record_layer_t *rl = s->op.layers[0];
     s->op.busy = 1;
     s->op.ticket = rl->next_ticket++;
+    for (size_t l = 0; l < s->op.nlayers; ++l)
+        if (!repeated(&s->op, l))
+            ++s->op.layers[l]->inflight;
     if (ticket != NULL)
         *ticket = s->op.ticket;
+}
+
+/*
+ * The op is complete (waited, or dropped with its lead layer): every layer it names counts it out.  A layer with no
+ * window left in flight has no speculative receive position ahead of its delivered one (spec_seq = seq: a window
+ * that failed or came back STALE out of order leaves nothing to follow), and a layer freed meanwhile goes now.
+ */
+static void op_release_layers(rl_op_t *op)
+{
+    for (size_t l = 0; l < op->nlayers; ++l) {
+        ptls_mi355x_record_layer_t *x = op->layers[l];
+        if (repeated(op, l) || x->inflight == 0)
+            continue;
+        if (--x->inflight == 0) {
+            x->spec_seq = x->seq;
+            if (x->zombie && x != op->layers[0])
+                layer_dispose(x);
+        }
+    }
 }
 
 /* a copy list of up to n entries (dma windows: one allocation for both directions) */
@@ -701,6 +755,9 @@ static int open_submit(ptls_mi355x_record_layer_t *const *layers, size_t nlayers
         return -1;
     rl_op_t *op = &s->op;
     op->any_type = any_type;
+    for (size_t l = 0; l < nlayers; ++l) /* nothing in flight: the next record to submit is the next to deliver */
+        if (layers[l]->inflight == 0)
+            layers[l]->spec_seq = layers[l]->seq;
     size_t max = 0, nrec = 0, srcbytes = 0, ptbytes = 0, slots16 = 0;
     for (size_t l = 0; l < nlayers; ++l) /* a record takes at least 5 wire bytes */
         max += any_type ? 1 : inlen[l] / PTLS_MI355X_TLS_HEADER_SIZE + 1;
@@ -869,6 +926,16 @@ static void finish_seal(rl_slot_t *s, size_t *outlen, size_t *nrecords, size_t *
     rl_op_t *op = &s->op;
     for (size_t l = 0, off = 0; l < op->nlayers; ++l) {
         const rl_part_t *p = &op->part[l];
+        if (op->layers[l]->zombie) { /* freed meanwhile: nothing is delivered to it */
+            off += op->direct ? 0 : p->wire;
+            outlen[l] = 0;
+            if (nrecords != NULL)
+                nrecords[l] = 0;
+            if (consumed != NULL)
+                consumed[l] = 0;
+            alerts[l] = PTLS_MI355X_RECORD_LAYER_STALE;
+            continue;
+        }
         if (!op->direct && p->wire != 0) {
             memcpy(op->out[l], s->h_buf + op->off_dst + off, p->wire);
             off += p->wire;
@@ -895,6 +962,15 @@ static void finish_open(rl_slot_t *s, size_t *outlen, size_t *nrecords, size_t *
         uint8_t *slots = op->direct ? (uint8_t *)op->out[l] : s->h_buf + op->off_dst + p->dst_add;
         size_t done = 0, wire_done = 0, olen = 0;
         int a = 0;
+        if (x->zombie) { /* freed meanwhile: nothing is delivered to it */
+            consumed[l] = outlen[l] = 0;
+            if (nrecords != NULL)
+                nrecords[l] = 0;
+            alerts[l] = PTLS_MI355X_RECORD_LAYER_STALE;
+            if (p->n != 0 && !op->direct)
+                memset(slots, 0, p->ptbytes);
+            continue;
+        }
         if (p->seq0 != x->seq) {
             a = PTLS_MI355X_RECORD_LAYER_STALE; /* a window before this one stopped early */
         } else if (p->n != 0) {
@@ -959,6 +1035,10 @@ static int op_wait(ptls_mi355x_record_layer_t *rl, uint64_t ticket, size_t *outl
     if (op->nrec != 0 && (e = hipStreamSynchronize(s->stream)) != hipSuccess) {
         rl_fail("synchronize", e);
         op_scrub(s);
+        if (!op->is_seal) /* nothing delivered: the next window starts at the delivered position */
+            for (size_t l = 0; l < op->nlayers; ++l)
+                if (!op->layers[l]->zombie)
+                    op->layers[l]->spec_seq = op->layers[l]->seq;
         for (size_t l = 0; l < op->nlayers; ++l) {
             outlen[l] = 0;
             if (nrecords != NULL)
@@ -975,6 +1055,7 @@ static int op_wait(ptls_mi355x_record_layer_t *rl, uint64_t ticket, size_t *outl
         finish_open(s, outlen, nrecords, consumed != NULL ? consumed : dummy, alerts, type);
     }
     ++rl->oldest;
+    op_release_layers(op); /* (a failed window's open parts: spec_seq back to seq when nothing else is in flight) */
     op_discard(op);
     return ret;
 }
@@ -991,7 +1072,7 @@ int ptls_mi355x_record_layer_wait(ptls_mi355x_record_layer_t *rl, uint64_t ticke
 static int no_pending(ptls_mi355x_record_layer_t *const *layers, size_t nlayers)
 {
     for (size_t l = 0; l < nlayers; ++l) {
-        if (layers[l]->next_ticket != layers[l]->oldest) {
+        if (layers[l]->next_ticket != layers[l]->oldest || layers[l]->inflight != 0) {
             rl_msg("asynchronous windows outstanding (wait for them first)");
             return 0;
         }

@@ -2,12 +2,14 @@
 
 - seal -> open round trip over the whole batch: every status equals the record length, and the
   opened plaintext equals the source byte-for-byte (compared on the device);
-- a random sample of sealed records is bit-exact against the CPU oracle;
+- a random sample of sealed records (SAMPLE = 1024 per config) is bit-exact against the CPU oracle (its multithreaded
+  batch entry point over the sampled records, compacted);
 - flipping one bit in a sample of records (ciphertext, tag) fails exactly those records, zeroes their
   output, and leaves every other record verified.
 
-Configs (BASELINE.json configs[1..3]): 1 M x 1400 B AES-128, 256 K x 16 KiB AES-256, 1 M ragged
-U{64..16384} AES-128 (ordered launches).  Each case holds ~3 copies of its batch in HBM (<= 24 GB).
+Configs (BASELINE.json configs[1..3] and the north-star shape): 1 M x 1400 B AES-128, 256 K x 16 KiB AES-128 (north
+star), 256 K x 16 KiB AES-256, 256 K x 16385 B AES-128 (TLS-max inner plaintext), 1 M ragged U{64..16384} AES-128
+(ordered launches).  Each case holds ~3 copies of its batch in HBM (<= 24 GB).
 """
 import zlib
 
@@ -20,8 +22,11 @@ from rapido_amd import records
 
 pytestmark = pytest.mark.gpu
 
+SAMPLE = 1024
+
 CASES = [
     ("1400", 16, 1 << 20, 1400),
+    ("16k-aes128", 16, 1 << 18, 16384),  # the north-star shape (BASELINE.json north_star)
     ("16k-aes256", 32, 1 << 18, 16384),
     ("16k-max-aes128", 16, 1 << 18, 16385),  # TLS-max inner plaintext: a 1-byte tail block per record
     ("ragged", 16, 1 << 20, None),
@@ -83,14 +88,28 @@ def test_full_size_round_trip(gpu, name, keylen, n, length):
     assert int(mask.sum(dtype=torch.int64).item()) == int(recs["len"].sum())
     assert not bool(((d_pt != d_src) & mask).any().item())  # elementwise: no >2^32-element boolean gather
 
-    # a sample is bit-exact against the oracle
-    sample = rng.choice(n, size=24, replace=False)
-    for i in sample:
-        r = recs[i]
-        a, ln = int(r["src"]), int(r["len"])
-        want = oracle.seal(key, oracle.build_iv(iv, int(r["seq"])), aad[int(r["aad"]): int(r["aad"]) + 5].tobytes(),
-                           d_src[a: a + ln].cpu().numpy().tobytes())
-        assert d_ct[a: a + ln + 16].cpu().numpy().tobytes() == want
+    # a sample of SAMPLE records is bit-exact against the oracle: the sampled plaintexts compacted into a small batch
+    # of their own (same keys, nonces and AADs), sealed by the oracle's multithreaded batch entry point
+    sample = np.sort(rng.choice(n, size=SAMPLE, replace=False))
+    sub = recs[sample].copy()
+    ln_s = sub["len"].astype(np.int64)
+    slot = (ln_s + 16 + 255) // 256 * 256
+    offs = np.concatenate([[0], np.cumsum(slot)[:-1]]).astype(np.int64)
+    sub_src = np.zeros(int(slot.sum()), np.uint8)
+    got = np.zeros_like(sub_src)
+    for k, i in enumerate(sample):
+        a, ln, o = int(recs[i]["src"]), int(ln_s[k]), int(offs[k])
+        sub_src[o: o + ln] = d_src[a: a + ln].cpu().numpy()
+        got[o: o + ln + 16] = d_ct[a: a + ln + 16].cpu().numpy()
+    sub_aad = np.concatenate([aad[int(r["aad"]): int(r["aad"]) + 5] for r in sub])
+    sub["src"] = offs.astype(np.uint64)
+    sub["dst"] = offs.astype(np.uint64)
+    sub["aad"] = np.arange(SAMPLE, dtype=np.uint64) * 5
+    want = np.zeros_like(sub_src)
+    oracle.batch(True, key, iv, sub, sub_src, want, sub_aad)
+    for k in range(SAMPLE):
+        o, ln = int(offs[k]), int(ln_s[k])
+        assert np.array_equal(got[o: o + ln + 16], want[o: o + ln + 16]), f"record {int(sample[k])}"
 
     # tamper: one ciphertext bit in some records, one tag bit in others
     bad_ct = rng.choice(n, size=8, replace=False)

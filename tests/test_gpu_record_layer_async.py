@@ -308,3 +308,58 @@ def test_seal_output_over_its_fragments(gpu, transport):
     want, seq = oracle_window(key, iv, 11, frags_b)
     assert region[:olen].tobytes() == want and nrec == 4 and tx.seq == seq
     tx.close()
+
+
+@pytest.mark.parametrize("transport", ["direct", "zero_copy"])
+def test_free_and_rekey_of_a_layer_named_by_another_layers_window(gpu, transport):
+    """A window led by layer A that also names layer B (a multi-layer submit): B cannot be rekeyed or used
+    synchronously while it is in flight; B freed meanwhile (its registered range unregistered after the device has
+    finished with it) completes STALE in A's wait, with A's part delivered and bit-exact."""
+    rng = np.random.default_rng(404)
+    key, iv = rng.integers(0, 256, 16, dtype=np.uint8).tobytes(), rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    a, b = ra.RecordLayer(key, conn_iv(iv, 0), seq=3), ra.RecordLayer(key, conn_iv(iv, 1), seq=40)
+    h = Host(transport, [b, a], 1 << 21)  # direct: the range is B's own registration (A reuses it)
+    wins_b = [[rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in (16384, 999, 5)] for _ in range(2)]
+    wins = [[h.take(len(f), f) for f in w] for w in wins_b]
+    outs = [h.take(sum(len(f) + ra.TLS_OVERHEAD for f in w)) for w in wins_b]
+    t = ra.record_layer_seal_submit_multi([a, b], wins, outs)
+    assert b.pending == 0  # the window is on A's queue ...
+    with pytest.raises(RuntimeError):
+        b.rekey(key, conn_iv(iv, 1))  # ... but names B
+    with pytest.raises(RuntimeError):
+        b.seal([wins_b[1][0]])
+    b.close()
+    res = a.wait_multi(t, 2)
+    want, s = oracle_window(key, conn_iv(iv, 0), 3, wins_b[0])
+    assert res[0][:2] == (len(want), 3) and outs[0][:len(want)].tobytes() == want and a.seq == s
+    assert res[1] == (0, 0, 0, ra.RECORD_LAYER_STALE)
+    a.close()
+
+
+def test_open_windows_waited_out_of_order_across_leads(gpu):
+    """Layer B's receive windows in two submits led by different layers, the later one waited first: it comes back
+    STALE for B, the earlier one delivers, and B's next window opens normally (its speculative position resyncs once
+    nothing names it in flight)."""
+    rng = np.random.default_rng(505)
+    key, iv = rng.integers(0, 256, 16, dtype=np.uint8).tobytes(), rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    ivs = [conn_iv(iv, c) for c in range(3)]
+    frags = [[rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in (3000, 17, 16384)] for _ in range(4)]
+    w_a, _ = oracle_window(key, ivs[0], 0, frags[0])
+    w_b1, sb = oracle_window(key, ivs[1], 9, frags[1])
+    w_b2, sb2 = oracle_window(key, ivs[1], sb, frags[2])
+    w_c, _ = oracle_window(key, ivs[2], 0, frags[3])
+    a, b, c = ra.RecordLayer(key, ivs[0]), ra.RecordLayer(key, ivs[1], seq=9), ra.RecordLayer(key, ivs[2])
+    arr = [np.frombuffer(w, np.uint8).copy() for w in (w_a, w_b1, w_c, w_b2)]
+    outs = [np.zeros(len(w), np.uint8) for w in arr]
+    t1, _ = ra.record_layer_open_submit_multi([a, b], arr[:2], outs[:2])
+    t2, _ = ra.record_layer_open_submit_multi([c, b], arr[2:], outs[2:])
+    r2 = c.wait_multi(t2, 2)
+    assert r2[0][3] == 0 and outs[2][:r2[0][0]].tobytes() == b"".join(frags[3])
+    assert r2[1] == (0, 0, 0, ra.RECORD_LAYER_STALE)  # B's first window was not delivered yet
+    r1 = a.wait_multi(t1, 2)
+    assert r1[1][:2] == (sum(map(len, frags[1])), 3) and b.seq == sb
+    # B's second window again, alone: delivered (before the fix its submits stayed STALE until set_seq)
+    alert, pt, cons, n = ra.record_layer_open_multi([b], [w_b2])[0]
+    assert (alert, n, cons) == (0, 3, len(w_b2)) and pt == b"".join(frags[2]) and b.seq == sb2
+    for rl in (a, b, c):
+        rl.close()

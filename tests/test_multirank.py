@@ -105,3 +105,62 @@ def test_ragged_byte_shards_cover_the_batch():
         for i, sealed in merged.items():
             pt = (hashlib.sha256(b"rec%d" % i).digest() * (int(lengths[i]) // 32 + 1))[: int(lengths[i])]
             assert sealed == oracle.seal(key, oracle.build_iv(iv, i), bytes(records.tls_aad(lengths[i:i + 1])), pt)
+
+
+def _line_worker(rank, world, port, q, dev_index, same_ok):
+    """bench.py's N > 1 bookkeeping on gloo: the rank-to-GPU map check and the per-rank figures gathered for the line."""
+    import torch.distributed as dist
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        placement = bench.check_device_map(dev_index(rank), same_ok, 2)
+    except SystemExit as e:
+        q.put((rank, "exit", str(e)))
+        dist.destroy_process_group()
+        return
+    ranks = bench.gather_rank_stats({"rank": rank, "host": "h", "device": dev_index(rank), "device_name": "gfx950",
+                                     "rank_gibps": 100.0 + rank, "rank_ms_per_step": 2.0 - rank, "seal_gibps": 1.0,
+                                     "open_gibps": 2.0, "launch_ms": 1.5})
+    q.put((rank, placement, ranks))
+    dist.destroy_process_group()
+
+
+def _run_line(dev_index, same_ok):
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_line_worker, args=(r, world, port, q, dev_index, same_ok)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def _dev_per_rank(r):
+    return r
+
+
+def _dev_zero(r):
+    return 0
+
+
+def test_bench_line_per_rank_figures():
+    """The N > 1 line carries every rank's own figures (device ordinal, rates, launch time) in rank order."""
+    import bench
+    for rank, placement, ranks in _run_line(_dev_per_rank, False):
+        assert [p[1] for p in placement] == [0, 1]
+        assert [r["rank"] for r in ranks] == [0, 1] and [r["device"] for r in ranks] == [0, 1]
+        assert all(set(r) == set(bench.RANK_KEYS) for r in ranks)
+        assert [r["rank_gibps"] for r in ranks] == [100.0, 101.0]
+
+
+def test_bench_refuses_two_ranks_on_one_gpu():
+    """Two ranks mapped to one device fail fast unless RAPIDO_BENCH_SAME_DEVICE (the rehearsal) allows it."""
+    res = _run_line(_dev_zero, False)
+    assert all(r[1] == "exit" and "share a GPU" in r[2] for r in res)
+    for rank, placement, ranks in _run_line(_dev_zero, True):
+        assert [p[1] for p in placement] == [0, 0] and len(ranks) == 2
