@@ -171,6 +171,9 @@ static_assert(sizeof(TlsRecord) == sizeof(ptls_mi355x_tls_record_t), "descriptor
 #ifndef GCM_STATIC_GROUPS
 #define GCM_STATIC_GROUPS 0
 #endif
+#ifndef GCM_STAGGER
+#define GCM_STAGGER 0 /* measurement builds: batch-kernel waves start in four phases (gcm_batch_body) */
+#endif
 #ifndef GCM_FAST_STEP
 #define GCM_FAST_STEP 1 /* batch kernels: interior steps on lane_walk's fast path (scalar branch, no per-lane flags) */
 #endif
@@ -222,6 +225,16 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
 #endif
     const uint32_t lanesel = (lane & 31u) * 4u | 0x10000u; /* bank + image-B select (gcm_core.h) */
     const uint32_t ngroups = (nrecs + R - 1) / R;
+#if GCM_STAGGER
+    /*
+     * Measurement variant: the waves of a workgroup start their walks in four phases, GCM_STAGGER s_sleep 127 (~8K
+     * cycles each) apart -- wave w in phase w >> 2, so each SIMD holds one wave of every phase.  With records of one
+     * length every group takes the same time, so waves that start together stay in step, and their per-record phases
+     * (the closing multiply, the next group's ticket, descriptors and first loads) coincide on the CU.
+     */
+    for (uint32_t i = 0, n = (threadIdx.x >> 8) * (uint32_t)GCM_STAGGER; i < n; ++i)
+        __builtin_amdgcn_s_sleep(127);
+#endif
 
     /*
      * Record groups (64/K records) are handed out dynamically: one returning atomic per group

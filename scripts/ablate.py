@@ -16,7 +16,10 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-VDIR = os.path.join(ROOT, "rapido_amd", "_lib", "variants")
+# variant libraries: travel to the GPU box while they exist (delete the directory after an A/B: the round-end push
+# should carry only the product library); the "head" source snapshot stays under rapido_amd/_lib/variants
+VDIR = os.environ.get("ABLATE_VDIR") or os.path.join(ROOT, "scripts", "_abl")
+HEAD_SRC = os.path.join(ROOT, "rapido_amd", "_lib", "variants", "src_head")
 
 VARIANTS = {
     "base": [],
@@ -58,7 +61,11 @@ VARIANTS = {
     "noscale": ["-DGCM_ABLATE_SCALE=1"],  # no closing H^(K-j) multiply (wrong tags: timing only)  # r03: every step through the per-lane flags (no interior fast path)
     "gh8sel": ["-DGCM_GH8=1", "-DGCM_GH8_LANESEL=1"],  # GH8 byte permutation folded into per-lane address selectors  # 5-bit ds_read_b64 GHASH tables for K = 4 (evaluated: 33% slower, bank conflicts)
     # "@src=DIR": compile gcm_engine.hip from DIR (e.g. a `git show` of an older revision) instead of csrc/
-    "head": ["@src=" + os.path.join(VDIR, "src_head")],
+    "head": ["@src=" + HEAD_SRC],
+    # r04: waves start their walks in four phases (wave w >> 2), GCM_STAGGER x s_sleep 127 apart
+    "stagger2": ["-DGCM_STAGGER=2"],
+    "stagger5": ["-DGCM_STAGGER=5"],
+    "stagger10": ["-DGCM_STAGGER=10"],
     "no_ghash": ["-DGCM_ABLATE_GHASH=1"],
     "no_aes": ["-DGCM_ABLATE_AES=1"],
     "no_both": ["-DGCM_ABLATE_AES=1", "-DGCM_ABLATE_GHASH=1"],
