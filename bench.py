@@ -298,11 +298,17 @@ def measure(ra, wl_key, args, dev, rank, world, check):
         else:
             e.open_batch(iv, rp, cnt, d_ct.data_ptr(), d_pt.data_ptr(), d_aad.data_ptr(), d_st.data_ptr() + 4 * r0, s)
 
-    def step():
+    def step(ev=None):
+        if ev is not None:  # one chunk: HIP events around the step's two launches (the roofline's launch times)
+            ev[0].record(stream)
         for si, r0, r1 in chunks:
             seal_chunk(engs[si], streams[si].cuda_stream, r0, r1 - r0)
+        if ev is not None:
+            ev[1].record(stream)
         for si, r0, r1 in chunks:
             open_chunk(engs[si], streams[si].cuda_stream, r0, r1 - r0)
+        if ev is not None:
+            ev[2].record(stream)
 
     def fork(ev):
         ev.record(streams[0])
@@ -327,13 +333,14 @@ def measure(ra, wl_key, args, dev, rank, world, check):
     ev_t0 = torch.cuda.Event(enable_timing=True)
     ev_t1 = torch.cuda.Event(enable_timing=True)
     ev_join = [torch.cuda.Event() for _ in streams[1:]]
+    sev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)] if nchunk == 1 else None
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     fork(ev_t0)
     for i in range(args.steps):
-        step()
+        step(sev[i] if sev is not None else None)
     join(ev_join)
     ev_t1.record(streams[0])
     torch.cuda.synchronize(dev)
@@ -344,17 +351,19 @@ def measure(ra, wl_key, args, dev, rank, world, check):
         elapsed = max_over_ranks(elapsed, dev)
     region_ms = ev_t0.elapsed_time(ev_t1)  # the timed region on the GPU clock (HIP events)
 
-    # the kernels one launch at a time, after the timed region: the whole batch sealed, then opened, on one stream with
-    # HIP events around each launch (per-kernel launch times for the roofline's serial_launch and lds_roofline)
-    serial_steps = max(3, min(args.steps, 10))
-    sev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(serial_steps)]
-    for ev in sev:
-        ev[0].record(stream)
-        seal_chunk(eng, sh, 0, n)
-        ev[1].record(stream)
-        open_chunk(eng, sh, 0, n)
-        ev[2].record(stream)
-    torch.cuda.synchronize(dev)
+    launches_note = "the timed steps' launches only (HIP events on the launch stream), warmups excluded"
+    if sev is None:
+        # chunks > 1: launches overlap at their ends, so a launch's own time is taken one launch at a time after the
+        # timed region (the whole batch sealed, then opened, on one stream, HIP events around each launch)
+        sev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(max(3, min(args.steps, 10)))]
+        for ev in sev:
+            ev[0].record(stream)
+            seal_chunk(eng, sh, 0, n)
+            ev[1].record(stream)
+            open_chunk(eng, sh, 0, n)
+            ev[2].record(stream)
+        torch.cuda.synchronize(dev)
+        launches_note = f"{len(sev)} launches of the whole batch one at a time after the timed region (HIP events)"
     seal_all = [e[0].elapsed_time(e[1]) for e in sev]
     open_all = [e[1].elapsed_time(e[2]) for e in sev]
     seal_ms, open_ms = float(np.mean(seal_all)), float(np.mean(open_all))
@@ -378,10 +387,10 @@ def measure(ra, wl_key, args, dev, rank, world, check):
     dom_is_seal = seal_ms >= open_ms
     dom_ms = seal_ms if dom_is_seal else open_ms
     dom_bytes = seal_b if dom_is_seal else open_b
-    achieved_serial = dom_bytes / (dom_ms * 1e-3) / 1e9
-    # the timed region: every launch's algorithmic bytes over the region's HIP-event time (launches overlap at their
-    # ends when chunks > 1, so the per-launch time of one kernel is not defined there)
-    achieved = (seal_b + open_b) * args.steps / (region_ms * 1e-3) / 1e9
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    # the whole timed region: every launch's algorithmic bytes over the region's HIP-event time (with chunks > 1 the
+    # launches overlap at their ends)
+    achieved_region = (seal_b + open_b) * args.steps / (region_ms * 1e-3) / 1e9
     kname = ra.kernel_name(dom_is_seal, wl["key"], n)
     chunk_kernels = sorted({ra.kernel_name(s, wl["key"], r1 - r0) for s in (True, False) for _, r0, r1 in chunks})
 
@@ -414,20 +423,15 @@ def measure(ra, wl_key, args, dev, rank, world, check):
         "rank_ms_per_step": round(elapsed_rank / args.steps * 1e3, 4),
         "pipeline": {"chunks": len(chunks), "streams": nstream, "kernels": chunk_kernels,
                      "region_ms": round(region_ms, 4), "wall_ms": round(elapsed * 1e3, 4)},
-        "roofline": {"bound": "hbm", "kernel": kname if nchunk == 1 else "+".join(chunk_kernels),
-                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+        "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                     "algorithmic_bytes_per_step": seal_b + open_b,
-                     "launches": f"the timed region: {args.steps} steps x {2 * len(chunks)} launches (seal and open of "
-                                 f"{len(chunks)} chunk(s) on {nstream} stream(s)), algorithmic bytes / HIP-event time "
-                                 f"of the region; warmups excluded",
-                     "serial_launch": {"kernel": kname, "algorithmic_bytes_per_launch": dom_bytes,
-                                       "launch_ms": round(dom_ms, 4),
-                                       "launch_ms_median": round(float(np.median(seal_all if dom_is_seal else open_all)), 4),
-                                       "achieved": round(achieved_serial, 1),
-                                       "frac": round(achieved_serial / HBM_PEAK_GBPS, 4),
-                                       "launches": f"{serial_steps} launches of the whole batch one at a time after the "
-                                                   f"timed region (HIP events on the launch stream)"}},
+                     "algorithmic_bytes_per_launch": dom_bytes, "launch_ms": round(dom_ms, 4),
+                     "launch_ms_median": round(float(np.median(seal_all if dom_is_seal else open_all)), 4),
+                     "launches": launches_note,
+                     "region": {"frac": round(achieved_region / HBM_PEAK_GBPS, 4), "achieved": round(achieved_region, 1),
+                                "algorithmic_bytes_per_step": seal_b + open_b, "region_ms": round(region_ms, 4),
+                                "note": "every launch of the timed region (seal + open, all chunks) over its HIP-event "
+                                        "time"}},
         "lds_roofline": {"bound": "lds", "kernel": kname, "achieved": round(dom_payload, 1),
                          "peak": round(lds_ceiling, 1), "unit": "GB/s payload",
                          "frac": round(dom_payload / lds_ceiling, 4),
@@ -584,8 +588,9 @@ def main() -> None:
                     help="comma-separated side workloads measured at N=1 after the main one")
     ap.add_argument("--no-workloads", action="store_true", help="measure the main workload only")
     ap.add_argument("--side-steps", type=int, default=10, help="timed steps of each side workload")
-    ap.add_argument("--pipeline", type=int, default=2,
-                    help="chunks of the batch per step, alternating over two streams (1: one stream, one launch each)")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="chunks of the batch per step, alternating over two streams (1: one stream, one launch each; "
+                         "2 measured +0.1..1.9%%, profiles/r04a_pipeline_ab.jsonl)")
     ap.add_argument("--lanes", type=int, default=0, help="lanes per record (1/2/4/8); 0 = engine default")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e", action="store_true", help="time the PCIe-inclusive path (pinned host in/out); default at N=1")
@@ -662,7 +667,7 @@ def main() -> None:
             "rank": rank, "host": socket.gethostname(), "device": dev_index,
             "device_name": torch.cuda.get_device_name(dev), "rank_gibps": res["rank_gibps"],
             "rank_ms_per_step": res["rank_ms_per_step"], "seal_gibps": res["seal_gibps"],
-            "open_gibps": res["open_gibps"], "launch_ms": res["roofline"]["serial_launch"]["launch_ms"]})
+            "open_gibps": res["open_gibps"], "launch_ms": res["roofline"]["launch_ms"]})
         out["placement"] = [list(p) for p in placement]
     if world == 1 and not args.no_e2e:
         out["window_latency"] = window_latency(ra, extra, dev)

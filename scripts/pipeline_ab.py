@@ -39,7 +39,7 @@ def main():
                 del ex
                 torch.cuda.empty_cache()
                 line = {"round": rnd, "workload": wl, "chunks": c, "value": r["value"],
-                        "frac": r["roofline"]["frac"], "serial_frac": r["roofline"]["serial_launch"]["frac"],
+                        "frac": r["roofline"]["frac"], "region_frac": r["roofline"]["region"]["frac"],
                         "seal_gibps": r["seal_gibps"], "open_gibps": r["open_gibps"],
                         "ms_per_step": r["ms_per_step"]}
                 print(json.dumps(line), flush=True)

@@ -63,7 +63,7 @@ def run():
         print(f"AES-{8 * keylen}: bitsliced keystream on the GPU matches the oracle (256 blocks)", flush=True)
 
         nr = 10 if keylen == 16 else 14
-        nunits = ncu * 16 * 96
+        nunits = ncu * 16 * 96 * int(os.environ.get("PROBE_UNITS_MULT", "1"))
         d_work = torch.zeros(1, dtype=torch.int32, device=dev)
         d_out = torch.zeros(ncu * 1024, dtype=torch.int32, device=dev)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -71,7 +71,7 @@ def run():
         threads = int(os.environ.get("PROBE_THREADS", "1024"))
         for n_tt in [int(x) for x in os.environ.get("PROBE_NTT", "16,14,13,12,11,10,8,6,4,0").split(",")]:
             ts = []
-            for rep in range(4):
+            for rep in range(int(os.environ.get("PROBE_REPS", "4"))):
                 d_work.zero_()
                 ev[0].record()
                 assert lib.probe_run(d_ki.data_ptr(), nr, n_tt, nunits, ncu, d_work.data_ptr(), d_out.data_ptr(),
