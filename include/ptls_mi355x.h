@@ -381,10 +381,19 @@ int ptls_mi355x_record_layer_open_record(ptls_mi355x_record_layer_t *rl, const v
 int ptls_mi355x_record_layer_rekey(ptls_mi355x_record_layer_t *rl, const void *key, size_t key_size, const void *iv12);
 /*
  * Asynchronous windows: a submit plans and stages the window and launches it on the next of the layer's (layers[0]'s)
- * 4 slots -- each its own stream, staging and engine context -- and returns at once; so consecutive windows of one
- * connection, and windows of several connections, overlap their PCIe transfers and kernels.  Windows complete in
+ * 4 launch slots -- each its own stream, staging and engine context -- and returns at once; so consecutive windows of
+ * one connection, and windows of several connections, overlap their PCIe transfers and kernels.  Windows complete in
  * submission order: ptls_mi355x_record_layer_wait(rl, ticket, ...) for the oldest ticket of rl, then the next.  At
- * most 4 windows per layer are outstanding (a fifth submit returns -1).  A synchronous call or a rekey on a layer
+ * most 32 windows per layer are outstanding (a 33rd submit returns -1), in at most 4 launches.
+ *
+ * Coalescing (a single-layer submit, the default): a connection's windows are queued and go out together, ONE launch
+ * for a group (as if the layer had been given once per window in one submit), the group being the layer's outstanding
+ * windows spread over its 4 launch slots: ceil(outstanding / 4).  So up to 4 windows outstanding every window launches
+ * at its submit, as without coalescing; at 16 outstanding, 4 windows per launch, 4 launches in flight.  A queue goes
+ * out when its group is complete and a launch slot is free (checked at each submit and wait), when nothing of its
+ * layer runs on the GPU, at the first wait for one of its windows, when 16 are queued
+ * (ptls_mi355x_record_layer_set_coalesce), or at ptls_mi355x_record_layer_flush.  Tickets, seq and results are those
+ * of separate launches.  A synchronous call or a rekey on a layer
  * with windows outstanding -- its own, or another layer's windows that name it -- returns -1.  Buffers (fragments,
  * inputs, outputs) must stay untouched until the window's wait.  Freeing or unregistering a layer that another
  * layer's outstanding window names first waits for the device; that window then completes with alerts[l] =
@@ -411,8 +420,19 @@ int ptls_mi355x_record_layer_open_submit(ptls_mi355x_record_layer_t *const *laye
                                          uint64_t *ticket);
 int ptls_mi355x_record_layer_wait(ptls_mi355x_record_layer_t *rl, uint64_t ticket, size_t *outlen, size_t *nrecords,
                                   size_t *consumed, int *alerts);
-/* windows submitted and not yet waited for */
+/* windows submitted and not yet waited for (queued or launched) */
 size_t ptls_mi355x_record_layer_pending(const ptls_mi355x_record_layer_t *rl);
+/* launches the layer's queued windows now (when one of its 4 launch slots is free; else at the next wait); 0 or -1 */
+int ptls_mi355x_record_layer_flush(ptls_mi355x_record_layer_t *rl);
+/* at most `windows` (<= 16) of a connection's queued windows per launch; 0 or 1: every single-layer window launches at
+ * its submit.  Flushes the queue; returns the previous value (default 16). */
+size_t ptls_mi355x_record_layer_set_coalesce(ptls_mi355x_record_layer_t *rl, size_t windows);
+/* on != 0: single-layer windows queue even while nothing of the layer runs, until the queue holds `coalesce` windows,
+ * the first wait for one of them, or cork(rl, 0), which launches them (TCP_CORK for a burst of windows known to
+ * follow each other).  0 or -1 (the launch on uncorking failed). */
+int ptls_mi355x_record_layer_cork(ptls_mi355x_record_layer_t *rl, int on);
+/* launches this layer has led so far (diagnostics: coalesced windows share one) */
+uint64_t ptls_mi355x_record_layer_launches(const ptls_mi355x_record_layer_t *rl);
 const char *ptls_mi355x_record_layer_last_error(void);
 /* How the bytes travel (record_layer.c): a call whose fragments and output (seal), or input and output (open; out
  * at least as large as the records' ciphertexts), all lie in ranges registered below runs DIRECT: read and written in

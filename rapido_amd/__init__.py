@@ -70,6 +70,8 @@ EXPORTED_FUNCTIONS = (
     "ptls_mi355x_record_layer_seal_multi", "ptls_mi355x_record_layer_open_multi",
     "ptls_mi355x_record_layer_open_record", "ptls_mi355x_record_layer_rekey", "ptls_mi355x_record_layer_seal_submit",
     "ptls_mi355x_record_layer_open_submit", "ptls_mi355x_record_layer_wait", "ptls_mi355x_record_layer_pending",
+    "ptls_mi355x_record_layer_flush", "ptls_mi355x_record_layer_set_coalesce", "ptls_mi355x_record_layer_launches",
+    "ptls_mi355x_record_layer_cork",
     "ptls_mi355x_record_layer_set_direct_dma", "ptls_mi355x_tls_deliver_records",
 )
 EXPORTED_OBJECTS = ("ptls_mi355x_aes128gcm", "ptls_mi355x_aes256gcm", "ptls_mi355x_aes128ctr",
@@ -185,6 +187,12 @@ def lib() -> C.CDLL:
             L.ptls_mi355x_record_layer_wait.argtypes = [vp, u64, vp, vp, vp, vp]
             L.ptls_mi355x_record_layer_pending.argtypes = [vp]
             L.ptls_mi355x_record_layer_pending.restype = sz
+            L.ptls_mi355x_record_layer_flush.argtypes = [vp]
+            L.ptls_mi355x_record_layer_set_coalesce.argtypes = [vp, sz]
+            L.ptls_mi355x_record_layer_set_coalesce.restype = sz
+            L.ptls_mi355x_record_layer_launches.argtypes = [vp]
+            L.ptls_mi355x_record_layer_launches.restype = u64
+            L.ptls_mi355x_record_layer_cork.argtypes = [vp, C.c_int]
             L.ptls_mi355x_record_layer_set_direct_dma.argtypes = [vp, C.c_int]
         for name in ("ptls_mi355x_set_win16_records", "ptls_mi355x_set_split_records"):
             if hasattr(L, name):  # (absent from older builds used in A/B timing runs)
@@ -604,6 +612,23 @@ class RecordLayer:
     @property
     def pending(self) -> int:
         return lib().ptls_mi355x_record_layer_pending(self.handle)
+
+    def flush(self) -> None:
+        """Launches the queued (coalesced) windows now (ptls_mi355x_record_layer_flush)."""
+        self._check(lib().ptls_mi355x_record_layer_flush(self.handle), "flush")
+
+    @property
+    def launches(self) -> int:
+        """Launches this layer has led (ptls_mi355x_record_layer_launches)."""
+        return lib().ptls_mi355x_record_layer_launches(self.handle)
+
+    def cork(self, on: bool) -> None:
+        """Queue every window until uncorked (launched together), the first wait or a full queue."""
+        self._check(lib().ptls_mi355x_record_layer_cork(self.handle, 1 if on else 0), "cork")
+
+    def set_coalesce(self, windows: int) -> int:
+        """At most `windows` queued windows per launch (0/1: every window launches at its submit) -> previous."""
+        return lib().ptls_mi355x_record_layer_set_coalesce(self.handle, windows)
 
     def seal_submit(self, fragments, out: np.ndarray, content_type: int = 23) -> int:
         """Asynchronous seal of the fragments (uint8 numpy views) into `out` -> ticket (wait() completes it)."""

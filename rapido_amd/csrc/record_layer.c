@@ -54,7 +54,9 @@
 
 #define RL_MAX_REGIONS 8
 #define RL_ZERO_COPY_DEFAULT ((size_t)4 << 20)
-#define RL_SLOTS 4 /* windows in flight per layer */
+#define RL_SLOTS 4    /* launches in flight per layer */
+#define RL_TICKETS 32 /* windows outstanding per layer (submitted and not yet waited for) */
+#define RL_COALESCE_DEFAULT 16 /* a connection's queued windows per launch (ptls_mi355x_record_layer_set_coalesce) */
 
 typedef struct {
     uint8_t *base; /* host address as registered */
@@ -86,7 +88,12 @@ typedef struct {
 
 typedef struct {
     int busy, is_seal, any_type; /* any_type: open_record (one record of any inner content type) */
-    uint64_t ticket;
+    uint64_t ticket;             /* the first window's ticket */
+    size_t nwin, waited;         /* windows (tickets) in the launch, and how many of them have been waited for */
+    int coalesced;               /* one single-layer window per part (the layer's queued windows) */
+    int done, failed;            /* completed (results below), or its launch / synchronisation failed */
+    size_t *r_outlen, *r_nrec, *r_cons; /* per part, once done */
+    int *r_alert;
     size_t nlayers;
     ptls_mi355x_record_layer_t **layers;
     void **out;
@@ -126,10 +133,35 @@ struct st_ptls_mi355x_record_layer_t {
     size_t nreg;
     rl_slot_t slot[RL_SLOTS];
     uint64_t next_ticket, oldest; /* tickets [oldest, next_ticket) are outstanding */
-    /* windows in flight that name this layer, on its own slots or on another layer's (a multi-layer submit): counted
-     * once per window at submit, dropped when the window completes (its wait, or its lead layer's free) */
+    /* launches in flight that name this layer, on its own slots or on another layer's (a multi-layer submit): counted
+     * once per launch when it goes out, dropped when it completes (a wait, or its lead layer's free) */
     size_t inflight;
     int zombie; /* freed while windows of other layers still name it: its memory goes with the last of them */
+    uint64_t launches;                /* launches so far (slot = launches % RL_SLOTS) */
+    int8_t ticket_slot[RL_TICKETS];   /* ticket % RL_TICKETS -> slot of the launch holding it */
+    /*
+     * Coalescing: single-layer windows submitted while a launch of this layer is still running are queued here and go
+     * out together, one launch for all of them, when the layer's launches are done (checked at the next submit), at
+     * the first wait for one of them, when `coalesce` windows are queued, or at ptls_mi355x_record_layer_flush.
+     */
+    size_t coalesce;                  /* windows per launch at most; <= 1: every window launched at its submit */
+    int corked;                       /* windows queue even while nothing runs (ptls_mi355x_record_layer_cork) */
+    struct rl_queued *queue;          /* coalesce entries */
+    size_t nqueued;
+    int queue_is_seal;
+    uint8_t queue_type;
+    uint64_t queue_ticket;            /* ticket of queue[0] */
+};
+
+/* a window queued for coalescing: its submit arguments (the iovec array copied) and the seq it takes */
+struct rl_queued {
+    ptls_mi355x_iovec_t *frags; /* seal */
+    size_t nfrags;
+    const void *in; /* open */
+    size_t inlen;
+    void *out;
+    size_t capacity;
+    uint64_t seq0; /* seal: seq of its first record; open: the speculative seq its records take */
 };
 
 static char rl_err[160];
@@ -268,19 +300,32 @@ ptls_mi355x_record_layer_t *ptls_mi355x_record_layer_new(const void *key, size_t
     rl->seq = rl->spec_seq = seq;
     rl->zero_copy_bytes = RL_ZERO_COPY_DEFAULT;
     rl->direct_dma = 0;
-    if (slot_ready(rl, &rl->slot[0]) != 0) { /* the key is set up now: errors surface here, not at the first window */
+    rl->coalesce = RL_COALESCE_DEFAULT;
+    if ((rl->queue = calloc(RL_TICKETS, sizeof(*rl->queue))) == NULL || slot_ready(rl, &rl->slot[0]) != 0) {
+        /* the key is set up now: errors surface here, not at the first window */
         slot_release(&rl->slot[0]);
         memset(rl->key, 0, sizeof(rl->key));
+        free(rl->queue);
         free(rl);
         return NULL;
     }
     return rl;
 }
 
+/* drops the queued (not yet launched) windows */
+static void queue_clear(ptls_mi355x_record_layer_t *rl)
+{
+    for (size_t i = 0; i < rl->nqueued; ++i)
+        free(rl->queue[i].frags);
+    memset(rl->queue, 0, RL_TICKETS * sizeof(*rl->queue));
+    rl->nqueued = 0;
+}
+
 static void layer_dispose(ptls_mi355x_record_layer_t *rl)
 {
     memset(rl->key, 0, sizeof(rl->key));
     memset(rl->iv, 0, sizeof(rl->iv));
+    free(rl->queue);
     free(rl);
 }
 
@@ -288,12 +333,14 @@ void ptls_mi355x_record_layer_free(ptls_mi355x_record_layer_t *rl)
 {
     if (rl == NULL)
         return;
+    queue_clear(rl); /* queued windows never launched: dropped */
     for (int i = 0; i < RL_SLOTS; ++i) {
         rl_op_t *op = &rl->slot[i].op;
         if (rl->slot[i].stream != NULL) /* its own windows finish before their buffers and ranges go */
             (void)hipStreamSynchronize(rl->slot[i].stream);
-        if (op->busy) { /* never waited: completes here, its results dropped */
-            op_release_layers(op);
+        if (op->busy) { /* never waited (or not for all its windows): completes here, its results dropped */
+            if (!op->done)
+                op_release_layers(op);
             op_discard(op);
         }
     }
@@ -438,21 +485,22 @@ static int same_session(ptls_mi355x_record_layer_t *const *layers, size_t nlayer
     return 1;
 }
 
-/* a new op on layers[0]'s next slot: its arrays allocated, NULL when the queue is full or on error */
+/* a new op on layers[0]'s next launch slot: its arrays allocated, NULL when every slot is in flight or on error */
 static rl_slot_t *op_begin(ptls_mi355x_record_layer_t *const *layers, size_t nlayers, int is_seal)
 {
     ptls_mi355x_record_layer_t *rl = layers[0];
-    if (rl->next_ticket - rl->oldest >= RL_SLOTS) {
-        rl_msg("all window slots are in flight (wait for the oldest first)");
+    rl_slot_t *s = &rl->slot[rl->launches % RL_SLOTS];
+    if (s->op.busy) {
+        rl_msg("all launch slots are in flight (wait for the oldest window first)");
         return NULL;
     }
-    rl_slot_t *s = &rl->slot[rl->next_ticket % RL_SLOTS];
     if (slot_ready(rl, s) != 0)
         return NULL;
     rl_op_t *op = &s->op;
     memset(op, 0, sizeof(*op));
-    /* one allocation: layers | out | capacity | parts */
-    const size_t bytes = nlayers * (2 * sizeof(void *) + sizeof(size_t) + sizeof(rl_part_t));
+    /* one allocation: layers | out | capacity | parts | results (outlen, nrec, consumed, alert) */
+    const size_t bytes = nlayers * (2 * sizeof(void *) + sizeof(size_t) + sizeof(rl_part_t) + 3 * sizeof(size_t) +
+                                    sizeof(int));
     uint8_t *mem = calloc(1, bytes);
     if (mem == NULL) {
         rl_msg("out of memory");
@@ -462,6 +510,10 @@ static rl_slot_t *op_begin(ptls_mi355x_record_layer_t *const *layers, size_t nla
     op->out = (void **)(mem + nlayers * sizeof(void *));
     op->capacity = (size_t *)(mem + 2 * nlayers * sizeof(void *));
     op->part = (rl_part_t *)(mem + nlayers * (2 * sizeof(void *) + sizeof(size_t)));
+    op->r_outlen = (size_t *)(mem + nlayers * (2 * sizeof(void *) + sizeof(size_t) + sizeof(rl_part_t)));
+    op->r_nrec = op->r_outlen + nlayers;
+    op->r_cons = op->r_nrec + nlayers;
+    op->r_alert = (int *)(op->r_cons + nlayers);
     memcpy(op->layers, layers, nlayers * sizeof(void *));
     op->nlayers = nlayers;
     op->is_seal = is_seal;
@@ -484,17 +536,33 @@ static int repeated(const rl_op_t *op, size_t l)
     return 0;
 }
 
-/* launched: the op joins the queue, and every layer it names counts it in flight */
-static void op_commit(rl_slot_t *s, uint64_t *ticket)
+/*
+ * Launched: the op takes its lead layer's next launch slot and holds `nwin` windows from ticket0 on (a submit's one
+ * window, or the layer's coalesced windows, whose tickets were handed out at their submits); every layer it names
+ * counts it in flight.
+ */
+static void op_commit(ptls_mi355x_record_layer_t *rl, rl_slot_t *s, uint64_t ticket0, size_t nwin, int coalesced)
 {
-    ptls_mi355x_record_layer_t *rl = s->op.layers[0];
     s->op.busy = 1;
-    s->op.ticket = rl->next_ticket++;
+    s->op.ticket = ticket0;
+    s->op.nwin = nwin;
+    s->op.coalesced = coalesced;
+    for (uint64_t t = ticket0; t < ticket0 + nwin; ++t)
+        rl->ticket_slot[t % RL_TICKETS] = (int8_t)(s - rl->slot);
+    ++rl->launches;
     for (size_t l = 0; l < s->op.nlayers; ++l)
         if (!repeated(&s->op, l))
             ++s->op.layers[l]->inflight;
+}
+
+/* a submit's window: the lead layer's next ticket */
+static void op_commit_window(rl_slot_t *s, uint64_t *ticket)
+{
+    ptls_mi355x_record_layer_t *rl = s->op.layers[0];
+    const uint64_t t = rl->next_ticket++;
+    op_commit(rl, s, t, 1, 0);
     if (ticket != NULL)
-        *ticket = s->op.ticket;
+        *ticket = t;
 }
 
 /*
@@ -509,7 +577,8 @@ static void op_release_layers(rl_op_t *op)
         if (repeated(op, l) || x->inflight == 0)
             continue;
         if (--x->inflight == 0) {
-            x->spec_seq = x->seq;
+            if (x->nqueued == 0)
+                x->spec_seq = x->seq;
             if (x->zombie && x != op->layers[0])
                 layer_dispose(x);
         }
@@ -599,17 +668,15 @@ static void op_scrub(rl_slot_t *s)
 
 /* ---------------------------------------------------------------------------------------------------- seal ---- */
 
-int ptls_mi355x_record_layer_seal_submit(ptls_mi355x_record_layer_t *const *layers, size_t nlayers,
-                                         const ptls_mi355x_iovec_t *const *frags, const size_t *nfrags, uint8_t type,
-                                         void *const *out, const size_t *capacity, uint64_t *ticket)
+/*
+ * Plans, stages and launches a seal op on slot s (op_begin done): layers[l] seals frags[l] into out[l]; a layer given
+ * again takes its next window behind the earlier one.  The layers' seq advance past their records.  -1: nothing
+ * launched, the op discarded.
+ */
+static int seal_build(rl_slot_t *s, ptls_mi355x_record_layer_t *const *layers, size_t nlayers,
+                      const ptls_mi355x_iovec_t *const *frags, const size_t *nfrags, uint8_t type, void *const *out,
+                      const size_t *capacity)
 {
-    if (nlayers == 0)
-        return rl_msg("no layers");
-    if (!same_session(layers, nlayers))
-        return -1;
-    rl_slot_t *s = op_begin(layers, nlayers, 1);
-    if (s == NULL)
-        return -1;
     rl_op_t *op = &s->op;
     const int limited = type == 23; /* ptls_send's key-update check; handshake messages are pushed past it */
     size_t nrec = 0, srcbytes = 0, wire = 0;
@@ -645,10 +712,8 @@ int ptls_mi355x_record_layer_seal_submit(ptls_mi355x_record_layer_t *const *laye
         wire += p->wire;
     }
     op->nrec = nrec;
-    if (nrec == 0) { /* nothing to launch (empty or all at the limit): completes at its wait */
-        op_commit(s, ticket);
+    if (nrec == 0) /* nothing to launch (empty or all at the limit): completes at its wait */
         return 0;
-    }
     if (reserve_recs(s, nrec) != 0)
         goto Fail;
     /* direct: every sealed fragment and every output in registered ranges; addressed from the lowest of each.  In
@@ -733,7 +798,6 @@ int ptls_mi355x_record_layer_seal_submit(ptls_mi355x_record_layer_t *const *laye
     }
     for (size_t l = 0; l < nlayers; ++l) /* the records have their seq: the next window continues behind them */
         layers[l]->seq = op->part[l].seq0 + op->part[l].nrec;
-    op_commit(s, ticket);
     return 0;
 Fail:
     op_discard(op);
@@ -742,21 +806,19 @@ Fail:
 
 /* --------------------------------------------------------------------------------------------------- open ---- */
 
-static int open_submit(ptls_mi355x_record_layer_t *const *layers, size_t nlayers, const void *const *in,
-                       const size_t *inlen, void *const *out, const size_t *capacity, size_t *parsed, int any_type,
-                       uint64_t *ticket)
+/*
+ * Parses, stages and launches an open op on slot s (op_begin done): layers[l] opens the complete records at the start
+ * of in[l] into out[l], from its speculative seq (a layer given again: behind its earlier window).  resync: a layer
+ * with nothing in flight or queued first takes spec_seq = seq.  -1: nothing launched, the op discarded.
+ */
+static int open_build(rl_slot_t *s, ptls_mi355x_record_layer_t *const *layers, size_t nlayers, const void *const *in,
+                      const size_t *inlen, void *const *out, const size_t *capacity, size_t *parsed, int any_type,
+                      int resync)
 {
-    if (nlayers == 0)
-        return rl_msg("no layers");
-    if (!same_session(layers, nlayers))
-        return -1;
-    rl_slot_t *s = op_begin(layers, nlayers, 0);
-    if (s == NULL)
-        return -1;
     rl_op_t *op = &s->op;
     op->any_type = any_type;
-    for (size_t l = 0; l < nlayers; ++l) /* nothing in flight: the next record to submit is the next to deliver */
-        if (layers[l]->inflight == 0)
+    for (size_t l = 0; resync && l < nlayers; ++l) /* nothing in flight: the next record to submit is the next to deliver */
+        if (layers[l]->inflight == 0 && layers[l]->nqueued == 0)
             layers[l]->spec_seq = layers[l]->seq;
     size_t max = 0, nrec = 0, srcbytes = 0, ptbytes = 0, slots16 = 0;
     for (size_t l = 0; l < nlayers; ++l) /* a record takes at least 5 wire bytes */
@@ -792,10 +854,8 @@ static int open_submit(ptls_mi355x_record_layer_t *const *layers, size_t nlayers
             parsed[l] = p->cons;
     }
     op->nrec = nrec;
-    if (nrec == 0) {
-        op_commit(s, ticket);
+    if (nrec == 0)
         return 0;
-    }
     /* direct: every input and every plaintext buffer (at least as large as its slots) in registered ranges, and no
      * input overlapping a plaintext buffer (slots are packed tighter than records: an in-place open would overwrite
      * ciphertext another workgroup still reads) */
@@ -905,11 +965,255 @@ static int open_submit(ptls_mi355x_record_layer_t *const *layers, size_t nlayers
     }
     for (size_t l = 0; l < nlayers; ++l) /* speculative: the next window's records follow these */
         layers[l]->spec_seq = op->part[l].seq0 + op->part[l].n;
-    op_commit(s, ticket);
     return 0;
 Fail:
     op_discard(op);
     return -1;
+}
+
+/* ------------------------------------------------------------------------------------------- coalescing ---- */
+
+/* 1 while a launch of this layer's own slots is still running on the GPU */
+static int rl_busy(ptls_mi355x_record_layer_t *rl)
+{
+    int busy = 0;
+    for (int i = 0; i < RL_SLOTS && !busy; ++i) {
+        const rl_slot_t *s = &rl->slot[i];
+        busy = s->op.busy && !s->op.done && s->op.nrec != 0 && hipStreamQuery(s->stream) == hipErrorNotReady;
+    }
+    (void)hipGetLastError(); /* (hipErrorNotReady is an answer, not an error to leave behind) */
+    return busy;
+}
+
+/*
+ * When the queue goes out: the layer's outstanding windows spread over its RL_SLOTS launch slots, so a connection that
+ * keeps w windows outstanding launches groups of ceil(w / 4) -- one window per launch up to 4 outstanding, as without
+ * coalescing, 4 per launch at 16 -- with up to 4 launches in flight; a queue whose layer has nothing running goes at
+ * once (no window waits for company that may not come), a corked one only when full or uncorked.
+ */
+static int queue_due(ptls_mi355x_record_layer_t *rl)
+{
+    if (rl->nqueued == 0)
+        return 0;
+    if (rl->nqueued >= rl->coalesce)
+        return 1;
+    if (rl->corked)
+        return 0;
+    const size_t outstanding = (size_t)(rl->next_ticket - rl->oldest), group = (outstanding + RL_SLOTS - 1) / RL_SLOTS;
+    return rl->nqueued >= group || !rl_busy(rl);
+}
+
+/* windows whose launch failed: their waits report -1 (seq stays past them: no nonce is used twice) */
+static void op_fail_windows(ptls_mi355x_record_layer_t *rl, rl_slot_t *s, uint64_t ticket0, size_t n, int is_seal)
+{
+    rl_op_t *op = &s->op;
+    memset(op, 0, sizeof(*op)); /* names no layer: nothing counted in flight, nothing to finish */
+    op->is_seal = is_seal;
+    op->done = op->failed = 1;
+    op_commit(rl, s, ticket0, n, 1);
+}
+
+/*
+ * Launches the layer's queued windows as ONE op (each window a part of the layer given again), when a launch slot is
+ * free (else they stay queued: every slot is in flight, and the next wait frees one).  The seq / spec_seq the
+ * windows took at their submit is kept: the build re-derives the same values from the first window's.
+ */
+static int rl_flush(ptls_mi355x_record_layer_t *rl)
+{
+    const size_t n = rl->nqueued;
+    if (n == 0 || rl->slot[rl->launches % RL_SLOTS].op.busy)
+        return 0;
+    ptls_mi355x_record_layer_t *layers[RL_TICKETS];
+    const ptls_mi355x_iovec_t *frags[RL_TICKETS];
+    size_t nfrags[RL_TICKETS], capacity[RL_TICKETS], inlen[RL_TICKETS], parsed[RL_TICKETS];
+    void *out[RL_TICKETS];
+    const void *in[RL_TICKETS];
+    for (size_t i = 0; i < n; ++i) {
+        const struct rl_queued *q = &rl->queue[i];
+        layers[i] = rl;
+        frags[i] = q->frags;
+        nfrags[i] = q->nfrags;
+        in[i] = q->in;
+        inlen[i] = q->inlen;
+        out[i] = q->out;
+        capacity[i] = q->capacity;
+    }
+    const int is_seal = rl->queue_is_seal;
+    const uint64_t ticket0 = rl->queue_ticket;
+    rl_slot_t *s = op_begin(layers, n, is_seal);
+    int rc = -1;
+    if (s != NULL) {
+        if (is_seal) {
+            const uint64_t keep = rl->seq;
+            rl->seq = rl->queue[0].seq0;
+            rc = seal_build(s, layers, n, frags, nfrags, rl->queue_type, out, capacity);
+            rl->seq = keep;
+        } else {
+            const uint64_t keep = rl->spec_seq; /* (a window stopped meanwhile may have reset it: kept as it is) */
+            rl->spec_seq = rl->queue[0].seq0;
+            rc = open_build(s, layers, n, in, inlen, out, capacity, parsed, 0, 0);
+            rl->spec_seq = keep;
+        }
+    }
+    queue_clear(rl);
+    if (rc == 0) {
+        op_commit(rl, s, ticket0, n, 1);
+        return 0;
+    }
+    if (s == NULL)
+        s = &rl->slot[rl->launches % RL_SLOTS]; /* (free: checked above) */
+    op_fail_windows(rl, s, ticket0, n, is_seal);
+    return -1;
+}
+
+/* ptls_send's record count and wire bytes for frags from seq (stopping at the 2^24 limit for application data) */
+static size_t plan_window(const ptls_mi355x_iovec_t *frags, size_t nfrags, uint8_t type, uint64_t *seq, size_t *wire)
+{
+    size_t nrec = 0;
+    *wire = 0;
+    for (size_t f = 0; f < nfrags; ++f) {
+        if (type == 23 && *seq >= PTLS_MI355X_RECORD_LAYER_SEQ_LIMIT)
+            break;
+        size_t w = 0;
+        const size_t k = ptls_mi355x_tls_plan_send(frags[f].len, type, seq, 0, 0, NULL, 0, &w);
+        *seq += k;
+        nrec += k;
+        *wire += w;
+    }
+    return nrec;
+}
+
+/* the complete application_data records at the start of in (ptls_mi355x_tls_parse_records' walk, counting only) */
+static size_t count_records(const uint8_t *in, size_t inlen, size_t *consumed)
+{
+    size_t off = 0, n = 0;
+    while (inlen - off >= PTLS_MI355X_TLS_HEADER_SIZE) {
+        const uint8_t *h = in + off;
+        const uint32_t reclen = (uint32_t)h[3] << 8 | h[4];
+        if (h[0] != 23 || reclen > PTLS_MI355X_TLS_MAX_RECORD || inlen - off < PTLS_MI355X_TLS_HEADER_SIZE + (size_t)reclen)
+            break;
+        off += PTLS_MI355X_TLS_HEADER_SIZE + reclen;
+        ++n;
+    }
+    *consumed = off;
+    return n;
+}
+
+/* a single-layer window into the layer's queue; launched at once when nothing of the layer is running */
+static int queue_window(ptls_mi355x_record_layer_t *rl, int is_seal, uint8_t type, const ptls_mi355x_iovec_t *frags,
+                        size_t nfrags, const void *in, size_t inlen, void *out, size_t capacity, size_t *parsed,
+                        uint64_t *ticket)
+{
+    if (rl->next_ticket - rl->oldest >= RL_TICKETS)
+        return rl_msg("all windows are outstanding (wait for the oldest first)");
+    if (rl->nqueued != 0 && (rl->queue_is_seal != is_seal || rl->queue_type != type) && rl_flush(rl) != 0)
+        return -1;
+    if (rl->nqueued != 0 && rl->queue_is_seal != is_seal) /* not launched (no free slot): cannot queue behind it */
+        return rl_msg("windows of the other direction are queued and every launch slot is in flight");
+    struct rl_queued *q = &rl->queue[rl->nqueued];
+    memset(q, 0, sizeof(*q));
+    if (is_seal) {
+        uint64_t sq = rl->seq;
+        size_t wire = 0;
+        plan_window(frags, nfrags, type, &sq, &wire);
+        if (wire > capacity) {
+            snprintf(rl_err, sizeof(rl_err), "record layer: %zu wire bytes exceed the output capacity %zu (layer 0)", wire,
+                     capacity);
+            return -1;
+        }
+        if (nfrags != 0 && (q->frags = malloc(nfrags * sizeof(*frags))) == NULL)
+            return rl_msg("out of memory");
+        if (nfrags != 0)
+            memcpy(q->frags, frags, nfrags * sizeof(*frags));
+        q->nfrags = nfrags;
+        q->seq0 = rl->seq;
+        rl->seq = sq; /* the records take their seq at submit */
+    } else {
+        if (rl->inflight == 0 && rl->nqueued == 0)
+            rl->spec_seq = rl->seq;
+        size_t cons = 0;
+        const size_t n = count_records((const uint8_t *)in, inlen, &cons);
+        q->in = in;
+        q->inlen = inlen;
+        q->seq0 = rl->spec_seq;
+        rl->spec_seq += n;
+        if (parsed != NULL)
+            *parsed = cons;
+    }
+    q->out = out;
+    q->capacity = capacity;
+    if (rl->nqueued++ == 0) {
+        rl->queue_is_seal = is_seal;
+        rl->queue_type = type;
+        rl->queue_ticket = rl->next_ticket;
+    }
+    *ticket = rl->next_ticket++;
+    if (queue_due(rl))
+        return rl_flush(rl); /* (no free launch slot: stays queued; a failed launch: its windows' waits report it) */
+    return 0;
+}
+
+int ptls_mi355x_record_layer_cork(ptls_mi355x_record_layer_t *rl, int on)
+{
+    rl->corked = on != 0;
+    return on ? 0 : rl_flush(rl);
+}
+
+int ptls_mi355x_record_layer_flush(ptls_mi355x_record_layer_t *rl) { return rl_flush(rl); }
+
+uint64_t ptls_mi355x_record_layer_launches(const ptls_mi355x_record_layer_t *rl) { return rl->launches; }
+
+size_t ptls_mi355x_record_layer_set_coalesce(ptls_mi355x_record_layer_t *rl, size_t windows)
+{
+    const size_t prev = rl->coalesce;
+    (void)rl_flush(rl);
+    rl->coalesce = windows > RL_TICKETS ? RL_TICKETS : windows;
+    return prev;
+}
+
+/* a multi-layer (or uncoalesced) window: the named layers' queued windows go out first */
+static rl_slot_t *submit_begin(ptls_mi355x_record_layer_t *const *layers, size_t nlayers, int is_seal)
+{
+    if (nlayers == 0) {
+        rl_msg("no layers");
+        return NULL;
+    }
+    if (!same_session(layers, nlayers))
+        return NULL;
+    for (size_t l = 0; l < nlayers; ++l)
+        if (layers[l]->nqueued != 0 && rl_flush(layers[l]) != 0)
+            return NULL;
+    if (layers[0]->next_ticket - layers[0]->oldest >= RL_TICKETS) {
+        rl_msg("all windows are outstanding (wait for the oldest first)");
+        return NULL;
+    }
+    return op_begin(layers, nlayers, is_seal);
+}
+
+int ptls_mi355x_record_layer_seal_submit(ptls_mi355x_record_layer_t *const *layers, size_t nlayers,
+                                         const ptls_mi355x_iovec_t *const *frags, const size_t *nfrags, uint8_t type,
+                                         void *const *out, const size_t *capacity, uint64_t *ticket)
+{
+    if (nlayers == 1 && layers[0]->coalesce > 1)
+        return queue_window(layers[0], 1, type, frags[0], nfrags[0], NULL, 0, out[0], capacity[0], NULL, ticket);
+    rl_slot_t *s = submit_begin(layers, nlayers, 1);
+    if (s == NULL || seal_build(s, layers, nlayers, frags, nfrags, type, out, capacity) != 0)
+        return -1;
+    op_commit_window(s, ticket);
+    return 0;
+}
+
+static int open_submit(ptls_mi355x_record_layer_t *const *layers, size_t nlayers, const void *const *in,
+                       const size_t *inlen, void *const *out, const size_t *capacity, size_t *parsed, int any_type,
+                       uint64_t *ticket)
+{
+    if (nlayers == 1 && layers[0]->coalesce > 1 && !any_type)
+        return queue_window(layers[0], 0, 0, NULL, 0, in[0], inlen[0], out[0], capacity[0], parsed, ticket);
+    rl_slot_t *s = submit_begin(layers, nlayers, 0);
+    if (s == NULL || open_build(s, layers, nlayers, in, inlen, out, capacity, parsed, any_type, 1) != 0)
+        return -1;
+    op_commit_window(s, ticket);
+    return 0;
 }
 
 int ptls_mi355x_record_layer_open_submit(ptls_mi355x_record_layer_t *const *layers, size_t nlayers, const void *const *in,
@@ -921,37 +1225,34 @@ int ptls_mi355x_record_layer_open_submit(ptls_mi355x_record_layer_t *const *laye
 
 /* ---------------------------------------------------------------------------------------------------- wait ---- */
 
-static void finish_seal(rl_slot_t *s, size_t *outlen, size_t *nrecords, size_t *consumed, int *alerts)
+/* results per part into the op (r_outlen, r_nrec, r_cons = fragments sealed, r_alert) */
+static void finish_seal(rl_slot_t *s)
 {
     rl_op_t *op = &s->op;
     for (size_t l = 0, off = 0; l < op->nlayers; ++l) {
         const rl_part_t *p = &op->part[l];
         if (op->layers[l]->zombie) { /* freed meanwhile: nothing is delivered to it */
             off += op->direct ? 0 : p->wire;
-            outlen[l] = 0;
-            if (nrecords != NULL)
-                nrecords[l] = 0;
-            if (consumed != NULL)
-                consumed[l] = 0;
-            alerts[l] = PTLS_MI355X_RECORD_LAYER_STALE;
+            op->r_outlen[l] = op->r_nrec[l] = op->r_cons[l] = 0;
+            op->r_alert[l] = PTLS_MI355X_RECORD_LAYER_STALE;
             continue;
         }
         if (!op->direct && p->wire != 0) {
             memcpy(op->out[l], s->h_buf + op->off_dst + off, p->wire);
             off += p->wire;
         }
-        outlen[l] = p->wire;
-        if (nrecords != NULL)
-            nrecords[l] = p->nrec;
-        if (consumed != NULL)
-            consumed[l] = p->nfrags;
-        alerts[l] = p->stopped ? PTLS_MI355X_RECORD_LAYER_KEY_UPDATE : 0;
+        op->r_outlen[l] = p->wire;
+        op->r_nrec[l] = p->nrec;
+        op->r_cons[l] = p->nfrags;
+        op->r_alert[l] = p->stopped ? PTLS_MI355X_RECORD_LAYER_KEY_UPDATE : 0;
     }
     if (!op->direct && op->srcbytes != 0)
         memset(s->h_buf + op->off_src, 0, op->srcbytes); /* no plaintext left in the staging */
 }
 
-static void finish_open(rl_slot_t *s, size_t *outlen, size_t *nrecords, size_t *consumed, int *alerts, uint8_t *type)
+/* results per part into the op (r_outlen, r_nrec, r_cons = wire bytes delivered, r_alert); *type: the last delivered
+ * record's inner content type (open_record) */
+static void finish_open(rl_slot_t *s, uint8_t *type)
 {
     rl_op_t *op = &s->op;
     const uint32_t *status = (const uint32_t *)(s->h_buf + op->off_st);
@@ -963,10 +1264,8 @@ static void finish_open(rl_slot_t *s, size_t *outlen, size_t *nrecords, size_t *
         size_t done = 0, wire_done = 0, olen = 0;
         int a = 0;
         if (x->zombie) { /* freed meanwhile: nothing is delivered to it */
-            consumed[l] = outlen[l] = 0;
-            if (nrecords != NULL)
-                nrecords[l] = 0;
-            alerts[l] = PTLS_MI355X_RECORD_LAYER_STALE;
+            op->r_cons[l] = op->r_outlen[l] = op->r_nrec[l] = 0;
+            op->r_alert[l] = PTLS_MI355X_RECORD_LAYER_STALE;
             if (p->n != 0 && !op->direct)
                 memset(slots, 0, p->ptbytes);
             continue;
@@ -1015,22 +1314,17 @@ static void finish_open(rl_slot_t *s, size_t *outlen, size_t *nrecords, size_t *
             a = p->perr; /* a DECODE_ERROR behind the parsed records */
         if (a != PTLS_MI355X_RECORD_LAYER_STALE && done < p->n)
             x->spec_seq = x->seq; /* stopped early: the windows behind this one are stale, new ones follow it */
-        consumed[l] = wire_done;
-        outlen[l] = olen;
-        if (nrecords != NULL)
-            nrecords[l] = done;
-        alerts[l] = a;
+        op->r_cons[l] = wire_done;
+        op->r_outlen[l] = olen;
+        op->r_nrec[l] = done;
+        op->r_alert[l] = a;
     }
 }
 
-static int op_wait(ptls_mi355x_record_layer_t *rl, uint64_t ticket, size_t *outlen, size_t *nrecords, size_t *consumed,
-                   int *alerts, uint8_t *type)
+/* the op's launch is done (or failed): results into the op, its layers count it out */
+static void op_complete(rl_slot_t *s, uint8_t *type)
 {
-    if (ticket != rl->oldest || rl->oldest == rl->next_ticket)
-        return rl_msg(rl->oldest == rl->next_ticket ? "no window outstanding" : "windows are completed in submission order");
-    rl_slot_t *s = &rl->slot[ticket % RL_SLOTS];
     rl_op_t *op = &s->op;
-    int ret = 0;
     hipError_t e;
     if (op->nrec != 0 && (e = hipStreamSynchronize(s->stream)) != hipSuccess) {
         rl_fail("synchronize", e);
@@ -1039,24 +1333,49 @@ static int op_wait(ptls_mi355x_record_layer_t *rl, uint64_t ticket, size_t *outl
             for (size_t l = 0; l < op->nlayers; ++l)
                 if (!op->layers[l]->zombie)
                     op->layers[l]->spec_seq = op->layers[l]->seq;
-        for (size_t l = 0; l < op->nlayers; ++l) {
-            outlen[l] = 0;
-            if (nrecords != NULL)
-                nrecords[l] = 0;
-            if (consumed != NULL)
-                consumed[l] = 0;
-            alerts[l] = 0;
-        }
-        ret = -1;
+        op->failed = 1;
     } else if (op->is_seal) {
-        finish_seal(s, outlen, nrecords, consumed, alerts);
+        finish_seal(s);
     } else {
-        size_t dummy[1];
-        finish_open(s, outlen, nrecords, consumed != NULL ? consumed : dummy, alerts, type);
+        finish_open(s, type);
     }
-    ++rl->oldest;
+    op->done = 1;
     op_release_layers(op); /* (a failed window's open parts: spec_seq back to seq when nothing else is in flight) */
-    op_discard(op);
+}
+
+static int op_wait(ptls_mi355x_record_layer_t *rl, uint64_t ticket, size_t *outlen, size_t *nrecords, size_t *consumed,
+                   int *alerts, uint8_t *type)
+{
+    if (ticket != rl->oldest || rl->oldest == rl->next_ticket)
+        return rl_msg(rl->oldest == rl->next_ticket ? "no window outstanding" : "windows are completed in submission order");
+    if (rl->nqueued != 0 && ticket >= rl->queue_ticket) { /* still queued: it goes out now (older windows are done) */
+        (void)rl_flush(rl);
+        if (rl->nqueued != 0 && ticket >= rl->queue_ticket)
+            return rl_msg("a queued window found no free launch slot");
+    }
+    rl_slot_t *s = &rl->slot[rl->ticket_slot[ticket % RL_TICKETS]];
+    rl_op_t *op = &s->op;
+    if (!op->done)
+        op_complete(s, type);
+    int ret = op->failed ? -1 : 0;
+    /* a coalesced launch: this ticket's window is part (ticket - first ticket); otherwise every part is this window */
+    const size_t first = op->coalesced ? (size_t)(ticket - op->ticket) : 0, n = op->coalesced ? 1 : op->nlayers;
+    for (size_t l = 0; l < n; ++l) {
+        const int ok = !op->failed;
+        outlen[l] = ok ? op->r_outlen[first + l] : 0;
+        if (nrecords != NULL)
+            nrecords[l] = ok ? op->r_nrec[first + l] : 0;
+        if (consumed != NULL)
+            consumed[l] = ok ? op->r_cons[first + l] : 0;
+        alerts[l] = ok ? op->r_alert[first + l] : 0;
+    }
+    if (op->failed && op->nlayers == 0 && ret == -1 && rl_err[0] == 0)
+        rl_msg("the window's launch failed");
+    ++rl->oldest;
+    if (++op->waited == op->nwin)
+        op_discard(op);
+    if (queue_due(rl)) /* a launch slot may have come free: the queue goes out when due */
+        (void)rl_flush(rl);
     return ret;
 }
 

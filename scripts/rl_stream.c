@@ -143,9 +143,9 @@ int main(int argc, char **argv)
     const char *transport = argc > 4 ? argv[4] : "direct";
     const size_t multi = argc > 5 ? (size_t)atoi(argv[5]) : 1; /* windows per launch (_multi) */
     const int one_conn = argc > 6 && strcmp(argv[6], "one") == 0; /* ... of one connection instead of `multi` */
-    if (depth < 1 || depth > 4 || nwin < 1 || (key_bytes != 16 && key_bytes != 32) || multi < 1 || multi > MAXM ||
+    if (depth < 1 || depth > 32 || nwin < 1 || (key_bytes != 16 && key_bytes != 32) || multi < 1 || multi > MAXM ||
         nwin % multi != 0) {
-        fprintf(stderr, "usage: rl_stream [nwin] [depth 1..4] [16|32] [direct|dma|dma_in|zero_copy|copy] [windows per launch 1..16] [one]\n");
+        fprintf(stderr, "usage: rl_stream [nwin] [depth 1..32] [16|32] [direct|dma|dma_in|zero_copy|copy] [windows per launch 1..16] [one]\n");
         return 2;
     }
     signal(SIGSEGV, on_fault);
@@ -193,6 +193,9 @@ int main(int argc, char **argv)
         all[nall++] = st.txs[c];
         all[nall++] = st.rxs[c];
     }
+    const char *co = getenv("RL_COALESCE"); /* windows per launch when coalescing (0/1: off; default 16) */
+    for (size_t i = 0; co != NULL && i < nall; ++i)
+        ptls_mi355x_record_layer_set_coalesce(all[i], (size_t)atoi(co));
     for (size_t i = 0; i < nall; ++i) {
         if (strcmp(transport, "direct") == 0 || strcmp(transport, "dma") == 0 || strcmp(transport, "dma_in") == 0) {
             if (ptls_mi355x_record_layer_register(all[i], st.send, nwin * WIN * FRAG) != 0 ||
@@ -210,8 +213,12 @@ int main(int argc, char **argv)
     double t_seal = 0, t_open = 0, t_seal1 = 0, t_open1 = 0;
     pass(&st, 1, depth, &inflight); /* untimed: every slot's stream, context and staging created */
     pass(&st, 0, depth, &inflight);
+    ptls_mi355x_record_layer_t *lead_tx = multi > 1 ? st.txs[0] : st.tx, *lead_rx = multi > 1 ? st.rxs[0] : st.rx;
+    const uint64_t l0s = ptls_mi355x_record_layer_launches(lead_tx), l0o = ptls_mi355x_record_layer_launches(lead_rx);
     t_seal = pass(&st, 1, depth, &inflight);
+    const uint64_t l1s = ptls_mi355x_record_layer_launches(lead_tx);
     t_open = pass(&st, 0, depth, &inflight);
+    const uint64_t l1o = ptls_mi355x_record_layer_launches(lead_rx);
     t_seal1 = pass(&st, 1, 1, &inflight);
     t_open1 = pass(&st, 0, 1, &inflight);
     for (size_t w = 0; w < nwin; ++w) {
@@ -223,9 +230,11 @@ int main(int argc, char **argv)
     const double bytes = (double)nwin * WIN * FRAG, gib = (double)(1u << 30);
     printf("{\"seal_gibps\": %.2f, \"open_gibps\": %.2f, \"seal_us_per_window\": %.2f, \"open_us_per_window\": %.2f, "
            "\"seal_gibps_sync\": %.2f, \"open_gibps_sync\": %.2f, \"windows\": %zu, \"depth\": %zu, \"max_in_flight\": %zu, "
-           "\"transport\": \"%s\", \"key_bits\": %zu, \"windows_per_launch\": %zu, \"connections_per_launch\": %zu}\n",
+           "\"transport\": \"%s\", \"key_bits\": %zu, \"windows_per_launch\": %zu, \"connections_per_launch\": %zu, "
+           "\"seal_launches\": %llu, \"open_launches\": %llu}\n",
            bytes / t_seal / gib, bytes / t_open / gib, t_seal / nwin * 1e6, t_open / nwin * 1e6, bytes / t_seal1 / gib,
-           bytes / t_open1 / gib, nwin, depth, inflight, transport, 8 * key_bytes, multi, one_conn ? (size_t)1 : multi);
+           bytes / t_open1 / gib, nwin, depth, inflight, transport, 8 * key_bytes, multi, one_conn ? (size_t)1 : multi,
+           (unsigned long long)(l1s - l0s), (unsigned long long)(l1o - l0o));
     for (size_t i = 0; i < nall; ++i)
         ptls_mi355x_record_layer_free(all[i]);
     free(st.send);

@@ -188,13 +188,15 @@ def test_async_stream_families(gpu, family):
                 rng.integers(0, 256, 12, dtype=np.uint8).tobytes(), rng)
 
 
+@pytest.mark.parametrize("coalesce", [0, 16])
 @pytest.mark.parametrize("transport", TRANSPORTS)
-def test_async_open_stale_after_failure(gpu, transport):
+def test_async_open_stale_after_failure(gpu, transport, coalesce):
     """Windows in flight behind a window that stops early (a bad record) complete STALE with nothing delivered;
-    resubmitted from the stop they open normally."""
+    resubmitted from the stop they open normally.  Without coalescing, four launches are the limit."""
     rng = np.random.default_rng(99)
     key, iv = rng.integers(0, 256, 16, dtype=np.uint8).tobytes(), rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
     rx = ra.RecordLayer(key, iv, seq=100)
+    rx.set_coalesce(coalesce)
     h = Host(transport, [rx], 1 << 21)
     frags = [[rng.integers(0, 256, 700 + 13 * i, dtype=np.uint8).tobytes() for i in range(8)] for _ in range(4)]
     wires_b = oracle_windows_parallel(key, iv, 100, frags)
@@ -208,8 +210,9 @@ def test_async_open_stale_after_failure(gpu, transport):
     wires = [h.take(len(w), w) for w in (wires_b[0], bytes(bad), wires_b[2], wires_b[3])]
     pts = [h.take(len(w)) for w in wires_b]
     tickets = [rx.open_submit(wires[w], pts[w])[0] for w in range(4)]
-    with pytest.raises(RuntimeError):
-        rx.open_submit(wires[0], pts[0])  # all four slots in flight
+    if coalesce == 0:
+        with pytest.raises(RuntimeError):
+            rx.open_submit(wires[0], pts[0])  # all four launch slots in flight
     with pytest.raises(RuntimeError):
         rx.wait(tickets[1])  # completion is in submission order
     with pytest.raises(RuntimeError):
@@ -363,3 +366,118 @@ def test_open_windows_waited_out_of_order_across_leads(gpu):
     assert (alert, n, cons) == (0, 3, len(w_b2)) and pt == b"".join(frags[2]) and b.seq == sb2
     for rl in (a, b, c):
         rl.close()
+
+
+@pytest.mark.parametrize("transport", ["direct", "direct_dma_in", "zero_copy", "copy"])
+def test_coalesced_windows_of_one_connection(gpu, transport):
+    """One window per submit, 12 submits without a wait: the windows queued while the layer's launch runs go out
+    together (fewer launches than windows), with every ticket's results, the wire bytes and seq exactly those of 12
+    separate ptls_send windows; then opened the same way (one window per submit) back to their fragments; with
+    coalescing off every window is a launch of its own."""
+    rng = np.random.default_rng(808)
+    key, iv = rng.integers(0, 256, 16, dtype=np.uint8).tobytes(), rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    nwin = 12
+    wins_b = [[rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in rng.integers(0, 16385, 6)]
+              for _ in range(nwin)]
+    wants, s = [], 40
+    for w in wins_b:
+        want, s = oracle_window(key, iv, s, w)
+        wants.append(want)
+    for coalesce in (16, 0):
+        tx, rx = ra.RecordLayer(key, iv, seq=40), ra.RecordLayer(key, iv, seq=40)
+        for rl in (tx, rx):
+            rl.set_coalesce(coalesce)
+        h = Host(transport, [tx, rx], 1 << 23)
+        wins = [[h.take(len(f), f) for f in w] for w in wins_b]
+        outs = [h.take(len(want) + 64) for want in wants]
+        l0 = tx.launches
+        if coalesce:
+            tx.cork(True)  # a burst known to follow: queued, then one launch (uncorked: queued while one runs)
+            tickets = [tx.seal_submit(w, o) for w, o in zip(wins, outs)]
+            assert tx.seq == s and tx.pending == nwin  # records take their seq at submit, queued or not
+            tx.cork(False)
+            res = [tx.wait(t) for t in tickets]
+        else:  # a launch per window: at most four in flight
+            res, tickets = [], []
+            for w, o in zip(wins, outs):
+                if len(tickets) == 4:
+                    res.append(tx.wait(tickets.pop(0)))
+                tickets.append(tx.seal_submit(w, o))
+            res += [tx.wait(t) for t in tickets]
+        for r, o, want, w in zip(res, outs, wants, wins_b):
+            assert r == (len(want), sum(max(1, -(-len(f) // 16384)) if f else 0 for f in w), len(w), 0)
+            assert o[:len(want)].tobytes() == want
+        assert tx.launches - l0 == (nwin if coalesce == 0 else 1)
+        wires = [h.take(len(want), want) for want in wants]
+        pts = [h.take(len(want)) for want in wants]
+        l0 = rx.launches
+        pending = []
+
+        def check(t, p, w, want):
+            r = rx.wait(t)
+            assert r == (sum(map(len, w)), sum(max(1, -(-len(f) // 16384)) if f else 0 for f in w), len(want), 0)
+            assert p[:r[0]].tobytes() == b"".join(w)
+
+        for x, p, w, want in zip(wires, pts, wins_b, wants):  # uncorked: queued only while a launch runs
+            if coalesce == 0 and len(pending) == 4:
+                check(*pending.pop(0))
+            t, parsed = rx.open_submit(x, p)
+            assert parsed == len(want)  # parsed at submit
+            pending.append((t, p, w, want))
+        for args in pending:
+            check(*args)
+        assert rx.seq == s and rx.pending == 0 and 1 <= rx.launches - l0 <= nwin
+        tx.close()
+        rx.close()
+
+
+def test_coalesced_open_stops_and_flush(gpu):
+    """Coalesced receive windows: a bad record in window 2 stops it (alert 20), windows 3.. come back STALE; the
+    layer's queue can be launched early (flush), and windows resubmitted from the stop open normally."""
+    rng = np.random.default_rng(909)
+    key, iv = rng.integers(0, 256, 32, dtype=np.uint8).tobytes(), rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    frags = [[rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in (1000, 16384, 77)] for _ in range(6)]
+    wires, s = [], 7
+    for f in frags:
+        w, s = oracle_window(key, iv, s, f)
+        wires.append(w)
+    rx = ra.RecordLayer(key, iv, seq=7)
+    bad = bytearray(wires[2])
+    bad[1022 + 300] ^= 4  # record 1 of window 2 (record 0: 5 + 1000 + 1 + 16 bytes)
+    arr = [np.frombuffer(w, np.uint8).copy() for w in wires[:2] + [bytes(bad)] + wires[3:]]
+    outs = [np.zeros(len(w), np.uint8) for w in wires]
+    tickets = [rx.open_submit(a, o)[0] for a, o in zip(arr, outs)]
+    rx.flush()
+    res = [rx.wait(t) for t in tickets]
+    assert [r[3] for r in res] == [0, 0, 20] + [ra.RECORD_LAYER_STALE] * 3
+    assert res[2][:2] == (1000, 1) and outs[2][:1000].tobytes() == frags[2][0]
+    assert rx.seq == 7 + 3 + 3 + 1 and rx.pending == 0
+    # resubmitted from the stop: the rest of window 2, then windows 3..5
+    rest = np.frombuffer(wires[2][1022:], np.uint8).copy()
+    again = [rest] + arr[3:]
+    outs2 = [np.zeros(len(a), np.uint8) for a in again]
+    tickets = [rx.open_submit(a, o)[0] for a, o in zip(again, outs2)]
+    res = [rx.wait(t) for t in tickets]
+    assert all(r[3] == 0 for r in res) and rx.seq == 7 + 18
+    assert outs2[0][:res[0][0]].tobytes() == b"".join(frags[2][1:])
+    assert outs2[3][:res[3][0]].tobytes() == b"".join(frags[5])
+    rx.close()
+
+
+def test_coalesced_windows_at_the_key_update_limit(gpu):
+    """Queued windows across the 2^24-record limit: the window that reaches it stops (KEY_UPDATE), the windows queued
+    behind it seal nothing (as separate ptls_send calls would: every fragment starts at or past the limit)."""
+    rng = np.random.default_rng(1001)
+    key, iv = rng.integers(0, 256, 16, dtype=np.uint8).tobytes(), rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    tx = ra.RecordLayer(key, iv, seq=LIMIT - 5)
+    wins = [[rng.integers(0, 256, 2000, dtype=np.uint8) for _ in range(3)] for _ in range(4)]
+    outs = [np.zeros(3 * (2000 + ra.TLS_OVERHEAD), np.uint8) for _ in wins]
+    tickets = [tx.seal_submit(w, o) for w, o in zip(wins, outs)]
+    res = [tx.wait(t) for t in tickets]
+    assert [r[1] for r in res] == [3, 2, 0, 0]
+    assert [r[3] for r in res] == [0, ra.RECORD_LAYER_KEY_UPDATE, ra.RECORD_LAYER_KEY_UPDATE, ra.RECORD_LAYER_KEY_UPDATE]
+    want0, s0 = oracle_window(key, iv, LIMIT - 5, [w.tobytes() for w in wins[0]])
+    want1, s1 = oracle_window(key, iv, s0, [w.tobytes() for w in wins[1][:2]])
+    assert outs[0][:len(want0)].tobytes() == want0 and outs[1][:len(want1)].tobytes() == want1
+    assert tx.seq == LIMIT
+    tx.close()
