@@ -168,6 +168,7 @@ static char rl_err[160];
 
 static void op_discard(rl_op_t *op);
 static void op_release_layers(rl_op_t *op);
+static int rl_flush_n(ptls_mi355x_record_layer_t *rl, size_t n);
 
 static size_t up16(size_t x) { return (x + 15) & ~(size_t)15; }
 
@@ -986,21 +987,34 @@ static int rl_busy(ptls_mi355x_record_layer_t *rl)
 }
 
 /*
- * When the queue goes out: the layer's outstanding windows spread over its RL_SLOTS launch slots, so a connection that
- * keeps w windows outstanding launches groups of ceil(w / 4) -- one window per launch up to 4 outstanding, as without
- * coalescing, 4 per launch at 16 -- with up to 4 launches in flight; a queue whose layer has nothing running goes at
- * once (no window waits for company that may not come), a corked one only when full or uncorked.
+ * How many queued windows go out now (0: none): the layer's outstanding windows spread over its RL_SLOTS launch
+ * slots, so a connection that keeps w windows outstanding launches groups of ceil(w / 4) -- one window per launch up
+ * to 4 outstanding, as without coalescing, 4 per launch at 16 -- with up to 4 launches in flight; a queue whose layer
+ * has nothing running goes at once (no window waits for company that may not come); a corked one only when full.
  */
-static int queue_due(ptls_mi355x_record_layer_t *rl)
+static size_t queue_due(ptls_mi355x_record_layer_t *rl)
 {
     if (rl->nqueued == 0)
         return 0;
-    if (rl->nqueued >= rl->coalesce)
-        return 1;
+    const size_t cap = rl->coalesce > 1 ? rl->coalesce : 1;
     if (rl->corked)
-        return 0;
-    const size_t outstanding = (size_t)(rl->next_ticket - rl->oldest), group = (outstanding + RL_SLOTS - 1) / RL_SLOTS;
-    return rl->nqueued >= group || !rl_busy(rl);
+        return rl->nqueued >= cap ? cap : 0;
+    const size_t outstanding = (size_t)(rl->next_ticket - rl->oldest);
+    size_t group = (outstanding + RL_SLOTS - 1) / RL_SLOTS;
+    group = group < 1 ? 1 : group > cap ? cap : group;
+    if (rl->nqueued >= group)
+        return group;
+    return rl_busy(rl) ? 0 : rl->nqueued;
+}
+
+/* the queue's due groups, while launch slots are free */
+static int queue_drain(ptls_mi355x_record_layer_t *rl)
+{
+    int rc = 0;
+    size_t n;
+    while (!rl->slot[rl->launches % RL_SLOTS].op.busy && (n = queue_due(rl)) != 0)
+        rc |= rl_flush_n(rl, n);
+    return rc;
 }
 
 /* windows whose launch failed: their waits report -1 (seq stays past them: no nonce is used twice) */
@@ -1014,13 +1028,15 @@ static void op_fail_windows(ptls_mi355x_record_layer_t *rl, rl_slot_t *s, uint64
 }
 
 /*
- * Launches the layer's queued windows as ONE op (each window a part of the layer given again), when a launch slot is
- * free (else they stay queued: every slot is in flight, and the next wait frees one).  The seq / spec_seq the
- * windows took at their submit is kept: the build re-derives the same values from the first window's.
+ * Launches the first `n` of the layer's queued windows (all: n = 0) as ONE op (each window a part of the layer given
+ * again), when a launch slot is free (else they stay queued: every slot is in flight, and the next wait frees one).
+ * The seq / spec_seq the windows took at their submit is kept: the build re-derives the same values from the first
+ * window's.  0: launched or left queued; -1: the launch failed (its windows' waits report it).
  */
-static int rl_flush(ptls_mi355x_record_layer_t *rl)
+static int rl_flush_n(ptls_mi355x_record_layer_t *rl, size_t n)
 {
-    const size_t n = rl->nqueued;
+    if (n == 0 || n > rl->nqueued)
+        n = rl->nqueued;
     if (n == 0 || rl->slot[rl->launches % RL_SLOTS].op.busy)
         return 0;
     ptls_mi355x_record_layer_t *layers[RL_TICKETS];
@@ -1055,7 +1071,12 @@ static int rl_flush(ptls_mi355x_record_layer_t *rl)
             rl->spec_seq = keep;
         }
     }
-    queue_clear(rl);
+    for (size_t i = 0; i < n; ++i) /* the launched windows leave the queue */
+        free(rl->queue[i].frags);
+    memmove(rl->queue, rl->queue + n, (rl->nqueued - n) * sizeof(*rl->queue));
+    memset(rl->queue + rl->nqueued - n, 0, n * sizeof(*rl->queue));
+    rl->nqueued -= n;
+    rl->queue_ticket += n;
     if (rc == 0) {
         op_commit(rl, s, ticket0, n, 1);
         return 0;
@@ -1064,6 +1085,14 @@ static int rl_flush(ptls_mi355x_record_layer_t *rl)
         s = &rl->slot[rl->launches % RL_SLOTS]; /* (free: checked above) */
     op_fail_windows(rl, s, ticket0, n, is_seal);
     return -1;
+}
+
+static int rl_flush(ptls_mi355x_record_layer_t *rl)
+{
+    int rc = 0;
+    while (rl->nqueued != 0 && !rl->slot[rl->launches % RL_SLOTS].op.busy)
+        rc |= rl_flush_n(rl, rl->coalesce > 1 ? rl->coalesce : 1);
+    return rc;
 }
 
 /* ptls_send's record count and wire bytes for frags from seq (stopping at the 2^24 limit for application data) */
@@ -1148,9 +1177,7 @@ static int queue_window(ptls_mi355x_record_layer_t *rl, int is_seal, uint8_t typ
         rl->queue_ticket = rl->next_ticket;
     }
     *ticket = rl->next_ticket++;
-    if (queue_due(rl))
-        return rl_flush(rl); /* (no free launch slot: stays queued; a failed launch: its windows' waits report it) */
-    return 0;
+    return queue_drain(rl); /* (no free launch slot: stays queued; a failed launch: its windows' waits report it) */
 }
 
 int ptls_mi355x_record_layer_cork(ptls_mi355x_record_layer_t *rl, int on)
@@ -1353,6 +1380,7 @@ static int op_wait(ptls_mi355x_record_layer_t *rl, uint64_t ticket, size_t *outl
         if (rl->nqueued != 0 && ticket >= rl->queue_ticket)
             return rl_msg("a queued window found no free launch slot");
     }
+    (void)queue_drain(rl);
     rl_slot_t *s = &rl->slot[rl->ticket_slot[ticket % RL_TICKETS]];
     rl_op_t *op = &s->op;
     if (!op->done)
@@ -1374,8 +1402,7 @@ static int op_wait(ptls_mi355x_record_layer_t *rl, uint64_t ticket, size_t *outl
     ++rl->oldest;
     if (++op->waited == op->nwin)
         op_discard(op);
-    if (queue_due(rl)) /* a launch slot may have come free: the queue goes out when due */
-        (void)rl_flush(rl);
+    (void)queue_drain(rl); /* a launch slot may have come free: the queue goes out when due */
     return ret;
 }
 

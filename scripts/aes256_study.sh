@@ -11,9 +11,9 @@ timeout -k 5 20 amd-smi metric -p -c --json > $OUT/idle.json 2>&1 || true
 PROBE_NTT=16,12,10,8,6,0 timeout -k 10 200 python scripts/probe_bs.py run > $OUT/probe_sweep.log 2>&1
 # 2. power and clock under the probe, AES-256, T-table only (16) vs the best mix (8 + 8), ~20 s each
 for ntt in 16 8; do
-  PROBE_KEYS=32 PROBE_NTT=$ntt PROBE_REPS=500 PROBE_UNITS_MULT=64 timeout -k 10 150 python scripts/probe_bs.py run > $OUT/probe_power_$ntt.log 2>&1 &
+  PROBE_KEYS=32 PROBE_NTT=$ntt PROBE_REPS=1400 PROBE_UNITS_MULT=64 timeout -k 10 150 python scripts/probe_bs.py run > $OUT/probe_power_$ntt.log 2>&1 &
   pid=$!
-  sleep 12
+  sleep 15
   for i in 1 2 3 4 5; do timeout -k 5 20 amd-smi metric -p -c --json > $OUT/probe_${ntt}_$i.json 2>&1 || true; sleep 1; done
   wait $pid
 done
