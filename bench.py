@@ -555,8 +555,8 @@ def record_layer_stream(key_bytes: int = 16, nwin: int = 64, depth: int = 4, tra
     submit to the last wait; every opened window is compared with its fragments.  *_sync: one launch at a time."""
     exe = os.path.join(ROOT, "scripts", "_build", "rl_stream")
 
-    def run(tr, *extra):
-        r = subprocess.run([exe, str(nwin), str(depth), str(key_bytes), tr, *map(str, extra)],
+    def run(tr, *extra, d=depth):
+        r = subprocess.run([exe, str(nwin), str(d), str(key_bytes), tr, *map(str, extra)],
                            capture_output=True, text=True, timeout=120)
         if r.returncode != 0:
             raise SystemExit("bench: record-layer stream failed -- " + r.stderr.strip())
@@ -566,12 +566,16 @@ def record_layer_stream(key_bytes: int = 16, nwin: int = 64, depth: int = 4, tra
     # one connection: its consecutive windows, `per_launch[0]` of them per launch (the layer given that many times)
     res["one_connection"] = run(transport, per_launch[0], "one")
     res["one_window_per_launch"] = run(transport, per_launch[1])
+    # one window per submit with more windows outstanding: the layer coalesces its queued windows (round 4)
+    res["one_window_per_submit_coalesced"] = {f"depth_{d}": run(transport, 1, d=d) for d in (16, 32)}
     res["inputs_read_in_place"] = run("direct", per_launch[0])
     res["note"] = (f"{nwin} back-to-back windows of 16 x 16384 B records, AES-{8 * key_bytes}, host memory to host "
                    f"memory (registered buffers, {transport}), {per_launch[0]} connections' windows per launch, {depth} "
                    "launches in flight (record_layer_seal_submit / open_submit + wait), C driver scripts/rl_stream.c; "
                    f"*_sync: one launch at a time; one_connection: {per_launch[0]} consecutive windows of a single "
-                   "connection per launch; one_window_per_launch: a single connection's windows, one per launch; "
+                   "connection per launch; one_window_per_launch: a single connection's windows, one per submit, 4 "
+                   "outstanding (four single-window launches); one_window_per_submit_coalesced: one per submit with 16 / 32 "
+                   "outstanding, coalesced by the layer into ceil(outstanding / 4)-window launches; "
                    "inputs_read_in_place: transport direct (kernels read the inputs over PCIe)")
     return res
 

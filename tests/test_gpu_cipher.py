@@ -180,3 +180,34 @@ def test_work_slots_reused_across_streams(gpu):
     for out in outs:
         assert np.array_equal(out.cpu().numpy(), want)
     eng.close()
+
+
+def test_shared_resources_across_destroyed_streams(gpu):
+    """A context's work slots and sort scratch used from streams that are destroyed and replaced between uses (their
+    handles may be reused): each use waits on the event recorded right after the previous one, never on a stored
+    stream handle; ordered (ragged) seals through order_by_length on rotating streams stay bit-exact."""
+    import torch
+    rng = np.random.default_rng(19)
+    n = 3000
+    lens = rng.integers(0, 700, n).astype(np.uint64)
+    recs, src_bytes, aad_bytes = records.layout(lens, np.zeros(n, np.uint64), align=16)
+    src = rng.integers(0, 256, src_bytes, dtype=np.uint8)
+    key, iv = bytes(range(16)), bytes(range(12))
+    want = np.zeros_like(src)
+    oracle.batch(True, key, iv, recs, src, want, np.zeros(1, np.uint8))
+    eng = ra.Engine(key)
+    d_recs, d_src = torch.from_numpy(recs.view(np.uint8)).cuda(), torch.from_numpy(src).cuda()
+    d_aad = torch.zeros(1, dtype=torch.uint8, device="cuda")
+    d_order = torch.zeros(n, dtype=torch.int32, device="cuda")
+    outs = [torch.zeros_like(d_src) for _ in range(4)]
+    torch.cuda.synchronize()
+    for i in range(40):
+        s = torch.cuda.Stream()  # a fresh stream each time; the previous one is released
+        eng.order_by_length(d_recs.data_ptr(), n, d_order.data_ptr(), s.cuda_stream)
+        eng.seal_batch_ordered(iv, d_recs.data_ptr(), d_order.data_ptr(), n, d_src.data_ptr(), outs[i % 4].data_ptr(),
+                               d_aad.data_ptr(), s.cuda_stream)
+        del s
+    torch.cuda.synchronize()
+    for out in outs:
+        assert np.array_equal(out.cpu().numpy(), want)
+    eng.close()
