@@ -456,8 +456,60 @@ int ptls_mi355x_record_layer_unregister(ptls_mi355x_record_layer_t *rl, void *ba
  * open: DESIGN.md section 2).  Results are identical.  Returns the previous value. */
 #define PTLS_MI355X_RECORD_LAYER_DMA_IN 2
 int ptls_mi355x_record_layer_set_direct_dma(ptls_mi355x_record_layer_t *rl, int on);
+/*
+ * on != 0: the layer's windows that need no copy -- registered buffers read and written in place (the DMA settings
+ * above are then ignored), or zero-copy staging -- run as jobs of the device's resident grid (section 6) instead of
+ * kernel launches: a submit posts the window's runs (and an open's delivery) into the grid's ring, a wait polls its
+ * completion word.  For a caller that submits one window at a time.  Results are identical.  Returns the previous
+ * value.
+ */
+int ptls_mi355x_record_layer_set_resident(ptls_mi355x_record_layer_t *rl, int on);
 /* zero-copy limit in bytes (default 4 MiB; 0 = always DMA copies); returns the previous value */
 size_t ptls_mi355x_record_layer_set_zero_copy_bytes(ptls_mi355x_record_layer_t *rl, size_t n);
+
+/* ---- 6. resident window engine (csrc/gcm_engine.hip mi355x_resident) ----
+ *
+ * The same window kernels (the split runs of section 4's small framing batches, and the delivery kernel) executed
+ * by ONE persistent grid per device that takes jobs from a ring in pinned host memory: a window costs the host a
+ * few stores into that ring and a poll of a completion word, not a kernel launch and a stream synchronisation.
+ * For callers that submit windows one at a time (rapido: one send window per connection, lib/rapido.c:2115-2126).
+ * The grid (1 + ptls_mi355x_set_resident_workers() workgroups, each holding a CU's whole LDS) starts with the first
+ * job and leaves after ptls_mi355x_set_resident_idle_us() without work; a job posted later starts it again.  While
+ * it runs, hipDeviceSynchronize() and the batch kernels (which want every CU) wait for it to leave.
+ *
+ * Pointers as in section 4 (device memory, or host memory the GPU addresses: mapped pinned buffers); the buffers
+ * must stay valid until the job is complete.  Results are bit-identical to the stream calls.  A context's run jobs
+ * execute one at a time (a new one waits for the previous one: they share its split buffer); a delivery job follows
+ * the context's previous job (its open).  *job receives the job number (PTLS_MI355X_RESIDENT_NONE for n = 0, always
+ * complete).  Returns 0, or -1 (ptls_mi355x_last_error). */
+#define PTLS_MI355X_RESIDENT_NONE (~(uint64_t)0)
+int ptls_mi355x_resident_tls_seal_records_multi(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12,
+                                                const ptls_mi355x_tls_record_t *recs, const uint32_t *conn_ids, size_t n,
+                                                const uint8_t *src, uint8_t *dst, uint64_t *job);
+int ptls_mi355x_resident_tls_open_records_multi(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12,
+                                                const ptls_mi355x_tls_record_t *recs, const uint32_t *conn_ids, size_t n,
+                                                const uint8_t *src, uint8_t *dst, uint32_t *status, uint8_t *types,
+                                                uint64_t *job);
+int ptls_mi355x_resident_tls_deliver_records(ptls_mi355x_aesgcm_context_t *ctx, const ptls_mi355x_tls_record_t *recs,
+                                             const uint32_t *status, const uint8_t *types,
+                                             const ptls_mi355x_tls_deliver_t *parts, size_t nparts, size_t max_records,
+                                             uint64_t *job);
+/* 1 when the job is complete (its outputs visible to the host), 0 while it runs, -1 on error */
+int ptls_mi355x_resident_done(ptls_mi355x_aesgcm_context_t *ctx, uint64_t job);
+/* waits for the job (polling its completion word; restarts the grid if it left before seeing the job) */
+int ptls_mi355x_resident_wait(ptls_mi355x_aesgcm_context_t *ctx, uint64_t job);
+/* waits for every posted job, ends the device's grid and frees its ring (the next job creates them again) */
+int ptls_mi355x_resident_stop(int device);
+/* the job's timeline on the GPU's constant clock, in ns: ns[0] from its publication to its first unit's start,
+ * ns[1] from there to its last unit's end, ns[2] from there to its completion, ns[3] publication to completion;
+ * -1 if the job is not complete or its ring entry holds a later job by now */
+int ptls_mi355x_resident_job_times(ptls_mi355x_aesgcm_context_t *ctx, uint64_t job, uint64_t ns[4]);
+/* launches of the device's grid so far (each start after an idle exit is one) */
+uint64_t ptls_mi355x_resident_launches(int device);
+/* workers of grids created after the call (SIZE_MAX, the default: half the CUs); returns the previous value */
+size_t ptls_mi355x_set_resident_workers(size_t n);
+/* idle time after which a grid created after the call leaves (default 2000 us); returns the previous value */
+uint64_t ptls_mi355x_set_resident_idle_us(uint64_t us);
 
 /* ---- tuning / introspection ---- */
 /* lanes per record used by the batch kernels (1, 2, 4 or 8; default 4); returns the previous value, or -1 */

@@ -39,6 +39,9 @@ assert RECORD_DTYPE.itemsize == 40
 
 #: numpy mirror of ptls_mi355x_tls_record_t (include/ptls_mi355x.h section 4)
 TLS_RECORD_DTYPE = np.dtype([("src", "<u8"), ("dst", "<u8"), ("seq", "<u8"), ("len", "<u4"), ("type", "<u4")])
+#: ptls_mi355x_tls_deliver_t: one part of a delivery (slots, out, capacity, first record, records, any_type)
+TLS_DELIVER_DTYPE = np.dtype([("slots", "<u8"), ("out", "<u8"), ("capacity", "<u8"), ("k0", "<u4"), ("n", "<u4"),
+                              ("any_type", "<u4"), ("pad", "<u4")])
 assert TLS_RECORD_DTYPE.itemsize == 32
 TLS_HEADER_SIZE = 5
 TLS_MAX_FRAGMENT = 16384
@@ -73,7 +76,12 @@ EXPORTED_FUNCTIONS = (
     "ptls_mi355x_record_layer_flush", "ptls_mi355x_record_layer_set_coalesce", "ptls_mi355x_record_layer_launches",
     "ptls_mi355x_record_layer_cork",
     "ptls_mi355x_record_layer_set_direct_dma", "ptls_mi355x_tls_deliver_records",
+    "ptls_mi355x_resident_tls_seal_records_multi", "ptls_mi355x_resident_tls_open_records_multi",
+    "ptls_mi355x_resident_tls_deliver_records", "ptls_mi355x_resident_done", "ptls_mi355x_resident_wait",
+    "ptls_mi355x_resident_stop", "ptls_mi355x_resident_launches", "ptls_mi355x_set_resident_workers",
+    "ptls_mi355x_set_resident_idle_us", "ptls_mi355x_record_layer_set_resident", "ptls_mi355x_resident_job_times",
 )
+RESIDENT_NONE = (1 << 64) - 1
 EXPORTED_OBJECTS = ("ptls_mi355x_aes128gcm", "ptls_mi355x_aes256gcm", "ptls_mi355x_aes128ctr",
                     "ptls_mi355x_aes256ctr", "ptls_mi355x_aes128ecb", "ptls_mi355x_aes256ecb")
 
@@ -194,6 +202,8 @@ def lib() -> C.CDLL:
             L.ptls_mi355x_record_layer_launches.restype = u64
             L.ptls_mi355x_record_layer_cork.argtypes = [vp, C.c_int]
             L.ptls_mi355x_record_layer_set_direct_dma.argtypes = [vp, C.c_int]
+            if hasattr(L, "ptls_mi355x_record_layer_set_resident"):
+                L.ptls_mi355x_record_layer_set_resident.argtypes = [vp, C.c_int]
         for name in ("ptls_mi355x_set_win16_records", "ptls_mi355x_set_split_records"):
             if hasattr(L, name):  # (absent from older builds used in A/B timing runs)
                 getattr(L, name).argtypes = [sz]
@@ -205,6 +215,23 @@ def lib() -> C.CDLL:
             L.ptls_mi355x_aes_free.argtypes = [vp]
             L.ptls_mi355x_aes_ecb.argtypes = [vp, C.c_int, vp, vp, sz]
             L.ptls_mi355x_aes_ecb_batch.argtypes = [vp, C.c_int, vp, vp, sz, vp]
+        if hasattr(L, "ptls_mi355x_tls_deliver_records"):
+            L.ptls_mi355x_tls_deliver_records.argtypes = [vp, vp, vp, vp, vp, sz, sz, vp]
+        if hasattr(L, "ptls_mi355x_resident_wait"):  # (absent from older builds used in A/B timing runs)
+            L.ptls_mi355x_resident_tls_seal_records_multi.argtypes = [vp, vp, vp, vp, sz, vp, vp, C.POINTER(u64)]
+            L.ptls_mi355x_resident_tls_open_records_multi.argtypes = [vp, vp, vp, vp, sz, vp, vp, vp, vp,
+                                                                      C.POINTER(u64)]
+            L.ptls_mi355x_resident_tls_deliver_records.argtypes = [vp, vp, vp, vp, vp, sz, sz, C.POINTER(u64)]
+            L.ptls_mi355x_resident_done.argtypes = [vp, u64]
+            L.ptls_mi355x_resident_wait.argtypes = [vp, u64]
+            L.ptls_mi355x_resident_stop.argtypes = [C.c_int]
+            L.ptls_mi355x_resident_job_times.argtypes = [vp, u64, C.POINTER(u64)]
+            L.ptls_mi355x_resident_launches.argtypes = [C.c_int]
+            L.ptls_mi355x_resident_launches.restype = u64
+            L.ptls_mi355x_set_resident_workers.argtypes = [sz]
+            L.ptls_mi355x_set_resident_workers.restype = sz
+            L.ptls_mi355x_set_resident_idle_us.argtypes = [u64]
+            L.ptls_mi355x_set_resident_idle_us.restype = u64
         L.ptls_mi355x_tls_plan_send.argtypes = [sz, C.c_uint32, C.POINTER(u64), u64, u64, vp, sz, C.POINTER(sz)]
         L.ptls_mi355x_tls_plan_send.restype = sz
         L.ptls_mi355x_tls_parse_records.argtypes = [vp, sz, u64, C.POINTER(u64), u64, vp, sz, C.POINTER(sz),
@@ -449,6 +476,65 @@ class Engine:
                                                  src_ptr, dst_ptr, status_ptr, types_ptr, flags, stream or None):
             raise RuntimeError("tls_open_records failed: " + last_error())
 
+    # the resident window engine (include/ptls_mi355x.h section 6): jobs of the device's persistent grid
+    def resident_tls_seal_records(self, static_iv: bytes, recs_ptr: int, n: int, src_ptr: int, dst_ptr: int,
+                                  conn_ptr: int = 0) -> int:
+        job = u64(0)
+        if lib().ptls_mi355x_resident_tls_seal_records_multi(self.handle, _cbuf(static_iv), recs_ptr, conn_ptr or None,
+                                                             n, src_ptr, dst_ptr, C.byref(job)):
+            raise RuntimeError("resident tls_seal_records failed: " + last_error())
+        return job.value
+
+    def resident_tls_open_records(self, static_iv: bytes, recs_ptr: int, n: int, src_ptr: int, dst_ptr: int,
+                                  status_ptr: int, types_ptr: int, conn_ptr: int = 0) -> int:
+        job = u64(0)
+        if lib().ptls_mi355x_resident_tls_open_records_multi(self.handle, _cbuf(static_iv), recs_ptr, conn_ptr or None,
+                                                             n, src_ptr, dst_ptr, status_ptr, types_ptr, C.byref(job)):
+            raise RuntimeError("resident tls_open_records failed: " + last_error())
+        return job.value
+
+    def resident_tls_deliver_records(self, recs_ptr: int, status_ptr: int, types_ptr: int, parts_ptr: int,
+                                     nparts: int, max_records: int) -> int:
+        job = u64(0)
+        if lib().ptls_mi355x_resident_tls_deliver_records(self.handle, recs_ptr, status_ptr, types_ptr, parts_ptr,
+                                                          nparts, max_records, C.byref(job)):
+            raise RuntimeError("resident tls_deliver_records failed: " + last_error())
+        return job.value
+
+    def resident_done(self, job: int) -> bool:
+        rc = lib().ptls_mi355x_resident_done(self.handle, job)
+        if rc < 0:
+            raise RuntimeError("resident_done failed: " + last_error())
+        return rc == 1
+
+    def resident_wait(self, job: int) -> None:
+        if lib().ptls_mi355x_resident_wait(self.handle, job):
+            raise RuntimeError("resident_wait failed: " + last_error())
+
+    def resident_job_times(self, job: int):
+        """(publication -> first unit, first unit -> last unit end, -> complete, publication -> complete) in ns, or
+        None once the job's ring entry has been reused."""
+        ns = (u64 * 4)()
+        return None if lib().ptls_mi355x_resident_job_times(self.handle, job, ns) else tuple(ns)
+
+
+def resident_stop(device: int = 0) -> None:
+    """Waits for every posted resident job, ends the device's grid and frees its ring."""
+    if lib().ptls_mi355x_resident_stop(device):
+        raise RuntimeError("resident_stop failed: " + last_error())
+
+
+def resident_launches(device: int = 0) -> int:
+    return lib().ptls_mi355x_resident_launches(device)
+
+
+def set_resident_workers(n: int) -> int:
+    return lib().ptls_mi355x_set_resident_workers(n)
+
+
+def set_resident_idle_us(us: int) -> int:
+    return lib().ptls_mi355x_set_resident_idle_us(us)
+
 
 class AesKeys:
     """ptls_mi355x_aes_context_t: round keys only (the ECB/CTR ciphers), on the current device."""
@@ -497,12 +583,17 @@ class RecordLayer:
     """ptls_mi355x_record_layer_t: one traffic direction of a connection, windows of records between host memory
     and the GPU (include/ptls_mi355x.h section 5)."""
 
+    #: new layers start with set_resident(default_resident) (the test suites run every record-layer test both ways)
+    default_resident = False
+
     def __init__(self, key: bytes, static_iv: bytes, seq: int = 0):
         assert len(static_iv) == 12
         self._registered = {}
         self.handle = lib().ptls_mi355x_record_layer_new(_cbuf(key), len(key), _cbuf(static_iv), seq)
         if not self.handle:
             raise RuntimeError("ptls_mi355x_record_layer_new failed: " + lib().ptls_mi355x_record_layer_last_error().decode())
+        if RecordLayer.default_resident:
+            self.set_resident(True)
 
     @property
     def seq(self) -> int:
@@ -549,6 +640,11 @@ class RecordLayer:
         mode."""
         mode = on if on == RECORD_LAYER_DMA_IN else (1 if on else 0)
         return lib().ptls_mi355x_record_layer_set_direct_dma(self.handle, mode)
+
+    def set_resident(self, on: bool) -> bool:
+        """Windows that need no copy run as jobs of the device's resident grid (include/ptls_mi355x.h section 6)
+        instead of kernel launches.  Returns the previous setting."""
+        return bool(lib().ptls_mi355x_record_layer_set_resident(self.handle, 1 if on else 0))
 
     def set_zero_copy_bytes(self, n: int) -> int:
         """Windows of at most n staged bytes run zero-copy on the pinned staging (0: DMA copies); -> previous."""

@@ -101,6 +101,8 @@ typedef struct {
     rl_part_t *part;
     int direct, zero_copy, dma; /* direct: the results land in the caller's buffers (mapped or dma) */
     int deliver;                /* mapped open: slots in device memory, the delivery kernel writes the plaintexts */
+    int resident;               /* run as jobs of the device's resident grid (set_resident; zero-copy windows only) */
+    uint64_t rjob;              /* resident: its last job (the delivery, or the runs) */
     int dma_in;                 /* direct, the inputs moved to device memory by DMA first (set_direct_dma 2) */
     size_t nrec, off_src, srcbytes, off_dst, dstbytes, off_st, off_ty, off_dp, max_part;
     rl_copy_t *h2d, *d2h; /* dma: registered host ranges <-> the slot's device buffer */
@@ -129,6 +131,7 @@ struct st_ptls_mi355x_record_layer_t {
     size_t zero_copy_bytes;
     int direct_dma; /* registered windows move by DMA to and from device memory (1), are read in place (0, default), or
                      * the inputs move by DMA and the outputs are written in place (2) */
+    int resident;   /* windows without copies run on the resident grid (ptls_mi355x_record_layer_set_resident) */
     rl_region_t reg[RL_MAX_REGIONS];
     size_t nreg;
     rl_slot_t slot[RL_SLOTS];
@@ -255,12 +258,20 @@ static int slot_ready(ptls_mi355x_record_layer_t *rl, rl_slot_t *s)
     return 0;
 }
 
+/* the slot's launches are done: its stream's, and its op's resident jobs */
+static void slot_sync(rl_slot_t *s)
+{
+    if (s->stream != NULL)
+        (void)hipStreamSynchronize(s->stream);
+    if (s->ctx != NULL && s->op.busy && s->op.resident)
+        (void)ptls_mi355x_resident_wait(s->ctx, s->op.rjob);
+}
+
 static void slot_release(rl_slot_t *s)
 {
-    if (s->stream != NULL) {
-        (void)hipStreamSynchronize(s->stream);
+    slot_sync(s);
+    if (s->stream != NULL)
         (void)hipStreamDestroy(s->stream);
-    }
     if (s->h_buf != NULL) {
         memset(s->h_buf, 0, s->cap); /* plaintexts passed through the staging */
         (void)hipHostFree(s->h_buf);
@@ -337,8 +348,7 @@ void ptls_mi355x_record_layer_free(ptls_mi355x_record_layer_t *rl)
     queue_clear(rl); /* queued windows never launched: dropped */
     for (int i = 0; i < RL_SLOTS; ++i) {
         rl_op_t *op = &rl->slot[i].op;
-        if (rl->slot[i].stream != NULL) /* its own windows finish before their buffers and ranges go */
-            (void)hipStreamSynchronize(rl->slot[i].stream);
+        slot_sync(&rl->slot[i]); /* its own windows finish before their buffers and ranges go */
         if (op->busy) { /* never waited (or not for all its windows): completes here, its results dropped */
             if (!op->done)
                 op_release_layers(op);
@@ -394,6 +404,13 @@ int ptls_mi355x_record_layer_rekey(ptls_mi355x_record_layer_t *rl, const void *k
     return 0;
 }
 
+int ptls_mi355x_record_layer_set_resident(ptls_mi355x_record_layer_t *rl, int on)
+{
+    const int prev = rl->resident;
+    rl->resident = on != 0;
+    return prev;
+}
+
 int ptls_mi355x_record_layer_set_direct_dma(ptls_mi355x_record_layer_t *rl, int on)
 {
     const int prev = rl->direct_dma;
@@ -436,7 +453,7 @@ int ptls_mi355x_record_layer_unregister(ptls_mi355x_record_layer_t *rl, void *ba
         if (rl->reg[i].base == base) {
             for (int k = 0; k < RL_SLOTS; ++k) /* no window of this layer still reads the range */
                 if (rl->slot[k].stream != NULL)
-                    (void)hipStreamSynchronize(rl->slot[k].stream);
+                    slot_sync(&rl->slot[k]);
             /* nor a window of another layer that names this one (its kernels may address the range): the device */
             if (rl->inflight != 0)
                 (void)hipDeviceSynchronize();
@@ -621,6 +638,22 @@ static int op_launch(rl_slot_t *s, const uint8_t *src_base, uint8_t *dst_base)
     const uint32_t *conn = op->nlayers > 1 ? (const uint32_t *)(base + up16(op->nrec * sizeof(ptls_mi355x_tls_record_t))) : NULL;
     hipError_t e;
     int rc;
+    /* resident: no copies -- the window's runs (and its delivery) become jobs of the device's persistent grid */
+    op->resident = op->layers[0]->resident && op->zero_copy && !op->dma && !op->dma_in;
+    if (op->resident) {
+        const ptls_mi355x_tls_record_t *recs = (const ptls_mi355x_tls_record_t *)base;
+        if (op->is_seal)
+            rc = ptls_mi355x_resident_tls_seal_records_multi(s->ctx, op->layers[0]->iv, recs, conn, op->nrec, src, dst,
+                                                            &op->rjob);
+        else
+            rc = ptls_mi355x_resident_tls_open_records_multi(s->ctx, op->layers[0]->iv, recs, conn, op->nrec, src, dst,
+                                                            (uint32_t *)(base + op->off_st), base + op->off_ty, &op->rjob);
+        if (rc == 0 && op->deliver)
+            rc = ptls_mi355x_resident_tls_deliver_records(s->ctx, recs, (uint32_t *)(base + op->off_st), base + op->off_ty,
+                                                          (const ptls_mi355x_tls_deliver_t *)(base + op->off_dp),
+                                                          op->nlayers, op->max_part, &op->rjob);
+        return rc != 0 ? rl_msg(ptls_mi355x_last_error()) : 0;
+    }
     if (!op->zero_copy &&
         (e = hipMemcpyAsync(s->d_buf, s->h_buf, op->dma ? op->off_src : op->off_src + op->srcbytes, hipMemcpyHostToDevice,
                             s->stream)) != hipSuccess)
@@ -658,8 +691,7 @@ static int op_launch(rl_slot_t *s, const uint8_t *src_base, uint8_t *dst_base)
 static void op_scrub(rl_slot_t *s)
 {
     rl_op_t *op = &s->op;
-    if (s->stream != NULL)
-        (void)hipStreamSynchronize(s->stream);
+    slot_sync(s);
     if (!op->direct && s->h_buf != NULL) {
         const size_t end = op->is_seal ? op->off_dst + op->dstbytes : op->off_st;
         if (end > op->off_src && end <= s->cap)
@@ -741,9 +773,9 @@ static int seal_build(rl_slot_t *s, ptls_mi355x_record_layer_t *const *layers, s
                 overlap |= overlaps(frags[l][f].base, frags[l][f].len, out[m], op->part[m].wire);
         }
     }
-    const int dma = direct && layers[0]->direct_dma == 1;
+    const int dma = direct && layers[0]->direct_dma == 1 && !layers[0]->resident;
     /* DMA in: the fragments copied into device memory (one copy per contiguous run) first, the wire written in place */
-    const int dma_in = direct && layers[0]->direct_dma == PTLS_MI355X_RECORD_LAYER_DMA_IN;
+    const int dma_in = direct && layers[0]->direct_dma == PTLS_MI355X_RECORD_LAYER_DMA_IN && !layers[0]->resident;
     if (direct && !dma && !dma_in && overlap)
         direct = 0;
     const int packed = !direct || dma; /* fragments and records back to back in the staging / device layout */
@@ -879,7 +911,8 @@ static int open_build(rl_slot_t *s, ptls_mi355x_record_layer_t *const *layers, s
         if (dst_base == NULL || dout < dst_base)
             dst_base = dout;
     }
-    const int dma = direct && layers[0]->direct_dma == 1; /* (the input reaches the device before any output is written) */
+    /* (the input reaches the device before any output is written) */
+    const int dma = direct && layers[0]->direct_dma == 1 && !layers[0]->resident;
     size_t max_part = 0;
     for (size_t l = 0; l < nlayers; ++l)
         max_part = op->part[l].n > max_part ? op->part[l].n : max_part;
@@ -889,7 +922,7 @@ static int open_build(rl_slot_t *s, ptls_mi355x_record_layer_t *const *layers, s
     if (direct && !dma && !deliver && overlap)
         direct = 0;
     /* DMA in: the records copied into device memory (one copy per contiguous run of inputs) before the launch */
-    const int dma_in = deliver && layers[0]->direct_dma == PTLS_MI355X_RECORD_LAYER_DMA_IN;
+    const int dma_in = deliver && layers[0]->direct_dma == PTLS_MI355X_RECORD_LAYER_DMA_IN && !layers[0]->resident;
     const int packed = !direct || dma;
     op->direct = direct;
     op->dma = dma;
@@ -980,7 +1013,9 @@ static int rl_busy(ptls_mi355x_record_layer_t *rl)
     int busy = 0;
     for (int i = 0; i < RL_SLOTS && !busy; ++i) {
         const rl_slot_t *s = &rl->slot[i];
-        busy = s->op.busy && !s->op.done && s->op.nrec != 0 && hipStreamQuery(s->stream) == hipErrorNotReady;
+        busy = s->op.busy && !s->op.done && s->op.nrec != 0 &&
+               (s->op.resident ? ptls_mi355x_resident_done(s->ctx, s->op.rjob) == 0
+                               : hipStreamQuery(s->stream) == hipErrorNotReady);
     }
     (void)hipGetLastError(); /* (hipErrorNotReady is an answer, not an error to leave behind) */
     return busy;
@@ -1353,7 +1388,15 @@ static void op_complete(rl_slot_t *s, uint8_t *type)
 {
     rl_op_t *op = &s->op;
     hipError_t e;
-    if (op->nrec != 0 && (e = hipStreamSynchronize(s->stream)) != hipSuccess) {
+    if (op->nrec != 0 && op->resident && ptls_mi355x_resident_wait(s->ctx, op->rjob) != 0) {
+        rl_msg(ptls_mi355x_last_error());
+        op_scrub(s);
+        if (!op->is_seal)
+            for (size_t l = 0; l < op->nlayers; ++l)
+                if (!op->layers[l]->zombie)
+                    op->layers[l]->spec_seq = op->layers[l]->seq;
+        op->failed = 1;
+    } else if (op->nrec != 0 && !op->resident && (e = hipStreamSynchronize(s->stream)) != hipSuccess) {
         rl_fail("synchronize", e);
         op_scrub(s);
         if (!op->is_seal) /* nothing delivered: the next window starts at the delivered position */

@@ -4,7 +4,9 @@
  * itself would drive it (its send loop, lib/rapido.c:2176-2301, keeps many windows moving; a window is 16 records of
  * 16 KiB, :2115-2126).
  *
- *   rl_stream [nwin] [depth] [key_bytes] [transport: direct|dma|dma_in|zero_copy|copy] [windows per launch] [one]
+ *   rl_stream [nwin] [depth] [key_bytes] [transport: direct|dma|dma_in|zero_copy|copy|resident] [windows per launch]
+ *             [one]
+ *   (resident: registered buffers in place, the windows as jobs of the resident grid, section 6)
  *   (windows per launch > 1: windows of that many connections per launch, or with "one" consecutive windows of one
  *   connection)
  *
@@ -145,7 +147,8 @@ int main(int argc, char **argv)
     const int one_conn = argc > 6 && strcmp(argv[6], "one") == 0; /* ... of one connection instead of `multi` */
     if (depth < 1 || depth > 32 || nwin < 1 || (key_bytes != 16 && key_bytes != 32) || multi < 1 || multi > MAXM ||
         nwin % multi != 0) {
-        fprintf(stderr, "usage: rl_stream [nwin] [depth 1..32] [16|32] [direct|dma|dma_in|zero_copy|copy] [windows per launch 1..16] [one]\n");
+        fprintf(stderr, "usage: rl_stream [nwin] [depth 1..32] [16|32] [direct|dma|dma_in|zero_copy|copy|resident] "
+                        "[windows per launch 1..16] [one]\n");
         return 2;
     }
     signal(SIGSEGV, on_fault);
@@ -197,7 +200,8 @@ int main(int argc, char **argv)
     for (size_t i = 0; co != NULL && i < nall; ++i)
         ptls_mi355x_record_layer_set_coalesce(all[i], (size_t)atoi(co));
     for (size_t i = 0; i < nall; ++i) {
-        if (strcmp(transport, "direct") == 0 || strcmp(transport, "dma") == 0 || strcmp(transport, "dma_in") == 0) {
+        if (strcmp(transport, "direct") == 0 || strcmp(transport, "dma") == 0 || strcmp(transport, "dma_in") == 0 ||
+            strcmp(transport, "resident") == 0) {
             if (ptls_mi355x_record_layer_register(all[i], st.send, nwin * WIN * FRAG) != 0 ||
                 ptls_mi355x_record_layer_register(all[i], st.wire, nwin * WIRE_WIN) != 0 ||
                 ptls_mi355x_record_layer_register(all[i], st.pt, nwin * PT_WIN) != 0)
@@ -208,6 +212,8 @@ int main(int argc, char **argv)
         } else if (strcmp(transport, "copy") == 0) {
             ptls_mi355x_record_layer_set_zero_copy_bytes(all[i], 0);
         }
+        if (strcmp(transport, "resident") == 0) /* registered, in place, as jobs of the resident grid */
+            ptls_mi355x_record_layer_set_resident(all[i], 1);
     }
     size_t inflight = 0;
     double t_seal = 0, t_open = 0, t_seal1 = 0, t_open1 = 0;

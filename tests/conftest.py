@@ -56,3 +56,16 @@ def kernel_family(name: str, framing: bool):
         ra.set_seg32_records(prev32)
         ra.set_win16_records(prev16)
         ra.set_split_records(prevs)
+
+
+@pytest.fixture(params=["launch", "resident"])
+def rl_mode(request, gpu):
+    """Record layers created during the test launch kernels per window, or post jobs to the resident grid
+    (include/ptls_mi355x.h section 6): the record-layer suites run both ways."""
+    import rapido_amd as ra
+    prev = ra.RecordLayer.default_resident
+    ra.RecordLayer.default_resident = request.param == "resident"
+    try:
+        yield request.param
+    finally:
+        ra.RecordLayer.default_resident = prev

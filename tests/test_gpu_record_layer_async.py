@@ -18,7 +18,7 @@ import rapido_amd as ra
 from conftest import kernel_family
 from test_gpu_record_layer import conn_iv, oracle_window, page_buffer
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("rl_mode")]
 
 # direct: registered buffers read in place by the kernels, plaintexts written by the delivery kernel (the default);
 # direct_dma: registered buffers moved by DMA around a device-resident launch; direct_dma_in: the inputs moved by DMA,
