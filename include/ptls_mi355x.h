@@ -504,6 +504,8 @@ int ptls_mi355x_resident_stop(int device);
  * ns[1] from there to its last unit's end, ns[2] from there to its completion, ns[3] publication to completion;
  * -1 if the job is not complete or its ring entry holds a later job by now */
 int ptls_mi355x_resident_job_times(ptls_mi355x_aesgcm_context_t *ctx, uint64_t job, uint64_t ns[4]);
+/* jobs posted on the device so far: the next job's number (job numbers go on across ptls_mi355x_resident_stop) */
+uint64_t ptls_mi355x_resident_jobs(int device);
 /* launches of the device's grid so far (each start after an idle exit is one) */
 uint64_t ptls_mi355x_resident_launches(int device);
 /* workers of grids created after the call (SIZE_MAX, the default: half the CUs); returns the previous value */

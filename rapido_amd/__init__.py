@@ -80,6 +80,7 @@ EXPORTED_FUNCTIONS = (
     "ptls_mi355x_resident_tls_deliver_records", "ptls_mi355x_resident_done", "ptls_mi355x_resident_wait",
     "ptls_mi355x_resident_stop", "ptls_mi355x_resident_launches", "ptls_mi355x_set_resident_workers",
     "ptls_mi355x_set_resident_idle_us", "ptls_mi355x_record_layer_set_resident", "ptls_mi355x_resident_job_times",
+    "ptls_mi355x_resident_jobs",
 )
 RESIDENT_NONE = (1 << 64) - 1
 EXPORTED_OBJECTS = ("ptls_mi355x_aes128gcm", "ptls_mi355x_aes256gcm", "ptls_mi355x_aes128ctr",
@@ -226,6 +227,8 @@ def lib() -> C.CDLL:
             L.ptls_mi355x_resident_wait.argtypes = [vp, u64]
             L.ptls_mi355x_resident_stop.argtypes = [C.c_int]
             L.ptls_mi355x_resident_job_times.argtypes = [vp, u64, C.POINTER(u64)]
+            L.ptls_mi355x_resident_jobs.argtypes = [C.c_int]
+            L.ptls_mi355x_resident_jobs.restype = u64
             L.ptls_mi355x_resident_launches.argtypes = [C.c_int]
             L.ptls_mi355x_resident_launches.restype = u64
             L.ptls_mi355x_set_resident_workers.argtypes = [sz]
