@@ -480,7 +480,8 @@ size_t ptls_mi355x_record_layer_set_zero_copy_bytes(ptls_mi355x_record_layer_t *
  * Pointers as in section 4 (device memory, or host memory the GPU addresses: mapped pinned buffers); the buffers
  * must stay valid until the job is complete.  Results are bit-identical to the stream calls.  A context's run jobs
  * execute one at a time (a new one waits for the previous one: they share its split buffer); a delivery job follows
- * the context's previous job (its open).  *job receives the job number (PTLS_MI355X_RESIDENT_NONE for n = 0, always
+ * the context's previous job (its open), and a run job the context's previous copy job (its input, below).  *job
+ * receives the job number (PTLS_MI355X_RESIDENT_NONE for n = 0, always
  * complete).  Returns 0, or -1 (ptls_mi355x_last_error). */
 #define PTLS_MI355X_RESIDENT_NONE (~(uint64_t)0)
 int ptls_mi355x_resident_tls_seal_records_multi(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12,
@@ -494,6 +495,20 @@ int ptls_mi355x_resident_tls_deliver_records(ptls_mi355x_aesgcm_context_t *ctx, 
                                              const uint32_t *status, const uint8_t *types,
                                              const ptls_mi355x_tls_deliver_t *parts, size_t nparts, size_t max_records,
                                              uint64_t *job);
+/*
+ * A copy job: n (at most PTLS_MI355X_RESIDENT_COPY_MAX) ranges, each n bytes from src to dst (GPU addresses: device
+ * memory, or mapped host memory), copied by the grid's workers in 8 KiB chunks -- a window's input staged into device
+ * memory by the grid itself, with no hipMemcpy call.  The context's next run job follows it.  `ranges` is read
+ * during the call only.
+ */
+#define PTLS_MI355X_RESIDENT_COPY_MAX 64
+typedef struct st_ptls_mi355x_copy_t {
+    void *dst;
+    const void *src;
+    uint64_t n;
+} ptls_mi355x_copy_t;
+int ptls_mi355x_resident_copy(ptls_mi355x_aesgcm_context_t *ctx, const ptls_mi355x_copy_t *ranges, size_t n,
+                              uint64_t *job);
 /* 1 when the job is complete (its outputs visible to the host), 0 while it runs, -1 on error */
 int ptls_mi355x_resident_done(ptls_mi355x_aesgcm_context_t *ctx, uint64_t job);
 /* waits for the job (polling its completion word; restarts the grid if it left before seeing the job) */

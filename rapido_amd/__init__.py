@@ -80,7 +80,7 @@ EXPORTED_FUNCTIONS = (
     "ptls_mi355x_resident_tls_deliver_records", "ptls_mi355x_resident_done", "ptls_mi355x_resident_wait",
     "ptls_mi355x_resident_stop", "ptls_mi355x_resident_launches", "ptls_mi355x_set_resident_workers",
     "ptls_mi355x_set_resident_idle_us", "ptls_mi355x_record_layer_set_resident", "ptls_mi355x_resident_job_times",
-    "ptls_mi355x_resident_jobs",
+    "ptls_mi355x_resident_jobs", "ptls_mi355x_resident_copy",
 )
 RESIDENT_NONE = (1 << 64) - 1
 EXPORTED_OBJECTS = ("ptls_mi355x_aes128gcm", "ptls_mi355x_aes256gcm", "ptls_mi355x_aes128ctr",
@@ -223,6 +223,7 @@ def lib() -> C.CDLL:
             L.ptls_mi355x_resident_tls_open_records_multi.argtypes = [vp, vp, vp, vp, sz, vp, vp, vp, vp,
                                                                       C.POINTER(u64)]
             L.ptls_mi355x_resident_tls_deliver_records.argtypes = [vp, vp, vp, vp, vp, sz, sz, C.POINTER(u64)]
+            L.ptls_mi355x_resident_copy.argtypes = [vp, vp, sz, C.POINTER(u64)]
             L.ptls_mi355x_resident_done.argtypes = [vp, u64]
             L.ptls_mi355x_resident_wait.argtypes = [vp, u64]
             L.ptls_mi355x_resident_stop.argtypes = [C.c_int]
@@ -502,6 +503,14 @@ class Engine:
         if lib().ptls_mi355x_resident_tls_deliver_records(self.handle, recs_ptr, status_ptr, types_ptr, parts_ptr,
                                                           nparts, max_records, C.byref(job)):
             raise RuntimeError("resident tls_deliver_records failed: " + last_error())
+        return job.value
+
+    def resident_copy(self, ranges) -> int:
+        """A copy job: ranges = [(dst_ptr, src_ptr, nbytes), ...] (GPU addresses); the context's next run job follows it."""
+        arr = (u64 * (3 * max(len(ranges), 1)))(*[int(x) for r in ranges for x in r])
+        job = u64(0)
+        if lib().ptls_mi355x_resident_copy(self.handle, arr, len(ranges), C.byref(job)):
+            raise RuntimeError("resident_copy failed: " + last_error())
         return job.value
 
     def resident_done(self, job: int) -> bool:

@@ -1401,13 +1401,45 @@ extern "C" __global__ __launch_bounds__(256) void mi355x_tls_deliver(const TlsRe
  *    (for dependent jobs) and in host memory (what the host polls).
  *  - A delivery job names the open job it follows (`after`); its units start once that job's fin is set.
  *  - Exit: the dispatcher leaves after `idle` ticks with every published job finished (telling the host through the
- *    ring's `alive` word, re-checking the tail after that store), on the host's stop, or at `lifetime`; it then sets
- *    the instance's stop epoch and the workers leave.  Every wave reaches the exit whatever the host does, and the
+ *    ring's `alive` word, re-checking the tail after that store), or on the host's stop or at `lifetime` once the jobs
+ *    it published are complete; it then sets the instance's stop epoch and the workers leave.  Every wave reaches the exit whatever the host does, and the
  *    host re-launches the grid (same stream: never two instances at once) when a job finds none running.
  */
 constexpr uint32_t RES_RING = 256;
 
-enum : uint32_t { RES_SEAL = 1u, RES_FRAME = 2u, RES_AES256 = 4u, RES_DELIVER = 8u };
+enum : uint32_t { RES_SEAL = 1u, RES_FRAME = 2u, RES_AES256 = 4u, RES_DELIVER = 8u, RES_COPY = 16u };
+
+/* a copy job's ranges (ptls_mi355x_resident_copy): unit u copies chunk u - first of the range holding it */
+struct ResCopy {
+    uint64_t dst, src, n, first;
+};
+constexpr uint32_t RES_COPY_CHUNK = 8192;
+constexpr uint32_t RES_COPY_MAX = PTLS_MI355X_RESIDENT_COPY_MAX;
+
+/* dst[0, len) <- src[0, len) by the workgroup: four 16-byte loads per thread in flight when both are 16-aligned */
+__device__ __forceinline__ void res_copy_bytes(uint8_t *dst, const uint8_t *src, uint32_t len)
+{
+    if ((((uintptr_t)dst | (uintptr_t)src) & 15u) != 0u) {
+        copy_bytes(dst, src, len, threadIdx.x, blockDim.x);
+        return;
+    }
+    const uint32_t body = len / 16u, nt = blockDim.x;
+    const u32x4 *s4 = (const u32x4 *)src;
+    u32x4 *d4 = (u32x4 *)dst;
+    for (uint32_t b = 0; b < body; b += 4u * nt) {
+        u32x4 v[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4u; ++k)
+            if (b + k * nt + threadIdx.x < body)
+                v[k] = s4[b + k * nt + threadIdx.x];
+#pragma unroll
+        for (uint32_t k = 0; k < 4u; ++k)
+            if (b + k * nt + threadIdx.x < body)
+                d4[b + k * nt + threadIdx.x] = v[k];
+    }
+    if (threadIdx.x < len - 16u * body)
+        dst[16u * body + threadIdx.x] = src[16u * body + threadIdx.x];
+}
 
 struct ResJob {
     uint64_t id;      /* the job's number (seqlock word: ~0 while the dispatcher rewrites the device copy) */
@@ -1482,9 +1514,25 @@ template <typename T> __device__ __forceinline__ void res_st_sys(T *p, typename 
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-/* one run or delivery unit of job jb (every thread of the 128; LDS is the split layout's) */
+/* one run, delivery or copy unit of job jb (every thread of the 128; LDS is the split layout's) */
 __device__ __forceinline__ void res_unit(const ResJob &jb, uint32_t u, uint8_t *lds, const u32x4 *win_aes)
 {
+    if (jb.kind & RES_COPY) {
+        const ResCopy *cp = (const ResCopy *)jb.descs;
+        uint32_t lo = 0u, hi = jb.nrecs; /* the range holding chunk u: first <= u < the next range's first */
+        while (hi - lo > 1u) {
+            const uint32_t mid = (lo + hi) / 2u;
+            if (res_ld(&cp[mid].first) <= u)
+                lo = mid;
+            else
+                hi = mid;
+        }
+        const ResCopy c = res_ld(cp + lo);
+        const uint64_t off = (u - c.first) * (uint64_t)RES_COPY_CHUNK;
+        const uint32_t len = (uint32_t)(c.n - off < RES_COPY_CHUNK ? c.n - off : RES_COPY_CHUNK);
+        res_copy_bytes((uint8_t *)c.dst + off, (const uint8_t *)c.src + off, len);
+        return;
+    }
     if (jb.kind & RES_DELIVER) {
         const uint32_t G = jb.nrecs;
         deliver_body<true>((const TlsRecord *)jb.descs, jb.status, jb.types, jb.parts, u / G, u % G, G,
@@ -1524,8 +1572,14 @@ extern "C" __global__ __launch_bounds__(SPLIT_THREADS) void mi355x_resident(ResR
         uint64_t pub = res_ld_dev64(&ds->tail), idle_since = born;
         for (;;) {
             const uint64_t now = wall_clock64();
-            if (res_ld_sys32(&ring->stop) != 0u || now - born > lifetime_ticks)
-                break;
+            /* the host's stop or the lifetime: publish nothing more, leave once every published job is complete (the
+             * host relaunches the grid for jobs posted meanwhile); past twice the lifetime, leave regardless */
+            if (res_ld_sys32(&ring->stop) != 0u || now - born > lifetime_ticks) {
+                if (res_ld_dev64(&ds->nfin) >= pub || now - born > 2u * lifetime_ticks)
+                    break;
+                __builtin_amdgcn_s_sleep(8);
+                continue;
+            }
             const uint64_t tail = res_ld_sys64(&ring->tail);
             if (tail > pub) {
                 /* each new job: its id word invalid, the other 15 words, then the id (sc1 stores, drained in order) */
@@ -1575,7 +1629,7 @@ extern "C" __global__ __launch_bounds__(SPLIT_THREADS) void mi355x_resident(ResR
     for (;;) {
         if (threadIdx.x == 0) {
             uint32_t state = 1u; /* 0 work, 1 idle, 2 exit */
-            if (res_ld_dev32(&ds->stop_epoch) == epoch || wall_clock64() - born > lifetime_ticks + idle_ticks) {
+            if (res_ld_dev32(&ds->stop_epoch) == epoch || wall_clock64() - born > 2u * lifetime_ticks + idle_ticks) {
                 state = 2u;
             } else {
                 const uint64_t tail = res_ld_dev64(&ds->tail);
@@ -1636,7 +1690,7 @@ extern "C" __global__ __launch_bounds__(SPLIT_THREADS) void mi355x_resident(ResR
                 /* a delivery: its open job's units must all be done (they never wait for this one) */
                 const uint32_t ea = (uint32_t)((jb.after - 1u) % RES_RING);
                 while (res_ld_dev64(&ds->fin[ea]) < jb.after) {
-                    if (wall_clock64() - born > lifetime_ticks + idle_ticks) {
+                    if (wall_clock64() - born > 2u * lifetime_ticks + idle_ticks) {
                         go = 0u; /* (only if the grid outlived its lifetime: leave, the job stays incomplete) */
                         break;
                     }
@@ -2005,7 +2059,7 @@ static size_t g_resident_workers = SIZE_MAX;
 static uint64_t g_resident_idle_us = 2000;
 /* and in any case after this long (a bound on every wave's life, whatever the host does; the environment's
  * PTLS_MI355X_RESIDENT_LIFETIME_S, read when a device's engine is created, shortens it for tests) */
-static const uint64_t RES_LIFETIME_S = 600;
+static const uint64_t RES_LIFETIME_S = 30;
 
 struct Resident {
     std::mutex mu;                 /* posts and launches */
@@ -2020,6 +2074,7 @@ struct Resident {
     uint64_t idle_ticks = 0, lifetime_ticks = 0;
     uint64_t wclk_khz = 0;
     const u32x4 *win_aes = nullptr;
+    ResCopy *cp = nullptr, *cp_dev = nullptr; /* copy jobs' ranges: RES_COPY_MAX per ring entry (pinned, mapped) */
 };
 
 static std::mutex g_res_mu;
@@ -2065,8 +2120,15 @@ static Resident *resident_of(int dev, DeviceShared *shared, int num_cu)
     }
     if (e == hipSuccess)
         e = hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking);
+    if (e == hipSuccess)
+        e = hipHostMalloc((void **)&r->cp, sizeof(ResCopy) * RES_COPY_MAX * RES_RING,
+                          hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess)
+        e = hipHostGetDevicePointer((void **)&r->cp_dev, r->cp, 0);
     if (e != hipSuccess || wclk_khz <= 0) {
         fail("resident grid setup", e);
+        if (r->cp)
+            (void)hipHostFree(r->cp);
         if (r->ring)
             (void)hipHostFree(r->ring);
         if (r->ds)
@@ -2140,7 +2202,8 @@ static int res_wait(Resident *r, uint64_t id)
  * Posts a job (units, pointers; id and base filled in here) and returns its id; launches the grid if none runs.
  * A context's runs share its split tickets: a context's previous run job is waited for first.
  */
-static int res_post(ptls_mi355x_aesgcm_context_t *ctx, ResJob jb, uint64_t *id_out)
+static int res_post(ptls_mi355x_aesgcm_context_t *ctx, ResJob jb, uint64_t *id_out,
+                    const ptls_mi355x_copy_t *copies = nullptr, size_t ncopies = 0)
 {
     Resident *r = resident_of(ctx->device, ctx->shared, ctx->num_cu);
     if (r == nullptr)
@@ -2157,6 +2220,15 @@ static int res_post(ptls_mi355x_aesgcm_context_t *ctx, ResJob jb, uint64_t *id_o
     }
     jb.id = id;
     jb.base = (uint32_t)(r->units % r->P);
+    if (copies != nullptr) { /* the entry's ranges, read by the copy units through its device address */
+        ResCopy *c = r->cp + (size_t)e * RES_COPY_MAX;
+        uint64_t first = 0;
+        for (size_t i = 0; i < ncopies; ++i) {
+            c[i] = ResCopy{(uint64_t)(uintptr_t)copies[i].dst, (uint64_t)(uintptr_t)copies[i].src, copies[i].n, first};
+            first += (copies[i].n + RES_COPY_CHUNK - 1) / RES_COPY_CHUNK;
+        }
+        jb.descs = r->cp_dev + (size_t)e * RES_COPY_MAX;
+    }
     volatile ResRing *ring = (volatile ResRing *)r->ring;
     const uint64_t *w = (const uint64_t *)&jb;
     volatile uint64_t *h = (volatile uint64_t *)&ring->jobs[e];
@@ -2229,6 +2301,11 @@ static int res_runs(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void *st
     jb.iv0 = le32(iv);
     jb.iv1 = le32(iv + 4);
     jb.iv2 = le32(iv + 8);
+    /* after the context's previous job (the copy staging this window's input), if that is not complete yet */
+    Resident *r = resident_of(ctx->device, ctx->shared, ctx->num_cu);
+    if (r == nullptr)
+        return -1;
+    jb.after = ctx->res_last != 0u && !res_done(r, ctx->res_last - 1u) ? ctx->res_last : 0u;
     if (res_post(ctx, jb, job) != 0)
         return -1;
     ctx->res_runs_last = ctx->res_last = *job + 1u;
@@ -2604,6 +2681,35 @@ int ptls_mi355x_resident_tls_deliver_records(ptls_mi355x_aesgcm_context_t *ctx, 
     return 0;
 }
 
+int ptls_mi355x_resident_copy(ptls_mi355x_aesgcm_context_t *ctx, const ptls_mi355x_copy_t *ranges, size_t n,
+                              uint64_t *job)
+{
+    *job = PTLS_MI355X_RESIDENT_NONE;
+    if (n > RES_COPY_MAX) {
+        snprintf(g_err, sizeof(g_err), "resident copy of %zu ranges (at most %u)", n, RES_COPY_MAX);
+        return -1;
+    }
+    uint64_t chunks = 0;
+    for (size_t i = 0; i < n; ++i)
+        chunks += (ranges[i].n + RES_COPY_CHUNK - 1) / RES_COPY_CHUNK;
+    if (chunks == 0)
+        return 0;
+    if (chunks > 0xffffffffull) {
+        snprintf(g_err, sizeof(g_err), "resident copy too large");
+        return -1;
+    }
+    DeviceGuard guard(ctx->device);
+    ResJob jb;
+    memset(&jb, 0, sizeof(jb));
+    jb.kind = RES_COPY;
+    jb.nunits = (uint32_t)chunks;
+    jb.nrecs = (uint32_t)n;
+    if (res_post(ctx, jb, job, ranges, n) != 0)
+        return -1;
+    ctx->res_last = *job + 1u;
+    return 0;
+}
+
 int ptls_mi355x_resident_done(ptls_mi355x_aesgcm_context_t *ctx, uint64_t job)
 {
     if (job == PTLS_MI355X_RESIDENT_NONE)
@@ -2640,6 +2746,7 @@ int ptls_mi355x_resident_stop(int device)
     if (e != hipSuccess)
         rc = fail("resident grid", e);
     (void)hipStreamDestroy(r->stream);
+    (void)hipHostFree(r->cp);
     (void)hipHostFree(r->ring);
     (void)hipFree(r->ds);
     delete r;

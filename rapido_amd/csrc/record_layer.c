@@ -638,7 +638,7 @@ static int op_launch(rl_slot_t *s, const uint8_t *src_base, uint8_t *dst_base)
     const uint32_t *conn = op->nlayers > 1 ? (const uint32_t *)(base + up16(op->nrec * sizeof(ptls_mi355x_tls_record_t))) : NULL;
     hipError_t e;
     int rc;
-    /* resident: no copies -- the window's runs (and its delivery) become jobs of the device's persistent grid */
+    /* resident: no launch -- the window's runs (and its delivery) become jobs of the device's persistent grid */
     op->resident = op->layers[0]->resident && op->zero_copy && !op->dma && !op->dma_in;
     if (op->resident) {
         const ptls_mi355x_tls_record_t *recs = (const ptls_mi355x_tls_record_t *)base;
@@ -775,6 +775,7 @@ static int seal_build(rl_slot_t *s, ptls_mi355x_record_layer_t *const *layers, s
     }
     const int dma = direct && layers[0]->direct_dma == 1 && !layers[0]->resident;
     /* DMA in: the fragments copied into device memory (one copy per contiguous run) first, the wire written in place */
+    /* (resident layers read in place: staging the inputs by the grid's own copy jobs measured slower) */
     const int dma_in = direct && layers[0]->direct_dma == PTLS_MI355X_RECORD_LAYER_DMA_IN && !layers[0]->resident;
     if (direct && !dma && !dma_in && overlap)
         direct = 0;

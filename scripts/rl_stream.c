@@ -4,9 +4,10 @@
  * itself would drive it (its send loop, lib/rapido.c:2176-2301, keeps many windows moving; a window is 16 records of
  * 16 KiB, :2115-2126).
  *
- *   rl_stream [nwin] [depth] [key_bytes] [transport: direct|dma|dma_in|zero_copy|copy|resident] [windows per launch]
- *             [one]
- *   (resident: registered buffers in place, the windows as jobs of the resident grid, section 6)
+ *   rl_stream [nwin] [depth] [key_bytes] [transport: direct|dma|dma_in|zero_copy|copy|resident|resident_dma_in]
+ *             [windows per launch] [one]
+ *   (resident: registered buffers in place, the windows as jobs of the resident grid, section 6; resident_dma_in: the
+ *   same with the DMA-in setting, which a resident layer ignores)
  *   (windows per launch > 1: windows of that many connections per launch, or with "one" consecutive windows of one
  *   connection)
  *
@@ -174,7 +175,7 @@ int main(int argc, char **argv)
     const int one_conn = argc > 6 && strcmp(argv[6], "one") == 0; /* ... of one connection instead of `multi` */
     if (depth < 1 || depth > 32 || nwin < 1 || (key_bytes != 16 && key_bytes != 32) || multi < 1 || multi > MAXM ||
         nwin % multi != 0) {
-        fprintf(stderr, "usage: rl_stream [nwin] [depth 1..32] [16|32] [direct|dma|dma_in|zero_copy|copy|resident] "
+        fprintf(stderr, "usage: rl_stream [nwin] [depth 1..32] [16|32] [direct|dma|dma_in|zero_copy|copy|resident|resident_dma_in] "
                         "[windows per launch 1..16] [one]\n");
         return 2;
     }
@@ -231,18 +232,21 @@ int main(int argc, char **argv)
         ptls_mi355x_record_layer_set_coalesce(all[i], (size_t)atoi(co));
     for (size_t i = 0; i < nall; ++i) {
         if (strcmp(transport, "direct") == 0 || strcmp(transport, "dma") == 0 || strcmp(transport, "dma_in") == 0 ||
-            strcmp(transport, "resident") == 0) {
+            strcmp(transport, "resident") == 0 || strcmp(transport, "resident_dma_in") == 0) {
             if (ptls_mi355x_record_layer_register(all[i], st.send, nwin * WIN * FRAG) != 0 ||
                 ptls_mi355x_record_layer_register(all[i], st.wire, nwin * WIRE_WIN) != 0 ||
                 ptls_mi355x_record_layer_register(all[i], st.pt, nwin * PT_WIN) != 0)
                 die("register");
-            ptls_mi355x_record_layer_set_direct_dma(all[i], strcmp(transport, "dma") == 0      ? 1
-                                                            : strcmp(transport, "dma_in") == 0 ? PTLS_MI355X_RECORD_LAYER_DMA_IN
-                                                                                                : 0);
+            ptls_mi355x_record_layer_set_direct_dma(all[i], strcmp(transport, "dma") == 0 ? 1
+                                                            : strcmp(transport, "dma_in") == 0 ||
+                                                                    strcmp(transport, "resident_dma_in") == 0
+                                                                ? PTLS_MI355X_RECORD_LAYER_DMA_IN
+                                                                : 0);
         } else if (strcmp(transport, "copy") == 0) {
             ptls_mi355x_record_layer_set_zero_copy_bytes(all[i], 0);
         }
-        if (strcmp(transport, "resident") == 0) /* registered, in place, as jobs of the resident grid */
+        /* registered, as jobs of the resident grid: in place, or the inputs staged by the grid's copy jobs */
+        if (strcmp(transport, "resident") == 0 || strcmp(transport, "resident_dma_in") == 0)
             ptls_mi355x_record_layer_set_resident(all[i], 1);
     }
     size_t inflight = 0;
@@ -251,7 +255,7 @@ int main(int argc, char **argv)
     pass(&st, 0, depth, &inflight);
     ptls_mi355x_record_layer_t *lead_tx = multi > 1 ? st.txs[0] : st.tx, *lead_rx = multi > 1 ? st.rxs[0] : st.rx;
     const uint64_t l0s = ptls_mi355x_record_layer_launches(lead_tx), l0o = ptls_mi355x_record_layer_launches(lead_rx);
-    const int resident = strcmp(transport, "resident") == 0;
+    const int resident = strncmp(transport, "resident", 8) == 0;
     const uint64_t j0 = resident ? ptls_mi355x_resident_jobs(0) : 0;
     t_seal = pass(&st, 1, depth, &inflight);
     const uint64_t l1s = ptls_mi355x_record_layer_launches(lead_tx);

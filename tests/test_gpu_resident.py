@@ -135,29 +135,29 @@ def test_resident_equals_stream_launches(gpu, keylen):
 
 
 def test_resident_many_jobs_in_flight_past_the_ring(gpu):
-    """300 windows posted before any wait (the ring holds 256: posts wait for the oldest entries), four contexts of
-    two keys taking turns, each window checked against the oracle."""
+    """260 windows of 260 contexts (a context's run jobs go one at a time) posted before any wait: the ring holds 256,
+    so the last posts wait for the oldest entries; two keys taking turns, each window checked against the oracle."""
     import torch
     rng = np.random.default_rng(7200)
     keys = [rng.integers(0, 256, 16, dtype=np.uint8).tobytes(), rng.integers(0, 256, 32, dtype=np.uint8).tobytes()]
     iv = rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
-    engs = [ra.Engine(keys[i % 2]) for i in range(4)]
-    jobs = []
-    for w in range(300):
-        lens = [int(x) for x in rng.integers(0, 2000, 4)]
-        trecs, _, src, wsize = window(rng, lens)
-        d_src, d_recs = dev(src), dev(trecs.view(np.uint8))
-        d_dst = torch.zeros(max(wsize, 1), dtype=torch.uint8, device="cuda")
-        torch.cuda.synchronize()
-        e = engs[w % 4]
-        job = e.resident_tls_seal_records(iv, d_recs.data_ptr(), len(trecs), d_src.data_ptr(), d_dst.data_ptr())
-        jobs.append((e, job, keys[w % 2], trecs, src, d_dst, d_src, d_recs))
-    for e, job, key, trecs, src, d_dst, _, _ in jobs:
-        e.resident_wait(job)
+    nwin = 260
+    engs = [ra.Engine(keys[i % 2]) for i in range(nwin)]
+    wins = []
+    for w in range(nwin):
+        trecs, _, src, wsize = window(rng, [int(x) for x in rng.integers(0, 2000, 4)])
+        wins.append((trecs, src, dev(src), dev(trecs.view(np.uint8)),
+                     torch.zeros(max(wsize, 1), dtype=torch.uint8, device="cuda")))
+    torch.cuda.synchronize()
+    jobs = [engs[w].resident_tls_seal_records(iv, d_recs.data_ptr(), len(trecs), d_src.data_ptr(), d_dst.data_ptr())
+            for w, (trecs, _, d_src, d_recs, d_dst) in enumerate(wins)]
+    assert jobs == list(range(jobs[0], jobs[0] + nwin))
+    for w, (trecs, src, _, _, d_dst) in enumerate(wins):
+        engs[w].resident_wait(jobs[w])
         wire = d_dst.cpu().numpy()
         for t in trecs:
             frag = src[int(t["src"]): int(t["src"]) + int(t["len"])].tobytes()
-            want = oracle.tls_seal_record(key, iv, int(t["seq"]), int(t["type"]), frag)
+            want = oracle.tls_seal_record(keys[w % 2], iv, int(t["seq"]), int(t["type"]), frag)
             assert wire[int(t["dst"]): int(t["dst"]) + len(want)].tobytes() == want
     for e in engs:
         e.close()
@@ -301,4 +301,60 @@ def test_resident_then_stream_on_one_context(gpu):
             frag = src[int(t["src"]): int(t["src"]) + int(t["len"])].tobytes()
             want = oracle.tls_seal_record(key, iv, int(t["seq"]), int(t["type"]), frag)
             assert w[int(t["dst"]): int(t["dst"]) + len(want)].tobytes() == want
+    eng.close()
+
+
+def test_resident_lifetime_exit_under_load(gpu, monkeypatch):
+    """A grid whose lifetime (1 s) runs out while jobs keep coming: it stops publishing, leaves once its jobs are
+    complete, and the host starts the next instance for the jobs posted meanwhile -- every window correct."""
+    rng = np.random.default_rng(7700)
+    key, iv = rng.integers(0, 256, 16, dtype=np.uint8).tobytes(), rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    ra.resident_stop(0)
+    monkeypatch.setenv("PTLS_MI355X_RESIDENT_LIFETIME_S", "1")
+    try:
+        eng = ra.Engine(key)
+        trecs, _, src, wsize = window(rng, [4000] * 4)
+        want = seal_stream(eng, iv, trecs, src, wsize).tobytes()
+        t0, n = time.time(), 0
+        while time.time() - t0 < 2.5:
+            assert seal_resident(eng, iv, trecs, src, wsize).tobytes() == want
+            n += 1
+        assert ra.resident_launches(0) >= 2 and n > 100
+        eng.close()
+    finally:
+        ra.resident_stop(0)  # (the next engine reads the restored environment)
+
+
+def test_resident_copy_job_then_runs(gpu):
+    """A copy job staging a window's input from pinned host memory into device memory (three ranges: whole, at an odd
+    offset and length, and a few bytes), then the run job reading the copy -- the wire bytes of the stream kernels on
+    the original; the copied bytes exact, nothing outside the ranges written."""
+    import ctypes
+
+    import torch
+    rng = np.random.default_rng(7800)
+    key, iv = rng.integers(0, 256, 16, dtype=np.uint8).tobytes(), rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    eng = ra.Engine(key)
+    trecs, _, src, wsize = window(rng, [16384] * 6 + [777, 5000])
+    host = torch.from_numpy(np.concatenate([src, rng.integers(0, 256, 9000, dtype=np.uint8)])).pin_memory()
+    hip = ctypes.CDLL("libamdhip64.so")
+    hp = ctypes.c_void_p()
+    assert hip.hipHostGetDevicePointer(ctypes.byref(hp), ctypes.c_void_p(host.data_ptr()), 0) == 0
+    d_in = torch.zeros(len(src) + 9000, dtype=torch.uint8, device="cuda")
+    d_recs = dev(trecs.view(np.uint8))
+    d_dst = torch.zeros(wsize, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    n = len(src)
+    ranges = [(d_in.data_ptr(), hp.value, n), (d_in.data_ptr() + n + 3, hp.value + n + 3, 8191), (d_in.data_ptr() + n + 8200, hp.value + n + 8200, 5)]
+    j1 = eng.resident_copy(ranges)
+    j2 = eng.resident_tls_seal_records(iv, d_recs.data_ptr(), len(trecs), d_in.data_ptr(), d_dst.data_ptr())
+    eng.resident_wait(j2)
+    assert eng.resident_done(j1)
+    got = d_in.cpu().numpy()
+    h = host.numpy()
+    assert got[:n].tobytes() == h[:n].tobytes()
+    assert got[n: n + 3].tobytes() == b"\0" * 3 and got[n + 3: n + 3 + 8191].tobytes() == h[n + 3: n + 3 + 8191].tobytes()
+    assert got[n + 3 + 8191: n + 8200].tobytes() == b"\0" * 6 and got[n + 8200: n + 8205].tobytes() == h[n + 8200: n + 8205].tobytes()
+    assert not got[n + 8205:].any()
+    assert d_dst.cpu().numpy().tobytes() == seal_stream(eng, iv, trecs, src, wsize).tobytes()
     eng.close()
