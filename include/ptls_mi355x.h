@@ -509,6 +509,11 @@ typedef struct st_ptls_mi355x_copy_t {
 } ptls_mi355x_copy_t;
 int ptls_mi355x_resident_copy(ptls_mi355x_aesgcm_context_t *ctx, const ptls_mi355x_copy_t *ranges, size_t n,
                               uint64_t *job);
+/* on != 0: the single-record calls (section 2, and through them the AEAD slot objects of section 1) run as jobs of
+ * the resident grid instead of a launch and a stream synchronisation each (records up to the slot zero-copy limit).
+ * Results are identical.  Returns the previous value (initially PTLS_MI355X_SLOT_RESIDENT from the environment, else
+ * 0). */
+int ptls_mi355x_set_slot_resident(int on);
 /* 1 when the job is complete (its outputs visible to the host), 0 while it runs, -1 on error */
 int ptls_mi355x_resident_done(ptls_mi355x_aesgcm_context_t *ctx, uint64_t job);
 /* waits for the job (polling its completion word; restarts the grid if it left before seeing the job) */

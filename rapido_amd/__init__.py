@@ -80,7 +80,7 @@ EXPORTED_FUNCTIONS = (
     "ptls_mi355x_resident_tls_deliver_records", "ptls_mi355x_resident_done", "ptls_mi355x_resident_wait",
     "ptls_mi355x_resident_stop", "ptls_mi355x_resident_launches", "ptls_mi355x_set_resident_workers",
     "ptls_mi355x_set_resident_idle_us", "ptls_mi355x_record_layer_set_resident", "ptls_mi355x_resident_job_times",
-    "ptls_mi355x_resident_jobs", "ptls_mi355x_resident_copy",
+    "ptls_mi355x_resident_jobs", "ptls_mi355x_resident_copy", "ptls_mi355x_set_slot_resident",
 )
 RESIDENT_NONE = (1 << 64) - 1
 EXPORTED_OBJECTS = ("ptls_mi355x_aes128gcm", "ptls_mi355x_aes256gcm", "ptls_mi355x_aes128ctr",
@@ -224,6 +224,7 @@ def lib() -> C.CDLL:
                                                                       C.POINTER(u64)]
             L.ptls_mi355x_resident_tls_deliver_records.argtypes = [vp, vp, vp, vp, vp, sz, sz, C.POINTER(u64)]
             L.ptls_mi355x_resident_copy.argtypes = [vp, vp, sz, C.POINTER(u64)]
+            L.ptls_mi355x_set_slot_resident.argtypes = [C.c_int]
             L.ptls_mi355x_resident_done.argtypes = [vp, u64]
             L.ptls_mi355x_resident_wait.argtypes = [vp, u64]
             L.ptls_mi355x_resident_stop.argtypes = [C.c_int]
@@ -538,6 +539,11 @@ def resident_stop(device: int = 0) -> None:
 
 def resident_launches(device: int = 0) -> int:
     return lib().ptls_mi355x_resident_launches(device)
+
+
+def set_slot_resident(on: bool) -> bool:
+    """Single-record calls (the AEAD slot objects) as jobs of the resident grid; returns the previous setting."""
+    return bool(lib().ptls_mi355x_set_slot_resident(1 if on else 0))
 
 
 def set_resident_workers(n: int) -> int:

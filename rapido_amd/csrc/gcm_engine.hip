@@ -1837,6 +1837,14 @@ static size_t g_win16_records = SIZE_MAX;
 /* window batches of at most this many records use the split kernels, SPLIT_MAXRUN workgroups per record
  * (ptls_mi355x_set_split_records; SIZE_MAX = CU count / SPLIT_MAXRUN); they take precedence over the others */
 static size_t g_split_records = SIZE_MAX;
+/* single-record slot calls run as jobs of the resident grid (ptls_mi355x_set_slot_resident; initially the
+ * environment's PTLS_MI355X_SLOT_RESIDENT, so unmodified C callers can be run either way) */
+static int slot_resident_env()
+{
+    const char *e = getenv("PTLS_MI355X_SLOT_RESIDENT");
+    return e != nullptr && atoi(e) != 0;
+}
+static int g_slot_resident = slot_resident_env();
 
 static int fail(const char *what, hipError_t e)
 {
@@ -2256,7 +2264,7 @@ static int res_ctx_wait(ptls_mi355x_aesgcm_context_t *ctx, uint64_t id1)
 /* a run job (records x SPLIT_MAXRUN units) of a TLS window */
 static int res_runs(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void *static_iv12, const void *recs,
                     const uint32_t *conn, size_t n, const uint8_t *src, uint8_t *dst, uint32_t *status, uint8_t *types,
-                    uint64_t *job)
+                    uint64_t *job, bool frame = true, const uint8_t *aad = nullptr)
 {
     *job = PTLS_MI355X_RESIDENT_NONE;
     if (n == 0)
@@ -2269,8 +2277,10 @@ static int res_runs(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void *st
     /* the tickets of the context's previous run job, and of its stream launches, are free */
     if (res_ctx_wait(ctx, ctx->res_runs_last) != 0)
         return -1;
-    if (ctx->home_set && (ctx->multi ? (ctx->split_ev_valid ? hipEventSynchronize(ctx->split_ev) : hipSuccess)
-                                     : hipStreamSynchronize(ctx->home)) != hipSuccess)
+    /* (the slot calls' own stream is idle between calls: each ends with its synchronisation, under the staging lock) */
+    if (ctx->home_set && !(ctx->home == ctx->shared->stream && !ctx->multi) &&
+        (ctx->multi ? (ctx->split_ev_valid ? hipEventSynchronize(ctx->split_ev) : hipSuccess)
+                    : hipStreamSynchronize(ctx->home)) != hipSuccess)
         return fail("resident: the context's stream launches", hipGetLastError());
     if (ctx->split_cap < n) {
         if (ctx->d_split)
@@ -2286,7 +2296,7 @@ static int res_runs(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void *st
     const uint8_t *iv = (const uint8_t *)static_iv12;
     ResJob jb;
     memset(&jb, 0, sizeof(jb));
-    jb.kind = (seal ? RES_SEAL : 0u) | RES_FRAME | (ctx->key_size == 32 ? RES_AES256 : 0u);
+    jb.kind = (seal ? RES_SEAL : 0u) | (frame ? RES_FRAME : 0u) | (ctx->key_size == 32 ? RES_AES256 : 0u);
     jb.nunits = (uint32_t)(n * SPLIT_MAXRUN);
     jb.nrecs = (uint32_t)n;
     jb.ki = ctx->d_ki;
@@ -2298,6 +2308,7 @@ static int res_runs(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void *st
     jb.conn = conn;
     jb.partials = ctx->d_split;
     jb.tickets = (uint32_t *)((uint8_t *)ctx->d_split + ctx->split_cap * SPLIT_PSLOTS * sizeof(u32x4));
+    jb.parts = (const DeliverPart *)aad; /* (AEAD records: their AAD base) */
     jb.iv0 = le32(iv);
     jb.iv1 = le32(iv + 4);
     jb.iv2 = le32(iv + 8);
@@ -2710,6 +2721,13 @@ int ptls_mi355x_resident_copy(ptls_mi355x_aesgcm_context_t *ctx, const ptls_mi35
     return 0;
 }
 
+int ptls_mi355x_set_slot_resident(int on)
+{
+    const int prev = g_slot_resident;
+    g_slot_resident = on != 0;
+    return prev;
+}
+
 int ptls_mi355x_resident_done(ptls_mi355x_aesgcm_context_t *ctx, uint64_t job)
 {
     if (job == PTLS_MI355X_RESIDENT_NONE)
@@ -2959,6 +2977,22 @@ int ptls_mi355x_order_by_length(ptls_mi355x_aesgcm_context_t *ctx, const ptls_mi
  * (device and pinned host alike):
  *   [0, 64) descriptor | [64, 64 + A) aad | [D, D + inlen + 16) data (in place) | status
  */
+
+/* the record's result out of the staging (which is then cleared): seal 0; open 1 verified, 0 not */
+static int finish_single(DeviceShared *d, bool seal, void *output, size_t inlen, size_t off_data, size_t off_status,
+                         size_t total)
+{
+    const size_t outlen = seal ? inlen + 16 : inlen;
+    if (outlen)
+        memcpy(output, d->h_stage + off_data, outlen);
+    uint32_t st;
+    memcpy(&st, d->h_stage + off_status, 4);
+    memset(d->h_stage, 0, total);
+    if (seal)
+        return 0;
+    return st == (uint32_t)inlen ? 1 : 0;
+}
+
 static int single_record(ptls_mi355x_aesgcm_context_t *ctx, bool seal, void *output, const void *input, size_t inlen,
                          const void *nonce12, const void *aad, size_t aadlen, const void *tag)
 {
@@ -2988,6 +3022,17 @@ static int single_record(ptls_mi355x_aesgcm_context_t *ctx, bool seal, void *out
      */
     const bool zc = total <= g_slot_zero_copy_bytes;
     uint8_t *base = zc ? d->h_stage_dev : d->d_stage;
+    if (zc && g_slot_resident) {
+        /* a job of the resident grid on the staging (no launch, no stream synchronisation: section 6) */
+        uint64_t job;
+        if (res_runs(ctx, seal, nonce12, base, nullptr, 1, base, base, (uint32_t *)(base + off_status), nullptr, &job,
+                     false, base) != 0 ||
+            res_ctx_wait(ctx, job + 1u) != 0) {
+            memset(d->h_stage, 0, total);
+            return -1;
+        }
+        return finish_single(d, seal, output, inlen, off_data, off_status, total);
+    }
     if (!zc)
         HIPCHK(hipMemcpyAsync(d->d_stage, d->h_stage, off_status, hipMemcpyHostToDevice, d->stream));
     /* one record: the window kernels (8-lane segments in parallel, leading pad steps skipped) are as fast as the
@@ -3003,16 +3048,9 @@ static int single_record(ptls_mi355x_aesgcm_context_t *ctx, bool seal, void *out
                                   d->stream));
     }
     HIPCHK(hipStreamSynchronize(d->stream));
-    if (outlen)
-        memcpy(output, d->h_stage + off_data, outlen);
-    uint32_t st;
-    memcpy(&st, d->h_stage + off_status, 4);
-    memset(d->h_stage, 0, total);
     if (!zc)
         HIPCHK(hipMemsetAsync(d->d_stage, 0, total, d->stream)); /* nothing of the record stays on the device */
-    if (seal)
-        return 0;
-    return st == (uint32_t)inlen ? 1 : 0;
+    return finish_single(d, seal, output, inlen, off_data, off_status, total);
 }
 
 int ptls_mi355x_aesgcm_encrypt(ptls_mi355x_aesgcm_context_t *ctx, void *output, const void *input, size_t inlen,
