@@ -1484,6 +1484,7 @@ struct ResDev {
     uint64_t fin[RES_RING];
     uint32_t done[RES_RING]; /* units done of the entry's current job */
     uint64_t first_c[RES_RING], last[RES_RING]; /* ~(first unit start), last unit end (atomic max; 0 between jobs) */
+    uint64_t started; /* workers of every instance so far that have read their starting job (see the dispatcher) */
 };
 
 __device__ __forceinline__ uint64_t res_ld_sys64(const uint64_t *p)
@@ -1561,7 +1562,7 @@ __device__ __forceinline__ void res_unit(const ResJob &jb, uint32_t u, uint8_t *
 
 extern "C" __global__ __launch_bounds__(SPLIT_THREADS) void mi355x_resident(ResRing *ring, ResDev *ds, const u32x4 *win_aes,
                                                                            uint32_t epoch, uint64_t idle_ticks,
-                                                                           uint64_t lifetime_ticks)
+                                                                           uint64_t lifetime_ticks, uint64_t started_target)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[LayoutSplit::bytes];
     const uint64_t born = wall_clock64();
@@ -1569,6 +1570,13 @@ extern "C" __global__ __launch_bounds__(SPLIT_THREADS) void mi355x_resident(ResR
         if (threadIdx.x != 0)
             return;
         res_st_sys(&ring->alive, 1u);
+        /*
+         * Every worker of this instance reads its starting job (the published count) before anything new is published:
+         * a worker starting after a publication would skip that job's units.  started counts the workers of all
+         * instances; the host passes P x the instances launched.
+         */
+        while (res_ld_dev64(&ds->started) < started_target && wall_clock64() - born <= lifetime_ticks)
+            __builtin_amdgcn_s_sleep(2);
         uint64_t pub = res_ld_dev64(&ds->tail), idle_since = born;
         for (;;) {
             const uint64_t now = wall_clock64();
@@ -1625,7 +1633,12 @@ extern "C" __global__ __launch_bounds__(SPLIT_THREADS) void mi355x_resident(ResR
     /* workers */
     const uint32_t P = gridDim.x - 1u, w = blockIdx.x - 1u;
     uint32_t *ctl = (uint32_t *)lds; /* [0] state, [1] first unit, [2..33] the job (aliases the unit's LDS) */
-    uint64_t cur = res_ld_dev64(&ds->tail); /* every job published before this instance is complete */
+    uint64_t cur = 0; /* (lane 0's) the next job: every job published before this instance is complete */
+    if (threadIdx.x == 0) {
+        cur = res_ld_dev64(&ds->tail);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        atomicAdd((unsigned long long *)&ds->started, 1ull); /* (the dispatcher publishes once all have read it) */
+    }
     for (;;) {
         if (threadIdx.x == 0) {
             uint32_t state = 1u; /* 0 work, 1 idle, 2 exit */
@@ -2167,10 +2180,11 @@ static int res_launch(Resident *r)
 {
     ((volatile ResRing *)r->ring)->alive = 1u;
     ++r->epoch;
-    ++r->launches;
+    /* (the dispatcher waits for P x the instances launched so far, this one included, to have started) */
     hipLaunchKernelGGL(mi355x_resident, dim3(r->P + 1u), dim3(SPLIT_THREADS), 0, r->stream, r->ring_dev, r->ds, r->win_aes,
-                       r->epoch, r->idle_ticks, r->lifetime_ticks);
+                       r->epoch, r->idle_ticks, r->lifetime_ticks, (uint64_t)r->P * (r->launches + 1u));
     HIPCHK(hipGetLastError());
+    ++r->launches;
     return 0;
 }
 

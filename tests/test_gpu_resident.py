@@ -358,3 +358,32 @@ def test_resident_copy_job_then_runs(gpu):
     assert not got[n + 8205:].any()
     assert d_dst.cpu().numpy().tobytes() == seal_stream(eng, iv, trecs, src, wsize).tobytes()
     eng.close()
+
+
+def test_resident_many_relaunches(gpu):
+    """A 300-us idle time and jobs arriving every 0-600 us: the grid leaves and starts again dozens of times (each new
+    instance's workers read their starting job before its dispatcher publishes anything) -- every window correct."""
+    rng = np.random.default_rng(7900)
+    key, iv = rng.integers(0, 256, 16, dtype=np.uint8).tobytes(), rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    ra.resident_stop(0)
+    prev_idle = ra.set_resident_idle_us(300)
+    try:
+        eng = ra.Engine(key)
+        trecs, _, src, wsize = window(rng, [3000, 100])
+        want = seal_stream(eng, iv, trecs, src, wsize).tobytes()
+        import torch
+        d_src, d_recs = dev(src), dev(trecs.view(np.uint8))
+        d_dst = torch.zeros(wsize, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        for i in range(150):
+            d_dst.zero_()
+            torch.cuda.synchronize()
+            job = eng.resident_tls_seal_records(iv, d_recs.data_ptr(), len(trecs), d_src.data_ptr(), d_dst.data_ptr())
+            eng.resident_wait(job)
+            assert d_dst.cpu().numpy().tobytes() == want, i
+            time.sleep(float(rng.uniform(0, 0.0006)))
+        assert ra.resident_launches(0) > 10
+        eng.close()
+    finally:
+        ra.resident_stop(0)
+        ra.set_resident_idle_us(prev_idle)
