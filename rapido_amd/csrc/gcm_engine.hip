@@ -2304,7 +2304,15 @@ static int res_runs(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void *st
         ctx->split_ev_valid = false;
         const size_t cap = n < 1024 ? 1024 : n;
         HIPCHK(hipMalloc(&ctx->d_split, cap * (SPLIT_PSLOTS * sizeof(u32x4) + sizeof(uint32_t))));
-        HIPCHK(hipMemset((uint8_t *)ctx->d_split + cap * SPLIT_PSLOTS * sizeof(u32x4), 0, cap * sizeof(uint32_t)));
+        /* zero tickets before any job can use them: a blocking copy (the grid's stream is not ordered after the null
+         * stream, so an asynchronous memset there could still be running when the first units take tickets) */
+        void *zeros = calloc(cap, sizeof(uint32_t));
+        if (zeros == nullptr)
+            return fail("resident: tickets", hipErrorOutOfMemory);
+        const hipError_t ez = hipMemcpy((uint8_t *)ctx->d_split + cap * SPLIT_PSLOTS * sizeof(u32x4), zeros,
+                                        cap * sizeof(uint32_t), hipMemcpyHostToDevice);
+        free(zeros);
+        HIPCHK(ez);
         ctx->split_cap = cap;
     }
     const uint8_t *iv = (const uint8_t *)static_iv12;
