@@ -29,7 +29,7 @@
 #include <new>
 #if defined(GCM_WIN_TIMING) && GCM_WIN_TIMING
 /* measurement build (scripts/window_phases.py): stamps inside the record walk of workgroup 0, thread 0 */
-__device__ uint64_t g_win_times[16];
+__device__ uint64_t g_win_times[32];
 #ifndef GCM_STAMP_BLOCK
 #define GCM_STAMP_BLOCK 0 /* the workgroup whose phases are stamped (split kernels: 3 r + k for run k of record r) */
 #endif
@@ -45,9 +45,15 @@ __device__ uint64_t g_win_times[16];
         if (r == 0u && threadIdx.x == 0)                                                                               \
             g_win_times[i] = __builtin_amdgcn_s_memrealtime();                                                         \
     } while (0)
+/* the resident grid (scripts/resident_phases.py): worker GCM_STAMP_BLOCK's job phases (16-21), the dispatcher's
+ * last publication (22) */
+#define RES_STAMP(i) GCM_WALK_STAMP(i)
+#define RES_STAMP_ANY(i) (g_win_times[i] = __builtin_amdgcn_s_memrealtime())
 #else
 #define SPLIT_STAMP(i) ((void)0)
 #define SPLIT_STAMP_LAST(i) ((void)0)
+#define RES_STAMP(i) ((void)0)
+#define RES_STAMP_ANY(i) ((void)0)
 #endif
 #include "gcm_core.h"
 #include "../../include/ptls_mi355x.h"
@@ -1610,6 +1616,7 @@ extern "C" __global__ __launch_bounds__(SPLIT_THREADS) void mi355x_resident(ResR
                 }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 res_st_dev(&ds->tail, pub);
+                RES_STAMP_ANY(22);
                 idle_since = now;
             } else if (res_ld_dev64(&ds->nfin) < pub) {
                 idle_since = now; /* published jobs still running */
@@ -1696,6 +1703,7 @@ extern "C" __global__ __launch_bounds__(SPLIT_THREADS) void mi355x_resident(ResR
         __builtin_memcpy(&jb, jw, sizeof(jb));
         const uint32_t u0 = __builtin_amdgcn_readfirstlane(ctl[1]);
         __syncthreads(); /* ctl read by everyone: the units may overwrite it */
+        RES_STAMP(16);
         const uint32_t e = (uint32_t)(jb.id % RES_RING);
         if (threadIdx.x == 0) {
             uint32_t go = 1u;
@@ -1712,6 +1720,7 @@ extern "C" __global__ __launch_bounds__(SPLIT_THREADS) void mi355x_resident(ResR
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); /* system scope: descriptors, inputs, keys as they are now */
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            RES_STAMP(17);
             ctl[0] = go;
         }
         __syncthreads();
@@ -1721,15 +1730,18 @@ extern "C" __global__ __launch_bounds__(SPLIT_THREADS) void mi355x_resident(ResR
             atomicMax((unsigned long long *)&ds->first_c[e], ~(unsigned long long)wall_clock64());
         __syncthreads(); /* ctl[0] read by everyone before the units overwrite it */
         uint32_t mine = 0u;
+        RES_STAMP(18);
         for (uint32_t u = u0; u < jb.nunits; u += P) {
             res_unit(jb, u, lds, win_aes);
             ++mine;
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* this wave's stores */
         __syncthreads();
+        RES_STAMP(19);
         if (threadIdx.x == 0) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, ""); /* system scope: every unit's output, for the host */
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            RES_STAMP(20);
             atomicMax((unsigned long long *)&ds->last[e], (unsigned long long)wall_clock64());
             const uint32_t old = atomicAdd(&ds->done[e], mine);
             if (old + mine == jb.nunits) {
@@ -1745,6 +1757,7 @@ extern "C" __global__ __launch_bounds__(SPLIT_THREADS) void mi355x_resident(ResR
                 res_st_sys(&ring->fin[e], jb.id + 1u);
                 atomicAdd((unsigned long long *)&ds->nfin, 1ull);
             }
+            RES_STAMP(21);
         }
         __syncthreads();
     }
@@ -3216,6 +3229,6 @@ int ptls_mi355x_aes_ecb_batch(ptls_mi355x_aes_context_t *ctx, int is_enc, uint8_
 /* measurement builds: the phase stamps of the last window launch (s_memrealtime ticks, 100 MHz) */
 extern "C" int ptls_mi355x_debug_window_times(uint64_t *out)
 {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_win_times), sizeof(uint64_t) * 16) == hipSuccess ? 0 : -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_win_times), sizeof(uint64_t) * 32) == hipSuccess ? 0 : -1;
 }
 #endif
