@@ -75,7 +75,7 @@ EXPORTED_FUNCTIONS = (
     "ptls_mi355x_record_layer_open_submit", "ptls_mi355x_record_layer_wait", "ptls_mi355x_record_layer_pending",
     "ptls_mi355x_record_layer_flush", "ptls_mi355x_record_layer_set_coalesce", "ptls_mi355x_record_layer_launches",
     "ptls_mi355x_record_layer_cork",
-    "ptls_mi355x_record_layer_set_direct_dma", "ptls_mi355x_tls_deliver_records",
+    "ptls_mi355x_record_layer_set_direct_dma", "ptls_mi355x_tls_deliver_records", "ptls_mi355x_prepare_copies",
     "ptls_mi355x_resident_tls_seal_records_multi", "ptls_mi355x_resident_tls_open_records_multi",
     "ptls_mi355x_resident_tls_deliver_records", "ptls_mi355x_resident_done", "ptls_mi355x_resident_wait",
     "ptls_mi355x_resident_stop", "ptls_mi355x_resident_launches", "ptls_mi355x_set_resident_workers",
@@ -228,6 +228,7 @@ def lib() -> C.CDLL:
             L.ptls_mi355x_resident_done.argtypes = [vp, u64]
             L.ptls_mi355x_resident_wait.argtypes = [vp, u64]
             L.ptls_mi355x_resident_stop.argtypes = [C.c_int]
+            L.ptls_mi355x_prepare_copies.argtypes = []
             L.ptls_mi355x_resident_job_times.argtypes = [vp, u64, C.POINTER(u64)]
             L.ptls_mi355x_resident_jobs.argtypes = [C.c_int]
             L.ptls_mi355x_resident_jobs.restype = u64
@@ -535,6 +536,13 @@ def resident_stop(device: int = 0) -> None:
     """Waits for every posted resident job, ends the device's grid and frees its ring."""
     if lib().ptls_mi355x_resident_stop(device):
         raise RuntimeError("resident_stop failed: " + last_error())
+
+
+def prepare_copies() -> None:
+    """Has the HIP runtime set up its copy machinery on the current device now rather than inside a later window
+    (include/ptls_mi355x.h; record layers call it before their first copy)."""
+    if lib().ptls_mi355x_prepare_copies():
+        raise RuntimeError("prepare_copies failed: " + last_error())
 
 
 def resident_launches(device: int = 0) -> int:

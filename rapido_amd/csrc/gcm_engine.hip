@@ -1802,6 +1802,7 @@ struct DeviceShared {
     uint8_t *h_stage_dev = nullptr; /* h_stage as the GPU addresses it */
     size_t cap = 0;
     u32x4 *d_win_aes = nullptr;     /* the 64 KiB AES image of the 16-lane window kernels (mi355x_win_aes_image) */
+    bool copies_ready = false;      /* ptls_mi355x_prepare_copies done */
 };
 
 struct st_ptls_mi355x_aesgcm_context {
@@ -1941,6 +1942,66 @@ static DeviceShared *device_shared(int dev)
         g_shared[dev] = d;
     }
     return g_shared[dev];
+}
+
+/* a kernel between the copies of ptls_mi355x_prepare_copies (it only has to run) */
+__global__ void mi355x_copy_warm(uint32_t *p) { p[threadIdx.x] = threadIdx.x; }
+
+/*
+ * The HIP runtime sets up parts of its copy machinery on first need, inside the hipMemcpyAsync call that needs it:
+ * the first host <-> device copy of 64 KiB or more, and the first time four streams each have a copy and a kernel in
+ * flight at once, stalled that call 8-30 ms (scripts/probe_h2d.c).  A record layer moving windows by DMA hit these
+ * mid-stream, at whatever window first grew its groups or its copies in flight that far -- a timed stream of 64
+ * coalesced windows then ran at 1-2 GiB/s instead of 21.  This pays them once per process and
+ * device, up front: two rounds of [256 KiB H2D, kernel, 256 KiB D2H] on four streams at once.
+ */
+int ptls_mi355x_prepare_copies(void)
+{
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    DeviceShared *d = device_shared(dev);
+    if (d == nullptr)
+        return -1;
+    std::lock_guard<std::mutex> lk(d->mu);
+    if (d->copies_ready)
+        return 0;
+    const size_t n = 256u << 10;
+    uint8_t *h = nullptr, *dv = nullptr;
+    hipStream_t st[4] = {};
+    hipError_t e = hipHostMalloc((void **)&h, 4 * n, hipHostMallocDefault);
+    if (e == hipSuccess)
+        e = hipMalloc((void **)&dv, 4 * n);
+    for (int i = 0; i < 4 && e == hipSuccess; ++i)
+        e = hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking);
+    if (e == hipSuccess)
+        memset(h, 0, 4 * n);
+    for (int round = 0; round < 2 && e == hipSuccess; ++round) {
+        for (int i = 0; i < 4 && e == hipSuccess; ++i) {
+            e = hipMemcpyAsync(dv + i * n, h + i * n, n, hipMemcpyHostToDevice, st[i]);
+            if (e == hipSuccess) {
+                hipLaunchKernelGGL(mi355x_copy_warm, dim3(1), dim3(64), 0, st[i], (uint32_t *)(dv + i * n));
+                e = hipGetLastError();
+            }
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(h + i * n, dv + i * n, n, hipMemcpyDeviceToHost, st[i]);
+        }
+        for (int i = 0; i < 4; ++i)
+            if (st[i] != nullptr) {
+                const hipError_t es = hipStreamSynchronize(st[i]);
+                e = e == hipSuccess ? es : e;
+            }
+    }
+    for (int i = 0; i < 4; ++i)
+        if (st[i] != nullptr)
+            (void)hipStreamDestroy(st[i]);
+    if (dv != nullptr)
+        (void)hipFree(dv);
+    if (h != nullptr)
+        (void)hipHostFree(h);
+    if (e != hipSuccess)
+        return fail("prepare copies", e);
+    d->copies_ready = true;
+    return 0;
 }
 
 /* grows the shared staging to `need` bytes (caller holds d->mu) */
@@ -2288,6 +2349,19 @@ static int res_ctx_wait(ptls_mi355x_aesgcm_context_t *ctx, uint64_t id1)
     return r == nullptr ? -1 : res_wait(r, id1 - 1u);
 }
 
+/*
+ * Records the split buffer (partials + tickets, 84 B a record) holds when it must hold n: at least 4096 (344 KiB), else
+ * the next power of two.  Growing it frees the old buffer, which synchronises the whole device -- a coalescing record
+ * layer whose groups grow mid-stream (1, 2, 4 ... windows a launch) stalled ~8 ms at every growth.
+ */
+static size_t split_cap_for(size_t n)
+{
+    size_t cap = 4096;
+    while (cap < n)
+        cap *= 2;
+    return cap;
+}
+
 /* a run job (records x SPLIT_MAXRUN units) of a TLS window */
 static int res_runs(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void *static_iv12, const void *recs,
                     const uint32_t *conn, size_t n, const uint8_t *src, uint8_t *dst, uint32_t *status, uint8_t *types,
@@ -2315,7 +2389,7 @@ static int res_runs(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void *st
         ctx->d_split = nullptr;
         ctx->split_cap = 0;
         ctx->split_ev_valid = false;
-        const size_t cap = n < 1024 ? 1024 : n;
+        const size_t cap = split_cap_for(n);
         HIPCHK(hipMalloc(&ctx->d_split, cap * (SPLIT_PSLOTS * sizeof(u32x4) + sizeof(uint32_t))));
         /* zero tickets before any job can use them: a blocking copy (the grid's stream is not ordered after the null
          * stream, so an asynchronous memset there could still be running when the first units take tickets) */
@@ -2415,7 +2489,7 @@ static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void
             ctx->d_split = nullptr;
             ctx->split_cap = 0;
             ctx->split_ev_valid = false;
-            const size_t cap = n < 64 ? 64 : n;
+            const size_t cap = split_cap_for(n);
             HIPCHK(hipMalloc(&ctx->d_split, cap * (SPLIT_PSLOTS * sizeof(u32x4) + sizeof(uint32_t))));
             HIPCHK(hipMemsetAsync((uint8_t *)ctx->d_split + cap * SPLIT_PSLOTS * sizeof(u32x4), 0, cap * sizeof(uint32_t),
                                   stream));
@@ -2479,6 +2553,7 @@ static int ensure_scratch(ptls_mi355x_aesgcm_context_t *ctx, size_t need, hipStr
         (void)hipFree(ctx->d_scratch);
     }
     ctx->d_scratch = nullptr;
+    need = need < 2 * ctx->scratch_cap ? 2 * ctx->scratch_cap : need; /* (doubling: few growths, each a sync) */
     ctx->scratch_cap = 0;
     HIPCHK(hipMalloc(&ctx->d_scratch, need));
     ctx->scratch_cap = need;

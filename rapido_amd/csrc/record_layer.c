@@ -119,6 +119,9 @@ typedef struct {
     size_t d_cap;
     ptls_mi355x_tls_record_t *recs; /* host descriptors */
     size_t recs_cap;
+    size_t grow; /* a coalesced op of n windows: its staging grows to this many times its need (cap / n), so a later,
+                  * larger group of the same windows finds room (no allocation, and no stall, mid-stream) */
+    int copies_prepared; /* ptls_mi355x_prepare_copies called for its first copy */
     rl_op_t op;
 } rl_slot_t;
 
@@ -205,11 +208,23 @@ static int reserve_recs(rl_slot_t *s, size_t nrecs)
     return 0;
 }
 
+/* PTLS_MI355X_RL_TRACE set: every allocation a window triggers (staging growth, slot creation) to stderr, with its
+ * slot -- they synchronise or stall, and belong at setup rather than mid-stream */
+static int rl_trace_on(void)
+{
+    static int on = -1;
+    if (on < 0)
+        on = getenv("PTLS_MI355X_RL_TRACE") != NULL;
+    return on;
+}
+
 static int reserve_stage(rl_slot_t *s, size_t bytes)
 {
     if (bytes <= s->cap)
         return 0;
     size_t c = s->cap ? s->cap : 1 << 16;
+    if (s->grow > 1)
+        bytes *= s->grow;
     while (c < bytes)
         c *= 2;
     hipError_t e;
@@ -225,6 +240,8 @@ static int reserve_stage(rl_slot_t *s, size_t bytes)
     if ((e = hipHostGetDevicePointer((void **)&s->h_dev, s->h_buf, 0)) != hipSuccess)
         return rl_fail("hipHostGetDevicePointer", e);
     s->cap = c;
+    if (rl_trace_on())
+        fprintf(stderr, "record layer: slot %p staging grown to %zu B\n", (void *)s, c);
     return 0;
 }
 
@@ -242,6 +259,8 @@ static int reserve_device(rl_slot_t *s)
     if ((e = hipMalloc((void **)&s->d_buf, s->cap)) != hipSuccess)
         return rl_fail("hipMalloc", e);
     s->d_cap = s->cap;
+    if (rl_trace_on())
+        fprintf(stderr, "record layer: slot %p device buffer grown to %zu B\n", (void *)s, s->cap);
     return 0;
 }
 
@@ -249,6 +268,8 @@ static int reserve_device(rl_slot_t *s)
 static int slot_ready(ptls_mi355x_record_layer_t *rl, rl_slot_t *s)
 {
     hipError_t e;
+    if (rl_trace_on() && (s->stream == NULL || s->ctx == NULL))
+        fprintf(stderr, "record layer: slot %p created\n", (void *)s);
     if (s->stream == NULL && (e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)) != hipSuccess) {
         s->stream = NULL;
         return rl_fail("hipStreamCreateWithFlags", e);
@@ -653,6 +674,12 @@ static int op_launch(rl_slot_t *s, const uint8_t *src_base, uint8_t *dst_base)
                                                           (const ptls_mi355x_tls_deliver_t *)(base + op->off_dp),
                                                           op->nlayers, op->max_part, &op->rjob);
         return rc != 0 ? rl_msg(ptls_mi355x_last_error()) : 0;
+    }
+    /* the runtime's one-time copy setup, before the first copy rather than inside some later window's */
+    if ((!op->zero_copy || op->nh2d != 0 || op->nd2h != 0) && !s->copies_prepared) {
+        if (ptls_mi355x_prepare_copies() != 0)
+            return rl_msg(ptls_mi355x_last_error());
+        s->copies_prepared = 1;
     }
     if (!op->zero_copy &&
         (e = hipMemcpyAsync(s->d_buf, s->h_buf, op->dma ? op->off_src : op->off_src + op->srcbytes, hipMemcpyHostToDevice,
@@ -1095,6 +1122,8 @@ static int rl_flush_n(ptls_mi355x_record_layer_t *rl, size_t n)
     rl_slot_t *s = op_begin(layers, n, is_seal);
     int rc = -1;
     if (s != NULL) {
+        const size_t cap = rl->coalesce > 1 ? rl->coalesce : 1;
+        s->grow = (cap + n - 1) / n;
         if (is_seal) {
             const uint64_t keep = rl->seq;
             rl->seq = rl->queue[0].seq0;
@@ -1106,6 +1135,7 @@ static int rl_flush_n(ptls_mi355x_record_layer_t *rl, size_t n)
             rc = open_build(s, layers, n, in, inlen, out, capacity, parsed, 0, 0);
             rl->spec_seq = keep;
         }
+        s->grow = 0;
     }
     for (size_t i = 0; i < n; ++i) /* the launched windows leave the queue */
         free(rl->queue[i].frags);

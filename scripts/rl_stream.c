@@ -110,13 +110,20 @@ static double pass(stream_t *st, int seal, size_t depth, size_t max_inflight_see
         ptls_mi355x_record_layer_set_seq(st->rxs[c], 0);
     }
     const double t0 = now();
+    /* RL_TRACE=<us>: every wait or submit over that many microseconds (default 1000), to stderr */
+    const double trace = getenv("RL_TRACE") != NULL ? (atof(getenv("RL_TRACE")) > 0 ? atof(getenv("RL_TRACE")) : 1000) * 1e-6 : 0;
     for (size_t w = 0; w < st->nwin + depth; ++w) {
         if (tail - head == depth || (w >= st->nwin && tail != head)) {
             size_t outlen[MAXM], nrec[MAXM], cons[MAXM];
             int alert[MAXM];
+            const double tw = now();
             if (ptls_mi355x_record_layer_wait(st->multi > 1 ? (seal ? st->txs[0] : st->rxs[0]) : rl, tickets[head % 64], outlen,
                                               nrec, cons, alert) != 0)
                 die("wait");
+            if (trace > 0 && now() - tw > trace)
+                fprintf(stderr, "rl_stream: %s wait for window %zu took %.3f ms (launches %llu)\n", seal ? "seal" : "open",
+                        (size_t)head, (now() - tw) * 1e3,
+                        (unsigned long long)ptls_mi355x_record_layer_launches(rl));
             for (size_t c = 0; c < (st->multi > 1 ? st->multi : 1); ++c)
                 if (nrec[c] != WIN || alert[c] != 0 || outlen[c] != (seal ? (size_t)WIRE_WIN : (size_t)WIN * FRAG)) {
                     fprintf(stderr, "rl_stream: window %zu: %zu records, %zu bytes, alert %d\n", (size_t)head, nrec[c],
@@ -149,15 +156,21 @@ static double pass(stream_t *st, int seal, size_t depth, size_t max_inflight_see
             const ptls_mi355x_iovec_t *f = st->frags[w];
             const size_t nf = WIN, cap = WIRE_WIN;
             void *out = st->wire + w * WIRE_WIN;
+            const double ts = now();
             if (ptls_mi355x_record_layer_seal_submit(&st->tx, 1, &f, &nf, 23, &out, &cap, &tickets[tail % 64]) != 0)
                 die("seal_submit");
+            if (trace > 0 && now() - ts > trace)
+                fprintf(stderr, "rl_stream: seal submit of window %zu took %.3f ms\n", w, (now() - ts) * 1e3);
         } else {
             const void *in = st->wire + w * WIRE_WIN;
             const size_t inlen = WIRE_WIN, cap = PT_WIN;
             void *out = st->pt + w * PT_WIN;
             size_t parsed;
+            const double ts = now();
             if (ptls_mi355x_record_layer_open_submit(&st->rx, 1, &in, &inlen, &out, &cap, &parsed, &tickets[tail % 64]) != 0)
                 die("open_submit");
+            if (trace > 0 && now() - ts > trace)
+                fprintf(stderr, "rl_stream: open submit of window %zu took %.3f ms\n", w, (now() - ts) * 1e3);
         }
         ++tail;
         if (tail - head > max_inflight_seen[0])

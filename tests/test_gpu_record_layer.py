@@ -295,3 +295,18 @@ def test_open_multi_session_windows(family, transport):
     assert got[3] == (0, b"".join(frags[3][:4]), whole4, 4) and layers[3].seq == 2 ** 33 + 4
     for lr in layers:
         lr.close()
+
+
+def test_prepare_copies_then_copy_windows(gpu):
+    """ptls_mi355x_prepare_copies is idempotent, and the copy windows after it are the oracle's (it only warms the
+    runtime: DESIGN.md section 2, coalesced DMA streams)."""
+    ra.prepare_copies()
+    ra.prepare_copies()
+    rng = np.random.default_rng(7)
+    key = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+    iv = rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    frags = [rng.integers(0, 256, 16384, dtype=np.uint8).tobytes() for _ in range(8)]
+    rl = layer("copy", key, iv)
+    wire, n = rl.seal(frags)
+    assert (wire, n) == (oracle_window(key, iv, 0, frags)[0], 8)
+    rl.close()
