@@ -457,8 +457,8 @@ int ptls_mi355x_record_layer_unregister(ptls_mi355x_record_layer_t *rl, void *ba
 #define PTLS_MI355X_RECORD_LAYER_DMA_IN 2
 int ptls_mi355x_record_layer_set_direct_dma(ptls_mi355x_record_layer_t *rl, int on);
 /* Once per process and device (the current one): has the HIP runtime set up its copy machinery now -- its first
- * copy of 64 KiB or more and its first copies on four streams at once each stalled that copy 8-30 ms -- instead of
- * inside a later window.  A record layer calls it before its first copy (DMA transports and
+ * copy of 64 KiB or more, its first copies on four streams at once and each new high of copies in flight stalled
+ * that copy 8-30 ms -- instead of inside a later window.  A record layer calls it before its first copy (DMA transports and
  * staged copy windows); a caller may call it at startup.  0, or -1 (ptls_mi355x_last_error). */
 int ptls_mi355x_prepare_copies(void);
 /*

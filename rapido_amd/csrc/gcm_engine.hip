@@ -1949,11 +1949,13 @@ __global__ void mi355x_copy_warm(uint32_t *p) { p[threadIdx.x] = threadIdx.x; }
 
 /*
  * The HIP runtime sets up parts of its copy machinery on first need, inside the hipMemcpyAsync call that needs it:
- * the first host <-> device copy of 64 KiB or more, and the first time four streams each have a copy and a kernel in
- * flight at once, stalled that call 8-30 ms (scripts/probe_h2d.c).  A record layer moving windows by DMA hit these
- * mid-stream, at whatever window first grew its groups or its copies in flight that far -- a timed stream of 64
- * coalesced windows then ran at 1-2 GiB/s instead of 21.  This pays them once per process and
- * device, up front: two rounds of [256 KiB H2D, kernel, 256 KiB D2H] on four streams at once.
+ * the first host <-> device copy of 64 KiB or more, the first time four streams each have a copy and a kernel in
+ * flight, and again whenever more copies are in flight than ever before (8 per stream) -- each stalled that call
+ * 8-30 ms (scripts/probe_h2d.c).  A record layer moving windows by DMA hit these mid-stream, at whatever window first
+ * grew its groups or its copies in flight that far: a timed stream of 64 coalesced windows then ran at 1-2 GiB/s
+ * instead of 21.  This pays them once per process and device, up front: [64 KiB H2D, kernel,
+ * 64 KiB D2H] x depth on four streams at once, depth 1, 4, 16 and 64 (768 copies in flight at the last), synchronised
+ * after each depth.
  */
 int ptls_mi355x_prepare_copies(void)
 {
@@ -1965,7 +1967,7 @@ int ptls_mi355x_prepare_copies(void)
     std::lock_guard<std::mutex> lk(d->mu);
     if (d->copies_ready)
         return 0;
-    const size_t n = 256u << 10;
+    const size_t n = 64u << 10;
     uint8_t *h = nullptr, *dv = nullptr;
     hipStream_t st[4] = {};
     hipError_t e = hipHostMalloc((void **)&h, 4 * n, hipHostMallocDefault);
@@ -1975,16 +1977,17 @@ int ptls_mi355x_prepare_copies(void)
         e = hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking);
     if (e == hipSuccess)
         memset(h, 0, 4 * n);
-    for (int round = 0; round < 2 && e == hipSuccess; ++round) {
-        for (int i = 0; i < 4 && e == hipSuccess; ++i) {
-            e = hipMemcpyAsync(dv + i * n, h + i * n, n, hipMemcpyHostToDevice, st[i]);
-            if (e == hipSuccess) {
-                hipLaunchKernelGGL(mi355x_copy_warm, dim3(1), dim3(64), 0, st[i], (uint32_t *)(dv + i * n));
-                e = hipGetLastError();
+    for (int depth = 1; depth <= 64 && e == hipSuccess; depth *= 4) {
+        for (int k = 0; k < depth && e == hipSuccess; ++k)
+            for (int i = 0; i < 4 && e == hipSuccess; ++i) { /* (one stream's copies are ordered: one buffer each) */
+                e = hipMemcpyAsync(dv + i * n, h + i * n, n, hipMemcpyHostToDevice, st[i]);
+                if (e == hipSuccess) {
+                    hipLaunchKernelGGL(mi355x_copy_warm, dim3(1), dim3(64), 0, st[i], (uint32_t *)(dv + i * n));
+                    e = hipGetLastError();
+                }
+                if (e == hipSuccess)
+                    e = hipMemcpyAsync(h + i * n, dv + i * n, n, hipMemcpyDeviceToHost, st[i]);
             }
-            if (e == hipSuccess)
-                e = hipMemcpyAsync(h + i * n, dv + i * n, n, hipMemcpyDeviceToHost, st[i]);
-        }
         for (int i = 0; i < 4; ++i)
             if (st[i] != nullptr) {
                 const hipError_t es = hipStreamSynchronize(st[i]);

@@ -48,6 +48,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include <stdio.h>
 #include <hip/hip_runtime_api.h>
 #include "../../include/ptls_mi355x.h"
@@ -216,6 +217,21 @@ static int rl_trace_on(void)
     if (on < 0)
         on = getenv("PTLS_MI355X_RL_TRACE") != NULL;
     return on;
+}
+
+static double rl_now(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec + t.tv_nsec * 1e-9;
+}
+
+/* traced: a call of op_launch that took over 1 ms */
+static void rl_slow(const char *what, double t0)
+{
+    const double dt = rl_now() - t0;
+    if (dt > 1e-3)
+        fprintf(stderr, "record layer: %s took %.3f ms\n", what, dt * 1e3);
 }
 
 static int reserve_stage(rl_slot_t *s, size_t bytes)
@@ -681,13 +697,22 @@ static int op_launch(rl_slot_t *s, const uint8_t *src_base, uint8_t *dst_base)
             return rl_msg(ptls_mi355x_last_error());
         s->copies_prepared = 1;
     }
+    const int tr = rl_trace_on();
+    double t0 = tr ? rl_now() : 0;
     if (!op->zero_copy &&
         (e = hipMemcpyAsync(s->d_buf, s->h_buf, op->dma ? op->off_src : op->off_src + op->srcbytes, hipMemcpyHostToDevice,
                             s->stream)) != hipSuccess)
         return rl_fail("H2D", e);
-    for (size_t i = 0; i < op->nh2d; ++i)
+    if (tr)
+        rl_slow("the staging H2D", t0);
+    for (size_t i = 0; i < op->nh2d; ++i) {
+        t0 = tr ? rl_now() : 0;
         if ((e = hipMemcpyAsync(op->h2d[i].dst, op->h2d[i].src, op->h2d[i].n, hipMemcpyHostToDevice, s->stream)) != hipSuccess)
             return rl_fail("H2D", e);
+        if (tr)
+            rl_slow("an input H2D", t0);
+    }
+    t0 = tr ? rl_now() : 0;
     if (op->is_seal)
         rc = ptls_mi355x_tls_seal_records_multi(s->ctx, op->layers[0]->iv, (const ptls_mi355x_tls_record_t *)base, conn,
                                                 op->nrec, src, dst, s->stream);
@@ -701,9 +726,16 @@ static int op_launch(rl_slot_t *s, const uint8_t *src_base, uint8_t *dst_base)
                                              op->nlayers, op->max_part, s->stream);
     if (rc != 0)
         return rl_msg(ptls_mi355x_last_error());
-    for (size_t i = 0; i < op->nd2h; ++i)
+    if (tr)
+        rl_slow("the launch", t0);
+    for (size_t i = 0; i < op->nd2h; ++i) {
+        t0 = tr ? rl_now() : 0;
         if ((e = hipMemcpyAsync(op->d2h[i].dst, op->d2h[i].src, op->d2h[i].n, hipMemcpyDeviceToHost, s->stream)) != hipSuccess)
             return rl_fail("D2H", e);
+        if (tr)
+            rl_slow("an output D2H", t0);
+    }
+    t0 = tr ? rl_now() : 0;
     if (!op->zero_copy && !(op->dma && op->is_seal)) {
         const size_t from = op->dma ? op->off_st : op->off_dst;
         const size_t to = op->is_seal ? op->off_dst + op->dstbytes : op->off_ty + op->nrec;
@@ -711,6 +743,8 @@ static int op_launch(rl_slot_t *s, const uint8_t *src_base, uint8_t *dst_base)
             (e = hipMemcpyAsync(s->h_buf + from, s->d_buf + from, to - from, hipMemcpyDeviceToHost, s->stream)) != hipSuccess)
             return rl_fail("D2H", e);
     }
+    if (tr)
+        rl_slow("the staging D2H", t0);
     return 0;
 }
 

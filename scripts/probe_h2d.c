@@ -85,6 +85,32 @@ int main(void)
                 printf("range %d d2h %9zu B: call %8.3f ms\n", r, n, (t1 - t0) * 1e3);
         }
     }
+    /* a range written by D2H first, then read by H2D (a sealed wire buffer, opened next) */
+    for (int r = 0; r < 2; ++r) {
+        void *h3 = NULL;
+        if (posix_memalign(&h3, 4096, 16u << 20) != 0)
+            return 1;
+        for (size_t i = 0; i < (16u << 20); i += 4096)
+            ((char *)h3)[i] = (char)i;
+        CHK(hipHostRegister(h3, 16u << 20, hipHostRegisterMapped));
+        for (int dir = 0; dir < 2; ++dir)
+            for (size_t n = 4096; n <= (16u << 20); n *= 4) {
+                const double t0 = now();
+                CHK(dir == 0 ? hipMemcpyAsync(h3, dev, n, hipMemcpyDeviceToHost, st[r])
+                             : hipMemcpyAsync(dev, h3, n, hipMemcpyHostToDevice, st[r]));
+                const double t1 = now();
+                CHK(hipStreamSynchronize(st[r]));
+                if (t1 - t0 > 1e-3)
+                    printf("d2h-first range %d %s %9zu B: call %8.3f ms\n", r, dir ? "h2d" : "d2h", n, (t1 - t0) * 1e3);
+            }
+        /* and with a kernel in flight on another stream */
+        hipLaunchKernelGGL(touch, dim3(1), dim3(64), 0, st[3], (unsigned *)dev);
+        const double t0 = now();
+        CHK(hipMemcpyAsync(dev, (char *)h3 + (8u << 20), 1u << 20, hipMemcpyHostToDevice, st[r]));
+        if (now() - t0 > 1e-3)
+            printf("range %d h2d beside a kernel: %.3f ms\n", r, (now() - t0) * 1e3);
+        CHK(hipDeviceSynchronize());
+    }
     /* copies and kernels interleaved on the four streams, more in flight each time */
     for (int d = 1; d <= 64; d *= 2) {
         const double t0 = now();
