@@ -569,8 +569,6 @@ def record_layer_stream(key_bytes: int = 16, nwin: int = 64, depth: int = 4, tra
     # one window per submit with more windows outstanding: the layer coalesces its queued windows (round 4)
     res["one_window_per_submit_coalesced"] = {f"depth_{d}": run(transport, 1, d=d) for d in (16, 32)}
     res["inputs_read_in_place"] = run("direct", per_launch[0])
-    # one window per submit as jobs of the resident grid (round 4, include/ptls_mi355x.h section 6): no launch, no copy
-    res["one_window_per_submit_resident"] = {f"depth_{d}": run("resident", 1, d=d) for d in (1, 4)}
     res["note"] = (f"{nwin} back-to-back windows of 16 x 16384 B records, AES-{8 * key_bytes}, host memory to host "
                    f"memory (registered buffers, {transport}), {per_launch[0]} connections' windows per launch, {depth} "
                    "launches in flight (record_layer_seal_submit / open_submit + wait), C driver scripts/rl_stream.c; "
@@ -578,10 +576,7 @@ def record_layer_stream(key_bytes: int = 16, nwin: int = 64, depth: int = 4, tra
                    "connection per launch; one_window_per_launch: a single connection's windows, one per submit, 4 "
                    "outstanding (four single-window launches); one_window_per_submit_coalesced: one per submit with 16 / 32 "
                    "outstanding, coalesced by the layer into ceil(outstanding / 4)-window launches; "
-                   "inputs_read_in_place: transport direct (kernels read the inputs over PCIe); "
-                   "one_window_per_submit_resident: one window per submit, 1 / 4 outstanding, each window's runs (and an "
-                   "open's delivery) posted as jobs of the device's persistent grid, registered buffers read and written "
-                   "in place")
+                   "inputs_read_in_place: transport direct (kernels read the inputs over PCIe)")
     return res
 
 

@@ -122,7 +122,15 @@ typedef struct st_ptls_mi355x_aesgcm_context ptls_mi355x_aesgcm_context_t;
 
 /* capacity is accepted for API parity (lib/fusion.c:775); tables do not depend on it. */
 ptls_mi355x_aesgcm_context_t *ptls_mi355x_aesgcm_new(const void *key, size_t key_size, size_t capacity);
+/* waits for the context's launches (any stream), clears the key image and frees it (ptls_fusion_aesgcm_free,
+ * lib/fusion.c:814-820).  An error met there -- an asynchronous fault of earlier GPU work surfaces at the
+ * synchronisation -- is printed and reported by the next ptls_mi355x_device_check. */
 void ptls_mi355x_aesgcm_free(ptls_mi355x_aesgcm_context_t *ctx);
+/* the same, returning 0, or -1 with the first error in ptls_mi355x_last_error (the context is freed either way) */
+int ptls_mi355x_aesgcm_release(ptls_mi355x_aesgcm_context_t *ctx);
+/* diagnostics: synchronises the current device; 0, or -1 with ptls_mi355x_last_error naming the first error seen
+ * since the previous check -- a fault of queued work, or one a free path met (which return nothing) */
+int ptls_mi355x_device_check(void);
 /* HIP device ordinal the context lives on */
 int ptls_mi355x_aesgcm_device(const ptls_mi355x_aesgcm_context_t *ctx);
 
@@ -441,9 +449,11 @@ const char *ptls_mi355x_record_layer_last_error(void);
  * output) is copied into the layer's pinned, mapped staging, which the kernel reads and writes over PCIe (one
  * launch, one synchronisation); larger windows move by one H2D and one D2H DMA copy.  Results are identical. */
 /* registers host memory [base, base+len) that stays allocated (a connection's socket buffers) for direct calls
- * (hipHostRegister, mapped); up to 8 ranges per layer.  A range that is already registered (by the application, or
- * by the layer of the other direction sharing a buffer) is used as it is and left registered on unregister; it must
- * stay registered while this layer uses it.  0, or -1 (ptls_mi355x_record_layer_last_error). */
+ * (hipHostRegister, mapped); up to 8 ranges per layer.  Layers share registrations process-wide: a range another
+ * layer registered (the other direction of the connection sharing a buffer) is counted, and unmapped only when the
+ * last layer holding it unregisters it or is freed.  A range the application registered itself is used as it is and
+ * never unregistered here; it must stay registered while a layer uses it.  0, or -1
+ * (ptls_mi355x_record_layer_last_error). */
 int ptls_mi355x_record_layer_register(ptls_mi355x_record_layer_t *rl, void *base, size_t len);
 /* unregisters a range given to ptls_mi355x_record_layer_register (by its base); 0 or -1.  The layer unregisters
  * its ranges when freed. */
@@ -461,82 +471,8 @@ int ptls_mi355x_record_layer_set_direct_dma(ptls_mi355x_record_layer_t *rl, int 
  * that copy 8-30 ms -- instead of inside a later window.  A record layer calls it before its first copy (DMA transports and
  * staged copy windows); a caller may call it at startup.  0, or -1 (ptls_mi355x_last_error). */
 int ptls_mi355x_prepare_copies(void);
-/*
- * on != 0: the layer's windows that need no copy -- registered buffers read and written in place (the DMA settings
- * above are then ignored), or zero-copy staging -- run as jobs of the device's resident grid (section 6) instead of
- * kernel launches: a submit posts the window's runs (and an open's delivery) into the grid's ring, a wait polls its
- * completion word.  For a caller that submits one window at a time.  Results are identical.  Returns the previous
- * value.
- */
-int ptls_mi355x_record_layer_set_resident(ptls_mi355x_record_layer_t *rl, int on);
 /* zero-copy limit in bytes (default 4 MiB; 0 = always DMA copies); returns the previous value */
 size_t ptls_mi355x_record_layer_set_zero_copy_bytes(ptls_mi355x_record_layer_t *rl, size_t n);
-
-/* ---- 6. resident window engine (csrc/gcm_engine.hip mi355x_resident) ----
- *
- * The same window kernels (the split runs of section 4's small framing batches, and the delivery kernel) executed
- * by ONE persistent grid per device that takes jobs from a ring in pinned host memory: a window costs the host a
- * few stores into that ring and a poll of a completion word, not a kernel launch and a stream synchronisation.
- * For callers that submit windows one at a time (rapido: one send window per connection, lib/rapido.c:2115-2126).
- * The grid (1 + ptls_mi355x_set_resident_workers() workgroups, each holding a CU's whole LDS) starts with the first
- * job and leaves after ptls_mi355x_set_resident_idle_us() without work; a job posted later starts it again.  While
- * it runs, hipDeviceSynchronize() and the batch kernels (which want every CU) wait for it to leave.
- *
- * Pointers as in section 4 (device memory, or host memory the GPU addresses: mapped pinned buffers); the buffers
- * must stay valid until the job is complete.  Results are bit-identical to the stream calls.  A context's run jobs
- * execute one at a time (a new one waits for the previous one: they share its split buffer); a delivery job follows
- * the context's previous job (its open), and a run job the context's previous copy job (its input, below).  *job
- * receives the job number (PTLS_MI355X_RESIDENT_NONE for n = 0, always
- * complete).  Returns 0, or -1 (ptls_mi355x_last_error). */
-#define PTLS_MI355X_RESIDENT_NONE (~(uint64_t)0)
-int ptls_mi355x_resident_tls_seal_records_multi(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12,
-                                                const ptls_mi355x_tls_record_t *recs, const uint32_t *conn_ids, size_t n,
-                                                const uint8_t *src, uint8_t *dst, uint64_t *job);
-int ptls_mi355x_resident_tls_open_records_multi(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12,
-                                                const ptls_mi355x_tls_record_t *recs, const uint32_t *conn_ids, size_t n,
-                                                const uint8_t *src, uint8_t *dst, uint32_t *status, uint8_t *types,
-                                                uint64_t *job);
-int ptls_mi355x_resident_tls_deliver_records(ptls_mi355x_aesgcm_context_t *ctx, const ptls_mi355x_tls_record_t *recs,
-                                             const uint32_t *status, const uint8_t *types,
-                                             const ptls_mi355x_tls_deliver_t *parts, size_t nparts, size_t max_records,
-                                             uint64_t *job);
-/*
- * A copy job: n (at most PTLS_MI355X_RESIDENT_COPY_MAX) ranges, each n bytes from src to dst (GPU addresses: device
- * memory, or mapped host memory), copied by the grid's workers in 8 KiB chunks -- a window's input staged into device
- * memory by the grid itself, with no hipMemcpy call.  The context's next run job follows it.  `ranges` is read
- * during the call only.
- */
-#define PTLS_MI355X_RESIDENT_COPY_MAX 64
-typedef struct st_ptls_mi355x_copy_t {
-    void *dst;
-    const void *src;
-    uint64_t n;
-} ptls_mi355x_copy_t;
-int ptls_mi355x_resident_copy(ptls_mi355x_aesgcm_context_t *ctx, const ptls_mi355x_copy_t *ranges, size_t n,
-                              uint64_t *job);
-/* on != 0: the single-record calls (section 2, and through them the AEAD slot objects of section 1) run as jobs of
- * the resident grid instead of a launch and a stream synchronisation each (records up to the slot zero-copy limit).
- * Results are identical.  Returns the previous value (initially PTLS_MI355X_SLOT_RESIDENT from the environment, else
- * 0). */
-int ptls_mi355x_set_slot_resident(int on);
-/* 1 when the job is complete (its outputs visible to the host), 0 while it runs, -1 on error */
-int ptls_mi355x_resident_done(ptls_mi355x_aesgcm_context_t *ctx, uint64_t job);
-/* waits for the job (polling its completion word; restarts the grid if it left before seeing the job) */
-int ptls_mi355x_resident_wait(ptls_mi355x_aesgcm_context_t *ctx, uint64_t job);
-/* waits for every posted job, ends the device's grid and frees its ring (the next job creates them again) */
-int ptls_mi355x_resident_stop(int device);
-/* the job's timeline on the GPU's constant clock, in ns: ns[0] from its publication to its first unit's start,
- * ns[1] from there to its last unit's end, ns[2] from there to its completion, ns[3] publication to completion;
- * -1 if the job is not complete or its ring entry holds a later job by now */
-int ptls_mi355x_resident_job_times(ptls_mi355x_aesgcm_context_t *ctx, uint64_t job, uint64_t ns[4]);
-/* jobs posted on the device so far: the next job's number (job numbers go on across ptls_mi355x_resident_stop) */
-uint64_t ptls_mi355x_resident_jobs(int device);
-/* launches of the device's grid so far (each start after an idle exit is one) */
-uint64_t ptls_mi355x_resident_launches(int device);
-/* workers of grids created after the call (SIZE_MAX, the default: half the CUs); returns the previous value */
-size_t ptls_mi355x_set_resident_workers(size_t n);
-/* idle time after which a grid created after the call leaves (default 2000 us); returns the previous value */
-uint64_t ptls_mi355x_set_resident_idle_us(uint64_t us);
 
 /* ---- tuning / introspection ---- */
 /* lanes per record used by the batch kernels (1, 2, 4 or 8; default 4); returns the previous value, or -1 */

@@ -54,7 +54,8 @@ OPEN_STOP_AT_FAILURE = 1
 
 #: every symbol include/ptls_mi355x.h declares
 EXPORTED_FUNCTIONS = (
-    "ptls_mi355x_is_supported", "ptls_mi355x_aesgcm_new", "ptls_mi355x_aesgcm_free", "ptls_mi355x_aesgcm_device",
+    "ptls_mi355x_is_supported", "ptls_mi355x_aesgcm_new", "ptls_mi355x_aesgcm_free", "ptls_mi355x_aesgcm_release",
+    "ptls_mi355x_device_check", "ptls_mi355x_aesgcm_device",
     "ptls_mi355x_aesgcm_encrypt", "ptls_mi355x_aesgcm_decrypt", "ptls_mi355x_aesecb_encrypt",
     "ptls_mi355x_seal_batch", "ptls_mi355x_open_batch", "ptls_mi355x_order_by_length",
     "ptls_mi355x_seal_batch_ordered", "ptls_mi355x_open_batch_ordered", "ptls_mi355x_set_lanes_per_record",
@@ -76,13 +77,7 @@ EXPORTED_FUNCTIONS = (
     "ptls_mi355x_record_layer_flush", "ptls_mi355x_record_layer_set_coalesce", "ptls_mi355x_record_layer_launches",
     "ptls_mi355x_record_layer_cork",
     "ptls_mi355x_record_layer_set_direct_dma", "ptls_mi355x_tls_deliver_records", "ptls_mi355x_prepare_copies",
-    "ptls_mi355x_resident_tls_seal_records_multi", "ptls_mi355x_resident_tls_open_records_multi",
-    "ptls_mi355x_resident_tls_deliver_records", "ptls_mi355x_resident_done", "ptls_mi355x_resident_wait",
-    "ptls_mi355x_resident_stop", "ptls_mi355x_resident_launches", "ptls_mi355x_set_resident_workers",
-    "ptls_mi355x_set_resident_idle_us", "ptls_mi355x_record_layer_set_resident", "ptls_mi355x_resident_job_times",
-    "ptls_mi355x_resident_jobs", "ptls_mi355x_resident_copy", "ptls_mi355x_set_slot_resident",
 )
-RESIDENT_NONE = (1 << 64) - 1
 EXPORTED_OBJECTS = ("ptls_mi355x_aes128gcm", "ptls_mi355x_aes256gcm", "ptls_mi355x_aes128ctr",
                     "ptls_mi355x_aes256ctr", "ptls_mi355x_aes128ecb", "ptls_mi355x_aes256ecb")
 
@@ -143,6 +138,9 @@ def lib() -> C.CDLL:
         L.ptls_mi355x_aesgcm_new.argtypes = [vp, sz, sz]
         L.ptls_mi355x_aesgcm_new.restype = vp
         L.ptls_mi355x_aesgcm_free.argtypes = [vp]
+        if hasattr(L, "ptls_mi355x_aesgcm_release"):  # (absent from older builds used in A/B timing runs)
+            L.ptls_mi355x_aesgcm_release.argtypes = [vp]
+            L.ptls_mi355x_device_check.argtypes = []
         L.ptls_mi355x_aesgcm_device.argtypes = [vp]
         L.ptls_mi355x_aesgcm_encrypt.argtypes = [vp, vp, vp, sz, vp, vp, sz]
         L.ptls_mi355x_aesgcm_decrypt.argtypes = [vp, vp, vp, sz, vp, vp, sz, vp]
@@ -203,8 +201,6 @@ def lib() -> C.CDLL:
             L.ptls_mi355x_record_layer_launches.restype = u64
             L.ptls_mi355x_record_layer_cork.argtypes = [vp, C.c_int]
             L.ptls_mi355x_record_layer_set_direct_dma.argtypes = [vp, C.c_int]
-            if hasattr(L, "ptls_mi355x_record_layer_set_resident"):
-                L.ptls_mi355x_record_layer_set_resident.argtypes = [vp, C.c_int]
         for name in ("ptls_mi355x_set_win16_records", "ptls_mi355x_set_split_records"):
             if hasattr(L, name):  # (absent from older builds used in A/B timing runs)
                 getattr(L, name).argtypes = [sz]
@@ -218,26 +214,8 @@ def lib() -> C.CDLL:
             L.ptls_mi355x_aes_ecb_batch.argtypes = [vp, C.c_int, vp, vp, sz, vp]
         if hasattr(L, "ptls_mi355x_tls_deliver_records"):
             L.ptls_mi355x_tls_deliver_records.argtypes = [vp, vp, vp, vp, vp, sz, sz, vp]
-        if hasattr(L, "ptls_mi355x_resident_wait"):  # (absent from older builds used in A/B timing runs)
-            L.ptls_mi355x_resident_tls_seal_records_multi.argtypes = [vp, vp, vp, vp, sz, vp, vp, C.POINTER(u64)]
-            L.ptls_mi355x_resident_tls_open_records_multi.argtypes = [vp, vp, vp, vp, sz, vp, vp, vp, vp,
-                                                                      C.POINTER(u64)]
-            L.ptls_mi355x_resident_tls_deliver_records.argtypes = [vp, vp, vp, vp, vp, sz, sz, C.POINTER(u64)]
-            L.ptls_mi355x_resident_copy.argtypes = [vp, vp, sz, C.POINTER(u64)]
-            L.ptls_mi355x_set_slot_resident.argtypes = [C.c_int]
-            L.ptls_mi355x_resident_done.argtypes = [vp, u64]
-            L.ptls_mi355x_resident_wait.argtypes = [vp, u64]
-            L.ptls_mi355x_resident_stop.argtypes = [C.c_int]
+        if hasattr(L, "ptls_mi355x_prepare_copies"):
             L.ptls_mi355x_prepare_copies.argtypes = []
-            L.ptls_mi355x_resident_job_times.argtypes = [vp, u64, C.POINTER(u64)]
-            L.ptls_mi355x_resident_jobs.argtypes = [C.c_int]
-            L.ptls_mi355x_resident_jobs.restype = u64
-            L.ptls_mi355x_resident_launches.argtypes = [C.c_int]
-            L.ptls_mi355x_resident_launches.restype = u64
-            L.ptls_mi355x_set_resident_workers.argtypes = [sz]
-            L.ptls_mi355x_set_resident_workers.restype = sz
-            L.ptls_mi355x_set_resident_idle_us.argtypes = [u64]
-            L.ptls_mi355x_set_resident_idle_us.restype = u64
         L.ptls_mi355x_tls_plan_send.argtypes = [sz, C.c_uint32, C.POINTER(u64), u64, u64, vp, sz, C.POINTER(sz)]
         L.ptls_mi355x_tls_plan_send.restype = sz
         L.ptls_mi355x_tls_parse_records.argtypes = [vp, sz, u64, C.POINTER(u64), u64, vp, sz, C.POINTER(sz),
@@ -249,6 +227,28 @@ def lib() -> C.CDLL:
 
 def last_error() -> str:
     return lib().ptls_mi355x_last_error().decode()
+
+
+def device_check() -> None:
+    """Synchronises the current device and raises if any GPU work faulted, or a free path met an error, since the
+    previous check (ptls_mi355x_device_check).  The GPU tests run it after every test (tests/conftest.py)."""
+    if lib().ptls_mi355x_device_check():
+        raise RuntimeError("device check: " + last_error())
+
+
+#: errors raised by close() inside a finalizer (__del__ cannot raise): reported, and collected for the test suite
+FINALIZER_ERRORS: list = []
+
+
+def _finalize(obj, method: str = "close") -> None:
+    """obj.close() (or .free()) from __del__: an error is printed and kept in FINALIZER_ERRORS, never dropped."""
+    try:
+        getattr(obj, method)()
+    except Exception as e:  # noqa: BLE001 - __del__ must not raise; report instead
+        msg = f"{type(obj).__name__}.__del__: {e}"
+        FINALIZER_ERRORS.append(msg)
+        import sys
+        print("rapido_amd: " + msg, file=sys.stderr)
 
 
 def build_id() -> str:
@@ -338,10 +338,7 @@ class Aead:
         return self.ctx.do_encrypt_final(self.ptr, C.addressof(out) + out_off)
 
     def __del__(self):
-        try:
-            self.free()
-        except Exception:
-            pass
+        _finalize(self, "free")
 
 
 def aead_new_direct(name_or_algo, is_enc: bool, key: bytes, iv: bytes) -> Aead:
@@ -379,10 +376,7 @@ class Cipher:
             self._mem = None
 
     def __del__(self):
-        try:
-            self.free()
-        except Exception:
-            pass
+        _finalize(self, "free")
 
 
 def cipher_new(name: str, is_enc: bool, key: bytes) -> Cipher:
@@ -402,15 +396,15 @@ class Engine:
             raise RuntimeError("ptls_mi355x_aesgcm_new failed: " + last_error())
 
     def close(self) -> None:
+        """ptls_mi355x_aesgcm_release: waits for the context's launches, clears and frees its key image; raises if
+        that met an error (an asynchronous fault of earlier GPU work surfaces at its synchronisation)."""
         if self.handle:
-            lib().ptls_mi355x_aesgcm_free(self.handle)
-            self.handle = None
+            h, self.handle = self.handle, None
+            if lib().ptls_mi355x_aesgcm_release(h):
+                raise RuntimeError("ptls_mi355x_aesgcm_release: " + last_error())
 
     def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
+        _finalize(self)
 
     @property
     def device(self) -> int:
@@ -482,84 +476,12 @@ class Engine:
                                                  src_ptr, dst_ptr, status_ptr, types_ptr, flags, stream or None):
             raise RuntimeError("tls_open_records failed: " + last_error())
 
-    # the resident window engine (include/ptls_mi355x.h section 6): jobs of the device's persistent grid
-    def resident_tls_seal_records(self, static_iv: bytes, recs_ptr: int, n: int, src_ptr: int, dst_ptr: int,
-                                  conn_ptr: int = 0) -> int:
-        job = u64(0)
-        if lib().ptls_mi355x_resident_tls_seal_records_multi(self.handle, _cbuf(static_iv), recs_ptr, conn_ptr or None,
-                                                             n, src_ptr, dst_ptr, C.byref(job)):
-            raise RuntimeError("resident tls_seal_records failed: " + last_error())
-        return job.value
-
-    def resident_tls_open_records(self, static_iv: bytes, recs_ptr: int, n: int, src_ptr: int, dst_ptr: int,
-                                  status_ptr: int, types_ptr: int, conn_ptr: int = 0) -> int:
-        job = u64(0)
-        if lib().ptls_mi355x_resident_tls_open_records_multi(self.handle, _cbuf(static_iv), recs_ptr, conn_ptr or None,
-                                                             n, src_ptr, dst_ptr, status_ptr, types_ptr, C.byref(job)):
-            raise RuntimeError("resident tls_open_records failed: " + last_error())
-        return job.value
-
-    def resident_tls_deliver_records(self, recs_ptr: int, status_ptr: int, types_ptr: int, parts_ptr: int,
-                                     nparts: int, max_records: int) -> int:
-        job = u64(0)
-        if lib().ptls_mi355x_resident_tls_deliver_records(self.handle, recs_ptr, status_ptr, types_ptr, parts_ptr,
-                                                          nparts, max_records, C.byref(job)):
-            raise RuntimeError("resident tls_deliver_records failed: " + last_error())
-        return job.value
-
-    def resident_copy(self, ranges) -> int:
-        """A copy job: ranges = [(dst_ptr, src_ptr, nbytes), ...] (GPU addresses); the context's next run job follows it."""
-        arr = (u64 * (3 * max(len(ranges), 1)))(*[int(x) for r in ranges for x in r])
-        job = u64(0)
-        if lib().ptls_mi355x_resident_copy(self.handle, arr, len(ranges), C.byref(job)):
-            raise RuntimeError("resident_copy failed: " + last_error())
-        return job.value
-
-    def resident_done(self, job: int) -> bool:
-        rc = lib().ptls_mi355x_resident_done(self.handle, job)
-        if rc < 0:
-            raise RuntimeError("resident_done failed: " + last_error())
-        return rc == 1
-
-    def resident_wait(self, job: int) -> None:
-        if lib().ptls_mi355x_resident_wait(self.handle, job):
-            raise RuntimeError("resident_wait failed: " + last_error())
-
-    def resident_job_times(self, job: int):
-        """(publication -> first unit, first unit -> last unit end, -> complete, publication -> complete) in ns, or
-        None once the job's ring entry has been reused."""
-        ns = (u64 * 4)()
-        return None if lib().ptls_mi355x_resident_job_times(self.handle, job, ns) else tuple(ns)
-
-
-def resident_stop(device: int = 0) -> None:
-    """Waits for every posted resident job, ends the device's grid and frees its ring."""
-    if lib().ptls_mi355x_resident_stop(device):
-        raise RuntimeError("resident_stop failed: " + last_error())
-
 
 def prepare_copies() -> None:
     """Has the HIP runtime set up its copy machinery on the current device now rather than inside a later window
     (include/ptls_mi355x.h; record layers call it before their first copy)."""
     if lib().ptls_mi355x_prepare_copies():
         raise RuntimeError("prepare_copies failed: " + last_error())
-
-
-def resident_launches(device: int = 0) -> int:
-    return lib().ptls_mi355x_resident_launches(device)
-
-
-def set_slot_resident(on: bool) -> bool:
-    """Single-record calls (the AEAD slot objects) as jobs of the resident grid; returns the previous setting."""
-    return bool(lib().ptls_mi355x_set_slot_resident(1 if on else 0))
-
-
-def set_resident_workers(n: int) -> int:
-    return lib().ptls_mi355x_set_resident_workers(n)
-
-
-def set_resident_idle_us(us: int) -> int:
-    return lib().ptls_mi355x_set_resident_idle_us(us)
 
 
 class AesKeys:
@@ -589,10 +511,7 @@ class AesKeys:
             self.handle = None
 
     def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
+        _finalize(self)
 
 
 class _IoVec(C.Structure):
@@ -609,17 +528,12 @@ class RecordLayer:
     """ptls_mi355x_record_layer_t: one traffic direction of a connection, windows of records between host memory
     and the GPU (include/ptls_mi355x.h section 5)."""
 
-    #: new layers start with set_resident(default_resident) (the test suites run every record-layer test both ways)
-    default_resident = False
-
     def __init__(self, key: bytes, static_iv: bytes, seq: int = 0):
         assert len(static_iv) == 12
         self._registered = {}
         self.handle = lib().ptls_mi355x_record_layer_new(_cbuf(key), len(key), _cbuf(static_iv), seq)
         if not self.handle:
             raise RuntimeError("ptls_mi355x_record_layer_new failed: " + lib().ptls_mi355x_record_layer_last_error().decode())
-        if RecordLayer.default_resident:
-            self.set_resident(True)
 
     @property
     def seq(self) -> int:
@@ -666,11 +580,6 @@ class RecordLayer:
         mode."""
         mode = on if on == RECORD_LAYER_DMA_IN else (1 if on else 0)
         return lib().ptls_mi355x_record_layer_set_direct_dma(self.handle, mode)
-
-    def set_resident(self, on: bool) -> bool:
-        """Windows that need no copy run as jobs of the device's resident grid (include/ptls_mi355x.h section 6)
-        instead of kernel launches.  Returns the previous setting."""
-        return bool(lib().ptls_mi355x_record_layer_set_resident(self.handle, 1 if on else 0))
 
     def set_zero_copy_bytes(self, n: int) -> int:
         """Windows of at most n staged bytes run zero-copy on the pinned staging (0: DMA copies); -> previous."""
@@ -795,10 +704,7 @@ class RecordLayer:
             self.handle = None
 
     def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
+        _finalize(self)
 
 
 def record_layer_seal_multi(layers, windows, content_type: int = 23, outs=None):

@@ -2163,9 +2163,23 @@ GCM_HD uint32_t window_group_start(uint32_t g, uint32_t ns) { return g == 0u ? 0
 
 /* ------------------------------------------------------------------ per-lane record walk -- */
 
+/*
+ * GCM_READ(p, n): the walk is about to read bytes [p, p + n) of a record (or its AAD / descriptor).  Nothing in the
+ * kernels; the CPU test suite's host model (tests/cpp/kernel_model.cpp, GCM_HOST_READ_CHECK) checks every such range
+ * against the records' own bytes, so a read outside them -- a fault wherever a record ends at an unmapped page --
+ * fails on the CPU, deterministically.
+ */
+#if defined(GCM_HOST_READ_CHECK) && !defined(__HIP_DEVICE_COMPILE__)
+extern "C" void gcm_host_read_check(const void *p, size_t n);
+#define GCM_READ(p, n) gcm_host_read_check((const void *)(p), (size_t)(n))
+#else
+#define GCM_READ(p, n) ((void)0)
+#endif
+
 /* loads n (< 16) bytes zero-extended */
 GCM_HD u32x4 load_partial(const uint8_t *p, uint32_t n)
 {
+    GCM_READ(p, n);
     /* loop-free (n < 16): whole dwords, then up to 3 bytes of dword q = n / 4 */
     u32x4 v = {0u, 0u, 0u, 0u};
     const uint32_t q = n >> 2, rem = n & 3u;
@@ -2257,6 +2271,7 @@ GCM_HD u32x4 shr_bytes(u32x4 v, uint32_t n)
  * half-written output lines from L2) */
 GCM_HD u32x4 walk_load(const uint8_t *p)
 {
+    GCM_READ(p, 16);
 #if defined(__HIP_DEVICE_COMPILE__) && GCM_NT_LOADS
     return __builtin_nontemporal_load((const u32x4_u *)p);
 #else
@@ -2354,8 +2369,10 @@ GCM_HD u32x4 lane_walk_seg(const uint8_t *lds, uint32_t lanesel, const uint32_t 
             } else if (rec.aadlen < 16u) {
                 acc = load_partial(ad, rec.aadlen);
             } else if (16u * (uint32_t)pv + 16u <= rec.aadlen) {
+                GCM_READ(ad + 16u * (uint32_t)pv, 16);
                 acc = *(const u32x4_u *)(ad + 16u * (uint32_t)pv);
             } else { /* partial last block: its last 16 bytes, shifted */
+                GCM_READ(ad + rec.aadlen - 16u, 16);
                 acc = shr_bytes(*(const u32x4_u *)(ad + rec.aadlen - 16u), 16u - arem);
             }
         }

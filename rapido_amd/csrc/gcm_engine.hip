@@ -45,15 +45,9 @@ __device__ uint64_t g_win_times[32];
         if (r == 0u && threadIdx.x == 0)                                                                               \
             g_win_times[i] = __builtin_amdgcn_s_memrealtime();                                                         \
     } while (0)
-/* the resident grid (scripts/resident_phases.py): worker GCM_STAMP_BLOCK's job phases (16-21), the dispatcher's
- * last publication (22) */
-#define RES_STAMP(i) GCM_WALK_STAMP(i)
-#define RES_STAMP_ANY(i) (g_win_times[i] = __builtin_amdgcn_s_memrealtime())
 #else
 #define SPLIT_STAMP(i) ((void)0)
 #define SPLIT_STAMP_LAST(i) ((void)0)
-#define RES_STAMP(i) ((void)0)
-#define RES_STAMP_ANY(i) ((void)0)
 #endif
 #include "gcm_core.h"
 #include "../../include/ptls_mi355x.h"
@@ -719,41 +713,7 @@ __device__ __forceinline__ void window_body(const KeyImage *__restrict__ ki, uin
  * resets the record's ticket, so the counters are zero between launches.  No workgroup waits for another.
  * A record of more than SPLIT_RUNSEG x SPLIT_MAXRUN segments (larger than a TLS record) is walked whole by run 0.
  */
-/*
- * RES (the resident kernel, mi355x_resident): inputs that change between the jobs of one persistent grid -- descriptors,
- * connection ids, round keys -- are read by vector loads and made wave-uniform (res_ld), never through the scalar
- * cache, which nothing refreshes inside a kernel.
- */
-template <uint32_t N> __device__ __forceinline__ void res_ld_words(const void *p, uint32_t *w)
-{
-    /* buffer loads (vector memory, all issued before the first wait), then wave-uniform copies */
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)p, (short)0, 0x7fffffff, 0x00020000);
-#pragma unroll
-    for (uint32_t i = 0; i < N / 4; ++i) {
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(16 * i), 0, 0);
-        w[4 * i] = v.x;
-        w[4 * i + 1] = v.y;
-        w[4 * i + 2] = v.z;
-        w[4 * i + 3] = v.w;
-    }
-#pragma unroll
-    for (uint32_t i = N / 4 * 4; i < N; ++i)
-        w[i] = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(4 * i), 0, 0);
-#pragma unroll
-    for (uint32_t i = 0; i < N; ++i)
-        w[i] = __builtin_amdgcn_readfirstlane(w[i]);
-}
-template <typename T> __device__ __forceinline__ T res_ld(const T *p)
-{
-    static_assert(sizeof(T) % 4 == 0, "whole dwords");
-    uint32_t w[sizeof(T) / 4];
-    res_ld_words<sizeof(T) / 4>(p, w);
-    T v;
-    __builtin_memcpy(&v, w, sizeof(T));
-    return v;
-}
-
-template <int NR, bool SEAL, bool FRAME, bool RES = false>
+template <int NR, bool SEAL, bool FRAME>
 __device__ __forceinline__ void split_body(const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2,
                                            const void *__restrict__ descs, uint32_t nrecs, const uint8_t *src, uint8_t *dst,
                                            const uint8_t *__restrict__ aad, uint32_t *__restrict__ status,
@@ -775,7 +735,7 @@ __device__ __forceinline__ void split_body(const KeyImage *__restrict__ ki, uint
     uint32_t ctype = 0u;
     bool valid = true;
     if (FRAME) {
-        const TlsRecord t = RES ? res_ld((const TlsRecord *)descs + r) : ((const TlsRecord *)descs)[r];
+        const TlsRecord t = ((const TlsRecord *)descs)[r];
         rec.seq = t.seq;
         if (SEAL) {
             rec.src = t.src;
@@ -790,7 +750,7 @@ __device__ __forceinline__ void split_body(const KeyImage *__restrict__ ki, uint
             valid = t.len >= 16u;
         }
     } else {
-        rec = RES ? res_ld((const Record *)descs + r) : ((const Record *)descs)[r];
+        rec = ((const Record *)descs)[r];
     }
     const uint32_t plen = FRAME && SEAL ? rec.len + 1u : rec.len;
     const uint32_t A = FRAME ? 1u : (rec.aadlen + 15u) / 16u, C = (plen + 15u) / 16u;
@@ -857,18 +817,14 @@ __device__ __forceinline__ void split_body(const KeyImage *__restrict__ ki, uint
 #endif
     }
     uint32_t rk[4 * (NR + 1)];
-    if (RES) {
-        res_ld_words<4 * (NR + 1)>(&ki->rk[0], rk);
-    } else {
 #pragma unroll
-        for (int i = 0; i < 4 * (NR + 1); ++i)
-            rk[i] = ki->rk[i];
-    }
+    for (int i = 0; i < 4 * (NR + 1); ++i)
+        rk[i] = ki->rk[i];
     __syncthreads();
     SPLIT_STAMP(1);
 
     const uint32_t n1 = iv1 ^ bswap32((uint32_t)(rec.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)rec.seq);
-    const uint32_t n0 = conn != nullptr ? iv0 ^ bswap32(RES ? res_ld(conn + r) : conn[r]) : iv0;
+    const uint32_t n0 = conn != nullptr ? iv0 ^ bswap32(conn[r]) : iv0;
     u32x4 part = lane_walk_seg<NR, KW, SEAL, FRAME, LW, 1>(lds, lanesel, rk, j, rec, active, Tw, n0, n1, n2, src, dst, aad,
                                                           (const uint8_t *)descs, ctype, !whole, sw, t0);
     SPLIT_STAMP(2);
@@ -1335,24 +1291,22 @@ __device__ __forceinline__ void copy_bytes(uint8_t *dst, const uint8_t *src, uin
         dst[tail0 + tid] = src[tail0 + tid];
 }
 
-/* workgroup (part, g) of G: off[DELIVER_MAX + 1] and *ndone in LDS; RES: the part and descriptors by vector loads */
-template <bool RES>
+/* workgroup (part, g) of G: off[DELIVER_MAX + 1] and *ndone in LDS */
 __device__ __forceinline__ void deliver_body(const TlsRecord *__restrict__ recs, const uint32_t *__restrict__ status,
                                              const uint8_t *__restrict__ types, const DeliverPart *__restrict__ parts,
                                              uint32_t part, uint32_t g, uint32_t G, uint32_t *off, uint32_t *ndone_)
 {
     uint32_t &ndone = *ndone_;
-    const DeliverPart p = RES ? res_ld(parts + part) : parts[part];
+    const DeliverPart p = parts[part];
     const uint32_t n = p.n < DELIVER_MAX ? p.n : DELIVER_MAX;
     /*
      * Every thread loads some records' status and type (in parallel: one dependent load per record in thread 0's loop
      * cost ~2 us each, 92 us for a 16-record window), leaving in off[i] the plaintext length, or ~0 where the receive
      * loop stops (a failure, or another content type); thread 0 then walks off[] in LDS.
-     * (RES: volatile, i.e. vector loads -- the open job wrote them inside the same persistent grid.)
      */
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-        const uint32_t st = RES ? *(const volatile uint32_t *)&status[p.k0 + i] : status[p.k0 + i];
-        const uint8_t ty = RES ? *(const volatile uint8_t *)&types[p.k0 + i] : types[p.k0 + i];
+        const uint32_t st = status[p.k0 + i];
+        const uint8_t ty = types[p.k0 + i];
         off[i] = st >= PTLS_MI355X_TLS_NOT_PROCESSED || (!p.any_type && ty != 23u) ? 0xffffffffu : st;
     }
     __syncthreads();
@@ -1375,7 +1329,7 @@ __device__ __forceinline__ void deliver_body(const TlsRecord *__restrict__ recs,
     __syncthreads();
     const uint32_t nd = ndone;
     for (uint32_t i = g; i < nd; i += G) {
-        const uint64_t rdst = RES ? res_ld(&recs[p.k0 + i].dst) : recs[p.k0 + i].dst;
+        const uint64_t rdst = recs[p.k0 + i].dst;
         copy_bytes(p.out + off[i], p.slots + rdst, off[i + 1] - off[i], threadIdx.x, blockDim.x);
     }
 }
@@ -1387,380 +1341,7 @@ extern "C" __global__ __launch_bounds__(256) void mi355x_tls_deliver(const TlsRe
 {
     __shared__ uint32_t off[DELIVER_MAX + 1];
     __shared__ uint32_t ndone;
-    deliver_body<false>(recs, status, types, parts, blockIdx.x, blockIdx.y, gridDim.y, off, &ndone);
-}
-
-/* ==================================================================== the resident grid ===== */
-/*
- * The resident window engine (ptls_mi355x_resident_*): ONE persistent grid per device runs the split window kernels'
- * runs and the delivery as jobs posted through a ring in pinned host memory, so a window costs the host a few stores
- * instead of a kernel launch (a launch and its completion cost ~10 us of host time each, and several HIP calls per
- * window were the record layer's bound at one window per submit: DESIGN.md section 2).
- *  - Workgroup 0, one lane, is the dispatcher: it polls the host ring (relaxed system-scope loads: an acquire per
- *    poll would invalidate the caches every time), copies each new job into device memory and publishes it with an
- *    sc1 tail store.  Only it touches the ring across PCIe while waiting; the workers poll device memory.
- *  - Workers 1..P: unit u of job j runs on worker (base_j + u) % P, base_j = the units posted before j, mod P (no
- *    claiming: a CAS per unit over 255 workers serialised the units, scripts/probe_doorbell.hip).  A worker takes
- *    its jobs in order: one system-scope acquire when it starts a job's units (descriptors, inputs and key images
- *    are re-read fresh), its units, every wave's stores drained, one system-scope release, then an add to the job's
- *    done count; the add that completes the job resets the count and writes the job's fin word, in device memory
- *    (for dependent jobs) and in host memory (what the host polls).
- *  - A delivery job names the open job it follows (`after`); its units start once that job's fin is set.
- *  - Exit: the dispatcher leaves after `idle` ticks with every published job finished (telling the host through the
- *    ring's `alive` word, re-checking the tail after that store), or on the host's stop or at `lifetime` once the jobs
- *    it published are complete; it then sets the instance's stop epoch and the workers leave.  Every wave reaches the exit whatever the host does, and the
- *    host re-launches the grid (same stream: never two instances at once) when a job finds none running.
- */
-constexpr uint32_t RES_RING = 256;
-
-enum : uint32_t { RES_SEAL = 1u, RES_FRAME = 2u, RES_AES256 = 4u, RES_DELIVER = 8u, RES_COPY = 16u };
-
-/* a copy job's ranges (ptls_mi355x_resident_copy): unit u copies chunk u - first of the range holding it */
-struct ResCopy {
-    uint64_t dst, src, n, first;
-};
-constexpr uint32_t RES_COPY_CHUNK = 8192;
-constexpr uint32_t RES_COPY_MAX = PTLS_MI355X_RESIDENT_COPY_MAX;
-
-/* dst[0, len) <- src[0, len) by the workgroup: four 16-byte loads per thread in flight when both are 16-aligned */
-__device__ __forceinline__ void res_copy_bytes(uint8_t *dst, const uint8_t *src, uint32_t len)
-{
-    if ((((uintptr_t)dst | (uintptr_t)src) & 15u) != 0u) {
-        copy_bytes(dst, src, len, threadIdx.x, blockDim.x);
-        return;
-    }
-    const uint32_t body = len / 16u, nt = blockDim.x;
-    const u32x4 *s4 = (const u32x4 *)src;
-    u32x4 *d4 = (u32x4 *)dst;
-    for (uint32_t b = 0; b < body; b += 4u * nt) {
-        u32x4 v[4];
-#pragma unroll
-        for (uint32_t k = 0; k < 4u; ++k)
-            if (b + k * nt + threadIdx.x < body)
-                v[k] = s4[b + k * nt + threadIdx.x];
-#pragma unroll
-        for (uint32_t k = 0; k < 4u; ++k)
-            if (b + k * nt + threadIdx.x < body)
-                d4[b + k * nt + threadIdx.x] = v[k];
-    }
-    if (threadIdx.x < len - 16u * body)
-        dst[16u * body + threadIdx.x] = src[16u * body + threadIdx.x];
-}
-
-struct ResJob {
-    uint64_t id;      /* the job's number (seqlock word: ~0 while the dispatcher rewrites the device copy) */
-    uint32_t kind;    /* RES_SEAL | RES_FRAME | RES_AES256, or RES_DELIVER */
-    uint32_t nunits;  /* runs: records x SPLIT_MAXRUN; delivery: parts x groups */
-    uint32_t base;    /* unit u runs on worker (base + u) % P */
-    uint32_t nrecs;   /* runs: records; delivery: groups per part */
-    uint64_t after;   /* 0, or 1 + the job whose completion this one waits for */
-    const KeyImage *ki;
-    const void *descs;
-    const uint8_t *src;
-    uint8_t *dst;
-    uint32_t *status;
-    uint8_t *types;
-    const uint32_t *conn;
-    u32x4 *partials;
-    uint32_t *tickets;
-    const DeliverPart *parts; /* delivery: the parts; runs: the AAD base of AEAD records */
-    uint32_t iv0, iv1, iv2, pad;
-};
-static_assert(sizeof(ResJob) == 128, "ring entry");
-
-/* pinned, mapped, coherent host memory */
-struct ResRing {
-    uint64_t tail;  /* host: jobs posted */
-    uint32_t stop;  /* host: end the grid */
-    uint32_t alive; /* 1 from the host's launch until the dispatcher leaves */
-    uint64_t pad[6];
-    ResJob jobs[RES_RING];
-    uint64_t fin[RES_RING]; /* 1 + the id of the last job of this entry that is complete */
-    /* the entry's last job on the GPU's wall clock: published, first unit started, last unit ended, complete */
-    uint64_t times[RES_RING][4];
-};
-
-/* device memory, zeroed once; kept across instances */
-struct ResDev {
-    uint64_t tail;       /* jobs published to the workers */
-    uint64_t nfin;       /* jobs complete */
-    uint32_t stop_epoch; /* the instance told to leave */
-    uint32_t pad[11];
-    ResJob jobs[RES_RING];
-    uint64_t fin[RES_RING];
-    uint32_t done[RES_RING]; /* units done of the entry's current job */
-    uint64_t first_c[RES_RING], last[RES_RING]; /* ~(first unit start), last unit end (atomic max; 0 between jobs) */
-    uint64_t started; /* workers of every instance so far that have read their starting job (see the dispatcher) */
-};
-
-__device__ __forceinline__ uint64_t res_ld_sys64(const uint64_t *p)
-{
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ uint32_t res_ld_sys32(const uint32_t *p)
-{
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ uint64_t res_ld_dev64(const uint64_t *p)
-{
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t res_ld_dev32(const uint32_t *p)
-{
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <typename T> struct res_same {
-    typedef T type;
-};
-template <typename T> __device__ __forceinline__ void res_st_dev(T *p, typename res_same<T>::type v)
-{
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <typename T> __device__ __forceinline__ void res_st_sys(T *p, typename res_same<T>::type v)
-{
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-/* one run, delivery or copy unit of job jb (every thread of the 128; LDS is the split layout's) */
-__device__ __forceinline__ void res_unit(const ResJob &jb, uint32_t u, uint8_t *lds, const u32x4 *win_aes)
-{
-    if (jb.kind & RES_COPY) {
-        const ResCopy *cp = (const ResCopy *)jb.descs;
-        uint32_t lo = 0u, hi = jb.nrecs; /* the range holding chunk u: first <= u < the next range's first */
-        while (hi - lo > 1u) {
-            const uint32_t mid = (lo + hi) / 2u;
-            if (res_ld(&cp[mid].first) <= u)
-                lo = mid;
-            else
-                hi = mid;
-        }
-        const ResCopy c = res_ld(cp + lo);
-        const uint64_t off = (u - c.first) * (uint64_t)RES_COPY_CHUNK;
-        const uint32_t len = (uint32_t)(c.n - off < RES_COPY_CHUNK ? c.n - off : RES_COPY_CHUNK);
-        res_copy_bytes((uint8_t *)c.dst + off, (const uint8_t *)c.src + off, len);
-        return;
-    }
-    if (jb.kind & RES_DELIVER) {
-        const uint32_t G = jb.nrecs;
-        deliver_body<true>((const TlsRecord *)jb.descs, jb.status, jb.types, jb.parts, u / G, u % G, G,
-                           (uint32_t *)lds, (uint32_t *)lds + DELIVER_MAX + 1);
-        __syncthreads(); /* the next unit's fill may overwrite off[] */
-        return;
-    }
-    const uint32_t r = u / SPLIT_MAXRUN, k = u % SPLIT_MAXRUN;
-#define RES_SPLIT(NR, SEAL, FRAME)                                                                                     \
-    split_body<NR, SEAL, FRAME, true>(jb.ki, jb.iv0, jb.iv1, jb.iv2, jb.descs, jb.nrecs, jb.src, jb.dst,                \
-                                      (const uint8_t *)jb.parts,                                                       \
-                                      jb.status, jb.types, jb.conn, win_aes, jb.partials, jb.tickets, lds, r, k)
-    switch (jb.kind & 7u) {
-    case 0u: RES_SPLIT(10, false, false); break;
-    case 1u: RES_SPLIT(10, true, false); break;
-    case 2u: RES_SPLIT(10, false, true); break;
-    case 3u: RES_SPLIT(10, true, true); break;
-    case 4u: RES_SPLIT(14, false, false); break;
-    case 5u: RES_SPLIT(14, true, false); break;
-    case 6u: RES_SPLIT(14, false, true); break;
-    default: RES_SPLIT(14, true, true); break;
-    }
-#undef RES_SPLIT
-    __syncthreads(); /* (split_body returns uniformly; the next unit's fill overwrites the LDS) */
-}
-
-extern "C" __global__ __launch_bounds__(SPLIT_THREADS) void mi355x_resident(ResRing *ring, ResDev *ds, const u32x4 *win_aes,
-                                                                           uint32_t epoch, uint64_t idle_ticks,
-                                                                           uint64_t lifetime_ticks, uint64_t started_target)
-{
-    __shared__ __attribute__((aligned(16))) uint8_t lds[LayoutSplit::bytes];
-    const uint64_t born = wall_clock64();
-    if (blockIdx.x == 0) {
-        if (threadIdx.x != 0)
-            return;
-        res_st_sys(&ring->alive, 1u);
-        /*
-         * Every worker of this instance reads its starting job (the published count) before anything new is published:
-         * a worker starting after a publication would skip that job's units.  started counts the workers of all
-         * instances; the host passes P x the instances launched.
-         */
-        while (res_ld_dev64(&ds->started) < started_target && wall_clock64() - born <= lifetime_ticks)
-            __builtin_amdgcn_s_sleep(2);
-        uint64_t pub = res_ld_dev64(&ds->tail), idle_since = born;
-        for (;;) {
-            const uint64_t now = wall_clock64();
-            /* the host's stop or the lifetime: publish nothing more, leave once every published job is complete (the
-             * host relaunches the grid for jobs posted meanwhile); past twice the lifetime, leave regardless */
-            if (res_ld_sys32(&ring->stop) != 0u || now - born > lifetime_ticks) {
-                if (res_ld_dev64(&ds->nfin) >= pub || now - born > 2u * lifetime_ticks)
-                    break;
-                __builtin_amdgcn_s_sleep(8);
-                continue;
-            }
-            const uint64_t tail = res_ld_sys64(&ring->tail);
-            if (tail > pub) {
-                /* each new job: its id word invalid, the other 15 words, then the id (sc1 stores, drained in order) */
-                for (; pub < tail; ++pub) {
-                    const uint32_t e = (uint32_t)(pub % RES_RING);
-                    const uint64_t *h = (const uint64_t *)&ring->jobs[e];
-                    uint64_t *d = (uint64_t *)&ds->jobs[e];
-                    uint64_t w[16];
-#pragma unroll
-                    for (int i = 0; i < 16; ++i)
-                        w[i] = res_ld_sys64(h + i);
-                    res_st_dev(d, ~0ull);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-                    for (int i = 1; i < 16; ++i)
-                        res_st_dev(d + i, w[i]);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    res_st_dev(d, w[0]);
-                    res_st_sys(&ring->times[e][0], (uint64_t)wall_clock64());
-                }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                res_st_dev(&ds->tail, pub);
-                RES_STAMP_ANY(22);
-                idle_since = now;
-            } else if (res_ld_dev64(&ds->nfin) < pub) {
-                idle_since = now; /* published jobs still running */
-                __builtin_amdgcn_s_sleep(8);
-            } else if (now - idle_since > idle_ticks) {
-                /* leaving: say so, then look once more (the host posts, then reads alive: one of us sees the other) */
-                res_st_sys(&ring->alive, 0u);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (res_ld_sys64(&ring->tail) == pub)
-                    break;
-                res_st_sys(&ring->alive, 1u);
-            } else {
-                __builtin_amdgcn_s_sleep(8);
-            }
-        }
-        res_st_sys(&ring->alive, 0u);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        res_st_dev(&ds->stop_epoch, epoch);
-        return;
-    }
-    /* workers */
-    const uint32_t P = gridDim.x - 1u, w = blockIdx.x - 1u;
-    uint32_t *ctl = (uint32_t *)lds; /* [0] state, [1] first unit, [2..33] the job (aliases the unit's LDS) */
-    uint64_t cur = 0; /* (lane 0's) the next job: every job published before this instance is complete */
-    if (threadIdx.x == 0) {
-        cur = res_ld_dev64(&ds->tail);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        atomicAdd((unsigned long long *)&ds->started, 1ull); /* (the dispatcher publishes once all have read it) */
-    }
-    for (;;) {
-        if (threadIdx.x == 0) {
-            uint32_t state = 1u; /* 0 work, 1 idle, 2 exit */
-            if (res_ld_dev32(&ds->stop_epoch) == epoch || wall_clock64() - born > 2u * lifetime_ticks + idle_ticks) {
-                state = 2u;
-            } else {
-                const uint64_t tail = res_ld_dev64(&ds->tail);
-                while (cur < tail) {
-                    const uint32_t e = (uint32_t)(cur % RES_RING);
-                    const uint64_t *d = (const uint64_t *)&ds->jobs[e];
-                    uint64_t v[16];
-                    v[0] = res_ld_dev64(d);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    if (v[0] == ~0ull)
-                        break; /* being rewritten (its job is complete: a later one takes the entry) -- look again */
-                    if (v[0] != cur) {
-                        ++cur; /* the entry already holds a later job: job cur is complete */
-                        continue;
-                    }
-#pragma unroll
-                    for (int i = 1; i < 16; ++i)
-                        v[i] = res_ld_dev64(d + i);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    if (res_ld_dev64(d) != cur)
-                        break; /* rewritten meanwhile: look again */
-                    ResJob jb;
-                    __builtin_memcpy(&jb, v, sizeof(jb));
-                    const uint32_t u0 = (w + P - jb.base % P) % P;
-                    ++cur;
-                    if (u0 < jb.nunits) {
-                        __builtin_memcpy(ctl + 2, v, sizeof(jb));
-                        ctl[1] = u0;
-                        state = 0u;
-                        break;
-                    }
-                }
-            }
-            ctl[0] = state;
-        }
-        __syncthreads();
-        const uint32_t state = ctl[0];
-        if (state == 2u)
-            return;
-        if (state == 1u) {
-            __syncthreads(); /* everyone has read ctl[0] before lane 0 rewrites it */
-            __builtin_amdgcn_s_sleep(4);
-            continue;
-        }
-        /* the job, wave-uniform (scalar registers: the kernel switch and every pointer are uniform branches / bases) */
-        uint32_t jw[sizeof(ResJob) / 4];
-#pragma unroll
-        for (uint32_t i = 0; i < sizeof(ResJob) / 4; ++i)
-            jw[i] = __builtin_amdgcn_readfirstlane(ctl[2 + i]);
-        ResJob jb;
-        __builtin_memcpy(&jb, jw, sizeof(jb));
-        const uint32_t u0 = __builtin_amdgcn_readfirstlane(ctl[1]);
-        __syncthreads(); /* ctl read by everyone: the units may overwrite it */
-        RES_STAMP(16);
-        const uint32_t e = (uint32_t)(jb.id % RES_RING);
-        if (threadIdx.x == 0) {
-            uint32_t go = 1u;
-            if (jb.after != 0u) {
-                /* a delivery: its open job's units must all be done (they never wait for this one) */
-                const uint32_t ea = (uint32_t)((jb.after - 1u) % RES_RING);
-                while (res_ld_dev64(&ds->fin[ea]) < jb.after) {
-                    if (wall_clock64() - born > 2u * lifetime_ticks + idle_ticks) {
-                        go = 0u; /* (only if the grid outlived its lifetime: leave, the job stays incomplete) */
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(2);
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); /* system scope: descriptors, inputs, keys as they are now */
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            RES_STAMP(17);
-            ctl[0] = go;
-        }
-        __syncthreads();
-        if (ctl[0] == 0u)
-            return;
-        if (threadIdx.x == 0)
-            atomicMax((unsigned long long *)&ds->first_c[e], ~(unsigned long long)wall_clock64());
-        __syncthreads(); /* ctl[0] read by everyone before the units overwrite it */
-        uint32_t mine = 0u;
-        RES_STAMP(18);
-        for (uint32_t u = u0; u < jb.nunits; u += P) {
-            res_unit(jb, u, lds, win_aes);
-            ++mine;
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* this wave's stores */
-        __syncthreads();
-        RES_STAMP(19);
-        if (threadIdx.x == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, ""); /* system scope: every unit's output, for the host */
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            RES_STAMP(20);
-            atomicMax((unsigned long long *)&ds->last[e], (unsigned long long)wall_clock64());
-            const uint32_t old = atomicAdd(&ds->done[e], mine);
-            if (old + mine == jb.nunits) {
-                /* the job's timeline into the ring (ptls_mi355x_resident_job_times), its atomics reset */
-                const uint64_t t1 = ~atomicExch((unsigned long long *)&ds->first_c[e], 0ull);
-                const uint64_t t2 = atomicExch((unsigned long long *)&ds->last[e], 0ull);
-                res_st_sys(&ring->times[e][1], t1);
-                res_st_sys(&ring->times[e][2], t2);
-                res_st_sys(&ring->times[e][3], (uint64_t)wall_clock64());
-                res_st_dev(&ds->done[e], 0u);
-                res_st_dev(&ds->fin[e], jb.id + 1u);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                res_st_sys(&ring->fin[e], jb.id + 1u);
-                atomicAdd((unsigned long long *)&ds->nfin, 1ull);
-            }
-            RES_STAMP(21);
-        }
-        __syncthreads();
-    }
+    deliver_body(recs, status, types, parts, blockIdx.x, blockIdx.y, gridDim.y, off, &ndone);
 }
 
 /* keys = GHASH steps of each record (its work), values = record index */
@@ -1832,8 +1413,6 @@ struct st_ptls_mi355x_aesgcm_context {
     bool work_ev_valid[WORK_SLOTS];
     hipEvent_t split_ev, scratch_ev;
     bool split_ev_valid, scratch_ev_valid;
-    /* resident jobs (ptls_mi355x_resident_*): 1 + the id of the context's last job, and of its last run job */
-    uint64_t res_last, res_runs_last;
 };
 
 struct st_ptls_mi355x_aes_context {
@@ -1864,20 +1443,33 @@ static size_t g_win16_records = SIZE_MAX;
 /* window batches of at most this many records use the split kernels, SPLIT_MAXRUN workgroups per record
  * (ptls_mi355x_set_split_records; SIZE_MAX = CU count / SPLIT_MAXRUN); they take precedence over the others */
 static size_t g_split_records = SIZE_MAX;
-/* single-record slot calls run as jobs of the resident grid (ptls_mi355x_set_slot_resident; initially the
- * environment's PTLS_MI355X_SLOT_RESIDENT, so unmodified C callers can be run either way) */
-static int slot_resident_env()
-{
-    const char *e = getenv("PTLS_MI355X_SLOT_RESIDENT");
-    return e != nullptr && atoi(e) != 0;
-}
-static int g_slot_resident = slot_resident_env();
 
 static int fail(const char *what, hipError_t e)
 {
     snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
     return -1;
 }
+
+/*
+ * Errors met where the API returns nothing (the free paths: ptls_fusion_aesgcm_free is void, include/picotls/fusion.h:
+ * 60).  A synchronisation there is where an asynchronous fault of earlier work surfaces; it is printed, kept for
+ * ptls_mi355x_device_check, and never dropped, so the next unrelated call is not the one blamed for it.
+ */
+static std::mutex g_deferred_mu;
+static char g_deferred[256];
+
+extern "C" void ptls_mi355x_defer_error(const char *what, int err)
+{
+    if (err == (int)hipSuccess)
+        return;
+    const char *msg = hipGetErrorString((hipError_t)err);
+    fprintf(stderr, "ptls_mi355x: %s: %s\n", what, msg);
+    std::lock_guard<std::mutex> lk(g_deferred_mu);
+    if (g_deferred[0] == 0)
+        snprintf(g_deferred, sizeof(g_deferred), "%s: %s", what, msg);
+}
+
+static void defer(const char *what, hipError_t e) { ptls_mi355x_defer_error(what, (int)e); }
 
 #define HIPCHK(call)                                                                                                   \
     do {                                                                                                               \
@@ -1998,9 +1590,9 @@ int ptls_mi355x_prepare_copies(void)
         if (st[i] != nullptr)
             (void)hipStreamDestroy(st[i]);
     if (dv != nullptr)
-        (void)hipFree(dv);
+        defer("prepare copies: hipFree", hipFree(dv));
     if (h != nullptr)
-        (void)hipHostFree(h);
+        defer("prepare copies: hipHostFree", hipHostFree(h));
     if (e != hipSuccess)
         return fail("prepare copies", e);
     d->copies_ready = true;
@@ -2015,14 +1607,14 @@ static int ensure_stage(DeviceShared *d, size_t need)
     size_t cap = d->cap ? d->cap : 4096;
     while (cap < need)
         cap *= 2;
+    d->cap = 0; /* (nothing is left half-freed for a later call if a free below fails) */
     if (d->d_stage)
-        (void)hipFree(d->d_stage);
-    if (d->h_stage)
-        (void)hipHostFree(d->h_stage);
+        HIPCHK(hipFree(d->d_stage));
     d->d_stage = nullptr;
+    if (d->h_stage)
+        HIPCHK(hipHostFree(d->h_stage));
     d->h_stage = nullptr;
     d->h_stage_dev = nullptr;
-    d->cap = 0;
     HIPCHK(hipMalloc(&d->d_stage, cap));
     /* coherent: the GPU's zero-copy reads never see stale cache lines of a previous call */
     HIPCHK(hipHostMalloc(&d->h_stage, cap, hipHostMallocMapped | hipHostMallocCoherent));
@@ -2149,209 +1741,6 @@ static LaunchPlan plan_launch(bool seal, bool frame, uint32_t key_size, size_t n
 
 static inline uint32_t le32(const uint8_t *p) { return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24; }
 
-/* ------------------------------------------------------------------ the resident grid, host side ----- */
-
-/* workers of a device's resident grid (ptls_mi355x_set_resident_workers; SIZE_MAX = half the CUs) */
-static size_t g_resident_workers = SIZE_MAX;
-/* the grid leaves after this long with nothing to do (ptls_mi355x_set_resident_idle_us) */
-static uint64_t g_resident_idle_us = 2000;
-/* and in any case after this long (a bound on every wave's life, whatever the host does; the environment's
- * PTLS_MI355X_RESIDENT_LIFETIME_S, read when a device's engine is created, shortens it for tests) */
-static const uint64_t RES_LIFETIME_S = 30;
-
-struct Resident {
-    std::mutex mu;                 /* posts and launches */
-    ResRing *ring = nullptr;       /* pinned, mapped, coherent */
-    ResRing *ring_dev = nullptr;   /* its device address */
-    ResDev *ds = nullptr;
-    hipStream_t stream = nullptr;  /* the grid's own: one instance at a time */
-    uint64_t first = 0;            /* the id of this engine's first job (ids go on across engines of a device) */
-    uint64_t next = 0, units = 0;  /* jobs and units posted */
-    uint32_t P = 0, epoch = 0;
-    uint64_t launches = 0;
-    uint64_t idle_ticks = 0, lifetime_ticks = 0;
-    uint64_t wclk_khz = 0;
-    const u32x4 *win_aes = nullptr;
-    ResCopy *cp = nullptr, *cp_dev = nullptr; /* copy jobs' ranges: RES_COPY_MAX per ring entry (pinned, mapped) */
-};
-
-static std::mutex g_res_mu;
-static Resident *g_res[64];
-static uint64_t g_res_next_id[64]; /* the next job id of a device's next engine (ptls_mi355x_resident_stop) */
-
-static inline uint64_t res_now_ns()
-{
-    timespec ts;
-    clock_gettime(CLOCK_MONOTONIC, &ts);
-    return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
-}
-
-/* the device's resident engine, created on first use (the device must be current) */
-static Resident *resident_of(int dev, DeviceShared *shared, int num_cu)
-{
-    if (dev < 0 || dev >= 64)
-        return nullptr;
-    std::lock_guard<std::mutex> lk(g_res_mu);
-    if (g_res[dev] != nullptr)
-        return g_res[dev];
-    Resident *r = new (std::nothrow) Resident();
-    if (r == nullptr)
-        return nullptr;
-    int wclk_khz = 0;
-    hipError_t e = hipDeviceGetAttribute(&wclk_khz, hipDeviceAttributeWallClockRate, dev);
-    if (e == hipSuccess)
-        e = hipHostMalloc((void **)&r->ring, sizeof(ResRing), hipHostMallocMapped | hipHostMallocCoherent);
-    if (e == hipSuccess) {
-        memset((void *)r->ring, 0, sizeof(ResRing));
-        e = hipHostGetDevicePointer((void **)&r->ring_dev, r->ring, 0);
-    }
-    if (e == hipSuccess)
-        e = hipMalloc(&r->ds, sizeof(ResDev));
-    if (e == hipSuccess)
-        e = hipMemset(r->ds, 0, sizeof(ResDev));
-    /* job ids continue where the device's previous engine stopped: an id below `first` is a job that is complete */
-    r->first = r->next = g_res_next_id[dev];
-    if (e == hipSuccess) {
-        const uint64_t start[2] = {r->first, r->first}; /* tail, nfin */
-        ((volatile ResRing *)r->ring)->tail = r->first;
-        e = hipMemcpy(r->ds, start, sizeof(start), hipMemcpyHostToDevice);
-    }
-    if (e == hipSuccess)
-        e = hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking);
-    if (e == hipSuccess)
-        e = hipHostMalloc((void **)&r->cp, sizeof(ResCopy) * RES_COPY_MAX * RES_RING,
-                          hipHostMallocMapped | hipHostMallocCoherent);
-    if (e == hipSuccess)
-        e = hipHostGetDevicePointer((void **)&r->cp_dev, r->cp, 0);
-    if (e != hipSuccess || wclk_khz <= 0) {
-        fail("resident grid setup", e);
-        if (r->cp)
-            (void)hipHostFree(r->cp);
-        if (r->ring)
-            (void)hipHostFree(r->ring);
-        if (r->ds)
-            (void)hipFree(r->ds);
-        delete r;
-        return nullptr;
-    }
-    const size_t want = g_resident_workers == SIZE_MAX ? (size_t)num_cu / 2 : g_resident_workers;
-    r->P = (uint32_t)(want < 1 ? 1 : want > (size_t)num_cu - 1 ? (size_t)num_cu - 1 : want);
-    r->idle_ticks = g_resident_idle_us * (uint64_t)wclk_khz / 1000u;
-    r->wclk_khz = (uint64_t)wclk_khz;
-    uint64_t life_s = RES_LIFETIME_S;
-    if (const char *env = getenv("PTLS_MI355X_RESIDENT_LIFETIME_S"))
-        life_s = strtoull(env, nullptr, 10) > 0 ? strtoull(env, nullptr, 10) : RES_LIFETIME_S;
-    r->lifetime_ticks = life_s * 1000ull * (uint64_t)wclk_khz;
-    r->win_aes = shared->d_win_aes;
-    g_res[dev] = r;
-    return r;
-}
-
-static inline bool res_done(const Resident *r, uint64_t id)
-{
-    return id < r->first || ((volatile const ResRing *)r->ring)->fin[id % RES_RING] >= id + 1u;
-}
-
-/* a new instance of the grid behind any still running on its stream (r->mu held) */
-static int res_launch(Resident *r)
-{
-    ((volatile ResRing *)r->ring)->alive = 1u;
-    ++r->epoch;
-    /* (the dispatcher waits for P x the instances launched so far, this one included, to have started) */
-    hipLaunchKernelGGL(mi355x_resident, dim3(r->P + 1u), dim3(SPLIT_THREADS), 0, r->stream, r->ring_dev, r->ds, r->win_aes,
-                       r->epoch, r->idle_ticks, r->lifetime_ticks, (uint64_t)r->P * (r->launches + 1u));
-    HIPCHK(hipGetLastError());
-    ++r->launches;
-    return 0;
-}
-
-/*
- * Waits for job id; relaunches the grid if it has left with the job not done (it looked for the job before the host
- * posted it and left: the post's alive check and the grid's re-check make that rare, this makes it harmless).
- */
-static int res_wait(Resident *r, uint64_t id)
-{
-    const uint64_t t0 = res_now_ns();
-    uint64_t checked = t0;
-    while (!res_done(r, id)) {
-        __builtin_ia32_pause();
-        const uint64_t t = res_now_ns();
-        if (t - checked > 200000u) {
-            checked = t;
-            std::lock_guard<std::mutex> lk(r->mu);
-            const hipError_t q = hipStreamQuery(r->stream);
-            if (q == hipSuccess && !res_done(r, id)) {
-                if (res_launch(r) != 0)
-                    return -1;
-            } else if (q != hipSuccess && q != hipErrorNotReady) {
-                return fail("resident grid", q);
-            }
-            (void)hipGetLastError();
-        }
-        if (t - t0 > 60ull * 1000000000ull) {
-            snprintf(g_err, sizeof(g_err), "resident job %llu: not complete after 60 s", (unsigned long long)id);
-            return -1;
-        }
-    }
-    std::atomic_thread_fence(std::memory_order_acquire);
-    return 0;
-}
-
-/*
- * Posts a job (units, pointers; id and base filled in here) and returns its id; launches the grid if none runs.
- * A context's runs share its split tickets: a context's previous run job is waited for first.
- */
-static int res_post(ptls_mi355x_aesgcm_context_t *ctx, ResJob jb, uint64_t *id_out,
-                    const ptls_mi355x_copy_t *copies = nullptr, size_t ncopies = 0)
-{
-    Resident *r = resident_of(ctx->device, ctx->shared, ctx->num_cu);
-    if (r == nullptr)
-        return -1;
-    std::lock_guard<std::mutex> lk(r->mu);
-    const uint64_t id = r->next;
-    const uint32_t e = (uint32_t)(id % RES_RING);
-    if (id >= r->first + RES_RING && !res_done(r, id - RES_RING)) {
-        r->mu.unlock(); /* (res_wait may relaunch under the lock) */
-        const int rc = res_wait(r, id - RES_RING);
-        r->mu.lock();
-        if (rc != 0)
-            return -1;
-    }
-    jb.id = id;
-    jb.base = (uint32_t)(r->units % r->P);
-    if (copies != nullptr) { /* the entry's ranges, read by the copy units through its device address */
-        ResCopy *c = r->cp + (size_t)e * RES_COPY_MAX;
-        uint64_t first = 0;
-        for (size_t i = 0; i < ncopies; ++i) {
-            c[i] = ResCopy{(uint64_t)(uintptr_t)copies[i].dst, (uint64_t)(uintptr_t)copies[i].src, copies[i].n, first};
-            first += (copies[i].n + RES_COPY_CHUNK - 1) / RES_COPY_CHUNK;
-        }
-        jb.descs = r->cp_dev + (size_t)e * RES_COPY_MAX;
-    }
-    volatile ResRing *ring = (volatile ResRing *)r->ring;
-    const uint64_t *w = (const uint64_t *)&jb;
-    volatile uint64_t *h = (volatile uint64_t *)&ring->jobs[e];
-    for (int i = 0; i < 16; ++i)
-        h[i] = w[i];
-    std::atomic_thread_fence(std::memory_order_release);
-    ring->tail = id + 1u;
-    r->next = id + 1u;
-    r->units += jb.nunits;
-    std::atomic_thread_fence(std::memory_order_seq_cst); /* the tail store before the alive load (the grid: the reverse) */
-    if (ring->alive == 0u && res_launch(r) != 0)
-        return -1;
-    *id_out = id;
-    return 0;
-}
-
-static int res_ctx_wait(ptls_mi355x_aesgcm_context_t *ctx, uint64_t id1)
-{
-    if (id1 == 0u)
-        return 0;
-    Resident *r = resident_of(ctx->device, ctx->shared, ctx->num_cu);
-    return r == nullptr ? -1 : res_wait(r, id1 - 1u);
-}
-
 /*
  * Records the split buffer (partials + tickets, 84 B a record) holds when it must hold n: at least 4096 (344 KiB), else
  * the next power of two.  Growing it frees the old buffer, which synchronises the whole device -- a coalescing record
@@ -2363,76 +1752,6 @@ static size_t split_cap_for(size_t n)
     while (cap < n)
         cap *= 2;
     return cap;
-}
-
-/* a run job (records x SPLIT_MAXRUN units) of a TLS window */
-static int res_runs(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void *static_iv12, const void *recs,
-                    const uint32_t *conn, size_t n, const uint8_t *src, uint8_t *dst, uint32_t *status, uint8_t *types,
-                    uint64_t *job, bool frame = true, const uint8_t *aad = nullptr)
-{
-    *job = PTLS_MI355X_RESIDENT_NONE;
-    if (n == 0)
-        return 0;
-    if (n > 0xffffffffull / SPLIT_MAXRUN) {
-        snprintf(g_err, sizeof(g_err), "resident window of %zu records", n);
-        return -1;
-    }
-    DeviceGuard guard(ctx->device);
-    /* the tickets of the context's previous run job, and of its stream launches, are free */
-    if (res_ctx_wait(ctx, ctx->res_runs_last) != 0)
-        return -1;
-    /* (the slot calls' own stream is idle between calls: each ends with its synchronisation, under the staging lock) */
-    if (ctx->home_set && !(ctx->home == ctx->shared->stream && !ctx->multi) &&
-        (ctx->multi ? (ctx->split_ev_valid ? hipEventSynchronize(ctx->split_ev) : hipSuccess)
-                    : hipStreamSynchronize(ctx->home)) != hipSuccess)
-        return fail("resident: the context's stream launches", hipGetLastError());
-    if (ctx->split_cap < n) {
-        if (ctx->d_split)
-            (void)hipFree(ctx->d_split);
-        ctx->d_split = nullptr;
-        ctx->split_cap = 0;
-        ctx->split_ev_valid = false;
-        const size_t cap = split_cap_for(n);
-        HIPCHK(hipMalloc(&ctx->d_split, cap * (SPLIT_PSLOTS * sizeof(u32x4) + sizeof(uint32_t))));
-        /* zero tickets before any job can use them: a blocking copy (the grid's stream is not ordered after the null
-         * stream, so an asynchronous memset there could still be running when the first units take tickets) */
-        void *zeros = calloc(cap, sizeof(uint32_t));
-        if (zeros == nullptr)
-            return fail("resident: tickets", hipErrorOutOfMemory);
-        const hipError_t ez = hipMemcpy((uint8_t *)ctx->d_split + cap * SPLIT_PSLOTS * sizeof(u32x4), zeros,
-                                        cap * sizeof(uint32_t), hipMemcpyHostToDevice);
-        free(zeros);
-        HIPCHK(ez);
-        ctx->split_cap = cap;
-    }
-    const uint8_t *iv = (const uint8_t *)static_iv12;
-    ResJob jb;
-    memset(&jb, 0, sizeof(jb));
-    jb.kind = (seal ? RES_SEAL : 0u) | (frame ? RES_FRAME : 0u) | (ctx->key_size == 32 ? RES_AES256 : 0u);
-    jb.nunits = (uint32_t)(n * SPLIT_MAXRUN);
-    jb.nrecs = (uint32_t)n;
-    jb.ki = ctx->d_ki;
-    jb.descs = recs;
-    jb.src = src;
-    jb.dst = dst;
-    jb.status = status;
-    jb.types = types;
-    jb.conn = conn;
-    jb.partials = ctx->d_split;
-    jb.tickets = (uint32_t *)((uint8_t *)ctx->d_split + ctx->split_cap * SPLIT_PSLOTS * sizeof(u32x4));
-    jb.parts = (const DeliverPart *)aad; /* (AEAD records: their AAD base) */
-    jb.iv0 = le32(iv);
-    jb.iv1 = le32(iv + 4);
-    jb.iv2 = le32(iv + 8);
-    /* after the context's previous job (the copy staging this window's input), if that is not complete yet */
-    Resident *r = resident_of(ctx->device, ctx->shared, ctx->num_cu);
-    if (r == nullptr)
-        return -1;
-    jb.after = ctx->res_last != 0u && !res_done(r, ctx->res_last - 1u) ? ctx->res_last : 0u;
-    if (res_post(ctx, jb, job) != 0)
-        return -1;
-    ctx->res_runs_last = ctx->res_last = *job + 1u;
-    return 0;
 }
 
 /* a launch of ctx on `stream` is about to use shared resources (see the context's stream-ordering note) */
@@ -2484,11 +1803,11 @@ static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void
     DeviceGuard guard(ctx->device);
     if (p.split != nullptr) {
         /* partials and tickets for n records (tickets are zero between launches: each record's last run resets its) */
-        if (ctx_stream(ctx, stream) != 0 || res_ctx_wait(ctx, ctx->res_runs_last) != 0)
+        if (ctx_stream(ctx, stream) != 0)
             return -1;
         if (ctx->split_cap < n) {
             if (ctx->d_split)
-                (void)hipFree(ctx->d_split); /* synchronises the device: no launch still uses it */
+                HIPCHK(hipFree(ctx->d_split)); /* synchronises the device: no launch still uses it */
             ctx->d_split = nullptr;
             ctx->split_cap = 0;
             ctx->split_ev_valid = false;
@@ -2553,7 +1872,7 @@ static int ensure_scratch(ptls_mi355x_aesgcm_context_t *ctx, size_t need, hipStr
         return 0;
     if (ctx->d_scratch) {
         HIPCHK(hipStreamSynchronize(stream)); /* the last use (ordered before this stream's queue above) is done */
-        (void)hipFree(ctx->d_scratch);
+        HIPCHK(hipFree(ctx->d_scratch));
     }
     ctx->d_scratch = nullptr;
     need = need < 2 * ctx->scratch_cap ? 2 * ctx->scratch_cap : need; /* (doubling: few growths, each a sync) */
@@ -2721,217 +2040,64 @@ Fail:
     return nullptr;
 }
 
-void ptls_mi355x_aesgcm_free(ptls_mi355x_aesgcm_context_t *ctx)
+int ptls_mi355x_aesgcm_release(ptls_mi355x_aesgcm_context_t *ctx)
 {
     if (ctx == nullptr)
-        return;
+        return 0;
     DeviceGuard guard(ctx->device);
-    (void)res_ctx_wait(ctx, ctx->res_last); /* resident jobs of the context */
-    (void)hipDeviceSynchronize(); /* launches on caller streams may still read the key image */
+    int rc = 0;
+    auto chk = [&](const char *what, hipError_t e) {
+        if (e != hipSuccess && rc == 0)
+            rc = fail(what, e);
+        defer(what, e);
+    };
+    /* launches on caller streams may still read the key image; a fault of any earlier work surfaces here */
+    chk("context free: hipDeviceSynchronize", hipDeviceSynchronize());
     if (ctx->d_ki) {
-        (void)hipMemset(ctx->d_ki, 0, sizeof(KeyImage)); /* clear key material, as ptls_fusion_aesgcm_free does */
-        (void)hipFree(ctx->d_ki);
+        /* clear key material, as ptls_fusion_aesgcm_free does; ordered before the free on the null stream */
+        chk("context free: clearing the key image", hipMemsetAsync(ctx->d_ki, 0, sizeof(KeyImage), nullptr));
+        chk("context free: hipStreamSynchronize", hipStreamSynchronize(nullptr));
+        chk("context free: hipFree(key image)", hipFree(ctx->d_ki));
     }
     if (ctx->d_work)
-        (void)hipFree(ctx->d_work);
+        chk("context free: hipFree(work counters)", hipFree(ctx->d_work));
     if (ctx->d_scratch)
-        (void)hipFree(ctx->d_scratch);
+        chk("context free: hipFree(scratch)", hipFree(ctx->d_scratch));
     if (ctx->d_split)
-        (void)hipFree(ctx->d_split);
+        chk("context free: hipFree(split buffer)", hipFree(ctx->d_split));
     for (uint32_t i = 0; i < WORK_SLOTS; ++i)
         if (ctx->work_ev[i])
-            (void)hipEventDestroy(ctx->work_ev[i]);
+            chk("context free: hipEventDestroy", hipEventDestroy(ctx->work_ev[i]));
     if (ctx->split_ev)
-        (void)hipEventDestroy(ctx->split_ev);
+        chk("context free: hipEventDestroy", hipEventDestroy(ctx->split_ev));
     if (ctx->scratch_ev)
-        (void)hipEventDestroy(ctx->scratch_ev);
+        chk("context free: hipEventDestroy", hipEventDestroy(ctx->scratch_ev));
     free(ctx);
-}
-
-int ptls_mi355x_aesgcm_device(const ptls_mi355x_aesgcm_context_t *ctx) { return ctx->device; }
-
-/* ------------------------------------------------------------------------ resident grid (section 7) ---- */
-
-int ptls_mi355x_resident_tls_seal_records_multi(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12,
-                                                const ptls_mi355x_tls_record_t *recs, const uint32_t *conn_ids, size_t n,
-                                                const uint8_t *src, uint8_t *dst, uint64_t *job)
-{
-    return res_runs(ctx, true, static_iv12, recs, conn_ids, n, src, dst, nullptr, nullptr, job);
-}
-
-int ptls_mi355x_resident_tls_open_records_multi(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12,
-                                                const ptls_mi355x_tls_record_t *recs, const uint32_t *conn_ids, size_t n,
-                                                const uint8_t *src, uint8_t *dst, uint32_t *status, uint8_t *types,
-                                                uint64_t *job)
-{
-    if (n != 0 && (status == nullptr || types == nullptr)) {
-        snprintf(g_err, sizeof(g_err), "tls_open_records needs status and types");
-        return -1;
-    }
-    return res_runs(ctx, false, static_iv12, recs, conn_ids, n, src, dst, status, types, job);
-}
-
-int ptls_mi355x_resident_tls_deliver_records(ptls_mi355x_aesgcm_context_t *ctx, const ptls_mi355x_tls_record_t *recs,
-                                             const uint32_t *status, const uint8_t *types,
-                                             const ptls_mi355x_tls_deliver_t *parts, size_t nparts, size_t max_records,
-                                             uint64_t *job)
-{
-    *job = PTLS_MI355X_RESIDENT_NONE;
-    if (nparts == 0)
-        return 0;
-    if (max_records > DELIVER_MAX || nparts > 65535) {
-        snprintf(g_err, sizeof(g_err), "deliver: more than %u records in a part, or too many parts", DELIVER_MAX);
-        return -1;
-    }
-    DeviceGuard guard(ctx->device);
-    const uint32_t groups = (uint32_t)(max_records < 64 ? (max_records ? max_records : 1) : 64); /* a record per group */
-    ResJob jb;
-    memset(&jb, 0, sizeof(jb));
-    jb.kind = RES_DELIVER;
-    jb.nunits = (uint32_t)nparts * groups;
-    jb.nrecs = groups;
-    jb.descs = recs;
-    jb.status = (uint32_t *)status;
-    jb.types = (uint8_t *)types;
-    jb.parts = (const DeliverPart *)parts;
-    /* after the context's previous job (the open job whose slots it delivers), if that is not complete yet */
-    Resident *r = resident_of(ctx->device, ctx->shared, ctx->num_cu);
-    if (r == nullptr)
-        return -1;
-    jb.after = ctx->res_last != 0u && !res_done(r, ctx->res_last - 1u) ? ctx->res_last : 0u;
-    if (res_post(ctx, jb, job) != 0)
-        return -1;
-    ctx->res_last = *job + 1u;
-    return 0;
-}
-
-int ptls_mi355x_resident_copy(ptls_mi355x_aesgcm_context_t *ctx, const ptls_mi355x_copy_t *ranges, size_t n,
-                              uint64_t *job)
-{
-    *job = PTLS_MI355X_RESIDENT_NONE;
-    if (n > RES_COPY_MAX) {
-        snprintf(g_err, sizeof(g_err), "resident copy of %zu ranges (at most %u)", n, RES_COPY_MAX);
-        return -1;
-    }
-    uint64_t chunks = 0;
-    for (size_t i = 0; i < n; ++i)
-        chunks += (ranges[i].n + RES_COPY_CHUNK - 1) / RES_COPY_CHUNK;
-    if (chunks == 0)
-        return 0;
-    if (chunks > 0xffffffffull) {
-        snprintf(g_err, sizeof(g_err), "resident copy too large");
-        return -1;
-    }
-    DeviceGuard guard(ctx->device);
-    ResJob jb;
-    memset(&jb, 0, sizeof(jb));
-    jb.kind = RES_COPY;
-    jb.nunits = (uint32_t)chunks;
-    jb.nrecs = (uint32_t)n;
-    if (res_post(ctx, jb, job, ranges, n) != 0)
-        return -1;
-    ctx->res_last = *job + 1u;
-    return 0;
-}
-
-int ptls_mi355x_set_slot_resident(int on)
-{
-    const int prev = g_slot_resident;
-    g_slot_resident = on != 0;
-    return prev;
-}
-
-int ptls_mi355x_resident_done(ptls_mi355x_aesgcm_context_t *ctx, uint64_t job)
-{
-    if (job == PTLS_MI355X_RESIDENT_NONE)
-        return 1;
-    Resident *r = resident_of(ctx->device, ctx->shared, ctx->num_cu);
-    return r == nullptr ? -1 : res_done(r, job) ? 1 : 0;
-}
-
-int ptls_mi355x_resident_wait(ptls_mi355x_aesgcm_context_t *ctx, uint64_t job)
-{
-    if (job == PTLS_MI355X_RESIDENT_NONE)
-        return 0;
-    Resident *r = resident_of(ctx->device, ctx->shared, ctx->num_cu);
-    return r == nullptr ? -1 : res_wait(r, job);
-}
-
-int ptls_mi355x_resident_stop(int device)
-{
-    if (device < 0 || device >= 64)
-        return -1;
-    Resident *r;
-    {
-        std::lock_guard<std::mutex> lk(g_res_mu);
-        r = g_res[device];
-        g_res[device] = nullptr;
-    }
-    if (r == nullptr)
-        return 0;
-    DeviceGuard guard(device);
-    int rc = r->next != r->first ? res_wait(r, r->next - 1u) : 0; /* every posted job */
-    g_res_next_id[device] = r->next;
-    ((volatile ResRing *)r->ring)->stop = 1u;
-    const hipError_t e = hipStreamSynchronize(r->stream);
-    if (e != hipSuccess)
-        rc = fail("resident grid", e);
-    (void)hipStreamDestroy(r->stream);
-    (void)hipHostFree(r->cp);
-    (void)hipHostFree(r->ring);
-    (void)hipFree(r->ds);
-    delete r;
     return rc;
 }
 
-int ptls_mi355x_resident_job_times(ptls_mi355x_aesgcm_context_t *ctx, uint64_t job, uint64_t ns[4])
+void ptls_mi355x_aesgcm_free(ptls_mi355x_aesgcm_context_t *ctx) { (void)ptls_mi355x_aesgcm_release(ctx); }
+
+int ptls_mi355x_device_check(void)
 {
-    Resident *r = resident_of(ctx->device, ctx->shared, ctx->num_cu);
-    if (r == nullptr || job < r->first || job >= r->next)
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    const hipError_t s = hipDeviceSynchronize();
+    const hipError_t l = hipGetLastError();
+    std::lock_guard<std::mutex> lk(g_deferred_mu);
+    if (g_deferred[0] != 0) {
+        snprintf(g_err, sizeof(g_err), "%s", g_deferred);
+        g_deferred[0] = 0;
         return -1;
-    const volatile ResRing *ring = (const volatile ResRing *)r->ring;
-    const uint32_t e = (uint32_t)(job % RES_RING);
-    uint64_t t[4];
-    for (int i = 0; i < 4; ++i)
-        t[i] = ring->times[e][i];
-    if (ring->fin[e] != job + 1u) /* not complete, or the entry holds a later job by now */
-        return -1;
-    const uint64_t k = r->wclk_khz;
-    ns[0] = (t[1] - t[0]) * 1000000u / k; /* published -> first unit started */
-    ns[1] = (t[2] - t[1]) * 1000000u / k; /* first unit started -> last unit ended */
-    ns[2] = (t[3] - t[2]) * 1000000u / k; /* last unit ended -> complete */
-    ns[3] = (t[3] - t[0]) * 1000000u / k; /* published -> complete */
+    }
+    if (s != hipSuccess)
+        return fail("hipDeviceSynchronize", s);
+    if (l != hipSuccess)
+        return fail("pending HIP error", l);
     return 0;
 }
 
-uint64_t ptls_mi355x_resident_jobs(int device)
-{
-    std::lock_guard<std::mutex> lk(g_res_mu);
-    if (device < 0 || device >= 64)
-        return 0;
-    return g_res[device] != nullptr ? g_res[device]->next : g_res_next_id[device];
-}
-
-uint64_t ptls_mi355x_resident_launches(int device)
-{
-    std::lock_guard<std::mutex> lk(g_res_mu);
-    return device >= 0 && device < 64 && g_res[device] != nullptr ? g_res[device]->launches : 0u;
-}
-
-size_t ptls_mi355x_set_resident_workers(size_t n)
-{
-    const size_t prev = g_resident_workers;
-    g_resident_workers = n;
-    return prev;
-}
-
-uint64_t ptls_mi355x_set_resident_idle_us(uint64_t us)
-{
-    const uint64_t prev = g_resident_idle_us;
-    g_resident_idle_us = us;
-    return prev;
-}
-
+int ptls_mi355x_aesgcm_device(const ptls_mi355x_aesgcm_context_t *ctx) { return ctx->device; }
 
 int ptls_mi355x_seal_batch(ptls_mi355x_aesgcm_context_t *ctx, const void *static_iv12, const ptls_mi355x_record_t *recs,
                            size_t n, const uint8_t *src, uint8_t *dst, const uint8_t *aad, void *stream)
@@ -3135,17 +2301,6 @@ static int single_record(ptls_mi355x_aesgcm_context_t *ctx, bool seal, void *out
      */
     const bool zc = total <= g_slot_zero_copy_bytes;
     uint8_t *base = zc ? d->h_stage_dev : d->d_stage;
-    if (zc && g_slot_resident) {
-        /* a job of the resident grid on the staging (no launch, no stream synchronisation: section 6) */
-        uint64_t job;
-        if (res_runs(ctx, seal, nonce12, base, nullptr, 1, base, base, (uint32_t *)(base + off_status), nullptr, &job,
-                     false, base) != 0 ||
-            res_ctx_wait(ctx, job + 1u) != 0) {
-            memset(d->h_stage, 0, total);
-            return -1;
-        }
-        return finish_single(d, seal, output, inlen, off_data, off_status, total);
-    }
     if (!zc)
         HIPCHK(hipMemcpyAsync(d->d_stage, d->h_stage, off_status, hipMemcpyHostToDevice, d->stream));
     /* one record: the window kernels (8-lane segments in parallel, leading pad steps skipped) are as fast as the
@@ -3268,9 +2423,10 @@ void ptls_mi355x_aes_free(ptls_mi355x_aes_context_t *ctx)
         return;
     DeviceGuard guard(ctx->device);
     if (ctx->d_keys) {
-        (void)hipDeviceSynchronize();
-        (void)hipMemset(ctx->d_keys, 0, sizeof(AesKeys));
-        (void)hipFree(ctx->d_keys);
+        defer("cipher free: hipDeviceSynchronize", hipDeviceSynchronize());
+        defer("cipher free: clearing the round keys", hipMemsetAsync(ctx->d_keys, 0, sizeof(AesKeys), nullptr));
+        defer("cipher free: hipStreamSynchronize", hipStreamSynchronize(nullptr));
+        defer("cipher free: hipFree", hipFree(ctx->d_keys));
     }
     free(ctx);
 }

@@ -50,6 +50,7 @@
 #include <string.h>
 #include <time.h>
 #include <stdio.h>
+#include <pthread.h>
 #include <hip/hip_runtime_api.h>
 #include "../../include/ptls_mi355x.h"
 
@@ -58,12 +59,16 @@
 #define RL_SLOTS 4    /* launches in flight per layer */
 #define RL_TICKETS 32 /* windows outstanding per layer (submitted and not yet waited for) */
 #define RL_COALESCE_DEFAULT 16 /* a connection's queued windows per launch (ptls_mi355x_record_layer_set_coalesce) */
+/* a coalescing slot's staging grows with headroom for larger groups of the same windows (no allocation stall
+ * mid-stream), but never more than this beyond what the op needs: pinned memory per connection stays bounded for
+ * servers with hundreds of connections (4 slots x (need + 2 MiB) at most) */
+#define RL_STAGE_HEADROOM ((size_t)2 << 20)
 
 typedef struct {
     uint8_t *base; /* host address as registered */
     uint8_t *dev;  /* its device address */
     size_t len;
-    int owned;     /* registered by this layer (not already registered, e.g. by the other direction's layer) */
+    int owned;     /* holds a reference on the process-wide entry (g_reg) of the range */
 } rl_region_t;
 
 /* one layer's part of a window */
@@ -102,8 +107,6 @@ typedef struct {
     rl_part_t *part;
     int direct, zero_copy, dma; /* direct: the results land in the caller's buffers (mapped or dma) */
     int deliver;                /* mapped open: slots in device memory, the delivery kernel writes the plaintexts */
-    int resident;               /* run as jobs of the device's resident grid (set_resident; zero-copy windows only) */
-    uint64_t rjob;              /* resident: its last job (the delivery, or the runs) */
     int dma_in;                 /* direct, the inputs moved to device memory by DMA first (set_direct_dma 2) */
     size_t nrec, off_src, srcbytes, off_dst, dstbytes, off_st, off_ty, off_dp, max_part;
     rl_copy_t *h2d, *d2h; /* dma: registered host ranges <-> the slot's device buffer */
@@ -135,7 +138,6 @@ struct st_ptls_mi355x_record_layer_t {
     size_t zero_copy_bytes;
     int direct_dma; /* registered windows move by DMA to and from device memory (1), are read in place (0, default), or
                      * the inputs move by DMA and the outputs are written in place (2) */
-    int resident;   /* windows without copies run on the resident grid (ptls_mi355x_record_layer_set_resident) */
     rl_region_t reg[RL_MAX_REGIONS];
     size_t nreg;
     rl_slot_t slot[RL_SLOTS];
@@ -155,8 +157,6 @@ struct st_ptls_mi355x_record_layer_t {
     int corked;                       /* windows queue even while nothing runs (ptls_mi355x_record_layer_cork) */
     struct rl_queued *queue;          /* coalesce entries */
     size_t nqueued;
-    int queue_is_seal;
-    uint8_t queue_type;
     uint64_t queue_ticket;            /* ticket of queue[0] */
 };
 
@@ -169,9 +169,16 @@ struct rl_queued {
     void *out;
     size_t capacity;
     uint64_t seq0; /* seal: seq of its first record; open: the speculative seq its records take */
+    int is_seal;
+    uint8_t type; /* seal: the content type its records carry (a group never mixes types: rl_flush_n) */
 };
 
 static char rl_err[160];
+
+/* gcm_engine.hip: an error met where nothing can be returned (a free path) -- printed and kept for
+ * ptls_mi355x_device_check, never dropped */
+void ptls_mi355x_defer_error(const char *what, int err);
+#define RL_DEFER(what, call) ptls_mi355x_defer_error("record layer: " what, (int)(call))
 
 static void op_discard(rl_op_t *op);
 static void op_release_layers(rl_op_t *op);
@@ -239,14 +246,20 @@ static int reserve_stage(rl_slot_t *s, size_t bytes)
     if (bytes <= s->cap)
         return 0;
     size_t c = s->cap ? s->cap : 1 << 16;
-    if (s->grow > 1)
-        bytes *= s->grow;
+    if (s->grow > 1) { /* headroom for a larger group later, at most RL_STAGE_HEADROOM beyond the need */
+        const size_t want = bytes * s->grow, most = bytes + RL_STAGE_HEADROOM;
+        bytes = want < most ? want : most;
+    }
     while (c < bytes)
         c *= 2;
     hipError_t e;
     if (s->h_buf != NULL) {
         memset(s->h_buf, 0, s->cap);
-        (void)hipHostFree(s->h_buf);
+        const hipError_t ef = hipHostFree(s->h_buf);
+        s->h_buf = s->h_dev = NULL;
+        s->cap = 0;
+        if (ef != hipSuccess)
+            return rl_fail("hipHostFree (staging growth)", ef);
     }
     s->h_buf = s->h_dev = NULL;
     s->cap = 0;
@@ -267,8 +280,14 @@ static int reserve_device(rl_slot_t *s)
         return 0;
     hipError_t e;
     if (s->d_buf != NULL) {
-        (void)hipMemset(s->d_buf, 0, s->d_cap);
-        (void)hipFree(s->d_buf);
+        hipError_t ef = hipMemsetAsync(s->d_buf, 0, s->d_cap, s->stream);
+        if (ef == hipSuccess)
+            ef = hipStreamSynchronize(s->stream);
+        const hipError_t ef2 = hipFree(s->d_buf);
+        s->d_buf = NULL;
+        s->d_cap = 0;
+        if (ef != hipSuccess || ef2 != hipSuccess)
+            return rl_fail("clearing and freeing the device buffer (growth)", ef != hipSuccess ? ef : ef2);
     }
     s->d_buf = NULL;
     s->d_cap = 0;
@@ -295,27 +314,26 @@ static int slot_ready(ptls_mi355x_record_layer_t *rl, rl_slot_t *s)
     return 0;
 }
 
-/* the slot's launches are done: its stream's, and its op's resident jobs */
+/* the slot's launches are done */
 static void slot_sync(rl_slot_t *s)
 {
     if (s->stream != NULL)
-        (void)hipStreamSynchronize(s->stream);
-    if (s->ctx != NULL && s->op.busy && s->op.resident)
-        (void)ptls_mi355x_resident_wait(s->ctx, s->op.rjob);
+        RL_DEFER("slot synchronisation", hipStreamSynchronize(s->stream));
 }
 
 static void slot_release(rl_slot_t *s)
 {
     slot_sync(s);
+    if (s->d_buf != NULL) { /* cleared on the slot's stream, before that stream goes */
+        RL_DEFER("clearing the device buffer", hipMemsetAsync(s->d_buf, 0, s->d_cap, s->stream));
+        RL_DEFER("slot synchronisation", hipStreamSynchronize(s->stream));
+        RL_DEFER("hipFree (device buffer)", hipFree(s->d_buf));
+    }
     if (s->stream != NULL)
-        (void)hipStreamDestroy(s->stream);
+        RL_DEFER("hipStreamDestroy", hipStreamDestroy(s->stream));
     if (s->h_buf != NULL) {
         memset(s->h_buf, 0, s->cap); /* plaintexts passed through the staging */
-        (void)hipHostFree(s->h_buf);
-    }
-    if (s->d_buf != NULL) {
-        (void)hipMemset(s->d_buf, 0, s->d_cap);
-        (void)hipFree(s->d_buf);
+        RL_DEFER("hipHostFree (staging)", hipHostFree(s->h_buf));
     }
     free(s->recs);
     ptls_mi355x_aesgcm_free(s->ctx);
@@ -427,7 +445,7 @@ int ptls_mi355x_record_layer_rekey(ptls_mi355x_record_layer_t *rl, const void *k
         rl_slot_t *s = &rl->slot[i];
         if (s->ctx != NULL) {
             if (s->stream != NULL)
-                (void)hipStreamSynchronize(s->stream);
+                RL_DEFER("rekey: slot synchronisation", hipStreamSynchronize(s->stream));
             ptls_mi355x_aesgcm_free(s->ctx);
             s->ctx = NULL;
         }
@@ -439,13 +457,6 @@ int ptls_mi355x_record_layer_rekey(ptls_mi355x_record_layer_t *rl, const void *k
     memcpy(rl->iv, iv12, 12);
     rl->seq = rl->spec_seq = 0; /* a new traffic key starts at record 0 (setup_traffic_protection, lib/picotls.c:1217) */
     return 0;
-}
-
-int ptls_mi355x_record_layer_set_resident(ptls_mi355x_record_layer_t *rl, int on)
-{
-    const int prev = rl->resident;
-    rl->resident = on != 0;
-    return prev;
 }
 
 int ptls_mi355x_record_layer_set_direct_dma(ptls_mi355x_record_layer_t *rl, int on)
@@ -462,25 +473,77 @@ size_t ptls_mi355x_record_layer_set_zero_copy_bytes(ptls_mi355x_record_layer_t *
     return prev;
 }
 
+/*
+ * Host ranges registered through the layers, process-wide and counted: the first layer to register a range maps it
+ * (hipHostRegister), the others share that mapping, and it is unmapped when the LAST of them lets go.  Two layers
+ * share ranges whenever the two directions of a connection use the same socket buffers; with a per-layer "first one
+ * owns it" rule the owner's free unmapped a range the other layer still ran windows on, and those kernels then
+ * faulted on the unmapped host addresses.  A range the application registered itself (hipHostRegister answers
+ * already-registered and the table does not hold it) is used and never unregistered here.
+ */
+typedef struct {
+    uint8_t *base, *dev;
+    size_t len;
+    int refs;  /* layers holding it */
+    int owned; /* mapped by this table (else the application's: never unmapped here) */
+} rl_shared_range_t;
+
+#define RL_MAX_SHARED 1024
+static pthread_mutex_t g_reg_mu = PTHREAD_MUTEX_INITIALIZER;
+static rl_shared_range_t g_reg[RL_MAX_SHARED];
+static size_t g_nreg;
+
+/* the table entry of the range starting at base, or NULL (g_reg_mu held) */
+static rl_shared_range_t *shared_range(const void *base)
+{
+    for (size_t i = 0; i < g_nreg; ++i)
+        if (g_reg[i].base == base)
+            return &g_reg[i];
+    return NULL;
+}
+
 int ptls_mi355x_record_layer_register(ptls_mi355x_record_layer_t *rl, void *base, size_t len)
 {
     if (rl->nreg == RL_MAX_REGIONS || base == NULL || len == 0)
         return rl_msg(base == NULL || len == 0 ? "empty range" : "too many ranges");
+    for (size_t i = 0; i < rl->nreg; ++i)
+        if (rl->reg[i].base == base)
+            return rl_msg("range already registered with this layer");
+    pthread_mutex_lock(&g_reg_mu);
+    rl_shared_range_t *sr = shared_range(base);
+    if (sr != NULL && sr->len >= len) { /* mapped already (by another layer): shared */
+        ++sr->refs;
+        rl->reg[rl->nreg++] = (rl_region_t){(uint8_t *)base, sr->dev, len, 1};
+        pthread_mutex_unlock(&g_reg_mu);
+        return 0;
+    }
+    if (sr == NULL && g_nreg == RL_MAX_SHARED) {
+        pthread_mutex_unlock(&g_reg_mu);
+        return rl_msg("too many registered ranges in the process");
+    }
     hipError_t e;
     uint8_t *dev = NULL;
     int owned = 1;
     if ((e = hipHostRegister(base, len, hipHostRegisterMapped)) == hipErrorHostMemoryAlreadyRegistered) {
         (void)hipGetLastError();
-        owned = 0; /* a range the application (or another layer) registered: used, never unregistered here */
+        owned = 0; /* registered by the application (or overlapping a range mapped here): used, never unmapped here */
     } else if (e != hipSuccess) {
+        pthread_mutex_unlock(&g_reg_mu);
         return rl_fail("hipHostRegister", e);
     }
     if ((e = hipHostGetDevicePointer((void **)&dev, base, 0)) != hipSuccess) {
         if (owned)
-            (void)hipHostUnregister(base);
+            RL_DEFER("hipHostUnregister (after a failed registration)", hipHostUnregister(base));
+        pthread_mutex_unlock(&g_reg_mu);
         return rl_fail("hipHostGetDevicePointer", e);
     }
-    rl->reg[rl->nreg++] = (rl_region_t){(uint8_t *)base, dev, len, owned};
+    if (sr == NULL) {
+        g_reg[g_nreg++] = (rl_shared_range_t){(uint8_t *)base, dev, len, 1, owned};
+        rl->reg[rl->nreg++] = (rl_region_t){(uint8_t *)base, dev, len, 1};
+    } else { /* a longer range over a shorter one mapped here: the application's, or unmappable; not counted */
+        rl->reg[rl->nreg++] = (rl_region_t){(uint8_t *)base, dev, len, 0};
+    }
+    pthread_mutex_unlock(&g_reg_mu);
     return 0;
 }
 
@@ -493,11 +556,17 @@ int ptls_mi355x_record_layer_unregister(ptls_mi355x_record_layer_t *rl, void *ba
                     slot_sync(&rl->slot[k]);
             /* nor a window of another layer that names this one (its kernels may address the range): the device */
             if (rl->inflight != 0)
-                (void)hipDeviceSynchronize();
-            hipError_t e = rl->reg[i].owned ? hipHostUnregister(base) : hipSuccess;
-            if (e == hipErrorHostMemoryNotRegistered) { /* registered twice, already released by the other owner */
-                (void)hipGetLastError();
-                e = hipSuccess;
+                RL_DEFER("unregister: hipDeviceSynchronize", hipDeviceSynchronize());
+            hipError_t e = hipSuccess;
+            if (rl->reg[i].owned) { /* holds a reference on the shared entry */
+                pthread_mutex_lock(&g_reg_mu);
+                rl_shared_range_t *sr = shared_range(base);
+                if (sr != NULL && --sr->refs == 0) {
+                    if (sr->owned)
+                        e = hipHostUnregister(base);
+                    *sr = g_reg[--g_nreg];
+                }
+                pthread_mutex_unlock(&g_reg_mu);
             }
             rl->reg[i] = rl->reg[--rl->nreg];
             return e == hipSuccess ? 0 : rl_fail("hipHostUnregister", e);
@@ -675,22 +744,6 @@ static int op_launch(rl_slot_t *s, const uint8_t *src_base, uint8_t *dst_base)
     const uint32_t *conn = op->nlayers > 1 ? (const uint32_t *)(base + up16(op->nrec * sizeof(ptls_mi355x_tls_record_t))) : NULL;
     hipError_t e;
     int rc;
-    /* resident: no launch -- the window's runs (and its delivery) become jobs of the device's persistent grid */
-    op->resident = op->layers[0]->resident && op->zero_copy && !op->dma && !op->dma_in;
-    if (op->resident) {
-        const ptls_mi355x_tls_record_t *recs = (const ptls_mi355x_tls_record_t *)base;
-        if (op->is_seal)
-            rc = ptls_mi355x_resident_tls_seal_records_multi(s->ctx, op->layers[0]->iv, recs, conn, op->nrec, src, dst,
-                                                            &op->rjob);
-        else
-            rc = ptls_mi355x_resident_tls_open_records_multi(s->ctx, op->layers[0]->iv, recs, conn, op->nrec, src, dst,
-                                                            (uint32_t *)(base + op->off_st), base + op->off_ty, &op->rjob);
-        if (rc == 0 && op->deliver)
-            rc = ptls_mi355x_resident_tls_deliver_records(s->ctx, recs, (uint32_t *)(base + op->off_st), base + op->off_ty,
-                                                          (const ptls_mi355x_tls_deliver_t *)(base + op->off_dp),
-                                                          op->nlayers, op->max_part, &op->rjob);
-        return rc != 0 ? rl_msg(ptls_mi355x_last_error()) : 0;
-    }
     /* the runtime's one-time copy setup, before the first copy rather than inside some later window's */
     if ((!op->zero_copy || op->nh2d != 0 || op->nd2h != 0) && !s->copies_prepared) {
         if (ptls_mi355x_prepare_copies() != 0)
@@ -834,10 +887,9 @@ static int seal_build(rl_slot_t *s, ptls_mi355x_record_layer_t *const *layers, s
                 overlap |= overlaps(frags[l][f].base, frags[l][f].len, out[m], op->part[m].wire);
         }
     }
-    const int dma = direct && layers[0]->direct_dma == 1 && !layers[0]->resident;
+    const int dma = direct && layers[0]->direct_dma == 1;
     /* DMA in: the fragments copied into device memory (one copy per contiguous run) first, the wire written in place */
-    /* (resident layers read in place: staging the inputs by the grid's own copy jobs measured slower) */
-    const int dma_in = direct && layers[0]->direct_dma == PTLS_MI355X_RECORD_LAYER_DMA_IN && !layers[0]->resident;
+    const int dma_in = direct && layers[0]->direct_dma == PTLS_MI355X_RECORD_LAYER_DMA_IN;
     if (direct && !dma && !dma_in && overlap)
         direct = 0;
     const int packed = !direct || dma; /* fragments and records back to back in the staging / device layout */
@@ -974,7 +1026,7 @@ static int open_build(rl_slot_t *s, ptls_mi355x_record_layer_t *const *layers, s
             dst_base = dout;
     }
     /* (the input reaches the device before any output is written) */
-    const int dma = direct && layers[0]->direct_dma == 1 && !layers[0]->resident;
+    const int dma = direct && layers[0]->direct_dma == 1;
     size_t max_part = 0;
     for (size_t l = 0; l < nlayers; ++l)
         max_part = op->part[l].n > max_part ? op->part[l].n : max_part;
@@ -984,7 +1036,7 @@ static int open_build(rl_slot_t *s, ptls_mi355x_record_layer_t *const *layers, s
     if (direct && !dma && !deliver && overlap)
         direct = 0;
     /* DMA in: the records copied into device memory (one copy per contiguous run of inputs) before the launch */
-    const int dma_in = deliver && layers[0]->direct_dma == PTLS_MI355X_RECORD_LAYER_DMA_IN && !layers[0]->resident;
+    const int dma_in = deliver && layers[0]->direct_dma == PTLS_MI355X_RECORD_LAYER_DMA_IN;
     const int packed = !direct || dma;
     op->direct = direct;
     op->dma = dma;
@@ -1075,9 +1127,7 @@ static int rl_busy(ptls_mi355x_record_layer_t *rl)
     int busy = 0;
     for (int i = 0; i < RL_SLOTS && !busy; ++i) {
         const rl_slot_t *s = &rl->slot[i];
-        busy = s->op.busy && !s->op.done && s->op.nrec != 0 &&
-               (s->op.resident ? ptls_mi355x_resident_done(s->ctx, s->op.rjob) == 0
-                               : hipStreamQuery(s->stream) == hipErrorNotReady);
+        busy = s->op.busy && !s->op.done && s->op.nrec != 0 && hipStreamQuery(s->stream) == hipErrorNotReady;
     }
     (void)hipGetLastError(); /* (hipErrorNotReady is an answer, not an error to leave behind) */
     return busy;
@@ -1136,6 +1186,14 @@ static int rl_flush_n(ptls_mi355x_record_layer_t *rl, size_t n)
         n = rl->nqueued;
     if (n == 0 || rl->slot[rl->launches % RL_SLOTS].op.busy)
         return 0;
+    /* one op seals one content type (one direction): the group ends where the queue's next window differs */
+    const int is_seal = rl->queue[0].is_seal;
+    const uint8_t type = rl->queue[0].type;
+    for (size_t i = 1; i < n; ++i)
+        if (rl->queue[i].is_seal != is_seal || rl->queue[i].type != type) {
+            n = i;
+            break;
+        }
     ptls_mi355x_record_layer_t *layers[RL_TICKETS];
     const ptls_mi355x_iovec_t *frags[RL_TICKETS];
     size_t nfrags[RL_TICKETS], capacity[RL_TICKETS], inlen[RL_TICKETS], parsed[RL_TICKETS];
@@ -1151,7 +1209,6 @@ static int rl_flush_n(ptls_mi355x_record_layer_t *rl, size_t n)
         out[i] = q->out;
         capacity[i] = q->capacity;
     }
-    const int is_seal = rl->queue_is_seal;
     const uint64_t ticket0 = rl->queue_ticket;
     rl_slot_t *s = op_begin(layers, n, is_seal);
     int rc = -1;
@@ -1161,7 +1218,7 @@ static int rl_flush_n(ptls_mi355x_record_layer_t *rl, size_t n)
         if (is_seal) {
             const uint64_t keep = rl->seq;
             rl->seq = rl->queue[0].seq0;
-            rc = seal_build(s, layers, n, frags, nfrags, rl->queue_type, out, capacity);
+            rc = seal_build(s, layers, n, frags, nfrags, type, out, capacity);
             rl->seq = keep;
         } else {
             const uint64_t keep = rl->spec_seq; /* (a window stopped meanwhile may have reset it: kept as it is) */
@@ -1235,9 +1292,11 @@ static int queue_window(ptls_mi355x_record_layer_t *rl, int is_seal, uint8_t typ
 {
     if (rl->next_ticket - rl->oldest >= RL_TICKETS)
         return rl_msg("all windows are outstanding (wait for the oldest first)");
-    if (rl->nqueued != 0 && (rl->queue_is_seal != is_seal || rl->queue_type != type) && rl_flush(rl) != 0)
+    /* a window of another content type starts a group of its own (rl_flush_n); the queued ones go out first if they can */
+    if (rl->nqueued != 0 && (rl->queue[rl->nqueued - 1].is_seal != is_seal || rl->queue[rl->nqueued - 1].type != type) &&
+        rl_flush(rl) != 0)
         return -1;
-    if (rl->nqueued != 0 && rl->queue_is_seal != is_seal) /* not launched (no free slot): cannot queue behind it */
+    if (rl->nqueued != 0 && rl->queue[0].is_seal != is_seal) /* not launched (no free slot): cannot queue behind it */
         return rl_msg("windows of the other direction are queued and every launch slot is in flight");
     struct rl_queued *q = &rl->queue[rl->nqueued];
     memset(q, 0, sizeof(*q));
@@ -1271,11 +1330,10 @@ static int queue_window(ptls_mi355x_record_layer_t *rl, int is_seal, uint8_t typ
     }
     q->out = out;
     q->capacity = capacity;
-    if (rl->nqueued++ == 0) {
-        rl->queue_is_seal = is_seal;
-        rl->queue_type = type;
+    q->is_seal = is_seal;
+    q->type = type;
+    if (rl->nqueued++ == 0)
         rl->queue_ticket = rl->next_ticket;
-    }
     *ticket = rl->next_ticket++;
     return queue_drain(rl); /* (no free launch slot: stays queued; a failed launch: its windows' waits report it) */
 }
@@ -1453,15 +1511,7 @@ static void op_complete(rl_slot_t *s, uint8_t *type)
 {
     rl_op_t *op = &s->op;
     hipError_t e;
-    if (op->nrec != 0 && op->resident && ptls_mi355x_resident_wait(s->ctx, op->rjob) != 0) {
-        rl_msg(ptls_mi355x_last_error());
-        op_scrub(s);
-        if (!op->is_seal)
-            for (size_t l = 0; l < op->nlayers; ++l)
-                if (!op->layers[l]->zombie)
-                    op->layers[l]->spec_seq = op->layers[l]->seq;
-        op->failed = 1;
-    } else if (op->nrec != 0 && !op->resident && (e = hipStreamSynchronize(s->stream)) != hipSuccess) {
+    if (op->nrec != 0 && (e = hipStreamSynchronize(s->stream)) != hipSuccess) {
         rl_fail("synchronize", e);
         op_scrub(s);
         if (!op->is_seal) /* nothing delivered: the next window starts at the delivered position */

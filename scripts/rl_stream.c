@@ -4,10 +4,7 @@
  * itself would drive it (its send loop, lib/rapido.c:2176-2301, keeps many windows moving; a window is 16 records of
  * 16 KiB, :2115-2126).
  *
- *   rl_stream [nwin] [depth] [key_bytes] [transport: direct|dma|dma_in|zero_copy|copy|resident|resident_dma_in]
- *             [windows per launch] [one]
- *   (resident: registered buffers in place, the windows as jobs of the resident grid, section 6; resident_dma_in: the
- *   same with the DMA-in setting, which a resident layer ignores)
+ *   rl_stream [nwin] [depth] [key_bytes] [transport: direct|dma|dma_in|zero_copy|copy] [windows per launch] [one]
  *   (windows per launch > 1: windows of that many connections per launch, or with "one" consecutive windows of one
  *   connection)
  *
@@ -61,33 +58,6 @@ static void die(const char *what)
 {
     fprintf(stderr, "rl_stream: %s: %s\n", what, ptls_mi355x_record_layer_last_error());
     exit(1);
-}
-
-static int cmp_double(const void *a, const void *b)
-{
-    const double x = *(const double *)a, y = *(const double *)b;
-    return x < y ? -1 : x > y;
-}
-
-/* medians (us) of the resident job timelines of jobs j0, j0 + step, ... below j1 (the ring keeps the last 256) */
-static void timelines(const uint8_t *key, size_t key_bytes, uint64_t j0, uint64_t j1, uint64_t step, double tl[4])
-{
-    ptls_mi355x_aesgcm_context_t *qc = ptls_mi355x_aesgcm_new(key, key_bytes, 0);
-    static double v[4][256];
-    size_t m = 0;
-    for (uint64_t j = j0; qc != NULL && j < j1; j += step) {
-        uint64_t ns[4];
-        if (j + 256 > j1 && ptls_mi355x_resident_job_times(qc, j, ns) == 0 && m < 256) {
-            for (int i = 0; i < 4; ++i)
-                v[i][m] = ns[i] / 1e3;
-            ++m;
-        }
-    }
-    for (int i = 0; i < 4 && m != 0; ++i) {
-        qsort(v[i], m, sizeof(double), cmp_double);
-        tl[i] = v[i][m / 2];
-    }
-    ptls_mi355x_aesgcm_free(qc);
 }
 
 typedef struct {
@@ -188,7 +158,7 @@ int main(int argc, char **argv)
     const int one_conn = argc > 6 && strcmp(argv[6], "one") == 0; /* ... of one connection instead of `multi` */
     if (depth < 1 || depth > 32 || nwin < 1 || (key_bytes != 16 && key_bytes != 32) || multi < 1 || multi > MAXM ||
         nwin % multi != 0) {
-        fprintf(stderr, "usage: rl_stream [nwin] [depth 1..32] [16|32] [direct|dma|dma_in|zero_copy|copy|resident|resident_dma_in] "
+        fprintf(stderr, "usage: rl_stream [nwin] [depth 1..32] [16|32] [direct|dma|dma_in|zero_copy|copy] "
                         "[windows per launch 1..16] [one]\n");
         return 2;
     }
@@ -237,30 +207,21 @@ int main(int argc, char **argv)
         all[nall++] = st.txs[c];
         all[nall++] = st.rxs[c];
     }
-    const char *rw = getenv("RL_RESIDENT_WORKERS"); /* workers of the resident grid (default: half the CUs) */
-    if (rw != NULL)
-        ptls_mi355x_set_resident_workers((size_t)atoi(rw));
     const char *co = getenv("RL_COALESCE"); /* windows per launch when coalescing (0/1: off; default 16) */
     for (size_t i = 0; co != NULL && i < nall; ++i)
         ptls_mi355x_record_layer_set_coalesce(all[i], (size_t)atoi(co));
     for (size_t i = 0; i < nall; ++i) {
-        if (strcmp(transport, "direct") == 0 || strcmp(transport, "dma") == 0 || strcmp(transport, "dma_in") == 0 ||
-            strcmp(transport, "resident") == 0 || strcmp(transport, "resident_dma_in") == 0) {
+        if (strcmp(transport, "direct") == 0 || strcmp(transport, "dma") == 0 || strcmp(transport, "dma_in") == 0) {
             if (ptls_mi355x_record_layer_register(all[i], st.send, nwin * WIN * FRAG) != 0 ||
                 ptls_mi355x_record_layer_register(all[i], st.wire, nwin * WIRE_WIN) != 0 ||
                 ptls_mi355x_record_layer_register(all[i], st.pt, nwin * PT_WIN) != 0)
                 die("register");
-            ptls_mi355x_record_layer_set_direct_dma(all[i], strcmp(transport, "dma") == 0 ? 1
-                                                            : strcmp(transport, "dma_in") == 0 ||
-                                                                    strcmp(transport, "resident_dma_in") == 0
-                                                                ? PTLS_MI355X_RECORD_LAYER_DMA_IN
-                                                                : 0);
+            ptls_mi355x_record_layer_set_direct_dma(all[i], strcmp(transport, "dma") == 0      ? 1
+                                                            : strcmp(transport, "dma_in") == 0 ? PTLS_MI355X_RECORD_LAYER_DMA_IN
+                                                                                               : 0);
         } else if (strcmp(transport, "copy") == 0) {
             ptls_mi355x_record_layer_set_zero_copy_bytes(all[i], 0);
         }
-        /* registered, as jobs of the resident grid: in place, or the inputs staged by the grid's copy jobs */
-        if (strcmp(transport, "resident") == 0 || strcmp(transport, "resident_dma_in") == 0)
-            ptls_mi355x_record_layer_set_resident(all[i], 1);
     }
     size_t inflight = 0;
     double t_seal = 0, t_open = 0, t_seal1 = 0, t_open1 = 0;
@@ -268,21 +229,10 @@ int main(int argc, char **argv)
     pass(&st, 0, depth, &inflight);
     ptls_mi355x_record_layer_t *lead_tx = multi > 1 ? st.txs[0] : st.tx, *lead_rx = multi > 1 ? st.rxs[0] : st.rx;
     const uint64_t l0s = ptls_mi355x_record_layer_launches(lead_tx), l0o = ptls_mi355x_record_layer_launches(lead_rx);
-    const int resident = strncmp(transport, "resident", 8) == 0;
-    const uint64_t j0 = resident ? ptls_mi355x_resident_jobs(0) : 0;
     t_seal = pass(&st, 1, depth, &inflight);
     const uint64_t l1s = ptls_mi355x_record_layer_launches(lead_tx);
-    /* resident: the medians of the seal pass's job timelines (ptls_mi355x_resident_job_times), in us */
-    double tl[4] = {0, 0, 0, 0}, tlo[2][4] = {{0}};
-    if (resident)
-        timelines(key, key_bytes, j0, ptls_mi355x_resident_jobs(0), 1, tl);
-    const uint64_t j2 = resident ? ptls_mi355x_resident_jobs(0) : 0;
     t_open = pass(&st, 0, depth, &inflight);
     const uint64_t l1o = ptls_mi355x_record_layer_launches(lead_rx);
-    if (resident) { /* an open window: its runs job, then its delivery job */
-        timelines(key, key_bytes, j2, ptls_mi355x_resident_jobs(0), 2, tlo[0]);
-        timelines(key, key_bytes, j2 + 1, ptls_mi355x_resident_jobs(0), 2, tlo[1]);
-    }
     t_seal1 = pass(&st, 1, 1, &inflight);
     t_open1 = pass(&st, 0, 1, &inflight);
     for (size_t w = 0; w < nwin; ++w) {
@@ -295,12 +245,10 @@ int main(int argc, char **argv)
     printf("{\"seal_gibps\": %.2f, \"open_gibps\": %.2f, \"seal_us_per_window\": %.2f, \"open_us_per_window\": %.2f, "
            "\"seal_gibps_sync\": %.2f, \"open_gibps_sync\": %.2f, \"windows\": %zu, \"depth\": %zu, \"max_in_flight\": %zu, "
            "\"transport\": \"%s\", \"key_bits\": %zu, \"windows_per_launch\": %zu, \"connections_per_launch\": %zu, "
-           "\"seal_launches\": %llu, \"open_launches\": %llu, \"resident_seal_timeline_us\": [%.2f, %.2f, %.2f, %.2f], "
-           "\"resident_open_timeline_us\": [%.2f, %.2f, %.2f, %.2f], \"resident_deliver_timeline_us\": [%.2f, %.2f, %.2f, %.2f]}\n",
+           "\"seal_launches\": %llu, \"open_launches\": %llu}\n",
            bytes / t_seal / gib, bytes / t_open / gib, t_seal / nwin * 1e6, t_open / nwin * 1e6, bytes / t_seal1 / gib,
            bytes / t_open1 / gib, nwin, depth, inflight, transport, 8 * key_bytes, multi, one_conn ? (size_t)1 : multi,
-           (unsigned long long)(l1s - l0s), (unsigned long long)(l1o - l0o), tl[0], tl[1], tl[2], tl[3], tlo[0][0], tlo[0][1], tlo[0][2],
-           tlo[0][3], tlo[1][0], tlo[1][1], tlo[1][2], tlo[1][3]);
+           (unsigned long long)(l1s - l0s), (unsigned long long)(l1o - l0o));
     for (size_t i = 0; i < nall; ++i)
         ptls_mi355x_record_layer_free(all[i]);
     free(st.send);

@@ -23,6 +23,30 @@ def engine_lib():
     return rapido_amd.lib()
 
 
+@pytest.fixture(autouse=True)
+def _gpu_work_checked(request):
+    """After every GPU test: the objects it dropped are finalised now (their free paths synchronise and report), the
+    device is synchronised, and any fault of the test's GPU work -- or an error a free path met -- fails THIS test.
+    A fault is reported by whatever HIP call comes next; without this check the next test's first call takes the
+    blame (round 4: an illegal address surfaced at the first H2D copy of an unrelated test).  A page fault is signalled
+    asynchronously, possibly after the kernel has completed, so the check runs twice, a moment apart."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import gc
+    import time
+
+    import rapido_amd as ra
+    nerr = len(ra.FINALIZER_ERRORS)
+    gc.collect()
+    ra.device_check()
+    time.sleep(0.003)
+    ra.device_check()
+    new = ra.FINALIZER_ERRORS[nerr:]
+    if new:
+        pytest.fail("finalizer errors: " + "; ".join(new))
+
+
 @pytest.fixture(scope="session")
 def gpu(engine_lib):
     import rapido_amd
@@ -56,16 +80,3 @@ def kernel_family(name: str, framing: bool):
         ra.set_seg32_records(prev32)
         ra.set_win16_records(prev16)
         ra.set_split_records(prevs)
-
-
-@pytest.fixture(params=["launch", "resident"])
-def rl_mode(request, gpu):
-    """Record layers created during the test launch kernels per window, or post jobs to the resident grid
-    (include/ptls_mi355x.h section 6): the record-layer suites run both ways."""
-    import rapido_amd as ra
-    prev = ra.RecordLayer.default_resident
-    ra.RecordLayer.default_resident = request.param == "resident"
-    try:
-        yield request.param
-    finally:
-        ra.RecordLayer.default_resident = prev

@@ -12,10 +12,52 @@
 #include <stdlib.h>
 #include <string.h>
 #include <type_traits>
+#include <vector>
+#define GCM_HOST_READ_CHECK 1 /* every record read of the walk checked against the allowed ranges below */
 #include "../../rapido_amd/csrc/gcm_core.h"
 #include "../../scripts/gcm_bitslice.h"
 
 using namespace mi355x;
+
+/*
+ * Read checking (GCM_READ in gcm_core.h): with ranges set, every byte range the walk reads must lie inside one of
+ * them -- the records' own bytes (input, AAD, the received tag) and the descriptor array the idle loads point at.
+ * Reads outside count as violations; the first one is kept.  No ranges set: nothing is checked.
+ */
+static std::vector<std::pair<uintptr_t, uintptr_t>> g_read_ok;
+static uint64_t g_read_bad = 0, g_read_first[2] = {0, 0};
+
+extern "C" void gcm_host_read_check(const void *p, size_t n)
+{
+    if (g_read_ok.empty() || n == 0)
+        return;
+    const uintptr_t a = (uintptr_t)p, b = a + n;
+    for (const auto &r : g_read_ok)
+        if (a >= r.first && b <= r.second)
+            return;
+    if (g_read_bad++ == 0) {
+        g_read_first[0] = a;
+        g_read_first[1] = n;
+    }
+}
+
+/* the allowed ranges: n pairs (lo, hi) of host addresses; n = 0 stops checking.  Clears the violation count. */
+extern "C" void model_set_read_ranges(const uint64_t *lohi, size_t n)
+{
+    g_read_ok.clear();
+    for (size_t i = 0; i < n; ++i)
+        g_read_ok.emplace_back((uintptr_t)lohi[2 * i], (uintptr_t)lohi[2 * i + 1]);
+    g_read_bad = 0;
+    g_read_first[0] = g_read_first[1] = 0;
+}
+
+/* violations since the ranges were set; first[0..1] = address and length of the first */
+extern "C" uint64_t model_read_violations(uint64_t *first)
+{
+    first[0] = g_read_first[0];
+    first[1] = g_read_first[1];
+    return g_read_bad;
+}
 
 static constexpr AesTables kTabs{};
 

@@ -11,11 +11,8 @@ EXE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 
 
 
 @pytest.mark.skipif(not os.path.exists(EXE), reason="conformance binary not built (needs /root/reference at build time)")
-@pytest.mark.parametrize("slot_mode", ["launch", "resident"])
-def test_slot_conformance_against_reference_picotls_and_fusion(gpu, slot_mode):
-    """slot_mode resident: the slot calls as jobs of the resident grid (PTLS_MI355X_SLOT_RESIDENT)."""
-    env = dict(os.environ, PTLS_MI355X_SLOT_RESIDENT="1" if slot_mode == "resident" else "0")
-    r = subprocess.run([EXE, "500"], capture_output=True, text=True, timeout=600, env=env)
+def test_slot_conformance_against_reference_picotls_and_fusion(gpu):
+    r = subprocess.run([EXE, "500"], capture_output=True, text=True, timeout=600)
     print(r.stdout[-3000:])
     if r.returncode == 3:
         pytest.skip("host CPU lacks AES-NI (fusion cannot run)")

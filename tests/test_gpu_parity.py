@@ -13,16 +13,6 @@ from rapido_amd import records
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["launch", "resident"])
-def slot_mode(request, gpu):
-    """The single-record (slot) calls by a launch each, or as jobs of the resident grid (ptls_mi355x_set_slot_resident)."""
-    prev = ra.set_slot_resident(request.param == "resident")
-    try:
-        yield request.param
-    finally:
-        ra.set_slot_resident(prev)
-
-
 @pytest.fixture(autouse=True, params=FAMILIES)
 def aead_kernels(request, engine_lib):
     """Every test here runs on each kernel family (conftest.FAMILIES): the window kernels with 64-block segments
@@ -130,7 +120,7 @@ def test_inplace_and_zero_length(gpu):
     assert slices(pt, recs, 0) == [bytes(src[int(r["src"]): int(r["src"]) + int(r["len"])]) for r in recs]
 
 
-def test_direct_api_fusion_vectors(gpu, slot_mode):
+def test_direct_api_fusion_vectors(gpu):
     # t/fusion.c:89-97 gcm_basic (1): zero key/nonce, AAD "hello", 16 zero bytes
     eng = ra.Engine(bytes(16))
     out = eng.encrypt(bytes(12), b"hello", bytes(16))
@@ -159,7 +149,7 @@ GCM_VECTORS = [  # t/fusion.c:161-183: (aadlen, ptlen, tag) with zero key, nonce
 
 
 @pytest.mark.parametrize("aadlen,ptlen,tag", GCM_VECTORS)
-def test_fusion_tag_vectors(gpu, slot_mode, aadlen, ptlen, tag):
+def test_fusion_tag_vectors(gpu, aadlen, ptlen, tag):
     eng = ra.Engine(bytes(16))
     out = eng.encrypt(bytes(12), bytes(aadlen), bytes(ptlen))
     assert out[ptlen:].hex() == tag
@@ -174,7 +164,7 @@ HELLO_EXPECTED = (  # t/fusion.c:110-116
 ).replace(" ", "")
 
 
-def test_slot_gcm_basic_and_iv96(gpu, slot_mode):
+def test_slot_gcm_basic_and_iv96(gpu):
     aad = bytes(range(20))
     # t/fusion.c:99-125: through ptls_aead_new_direct / ptls_aead_encrypt / ptls_aead_decrypt
     a = ra.aead_new_direct("aes128gcm", False, HELLO_KEY, bytes(range(20, 32)))
@@ -199,7 +189,7 @@ def test_slot_gcm_basic_and_iv96(gpu, slot_mode):
 
 
 @pytest.mark.parametrize("zero_copy", [True, False])
-def test_slot_zero_copy_and_copied(gpu, slot_mode, zero_copy):
+def test_slot_zero_copy_and_copied(gpu, zero_copy):
     """The slot's two staging paths (the kernel reading/writing pinned host memory, or DMA copies in and out) give
     the oracle's bytes for every size class, and a tampered tag fails without releasing plaintext."""
     prev = ra.set_slot_zero_copy_bytes(1 << 30 if zero_copy else 0)
@@ -225,7 +215,7 @@ def test_slot_zero_copy_and_copied(gpu, slot_mode, zero_copy):
 
 
 @pytest.mark.parametrize("algo,keylen", [("aes128gcm", 16), ("aes256gcm", 32)])
-def test_slot_streaming_and_record_layer(gpu, slot_mode, algo, keylen):
+def test_slot_streaming_and_record_layer(gpu, algo, keylen):
     """The TLS record-layer call sequence (lib/picotls.c:630-643) and t/picotls.c:161-198."""
     key, iv = bytes(range(1, keylen + 1)), bytes(range(40, 52))
     enc = ra.aead_new_direct(algo, True, key, iv)
@@ -251,7 +241,7 @@ def test_slot_streaming_and_record_layer(gpu, slot_mode, algo, keylen):
     assert dec.decrypt(b"short", 0, b"") is None  # inlen < 16 -> SIZE_MAX
 
 
-def test_slot_supplementary_encryption(gpu, slot_mode):
+def test_slot_supplementary_encryption(gpu):
     """t/fusion.c:185-191: supp output = AES-ECB(supp key, sample of the written record)."""
     a = ra.aead_new_direct("aes128gcm", True, bytes(16), bytes(12))
     supp_cipher = ra.cipher_new("aes128ctr", True, bytes([1] * 16))

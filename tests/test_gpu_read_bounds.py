@@ -1,0 +1,173 @@
+"""Every kernel family against guard pages: records, AAD, descriptors and outputs flush against unmapped memory.
+
+tests/cpp/guard_alloc.c maps the middle third of a reserved virtual range (HIP virtual memory) and leaves the two
+outer thirds unmapped, so one byte read or written past a buffer's end (or before its start) is a GPU page fault,
+reported by the device check after each case.  Round 4's intermittent illegal address needed an allocation that
+happened to end at a page edge; here every case puts its record at both edges, for each kernel family of
+conftest.FAMILIES, AEAD (section 3) and TLS-framed (section 4), sealing and opening, separate and in place (seal with
+the fragment 5 bytes into its record slot, dst = src - 5; open over the wire record, dst = src + 5).  The CPU
+counterpart, tests/test_read_bounds.py, checks the walk's every read against the record bounds in the host model."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle
+import rapido_amd as ra
+from conftest import FAMILIES, kernel_family
+from rapido_amd.records import xorshift64star
+
+pytestmark = pytest.mark.gpu
+
+LENS = [0, 1, 15, 16, 17, 100, 1399, 1400, 4097, 16383, 16384]
+AADS = [0, 5, 13, 16, 17, 32]
+REGION = 64 << 10  # rounded up to the allocation granularity
+
+
+class Guard(C.Structure):
+    _fields_ = [("reserved", C.c_void_p), ("reserved_len", C.c_size_t), ("data", C.c_void_p), ("len", C.c_size_t),
+                ("handle", C.c_void_p)]
+
+
+@pytest.fixture(scope="module")
+def guards(gpu):
+    from rapido_amd import build
+    lib = C.CDLL(build.build_guard())
+    lib.guard_alloc.argtypes = [C.c_size_t, C.POINTER(Guard)]
+    lib.guard_free.argtypes = [C.POINTER(Guard)]
+    for f in ("guard_h2d", "guard_d2h"):
+        getattr(lib, f).argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+    lib.guard_memset.argtypes = [C.c_void_p, C.c_int, C.c_size_t]
+    assert lib.guard_struct_size() == C.sizeof(Guard)
+    gs = []
+    for _ in range(3):  # inputs | descriptors, AAD, statuses | outputs
+        g = Guard()
+        rc = lib.guard_alloc(REGION, C.byref(g))
+        if rc == -1:
+            pytest.skip("device without HIP virtual memory management")
+        assert rc == 0, f"guard_alloc: HIP error {rc}"
+        gs.append(g)
+    yield lib, gs
+    for g in gs:
+        assert lib.guard_free(C.byref(g)) == 0
+
+
+class Region:
+    """A guarded region: place(bytes, at="start"|"end") -> device address of bytes copied flush against that edge."""
+
+    def __init__(self, lib, g):
+        self.lib, self.base, self.len = lib, g.data, g.len
+
+    def addr(self, nbytes, at):
+        assert nbytes <= self.len
+        return self.base if at == "start" else self.base + self.len - nbytes
+
+    def put(self, data, at):
+        data = np.ascontiguousarray(np.frombuffer(bytes(data), np.uint8))
+        a = self.addr(len(data), at)
+        assert self.lib.guard_h2d(a, data.ctypes.data, len(data)) == 0
+        return a
+
+    def get(self, a, n):
+        out = np.zeros(max(n, 1), np.uint8)
+        assert self.lib.guard_d2h(out.ctypes.data, a, n) == 0
+        return out[:n].tobytes()
+
+    def clear(self):
+        assert self.lib.guard_memset(self.base, 0, self.len) == 0
+
+
+def checked():
+    ra.device_check()  # a page fault of the case just launched fails here, naming it
+
+
+@pytest.mark.parametrize("family", FAMILIES)
+@pytest.mark.parametrize("at", ["start", "end"])
+def test_aead_records_at_guard_edges(guards, family, at):
+    lib, gs = guards
+    IN, AUX, OUT = (Region(lib, g) for g in gs)
+    key, iv = bytes(range(16)), bytes(range(70, 82))
+    eng = ra.Engine(key)
+    other = "end" if at == "start" else "start"
+    with kernel_family(family, framing=False):
+        for i, ln in enumerate(LENS):
+            alen = AADS[i % len(AADS)]
+            pt = xorshift64star(900 + i, ln).tobytes()
+            aad = xorshift64star(950 + i, alen).tobytes()
+            for r in (IN, AUX, OUT):
+                r.clear()
+            # seal: input and AAD at the edge, descriptor at the other end, output (ciphertext || tag) at the edge
+            src = IN.put(pt, at)
+            d_aad = AUX.put(aad, at) if alen else AUX.base + AUX.len // 2
+            dst = OUT.addr(ln + 16, at)
+            rec = np.zeros(1, ra.RECORD_DTYPE)
+            rec[0] = (0, 0, 0, 7 + i, ln, alen)
+            d_rec = AUX.put(rec.view(np.uint8), other)  # (offsets 0: each arena base is the record itself)
+            eng.seal_batch(iv, d_rec, 1, src, dst, d_aad)
+            checked()
+            ct = OUT.get(dst, ln + 16)
+            assert ct == oracle.seal(key, oracle.build_iv(iv, 7 + i), aad, pt), (family, at, ln)
+            # open: ciphertext || tag at the edge, plaintext at the edge, status at the other end
+            for r in (IN, OUT):
+                r.clear()
+            src = IN.put(ct, at)
+            dst = OUT.addr(max(ln, 1), at) if ln else OUT.base + OUT.len // 2
+            st = AUX.base + AUX.len // 2 + 64
+            eng.open_batch(iv, d_rec, 1, src, dst, d_aad, st)
+            checked()
+            assert np.frombuffer(AUX.get(st, 4), np.uint32)[0] == ln
+            assert OUT.get(dst, ln) == pt, (family, at, ln)
+    eng.close()
+    checked()
+
+
+@pytest.mark.parametrize("family", FAMILIES)
+@pytest.mark.parametrize("at", ["start", "end"])
+def test_tls_records_at_guard_edges(guards, family, at):
+    lib, gs = guards
+    IN, AUX, OUT = (Region(lib, g) for g in gs)
+    key, iv = bytes(range(5, 21)), bytes(range(90, 102))
+    eng = ra.Engine(key)
+    other = "end" if at == "start" else "start"
+    mid = AUX.base + AUX.len // 2
+    with kernel_family(family, framing=True):
+        for i, ln in enumerate(LENS):
+            frag = xorshift64star(700 + i, ln).tobytes()
+            want = oracle.tls_seal_record(key, iv, 40 + i, 23, frag)
+            for r in (IN, AUX, OUT):
+                r.clear()
+            # seal, separate buffers: fragment and wire record flush against the edge
+            src = IN.put(frag, at)
+            dst = OUT.addr(ln + 22, at)
+            t = np.zeros(1, ra.TLS_RECORD_DTYPE)
+            t[0] = (0, 0, 40 + i, ln, 23)
+            d_t = AUX.put(t.view(np.uint8), other)
+            eng.tls_seal_records(iv, d_t, 1, src, dst)
+            checked()
+            assert OUT.get(dst, ln + 22) == want, (family, at, ln)
+            # open, separate buffers: wire record and plaintext slot (fragment + type) flush against the edge
+            src = IN.put(want, at)
+            dst = OUT.addr(ln + 1, at)
+            o = np.zeros(1, ra.TLS_RECORD_DTYPE)
+            o[0] = (0, 0, 40 + i, ln + 17, 0)
+            d_o = mid + 4096  # (the seal's descriptor stays at the edge for the in-place seal below)
+            assert lib.guard_h2d(d_o, o.ctypes.data, o.nbytes) == 0
+            eng.tls_open_records(iv, d_o, 1, src, dst, mid, mid + 64)
+            checked()
+            assert np.frombuffer(AUX.get(mid, 4), np.uint32)[0] == ln and AUX.get(mid + 64, 1) == b"\x17"
+            assert OUT.get(dst, ln) == frag, (family, at, ln)
+            # in place, as picotls's buffer: seal the fragment 5 bytes into its record slot (dst = src - 5) ...
+            OUT.clear()
+            slot = OUT.addr(ln + 22, at)
+            fb = np.frombuffer(frag, np.uint8).copy()
+            assert lib.guard_h2d(slot + 5, fb.ctypes.data, ln) == 0
+            eng.tls_seal_records(iv, d_t, 1, slot + 5, slot)  # (descriptor offsets 0: src = slot + 5, dst = slot)
+            checked()
+            assert OUT.get(slot, ln + 22) == want, (family, at, "in place", ln)
+            # ... and open it where it lies, plaintext over header + ciphertext (dst = src + 5)
+            eng.tls_open_records(iv, d_o, 1, slot, slot + 5, mid, mid + 64)
+            checked()
+            assert np.frombuffer(AUX.get(mid, 4), np.uint32)[0] == ln
+            assert OUT.get(slot + 5, ln) == frag, (family, at, "in place", ln)
+    eng.close()
+    checked()

@@ -40,19 +40,16 @@ def family(request, gpu):
         yield request.param
 
 
-@pytest.fixture(params=["zero_copy", "copy", "resident"])
+@pytest.fixture(params=["zero_copy", "copy"])
 def transport(request, gpu):
     return request.param
 
 
 def layer(transport, key, iv, seq=0):
-    """A record layer whose windows go through the pinned staging zero-copy (the default), by DMA copies, or
-    zero-copy as jobs of the resident grid."""
+    """A record layer whose windows go through the pinned staging zero-copy (the default) or by DMA copies."""
     rl = ra.RecordLayer(key, iv, seq=seq)
     if transport == "copy":
         rl.set_zero_copy_bytes(0)
-    if transport == "resident":
-        rl.set_resident(True)
     return rl
 
 

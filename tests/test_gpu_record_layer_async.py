@@ -18,7 +18,7 @@ import rapido_amd as ra
 from conftest import kernel_family
 from test_gpu_record_layer import conn_iv, oracle_window, page_buffer
 
-pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("rl_mode")]
+pytestmark = pytest.mark.gpu
 
 # direct: registered buffers read in place by the kernels, plaintexts written by the delivery kernel (the default);
 # direct_dma: registered buffers moved by DMA around a device-resident launch; direct_dma_in: the inputs moved by DMA,
@@ -481,3 +481,72 @@ def test_coalesced_windows_at_the_key_update_limit(gpu):
     assert outs[0][:len(want0)].tobytes() == want0 and outs[1][:len(want1)].tobytes() == want1
     assert tx.seq == LIMIT
     tx.close()
+
+
+@pytest.mark.parametrize("transport", ["direct", "zero_copy"])
+def test_coalesced_windows_of_mixed_content_types(gpu, transport):
+    """Windows of other content types among queued application-data windows (a KeyUpdate or alert sealed
+    while every launch slot is busy was appended to the queued type-23 group and sealed as type 23): a group never
+    mixes types, so every window's records carry their own type and seq, as separate ptls_send calls would."""
+    rng = np.random.default_rng(1212)
+    key, iv = rng.integers(0, 256, 16, dtype=np.uint8).tobytes(), rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    types = [23] * 10 + [22] + [23] * 6 + [21, 21] + [23] * 9
+    wins_b = [[rng.integers(0, 256, 16384, dtype=np.uint8).tobytes() for _ in range(4 if t == 23 else 1)]
+              for t in types]
+    tx = ra.RecordLayer(key, iv, seq=3)
+    h = Host(transport, [tx], 1 << 23)
+    wins = [[h.take(len(f), f) for f in w] for w in wins_b]
+    wants, s = [], 3
+    for t, w in zip(types, wins_b):
+        want, s = oracle_window(key, iv, s, w, t)
+        wants.append(want)
+    outs = [h.take(len(want) + 64) for want in wants]
+    tickets = []
+    for t, w, o in zip(types, wins, outs):  # up to 24 outstanding: launches in flight while others queue
+        if len(tickets) == 24:
+            r = tx.wait(tickets.pop(0))
+            assert r[3] == 0
+        tickets.append(tx.seal_submit(w, o, content_type=t))
+    for tk in tickets:
+        assert tx.wait(tk)[3] == 0
+    for i, (o, want) in enumerate(zip(outs, wants)):
+        assert o[:len(want)].tobytes() == want, (i, types[i])
+    assert tx.seq == s
+    tx.close()
+
+
+def test_shared_registration_outlives_its_first_layer(gpu):
+    """Two layers (the two directions of a connection) register one socket buffer: the registration is shared and
+    counted, so freeing the layer that registered it first leaves it mapped for the other one, whose windows keep
+    reading and writing it in place (round 4 unmapped it under the second layer); the last one unmaps it."""
+    rng = np.random.default_rng(1313)
+    key, iv = rng.integers(0, 256, 16, dtype=np.uint8).tobytes(), rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    buf = page_buffer(1 << 21)
+    frags_b = [rng.integers(0, 256, 16384, dtype=np.uint8).tobytes() for _ in range(8)]
+    want, _ = oracle_window(key, iv, 0, frags_b)
+    for first_closed in ("tx", "rx"):
+        tx, rx = ra.RecordLayer(key, iv), ra.RecordLayer(key, iv)
+        tx.register(buf)
+        rx.register(buf)
+        frags = []
+        for i, f in enumerate(frags_b):
+            v = buf[i * 16384:(i + 1) * 16384]
+            v[:] = np.frombuffer(f, np.uint8)
+            frags.append(v)
+        wire = buf[1 << 19:(1 << 19) + len(want)]
+        olen, n = tx.seal_into(frags, wire)
+        assert wire[:olen].tobytes() == want and n == 8
+        (tx if first_closed == "tx" else rx).close()
+        ra.device_check()
+        other = rx if first_closed == "tx" else tx
+        pt = buf[1 << 20:(1 << 20) + len(want)]
+        if other is rx:  # the surviving layer runs in place on the shared range
+            rc, plen, cons, nrec = rx.open_into(wire, pt)
+            assert (rc, cons, nrec) == (0, len(want), 8) and pt[:plen].tobytes() == b"".join(frags_b)
+        else:
+            olen2, _ = tx.seal_into(frags, pt)
+            want2, _ = oracle_window(key, iv, 8, frags_b)
+            assert pt[:olen2].tobytes() == want2
+        ra.device_check()
+        other.close()
+    ra.device_check()

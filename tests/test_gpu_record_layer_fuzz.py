@@ -14,7 +14,7 @@ import rapido_amd as ra
 from test_gpu_record_layer import conn_iv
 from test_gpu_record_layer_async import Host
 
-pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("rl_mode")]
+pytestmark = pytest.mark.gpu
 LIMIT = ra.RECORD_LAYER_SEQ_LIMIT
 MAXREC = 16384
 

@@ -174,14 +174,12 @@ def test_rapido_harness_pinned_by_minicrypto_without_gpu():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("keylen", [16, 32])
-@pytest.mark.parametrize("slot_mode", ["launch", "resident"])
-def test_rapido_sessions_over_engine_cipher_suite(gpu, keylen, slot_mode):
+def test_rapido_sessions_over_engine_cipher_suite(gpu, keylen):
     """rapido (lib/rapido.c, unmodified) with the engine as its context's only cipher suite: handshakes over loopback
     TCP, 1 MB stream transfers each way (t/rapido_tests.c:290-340), a joined second connection carrying the stream
     under its own IV (t/rapido_tests.c:347-420), and engine <-> minicrypto sessions in both roles."""
     assert os.path.exists(RAPIDO), "oracle/_ref/ref_rapido_harness not built (oracle/Makefile, needs /root/reference)"
-    env = dict(os.environ, PTLS_MI355X_SLOT_RESIDENT="1" if slot_mode == "resident" else "0")
-    r = subprocess.run([RAPIDO, str(keylen)], capture_output=True, text=True, timeout=110, env=env)
+    r = subprocess.run([RAPIDO, str(keylen)], capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
     want = "TLS_AES_256_GCM_SHA384 (AES256-GCM)" if keylen == 32 else "TLS_AES_128_GCM_SHA256 (AES128-GCM)"
     assert r.stdout.startswith("ok 61 checks, rapido over " + want), r.stdout
