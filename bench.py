@@ -39,7 +39,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
-DESC_BYTES = 40         # sizeof(ptls_mi355x_record_t)
+DESC_BYTES = 40         # sizeof(ptls_mi355x_record_t): the engine's descriptor (src, dst, aad, seq u64; len, aadlen u32)
+# SURVEY.md 8(d)'s algorithmic bytes count a 16-B descriptor plus the 8-B seq per record (2845 B per 1400-B seal); the
+# engine's 40-B descriptor reads 16 B more per record, which the roofline does not credit (0.6 % at 1400 B)
+SURVEY_DESC_BYTES = 16 + 8
 LDS_CLOCK_GHZ = 2.4     # MI355X peak engine clock (the LDS roofline is priced at it, as HBM at its spec peak)
 GIB = float(1 << 30)
 METRIC = "device-resident AES-GCM GiB/s, 1.4 KB & 16 KiB record batches, 1/2/4/8 GPU"
@@ -100,6 +103,8 @@ def check_device_map(dev_index: int, same_device_ok: bool, device_count: int):
 
 RANK_KEYS = ("rank", "host", "device", "device_name", "rank_gibps", "rank_ms_per_step", "seal_gibps", "open_gibps",
              "launch_ms")
+# optional per-rank figures carried when present: each GPU's own PCIe-inclusive rate (north_star: PCIe is per GPU)
+RANK_OPTIONAL_KEYS = ("e2e_pcie",)
 
 
 def gather_rank_stats(mine: dict):
@@ -110,15 +115,16 @@ def gather_rank_stats(mine: dict):
     if missing:
         raise ValueError(f"rank stats miss {missing}")
     out = [None] * dist.get_world_size()
-    dist.all_gather_object(out, {k: mine[k] for k in RANK_KEYS})
+    dist.all_gather_object(out, {k: mine[k] for k in RANK_KEYS + RANK_OPTIONAL_KEYS if k in mine})
     return out
 
 
 def algorithmic_bytes(lengths_sum: int, n: int, aad_sum: int, seal: bool) -> int:
-    """seal: read L + aad + descriptor, write L + 16; open: read L + 16 + aad + descriptor, write L + 4."""
+    """seal = read (L + aad + 8 seq + 16 descriptor) + write (L + 16 tag); open = read (L + 16 tag + aad
+    + 8 + 16) + write (L + 4 status).  2845 B per 1400-B seal with the 5-B TLS AAD."""
     if seal:
-        return lengths_sum + aad_sum + DESC_BYTES * n + lengths_sum + 16 * n
-    return lengths_sum + 16 * n + aad_sum + DESC_BYTES * n + lengths_sum + 4 * n
+        return lengths_sum + aad_sum + SURVEY_DESC_BYTES * n + lengths_sum + 16 * n
+    return lengths_sum + 16 * n + aad_sum + SURVEY_DESC_BYTES * n + lengths_sum + 4 * n
 
 
 # ------------------------------------------------------------------------------------------- CPU baseline ----
@@ -394,13 +400,17 @@ def measure(ra, wl_key, args, dev, rank, world, check):
     kname = ra.kernel_name(dom_is_seal, wl["key"], n)
     chunk_kernels = sorted({ra.kernel_name(s, wl["key"], r1 - r0) for s in (True, False) for _, r0, r1 in chunks})
 
-    traffic = None
+    # HBM bytes per launch from PMC counters: rocprofv3 cannot run inside this process, so this is the builder's
+    # counter pass of the same workload and kernel (scripts/collect_profiles.py), labelled as such in the line
+    traffic, traffic_source = None, None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_path):
         try:
             ent = json.load(open(pmc_path)).get(wl_key, {}).get(kname)
             if ent:
                 traffic = ent["hbm_bytes_per_launch"]
+                traffic_source = ("profiles/pmc_traffic.json: the builder's rocprofv3 PMC pass of this workload and "
+                                  "kernel (2 x FETCH_SIZE + WRITE_SIZE), not measured in this run")
         except (ValueError, KeyError):
             traffic = None
 
@@ -411,7 +421,7 @@ def measure(ra, wl_key, args, dev, rank, world, check):
     b128_reads = ra.batch_ghash_reads()
     lds_cycles_per_block = (2.0 * b32_reads + 4.0 * b128_reads) / 64.0
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-    lds_ceiling = ncu * LDS_CLOCK_GHZ * 1e9 / lds_cycles_per_block * 16 / 1e9  # payload GB/s
+    lds_nominal = ncu * LDS_CLOCK_GHZ * 1e9 / lds_cycles_per_block * 16 / 1e9  # payload GB/s
     dom_payload = payload / (dom_ms * 1e-3) / 1e9
     res = {
         "workload": wl["name"], "records_per_gpu": n, "steps": args.steps, "warmup": args.warmup,
@@ -425,37 +435,94 @@ def measure(ra, wl_key, args, dev, rank, world, check):
                      "region_ms": round(region_ms, 4), "wall_ms": round(elapsed * 1e3, 4)},
         "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                     "traffic_source": traffic_source,
                      "algorithmic_bytes_per_launch": dom_bytes, "launch_ms": round(dom_ms, 4),
+                     "algorithmic_bytes_def": "SURVEY.md 8(d): per record seal L + aad + 24 + L + 16, open L + 16 + aad "
+                                              "+ 24 + L + 4 (16-B descriptor + 8-B seq); the engine's descriptors are "
+                                              "40 B, 16 B per record not credited",
                      "launch_ms_median": round(float(np.median(seal_all if dom_is_seal else open_all)), 4),
                      "launches": launches_note,
                      "region": {"frac": round(achieved_region / HBM_PEAK_GBPS, 4), "achieved": round(achieved_region, 1),
                                 "algorithmic_bytes_per_step": seal_b + open_b, "region_ms": round(region_ms, 4),
                                 "note": "every launch of the timed region (seal + open, all chunks) over its HIP-event "
                                         "time"}},
-        "lds_roofline": {"bound": "lds", "kernel": kname, "achieved": round(dom_payload, 1),
-                         "peak": round(lds_ceiling, 1), "unit": "GB/s payload",
-                         "frac": round(dom_payload / lds_ceiling, 4),
-                         "model": f"{b32_reads} ds_read_b32 + {b128_reads} ds_read_b128 per 16-B block = "
-                                  f"{lds_cycles_per_block:.2f} LDS clk/block/CU, {ncu} CU x {LDS_CLOCK_GHZ} GHz",
-                         "note": "this read mix alone sustains 0.78 of the nominal rate (profiles/r01c_lds_ceiling.json)"},
+        "lds_roofline": lds_roofline(kname, dom_payload, wl_key, wl["key"], b32_reads, b128_reads, lds_nominal, ncu,
+                                     getattr(args, "lds_probe", None)),
     }
-    # the clock the chip holds under this kernel (DVFS at the board power limit): GRBM_GUI_ACTIVE / 8 over the
-    # launch time in the PMC pass (scripts/collect_profiles.py -> profiles/held_clock.json)
+    for e in engs[1:]:
+        e.close()
+    extra = dict(eng=eng, iv=iv, d_src=d_src, d_ct=d_ct, d_recs=d_recs, d_aad=d_aad, recs=recs, n=n,
+                 src_bytes=src_bytes, payload=payload, stream=stream, key=wl["key"])
+    return res, extra
+
+
+def lds_probe(ncu: int):
+    """The LDS ceiling of the batch kernels' read mix, measured live (scripts/lds_ceiling.hip, built by
+    rapido_amd/build.py): per key size, the LDS cycles one wave step of 64 blocks costs when a CU does nothing but
+    those reads (133 / 197 ds_read_b32 + 16 ds_read_b128 per block, 16 waves), and the probe's own in-kernel clock.
+    ~1 s of settling and 3 timed launches per mode; None if the probe library is missing."""
+    import ctypes as C
+
+    import numpy as np
+    import torch
+    so = os.path.join(ROOT, "scripts", "_build", "liblds_ceiling.so")
+    if not os.path.exists(so):
+        return None
+    lib = C.CDLL(so)
+    lib.lds_ceiling_run.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
+    out = torch.zeros(ncu * 1024, dtype=torch.int32, device="cuda")
+    st = torch.zeros(2 * ncu, dtype=torch.int64, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    blocks, res = 2048, {}
+    for mode, key in ((0, 16), (1, 32)):
+        t0 = time.time()
+        while time.time() - t0 < 1.0:
+            if lib.lds_ceiling_run(mode, blocks, ncu, out.data_ptr(), st.data_ptr(), s) != 0:
+                return None
+            torch.cuda.synchronize()
+        cyc, ghz = [], []
+        for _ in range(3):
+            lib.lds_ceiling_run(mode, blocks, ncu, out.data_ptr(), st.data_ptr(), s)
+            torch.cuda.synchronize()
+            v = st.cpu().numpy().reshape(-1, 2).astype(np.float64)
+            ghz.append(float(np.median(v[:, 0] / v[:, 1] * 0.1)))
+            cyc.append(float(np.median(v[:, 0])) / (16.0 * blocks))
+        res[key] = {"cycles_per_64_blocks": round(float(np.median(cyc)), 2), "probe_clock_ghz": round(float(np.median(ghz)), 4)}
+    return res
+
+
+def lds_roofline(kname, achieved, wl_key, key, b32_reads, b128_reads, nominal, ncu, probe):
+    """The LDS bound of the batch kernel, priced against the ceiling measured live (lds_probe) at the clock the chip
+    holds under the kernel (profiles/held_clock.json: GRBM_GUI_ACTIVE / 8 over the launch time of the builder's PMC
+    pass); the nominal read model (2 / 4 LDS clk per b32 / b128 read, 2.4 GHz) beside it."""
+    nominal_cyc = 2.0 * b32_reads + 4.0 * b128_reads
+    r = {"bound": "lds", "kernel": kname, "achieved": round(achieved, 1), "unit": "GB/s payload",
+         "model": f"{b32_reads} ds_read_b32 + {b128_reads} ds_read_b128 per 16-B block: {nominal_cyc:.0f} LDS clk per 64 "
+                  f"blocks per CU nominal (MI355X_MICROARCH.md LDS table)",
+         "peak_nominal_2p4ghz": round(nominal, 1), "frac_nominal_2p4ghz": round(achieved / nominal, 4)}
+    held = None
     hpath = os.path.join(ROOT, "profiles", "held_clock.json")
     if os.path.exists(hpath):
         try:
             held = json.load(open(hpath)).get(wl_key, {}).get(kname)
         except ValueError:
             held = None
-        if held:
-            peak_held = lds_ceiling * held["ghz"] / LDS_CLOCK_GHZ
-            res["lds_roofline"].update({"held_clock_ghz": held["ghz"], "peak_held": round(peak_held, 1),
-                                        "frac_held": round(dom_payload / peak_held, 4), "held_clock_source": held["source"]})
-    for e in engs[1:]:
-        e.close()
-    extra = dict(eng=eng, iv=iv, d_src=d_src, d_ct=d_ct, d_recs=d_recs, d_aad=d_aad, recs=recs, n=n,
-                 src_bytes=src_bytes, payload=payload, stream=stream, key=wl["key"])
-    return res, extra
+    if held:
+        r.update({"held_clock_ghz": held["ghz"], "held_clock_source": held["source"]})
+    m = (probe or {}).get(key)
+    if m:
+        clock = held["ghz"] if held else m["probe_clock_ghz"]
+        peak = ncu * clock * 1e9 / (m["cycles_per_64_blocks"] / 64.0) * 16 / 1e9
+        r.update({"peak": round(peak, 1), "frac": round(achieved / peak, 4),
+                  "ceiling_cycles_per_64_blocks": m["cycles_per_64_blocks"], "probe_clock_ghz": m["probe_clock_ghz"],
+                  "ceiling_sustained_frac": round(nominal_cyc / m["cycles_per_64_blocks"], 4),
+                  "ceiling_source": "measured in this run: scripts/lds_ceiling.hip, the kernel's exact read mix alone "
+                                    "(16 waves/CU, no HBM), in-kernel clock; peak = CUs x clock / (cycles / 64) x 16 B "
+                                    "at the held clock"})
+    else:
+        r.update({"peak": round(nominal, 1), "frac": round(achieved / nominal, 4),
+                  "ceiling_source": "nominal model (the probe library scripts/_build/liblds_ceiling.so is missing)"})
+    return r
 
 
 def window_latency(ra, extra, dev):
@@ -597,7 +664,7 @@ def main() -> None:
                          "2 measured +0.1..1.9%%, profiles/r04a_pipeline_ab.jsonl)")
     ap.add_argument("--lanes", type=int, default=0, help="lanes per record (1/2/4/8); 0 = engine default")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--e2e", action="store_true", help="time the PCIe-inclusive path (pinned host in/out); default at N=1")
+    ap.add_argument("--e2e", action="store_true", help="(the default) time the PCIe-inclusive path, every rank")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive path")
     ap.add_argument("--check", type=int, default=64, help="records checked to round-trip after timing")
     args = ap.parse_args()
@@ -637,6 +704,7 @@ def main() -> None:
     if args.lanes:
         ra.set_lanes_per_record(args.lanes)
 
+    args.lds_probe = lds_probe(torch.cuda.get_device_properties(dev).multi_processor_count)
     res, extra = measure(ra, args.workload, args, dev, rank, world, args.check)
     out = {
         "metric": METRIC,
@@ -665,18 +733,25 @@ def main() -> None:
         "build_id_matches_sources": ra.build_id() == ra.source_build_id(),
     }
     out["device_count"] = device_count
-    if world > 1:
-        import socket
-        out["ranks"] = gather_rank_stats({
-            "rank": rank, "host": socket.gethostname(), "device": dev_index,
-            "device_name": torch.cuda.get_device_name(dev), "rank_gibps": res["rank_gibps"],
-            "rank_ms_per_step": res["rank_ms_per_step"], "seal_gibps": res["seal_gibps"],
-            "open_gibps": res["open_gibps"], "launch_ms": res["roofline"]["launch_ms"]})
-        out["placement"] = [list(p) for p in placement]
     if world == 1 and not args.no_e2e:
         out["window_latency"] = window_latency(ra, extra, dev)
-    if (args.e2e or world == 1) and not args.no_e2e:
-        out["e2e_pcie"] = e2e_pcie(ra, extra, dev, args.steps)
+    e2e = None
+    if not args.no_e2e:  # every rank at N > 1: each GPU's own link, all ranks at once (after the timed steps)
+        e2e = e2e_pcie(ra, extra, dev, args.steps)
+        out["e2e_pcie"] = e2e
+    if world > 1:
+        import socket
+        mine = {"rank": rank, "host": socket.gethostname(), "device": dev_index,
+                "device_name": torch.cuda.get_device_name(dev), "rank_gibps": res["rank_gibps"],
+                "rank_ms_per_step": res["rank_ms_per_step"], "seal_gibps": res["seal_gibps"],
+                "open_gibps": res["open_gibps"], "launch_ms": res["roofline"]["launch_ms"]}
+        if e2e is not None:
+            mine["e2e_pcie"] = {k: e2e[k] for k in ("seal_gibps_serial", "seal_gibps_pipelined")}
+        out["ranks"] = gather_rank_stats(mine)
+        out["placement"] = [list(p) for p in placement]
+        if e2e is not None:
+            out["e2e_pcie"] = dict(e2e, note=e2e["note"] + "; rank 0's figure here, every rank's in `ranks`, all ranks "
+                                   "copying at once (each GPU on its own PCIe link, one host)")
     if world == 1 and not args.no_e2e:
         out["record_layer_stream"] = record_layer_stream(16)
     extra["eng"].close()

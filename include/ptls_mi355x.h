@@ -131,6 +131,10 @@ int ptls_mi355x_aesgcm_release(ptls_mi355x_aesgcm_context_t *ctx);
 /* diagnostics: synchronises the current device; 0, or -1 with ptls_mi355x_last_error naming the first error seen
  * since the previous check -- a fault of queued work, or one a free path met (which return nothing) */
 int ptls_mi355x_device_check(void);
+/* the same on HIP device `device` (one thread serving several GPUs: a context per GPU, records sharded across them,
+ * SURVEY.md 8(e)); the caller's current device is left as it was.  NULL, with ptls_mi355x_last_error naming the
+ * ordinal, if that device is not present. */
+ptls_mi355x_aesgcm_context_t *ptls_mi355x_aesgcm_new_on(int device, const void *key, size_t key_size, size_t capacity);
 /* HIP device ordinal the context lives on */
 int ptls_mi355x_aesgcm_device(const ptls_mi355x_aesgcm_context_t *ctx);
 

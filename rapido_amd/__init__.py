@@ -55,7 +55,7 @@ OPEN_STOP_AT_FAILURE = 1
 #: every symbol include/ptls_mi355x.h declares
 EXPORTED_FUNCTIONS = (
     "ptls_mi355x_is_supported", "ptls_mi355x_aesgcm_new", "ptls_mi355x_aesgcm_free", "ptls_mi355x_aesgcm_release",
-    "ptls_mi355x_device_check", "ptls_mi355x_aesgcm_device",
+    "ptls_mi355x_device_check", "ptls_mi355x_aesgcm_new_on", "ptls_mi355x_aesgcm_device",
     "ptls_mi355x_aesgcm_encrypt", "ptls_mi355x_aesgcm_decrypt", "ptls_mi355x_aesecb_encrypt",
     "ptls_mi355x_seal_batch", "ptls_mi355x_open_batch", "ptls_mi355x_order_by_length",
     "ptls_mi355x_seal_batch_ordered", "ptls_mi355x_open_batch_ordered", "ptls_mi355x_set_lanes_per_record",
@@ -141,6 +141,8 @@ def lib() -> C.CDLL:
         if hasattr(L, "ptls_mi355x_aesgcm_release"):  # (absent from older builds used in A/B timing runs)
             L.ptls_mi355x_aesgcm_release.argtypes = [vp]
             L.ptls_mi355x_device_check.argtypes = []
+            L.ptls_mi355x_aesgcm_new_on.argtypes = [C.c_int, vp, sz, sz]
+            L.ptls_mi355x_aesgcm_new_on.restype = vp
         L.ptls_mi355x_aesgcm_device.argtypes = [vp]
         L.ptls_mi355x_aesgcm_encrypt.argtypes = [vp, vp, vp, sz, vp, vp, sz]
         L.ptls_mi355x_aesgcm_decrypt.argtypes = [vp, vp, vp, sz, vp, vp, sz, vp]
@@ -387,11 +389,16 @@ def cipher_new(name: str, is_enc: bool, key: bytes) -> Cipher:
 class Engine:
     """ptls_mi355x_aesgcm_context_t: the device-resident key image + batch launches."""
 
-    def __init__(self, key: bytes, capacity: int = 16384):
+    def __init__(self, key: bytes, capacity: int = 16384, device: int | None = None):
+        """device: the HIP ordinal to create the context on (ptls_mi355x_aesgcm_new_on); None: the current device."""
         if len(key) not in (16, 32):
             raise ValueError("key must be 16 or 32 bytes")
         self.key_size = len(key)
-        self.handle = lib().ptls_mi355x_aesgcm_new(_cbuf(key), len(key), capacity)
+        self.handle = None
+        if device is None:
+            self.handle = lib().ptls_mi355x_aesgcm_new(_cbuf(key), len(key), capacity)
+        else:
+            self.handle = lib().ptls_mi355x_aesgcm_new_on(device, _cbuf(key), len(key), capacity)
         if not self.handle:
             raise RuntimeError("ptls_mi355x_aesgcm_new failed: " + last_error())
 

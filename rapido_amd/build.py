@@ -8,6 +8,7 @@
                                            memory for the GPU read-bounds test, test only)
     scripts/_build/rl_stream            <- scripts/rl_stream.c (gcc, against the library: bench.py's host-to-host
                                            record-layer stream driver, a measurement tool)
+    scripts/_build/liblds_ceiling.so    <- scripts/lds_ceiling.hip (hipcc: the LDS ceiling probe bench.py runs live)
 
 The library is stamped with a hash of its sources (source_build_id: rapido_amd/csrc/* and include/ptls_mi355x.h).
 It is rebuilt from scratch whenever the stamp differs from the tree's hash, whatever the file times say, so the
@@ -151,11 +152,25 @@ def build_rl_stream(verbose: bool = False, force: bool = False) -> str:
     return RL_STREAM
 
 
+LDS_PROBE_SRC = os.path.join(ROOT, "scripts", "lds_ceiling.hip")
+LDS_PROBE = os.path.join(ROOT, "scripts", "_build", "liblds_ceiling.so")
+
+
+def build_lds_probe(verbose: bool = False, force: bool = False) -> str:
+    """The LDS-ceiling probe bench.py runs beside the batch kernels (measurement, not part of the product)."""
+    os.makedirs(os.path.dirname(LDS_PROBE), exist_ok=True)
+    if force or _newer(LDS_PROBE, [LDS_PROBE_SRC]):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", LDS_PROBE_SRC, "-o", LDS_PROBE],
+             verbose)
+    return LDS_PROBE
+
+
 def build_all(verbose: bool = False, force: bool = False) -> None:
     build_engine(verbose, force)
     build_model(verbose, force)
     build_guard(verbose, force)
     build_rl_stream(verbose, force)
+    build_lds_probe(verbose, force)
 
 
 if __name__ == "__main__":

@@ -1478,15 +1478,25 @@ static void defer(const char *what, hipError_t e) { ptls_mi355x_defer_error(what
             return fail(#call, e_);                                                                                    \
     } while (0)
 
-/* runs `body` with the context's device current, restoring the caller's device */
+/* runs `body` with the context's device current, restoring the caller's device; ok = false if it could not be made
+ * current (an absent ordinal: the caller's device stays current, so the caller must check before doing work) */
 struct DeviceGuard {
     int prev = -1;
+    bool ok = true;
     explicit DeviceGuard(int dev)
     {
-        if (hipGetDevice(&prev) == hipSuccess && prev != dev)
-            (void)hipSetDevice(dev);
-        else if (prev == dev)
+        if (hipGetDevice(&prev) != hipSuccess) {
+            ok = false;
             prev = -1;
+        } else if (prev != dev) {
+            ok = hipSetDevice(dev) == hipSuccess;
+            if (!ok) {
+                (void)hipGetLastError();
+                prev = -1;
+            }
+        } else {
+            prev = -1;
+        }
     }
     ~DeviceGuard()
     {
@@ -2077,6 +2087,26 @@ int ptls_mi355x_aesgcm_release(ptls_mi355x_aesgcm_context_t *ctx)
 }
 
 void ptls_mi355x_aesgcm_free(ptls_mi355x_aesgcm_context_t *ctx) { (void)ptls_mi355x_aesgcm_release(ctx); }
+
+ptls_mi355x_aesgcm_context_t *ptls_mi355x_aesgcm_new_on(int device, const void *key, size_t key_size, size_t capacity)
+{
+    int n = 0;
+    const hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || device < 0 || device >= n) {
+        if (e != hipSuccess)
+            (void)hipGetLastError();
+        snprintf(g_err, sizeof(g_err), "device ordinal %d is not present (%d HIP device%s%s%s)", device,
+                 e == hipSuccess ? n : 0, (e == hipSuccess ? n : 0) == 1 ? "" : "s", e == hipSuccess ? "" : ": ",
+                 e == hipSuccess ? "" : hipGetErrorString(e));
+        return nullptr;
+    }
+    DeviceGuard guard(device);
+    if (!guard.ok) {
+        snprintf(g_err, sizeof(g_err), "device ordinal %d could not be made current", device);
+        return nullptr;
+    }
+    return ptls_mi355x_aesgcm_new(key, key_size, capacity);
+}
 
 int ptls_mi355x_device_check(void)
 {

@@ -121,7 +121,8 @@ def _line_worker(rank, world, port, q, dev_index, same_ok):
         return
     ranks = bench.gather_rank_stats({"rank": rank, "host": "h", "device": dev_index(rank), "device_name": "gfx950",
                                      "rank_gibps": 100.0 + rank, "rank_ms_per_step": 2.0 - rank, "seal_gibps": 1.0,
-                                     "open_gibps": 2.0, "launch_ms": 1.5})
+                                     "open_gibps": 2.0, "launch_ms": 1.5,
+                                     "e2e_pcie": {"seal_gibps_serial": 20.0 + rank, "seal_gibps_pipelined": 30.0 + rank}})
     q.put((rank, placement, ranks))
     dist.destroy_process_group()
 
@@ -154,8 +155,10 @@ def test_bench_line_per_rank_figures():
     for rank, placement, ranks in _run_line(_dev_per_rank, False):
         assert [p[1] for p in placement] == [0, 1]
         assert [r["rank"] for r in ranks] == [0, 1] and [r["device"] for r in ranks] == [0, 1]
-        assert all(set(r) == set(bench.RANK_KEYS) for r in ranks)
+        assert all(set(r) == set(bench.RANK_KEYS) | {"e2e_pcie"} for r in ranks)
         assert [r["rank_gibps"] for r in ranks] == [100.0, 101.0]
+        # each GPU's own PCIe-inclusive rate rides with its rank (north_star: PCIe is per GPU)
+        assert [r["e2e_pcie"]["seal_gibps_pipelined"] for r in ranks] == [30.0, 31.0]
 
 
 def test_bench_refuses_two_ranks_on_one_gpu():
@@ -164,3 +167,50 @@ def test_bench_refuses_two_ranks_on_one_gpu():
     assert all(r[1] == "exit" and "share a GPU" in r[2] for r in res)
     for rank, placement, ranks in _run_line(_dev_zero, True):
         assert [p[1] for p in placement] == [0, 0] and len(ranks) == 2
+
+
+@pytest.mark.parametrize("ordinal", [1, 7, -1])
+def test_context_on_an_absent_device_fails_cleanly(engine_lib, ordinal):
+    """A context asked for on a device ordinal this host does not have (ptls_mi355x_aesgcm_new_on: a rank mapped to
+    GPU 7 of a smaller node) is refused with an error naming the ordinal -- never created silently on the current
+    device.  Runs without a GPU (there every ordinal is absent)."""
+    import rapido_amd as ra
+    try:
+        import torch
+        have = torch.cuda.device_count()
+    except Exception:  # noqa: BLE001
+        have = 0
+    if 0 <= ordinal < have:
+        pytest.skip(f"device {ordinal} is present here")
+    with pytest.raises(RuntimeError, match=f"device ordinal {ordinal} is not present"):
+        ra.Engine(bytes(16), device=ordinal)
+
+
+@pytest.mark.gpu
+def test_contexts_on_each_present_device(gpu):
+    """ptls_mi355x_aesgcm_new_on: a context on every present ordinal lives there (seal of one record checked against
+    the oracle), the caller's current device is unchanged, and the first absent ordinal is refused cleanly."""
+    import numpy as np
+    import torch
+
+    import oracle
+    import rapido_amd as ra
+    n = torch.cuda.device_count()
+    cur = torch.cuda.current_device()
+    key, iv = bytes(range(16)), bytes(range(12))
+    for d in range(n):
+        eng = ra.Engine(key, device=d)
+        assert eng.device == d and torch.cuda.current_device() == cur
+        with torch.cuda.device(d):
+            rec = np.zeros(1, ra.RECORD_DTYPE)
+            rec[0] = (0, 0, 0, 5, 100, 0)
+            src = torch.arange(100, dtype=torch.uint8, device=f"cuda:{d}")
+            dst = torch.zeros(116, dtype=torch.uint8, device=f"cuda:{d}")
+            d_rec = torch.from_numpy(rec.view(np.uint8).copy()).to(f"cuda:{d}")
+            eng.seal_batch(iv, d_rec.data_ptr(), 1, src.data_ptr(), dst.data_ptr(), src.data_ptr())
+            torch.cuda.synchronize(d)
+            assert dst.cpu().numpy().tobytes() == oracle.seal(key, oracle.build_iv(iv, 5), b"", bytes(range(100)))
+        eng.close()
+    with pytest.raises(RuntimeError, match=f"device ordinal {n} is not present"):
+        ra.Engine(key, device=n)
+    assert torch.cuda.current_device() == cur
