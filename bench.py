@@ -446,8 +446,7 @@ def measure(ra, wl_key, args, dev, rank, world, check):
                                 "algorithmic_bytes_per_step": seal_b + open_b, "region_ms": round(region_ms, 4),
                                 "note": "every launch of the timed region (seal + open, all chunks) over its HIP-event "
                                         "time"}},
-        "lds_roofline": lds_roofline(kname, dom_payload, wl_key, wl["key"], b32_reads, b128_reads, lds_nominal, ncu,
-                                     getattr(args, "lds_probe", None)),
+        "lds_roofline": lds_roofline(kname, dom_payload, wl_key, wl["key"], b32_reads, b128_reads, lds_nominal, ncu),
     }
     for e in engs[1:]:
         e.close()
@@ -456,49 +455,19 @@ def measure(ra, wl_key, args, dev, rank, world, check):
     return res, extra
 
 
-def lds_probe(ncu: int):
-    """The LDS ceiling of the batch kernels' read mix, measured live (scripts/lds_ceiling.hip, built by
-    rapido_amd/build.py): per key size, the LDS cycles one wave step of 64 blocks costs when a CU does nothing but
-    those reads (133 / 197 ds_read_b32 + 16 ds_read_b128 per block, 16 waves), and the probe's own in-kernel clock.
-    ~1 s of settling and 3 timed launches per mode; None if the probe library is missing."""
-    import ctypes as C
-
-    import numpy as np
-    import torch
-    so = os.path.join(ROOT, "scripts", "_build", "liblds_ceiling.so")
-    if not os.path.exists(so):
-        return None
-    lib = C.CDLL(so)
-    lib.lds_ceiling_run.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
-    out = torch.zeros(ncu * 1024, dtype=torch.int32, device="cuda")
-    st = torch.zeros(2 * ncu, dtype=torch.int64, device="cuda")
-    s = torch.cuda.current_stream().cuda_stream
-    blocks, res = 2048, {}
-    for mode, key in ((0, 16), (1, 32)):
-        t0 = time.time()
-        while time.time() - t0 < 1.0:
-            if lib.lds_ceiling_run(mode, blocks, ncu, out.data_ptr(), st.data_ptr(), s) != 0:
-                return None
-            torch.cuda.synchronize()
-        cyc, ghz = [], []
-        for _ in range(3):
-            lib.lds_ceiling_run(mode, blocks, ncu, out.data_ptr(), st.data_ptr(), s)
-            torch.cuda.synchronize()
-            v = st.cpu().numpy().reshape(-1, 2).astype(np.float64)
-            ghz.append(float(np.median(v[:, 0] / v[:, 1] * 0.1)))
-            cyc.append(float(np.median(v[:, 0])) / (16.0 * blocks))
-        res[key] = {"cycles_per_64_blocks": round(float(np.median(cyc)), 2), "probe_clock_ghz": round(float(np.median(ghz)), 4)}
-    return res
-
-
-def lds_roofline(kname, achieved, wl_key, key, b32_reads, b128_reads, nominal, ncu, probe):
-    """The LDS bound of the batch kernel, priced against the ceiling measured live (lds_probe) at the clock the chip
-    holds under the kernel (profiles/held_clock.json: GRBM_GUI_ACTIVE / 8 over the launch time of the builder's PMC
-    pass); the nominal read model (2 / 4 LDS clk per b32 / b128 read, 2.4 GHz) beside it."""
-    nominal_cyc = 2.0 * b32_reads + 4.0 * b128_reads
+def lds_roofline(kname, achieved, wl_key, key, b32_reads, b128_reads, nominal, ncu):
+    """The LDS bound of the batch kernel.  The ceiling is the LDS array busy every cycle: b32_reads x 2 + b128_reads x 4
+    array cycles per 64 blocks per CU (MI355X_MICROARCH.md LDS table), which the counters confirm exactly --
+    SQ_LDS_IDX_ACTIVE per 64 blocks is 330.0 / 458.0 for the AES-128 / AES-256 read mix alone and 333 / 461 in the
+    kernels (profiles/r05e_lds_ceiling.json).  Priced at the clock the chip holds under the kernel
+    (profiles/held_clock.json: GRBM_GUI_ACTIVE / 8 over the dispatch time of the builder's PMC pass), beside the
+    nominal 2.4 GHz."""
+    cyc = 2.0 * b32_reads + 4.0 * b128_reads
     r = {"bound": "lds", "kernel": kname, "achieved": round(achieved, 1), "unit": "GB/s payload",
-         "model": f"{b32_reads} ds_read_b32 + {b128_reads} ds_read_b128 per 16-B block: {nominal_cyc:.0f} LDS clk per 64 "
-                  f"blocks per CU nominal (MI355X_MICROARCH.md LDS table)",
+         "model": f"{b32_reads} ds_read_b32 + {b128_reads} ds_read_b128 per 16-B block: {cyc:.0f} LDS-array cycles per 64 "
+                  f"blocks per CU",
+         "ceiling_source": "the LDS array busy every cycle; SQ_LDS_IDX_ACTIVE per 64 blocks equals the model (probe "
+                           "330.0 / 458.0, kernels 333 / 461: profiles/r05e_lds_ceiling.json)",
          "peak_nominal_2p4ghz": round(nominal, 1), "frac_nominal_2p4ghz": round(achieved / nominal, 4)}
     held = None
     hpath = os.path.join(ROOT, "profiles", "held_clock.json")
@@ -508,20 +477,12 @@ def lds_roofline(kname, achieved, wl_key, key, b32_reads, b128_reads, nominal, n
         except ValueError:
             held = None
     if held:
-        r.update({"held_clock_ghz": held["ghz"], "held_clock_source": held["source"]})
-    m = (probe or {}).get(key)
-    if m:
-        clock = held["ghz"] if held else m["probe_clock_ghz"]
-        peak = ncu * clock * 1e9 / (m["cycles_per_64_blocks"] / 64.0) * 16 / 1e9
-        r.update({"peak": round(peak, 1), "frac": round(achieved / peak, 4),
-                  "ceiling_cycles_per_64_blocks": m["cycles_per_64_blocks"], "probe_clock_ghz": m["probe_clock_ghz"],
-                  "ceiling_sustained_frac": round(nominal_cyc / m["cycles_per_64_blocks"], 4),
-                  "ceiling_source": "measured in this run: scripts/lds_ceiling.hip, the kernel's exact read mix alone "
-                                    "(16 waves/CU, no HBM), in-kernel clock; peak = CUs x clock / (cycles / 64) x 16 B "
-                                    "at the held clock"})
+        peak = ncu * held["ghz"] * 1e9 / (cyc / 64.0) * 16 / 1e9
+        r.update({"peak": round(peak, 1), "frac": round(achieved / peak, 4), "held_clock_ghz": held["ghz"],
+                  "held_clock_source": held["source"]})
     else:
         r.update({"peak": round(nominal, 1), "frac": round(achieved / nominal, 4),
-                  "ceiling_source": "nominal model (the probe library scripts/_build/liblds_ceiling.so is missing)"})
+                  "held_clock_source": "none for this kernel and workload: priced at 2.4 GHz"})
     return r
 
 
@@ -704,7 +665,6 @@ def main() -> None:
     if args.lanes:
         ra.set_lanes_per_record(args.lanes)
 
-    args.lds_probe = lds_probe(torch.cuda.get_device_properties(dev).multi_processor_count)
     res, extra = measure(ra, args.workload, args, dev, rank, world, args.check)
     out = {
         "metric": METRIC,

@@ -27,8 +27,19 @@
  *   5. The 2^24-record limit: both at seq 2^24 - 3, a 16-fragment window stops after 3 records
  *      (PTLS_MI355X_RECORD_LAYER_KEY_UPDATE); S runs step 4 and seals the other 13; C receives all 16 in order.
  *
- *   ref_traffic_key_harness <direct|dma|zero_copy|copy> <16|32>   ->  prints "ok ..." and exits 0, or reports and exits 1
+ *   6. (argument "transfer") rapido's 1 MB stream (t/rapido_tests.c:290-340) both ways through the hook-installed
+ *      layers: S -> C in rapido send windows of 16 x 16 KiB fragments (lib/rapido.c:2115-2126), C's ptls_receive
+ *      checks every byte; C -> S by ptls_send, opened by S's layer in receive windows of at most 32 records
+ *      (lib/rapido.c:2030).  Then the host-to-host rate of the same 1 MB, same key, IV and seq, three ways, each
+ *      output compared byte for byte with the checked stream: the layer, one window at a time (rapido's loop); the
+ *      layer with all four windows submitted at once; and the engine's AEAD slot as rapido uses it today -- ptls_send
+ *      per 16 KiB record on a ptls_t whose traffic AEAD is ptls_mi355x_aes*gcm (ptls_set_traffic_protection,
+ *      lib/rapido.c:135-200).  Receive the same way (the layer's windows; ptls_receive over the slot).
+ *
+ *   ref_traffic_key_harness <direct|dma|dma_in|zero_copy|copy> <16|32> [transfer]
+ *       ->  prints "ok ..." (and with "transfer" a "rates ..." JSON line) and exits 0, or reports and exits 1
  */
+#include <time.h>
 #include "picotls.c" /* -I$(REF)/lib: the reference record layer and key schedule (static functions) */
 #include "picotls/minicrypto.h"
 #include "ptls_mi355x.h"
@@ -181,12 +192,235 @@ static void gpu_send_key_update(struct gpu_record_layer_cb *cb, ptls_t *s, ptls_
         FAIL("peer did not switch its receive key");
 }
 
+static double now(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec + t.tv_nsec * 1e-9;
+}
+
+#define XFER 1000000u /* t/rapido_tests.c:319: the 1 MB stream */
+#define XWIN 16       /* fragments per send window (lib/rapido.c:2115-2126) */
+#define XRECV 32      /* records per receive window (lib/rapido.c:2030) */
+
+/* the stream's fragments: 16 KiB each (rapido's TCPLS records), the last one short */
+static size_t xfer_frags(uint8_t *data, uint8_t **frag, size_t *len)
+{
+    size_t n = 0;
+    for (size_t off = 0; off < XFER; off += 16384, ++n) {
+        frag[n] = data + off;
+        len[n] = XFER - off < 16384 ? XFER - off : 16384;
+    }
+    return n;
+}
+
+/* seal the stream through `rl` in windows of XWIN fragments into wire; depth 1: one window at a time (submit, wait),
+ * else every window submitted, then waited.  Returns the wire bytes. */
+static size_t layer_send(ptls_mi355x_record_layer_t *rl, uint8_t **frag, size_t *len, size_t nfrag, uint8_t *wire,
+                         size_t cap, int all_at_once)
+{
+    ptls_mi355x_iovec_t iov[64];
+    uint64_t ticket[8];
+    void *out[8];
+    size_t off = 0, nwin = 0, outcap[8], nf[8];
+    for (size_t f = 0; f < nfrag; ++f)
+        iov[f] = (ptls_mi355x_iovec_t){frag[f], len[f]};
+    for (size_t f = 0; f < nfrag; f += XWIN, ++nwin) {
+        nf[nwin] = nfrag - f < XWIN ? nfrag - f : XWIN;
+        const ptls_mi355x_iovec_t *w = iov + f;
+        size_t bytes = 0;
+        for (size_t k = 0; k < nf[nwin]; ++k)
+            bytes += len[f + k] + PTLS_MI355X_TLS_OVERHEAD;
+        out[nwin] = wire + off;
+        outcap[nwin] = bytes;
+        off += bytes;
+        if (off > cap || ptls_mi355x_record_layer_seal_submit(&rl, 1, &w, &nf[nwin], PTLS_CONTENT_TYPE_APPDATA, &out[nwin],
+                                                              &outcap[nwin], &ticket[nwin]) != 0)
+            FAIL("seal_submit: %s", ptls_mi355x_record_layer_last_error());
+        if (!all_at_once) {
+            size_t ol, nr, cons;
+            int al;
+            if (ptls_mi355x_record_layer_wait(rl, ticket[nwin], &ol, &nr, &cons, &al) != 0 || al != 0 || ol != outcap[nwin])
+                FAIL("seal wait: %s", ptls_mi355x_record_layer_last_error());
+        }
+    }
+    for (size_t w = 0; all_at_once && w < nwin; ++w) {
+        size_t ol, nr, cons;
+        int al;
+        if (ptls_mi355x_record_layer_wait(rl, ticket[w], &ol, &nr, &cons, &al) != 0 || al != 0 || ol != outcap[w])
+            FAIL("seal wait: %s", ptls_mi355x_record_layer_last_error());
+    }
+    return off;
+}
+
+/* open the wire through `rl` in receive windows of at most XRECV records into pt; returns the plaintext bytes */
+static size_t layer_recv(ptls_mi355x_record_layer_t *rl, const uint8_t *wire, size_t wirelen, uint8_t *pt, size_t cap)
+{
+    size_t in = 0, got = 0;
+    while (in < wirelen) {
+        size_t win = 0, k = 0; /* XRECV complete records at most (a recv() of rapido's buffer) */
+        while (k < XRECV && in + win + 5 <= wirelen) {
+            const size_t rl_ = 5 + ((size_t)wire[in + win + 3] << 8 | wire[in + win + 4]);
+            if (in + win + rl_ > wirelen)
+                break;
+            win += rl_;
+            ++k;
+        }
+        size_t cons, olen, nrec;
+        const int rc = ptls_mi355x_record_layer_open(rl, wire + in, win, &cons, pt + got, cap - got, &olen, &nrec);
+        if (rc != 0 || cons != win || nrec != k)
+            FAIL("layer open: rc %d, %zu of %zu bytes: %s", rc, cons, win, ptls_mi355x_record_layer_last_error());
+        in += cons;
+        got += olen;
+    }
+    return got;
+}
+
+/* scenario 6: rapido's 1 MB stream through the hook-installed layers, then the rates (see the header) */
+static void rapido_transfer(struct gpu_record_layer_cb *cb, ptls_t *s, ptls_t *c, ptls_cipher_suite_t *cs,
+                            const char *transport, size_t keylen)
+{
+    uint8_t *data = take(XFER), *frag[64], *wire = take(XFER + 64 * PTLS_MI355X_TLS_OVERHEAD + 64), *pt = take(XFER + 64);
+    size_t len[64];
+    fill_random(data, XFER);
+    const size_t nfrag = xfer_frags(data, frag, len);
+    /* S -> C: the checked stream, from the send layer's current seq */
+    const uint64_t seq0 = ptls_mi355x_record_layer_get_seq(cb->layer[1]);
+    const size_t wl = layer_send(cb->layer[1], frag, len, nfrag, wire, XFER + 64 * PTLS_MI355X_TLS_OVERHEAD, 0);
+    peer_receive(c, wire, wl, data, XFER);
+    /* C -> S: ptls_send of the stream (rapido's per-record calls), the receive layer's windows */
+    {
+        ptls_buffer_t sb;
+        ptls_buffer_init(&sb, "", 0);
+        for (size_t f = 0; f < nfrag; ++f)
+            if (ptls_send(c, &sb, frag[f], len[f]) != 0)
+                FAIL("peer ptls_send");
+        uint8_t *in = take(sb.off);
+        memcpy(in, sb.base, sb.off);
+        if (layer_recv(cb->layer[0], in, sb.off, pt, XFER + 64) != XFER || memcmp(pt, data, XFER) != 0)
+            FAIL("the peer's 1 MB through the receive layer");
+        ptls_buffer_dispose(&sb);
+    }
+    /* the rates: the same key, IV and seq as the checked stream; every output equal to it */
+    uint8_t key[PTLS_MAX_SECRET_SIZE], iv[PTLS_MAX_IV_SIZE];
+    if (ptls_hkdf_expand_label(cs->hash, key, cs->aead->key_size, ptls_iovec_init(s->traffic_protection.enc.secret,
+                               cs->hash->digest_size), "key", ptls_iovec_init(NULL, 0), NULL) != 0 ||
+        ptls_hkdf_expand_label(cs->hash, iv, cs->aead->iv_size, ptls_iovec_init(s->traffic_protection.enc.secret,
+                               cs->hash->digest_size), "iv", ptls_iovec_init(NULL, 0), NULL) != 0)
+        FAIL("key derivation");
+    for (int i = 0; i < 4; ++i)
+        iv[i] ^= (uint8_t)(cb->connection_id >> (24 - 8 * i));
+    enum { REPS = 8 };
+    double t_layer1 = 0, t_layer4 = 0, t_slot = 0, t_layer_recv = 0, t_slot_recv = 0;
+    uint8_t *w2 = take(XFER + 64 * PTLS_MI355X_TLS_OVERHEAD + 64), *p2 = take(XFER + 64);
+    /* long-lived layers and AEADs, as a connection's (rep 0, untimed, creates their streams, staging and contexts);
+     * every rep restarts them at seq0, so each rep's output is the checked stream again */
+    ptls_mi355x_record_layer_t *txs[2], *rxs[2];
+    for (int mode = 0; mode < 2; ++mode) {
+        ptls_mi355x_record_layer_t *tx = txs[mode] = ptls_mi355x_record_layer_new(key, keylen, iv, seq0),
+                                   *rx = rxs[mode] = ptls_mi355x_record_layer_new(key, keylen, iv, seq0);
+        if (tx == NULL || rx == NULL)
+            FAIL("record_layer_new");
+        if (cb->direct_ranges) {
+            if (ptls_mi355x_record_layer_register(tx, arena, arena_cap) != 0 ||
+                ptls_mi355x_record_layer_register(rx, arena, arena_cap) != 0)
+                FAIL("register");
+            if (cb->dma) {
+                ptls_mi355x_record_layer_set_direct_dma(tx, cb->dma);
+                ptls_mi355x_record_layer_set_direct_dma(rx, cb->dma);
+            }
+        }
+        if (cb->zero_copy_off) {
+            ptls_mi355x_record_layer_set_zero_copy_bytes(tx, 0);
+            ptls_mi355x_record_layer_set_zero_copy_bytes(rx, 0);
+        }
+    }
+    /* the slot: ptls_send per record over a ptls_t whose traffic AEAD is the engine's (rapido today) */
+    ptls_context_t ectx = {fill_random, &ptls_get_time};
+    ptls_t *e = ptls_client_new(&ectx), *d = ptls_server_new(&ectx);
+    {
+        struct st_ptls_traffic_protection_t prot = {{0}}, dprot = {{0}};
+        prot.aead = ptls_aead_new_direct(keylen == 32 ? &ptls_mi355x_aes256gcm : &ptls_mi355x_aes128gcm, 1, key, iv);
+        dprot.aead = ptls_aead_new_direct(keylen == 32 ? &ptls_mi355x_aes256gcm : &ptls_mi355x_aes128gcm, 0, key, iv);
+        if (prot.aead == NULL || dprot.aead == NULL)
+            FAIL("ptls_aead_new_direct(engine)");
+        ptls_set_traffic_protection(e, &prot, 0);
+        ptls_set_traffic_protection(d, &dprot, 1);
+        e->state = PTLS_STATE_CLIENT_POST_HANDSHAKE;
+        d->state = PTLS_STATE_SERVER_POST_HANDSHAKE;
+    }
+    for (int rep = 0; rep < REPS + 1; ++rep) {
+        for (int mode = 0; mode < 2; ++mode) {
+            ptls_mi355x_record_layer_t *tx = txs[mode], *rx = rxs[mode];
+            ptls_mi355x_record_layer_set_seq(tx, seq0);
+            ptls_mi355x_record_layer_set_seq(rx, seq0);
+            memset(w2, 0, wl);
+            double t0 = now();
+            const size_t n2 = layer_send(tx, frag, len, nfrag, w2, XFER + 64 * PTLS_MI355X_TLS_OVERHEAD, mode);
+            const double dt = now() - t0;
+            if (n2 != wl || memcmp(w2, wire, wl) != 0)
+                FAIL("layer stream (mode %d) differs from the checked stream", mode);
+            t0 = now();
+            const size_t got = layer_recv(rx, w2, n2, p2, XFER + 64);
+            const double dr = now() - t0;
+            if (got != XFER || memcmp(p2, data, XFER) != 0)
+                FAIL("layer receive of the stream");
+            if (rep > 0) {
+                *(mode ? &t_layer4 : &t_layer1) += dt;
+                if (!mode)
+                    t_layer_recv += dr;
+            }
+        }
+        e->traffic_protection.enc.seq = seq0;
+        d->traffic_protection.dec.seq = seq0;
+        ptls_buffer_t sb;
+        ptls_buffer_init(&sb, "", 0);
+        double t0 = now();
+        for (size_t f = 0; f < nfrag; ++f)
+            if (ptls_send(e, &sb, frag[f], len[f]) != 0)
+                FAIL("ptls_send over the engine slot");
+        const double dt = now() - t0;
+        if (sb.off != wl || memcmp(sb.base, wire, wl) != 0)
+            FAIL("slot stream differs from the checked stream");
+        ptls_buffer_t rb;
+        ptls_buffer_init(&rb, "", 0);
+        t0 = now();
+        for (size_t off = 0; off < sb.off;) {
+            size_t n = sb.off - off;
+            if (ptls_receive(d, &rb, sb.base + off, &n) != 0)
+                FAIL("ptls_receive over the engine slot");
+            off += n;
+        }
+        const double dr = now() - t0;
+        if (rb.off != XFER || memcmp(rb.base, data, XFER) != 0)
+            FAIL("slot receive of the stream");
+        if (rep > 0) {
+            t_slot += dt;
+            t_slot_recv += dr;
+        }
+        ptls_buffer_dispose(&sb);
+        ptls_buffer_dispose(&rb);
+    }
+    ptls_free(e);
+    ptls_free(d);
+    for (int mode = 0; mode < 2; ++mode) {
+        ptls_mi355x_record_layer_free(txs[mode]);
+        ptls_mi355x_record_layer_free(rxs[mode]);
+    }
+    const double mb = XFER / 1e6 * REPS;
+    printf("rates {\"transport\": \"%s\", \"key_bits\": %zu, \"stream_bytes\": %u, \"reps\": %d, "
+           "\"layer_send_window_at_a_time_MBps\": %.1f, \"layer_send_all_windows_submitted_MBps\": %.1f, "
+           "\"layer_recv_windows_of_32_MBps\": %.1f, \"slot_ptls_send_MBps\": %.1f, \"slot_ptls_receive_MBps\": %.1f}\n",
+           transport, 8 * keylen, XFER, REPS, mb / t_layer1, mb / t_layer4, mb / t_layer_recv, mb / t_slot, mb / t_slot_recv);
+    ptls_clear_memory(key, sizeof(key));
+}
+
 int main(int argc, char **argv)
 {
     const char *transport = argc > 1 ? argv[1] : "zero_copy";
     const size_t keylen = argc > 2 ? (size_t)atoi(argv[2]) : 16;
     ptls_cipher_suite_t *cs = keylen == 32 ? suites256[0] : suites128[0];
-    arena_cap = 32u << 20;
+    arena_cap = 48u << 20;
     if (posix_memalign((void **)&arena, 4096, arena_cap) != 0)
         return 1;
     memset(arena, 0, arena_cap);
@@ -328,8 +562,12 @@ int main(int argc, char **argv)
         peer_receive(c, wire, wl, all + first, total - first);
         ++checks;
     }
-    printf("ok: %zu checks (5 scenarios), transport %s, AES-%zu, %u update_traffic_key callbacks\n", checks, transport, 8 * keylen,
-           cb.calls);
+    if (argc > 3 && strcmp(argv[3], "transfer") == 0) {
+        rapido_transfer(&cb, s, c, cs, transport, keylen);
+        checks += 2;
+    }
+    printf("ok: %zu checks (%s scenarios), transport %s, AES-%zu, %u update_traffic_key callbacks\n", checks,
+           argc > 3 && strcmp(argv[3], "transfer") == 0 ? "6" : "5", transport, 8 * keylen, cb.calls);
     ptls_free(s);
     ptls_free(c);
     ptls_mi355x_record_layer_free(cb.layer[0]);

@@ -8,7 +8,8 @@
                                            memory for the GPU read-bounds test, test only)
     scripts/_build/rl_stream            <- scripts/rl_stream.c (gcc, against the library: bench.py's host-to-host
                                            record-layer stream driver, a measurement tool)
-    scripts/_build/liblds_ceiling.so    <- scripts/lds_ceiling.hip (hipcc: the LDS ceiling probe bench.py runs live)
+    scripts/_build/liblds_ceiling.so    <- scripts/lds_ceiling.hip (hipcc, build_lds_probe: the LDS-ceiling probe of
+                                           scripts/gpu_lds_ceiling.sh, a measurement tool)
 
 The library is stamped with a hash of its sources (source_build_id: rapido_amd/csrc/* and include/ptls_mi355x.h).
 It is rebuilt from scratch whenever the stamp differs from the tree's hash, whatever the file times say, so the
@@ -170,7 +171,6 @@ def build_all(verbose: bool = False, force: bool = False) -> None:
     build_model(verbose, force)
     build_guard(verbose, force)
     build_rl_stream(verbose, force)
-    build_lds_probe(verbose, force)
 
 
 if __name__ == "__main__":
