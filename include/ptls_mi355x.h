@@ -475,6 +475,13 @@ int ptls_mi355x_record_layer_set_direct_dma(ptls_mi355x_record_layer_t *rl, int 
  * that copy 8-30 ms -- instead of inside a later window.  A record layer calls it before its first copy (DMA transports and
  * staged copy windows); a caller may call it at startup.  0, or -1 (ptls_mi355x_last_error). */
 int ptls_mi355x_prepare_copies(void);
+/* Sets up, now, everything a layer's windows would otherwise create at their first use: the stream and engine context
+ * of each of its 4 launch slots (a key setup each), their pinned staging and device buffers sized for
+ * `windows_per_launch` windows of up to `window_bytes` each (the wire or fragment bytes of one window), and the HIP
+ * copy path (ptls_mi355x_prepare_copies).  A fresh layer's first window on each slot otherwise costs ~3 ms of setup
+ * (DESIGN.md section 2); a connection calls this once, after creating its layers.  0, or -1 (windows outstanding, or
+ * an allocation failed). */
+int ptls_mi355x_record_layer_reserve(ptls_mi355x_record_layer_t *rl, size_t window_bytes, size_t windows_per_launch);
 /* zero-copy limit in bytes (default 4 MiB; 0 = always DMA copies); returns the previous value */
 size_t ptls_mi355x_record_layer_set_zero_copy_bytes(ptls_mi355x_record_layer_t *rl, size_t n);
 

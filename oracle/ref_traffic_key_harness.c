@@ -100,6 +100,9 @@ static int gpu_update_traffic_key(ptls_update_traffic_key_t *self, ptls_t *tls, 
             ptls_mi355x_record_layer_set_zero_copy_bytes(*l, 0);
         if (ret == 0 && cb->dma)
             ptls_mi355x_record_layer_set_direct_dma(*l, cb->dma);
+        /* every launch slot set up now, for rapido's windows: 16 send records, up to 32 received */
+        if (ret == 0 && ptls_mi355x_record_layer_reserve(*l, (is_enc ? 16 : 32) * (16384 + PTLS_MI355X_TLS_OVERHEAD), 1) != 0)
+            ret = PTLS_ERROR_LIBRARY;
     } else if (ptls_mi355x_record_layer_rekey(*l, key, cs->aead->key_size, iv) != 0) { /* a KeyUpdate epoch change */
         ret = PTLS_ERROR_LIBRARY;
     }
@@ -267,7 +270,10 @@ static size_t layer_recv(ptls_mi355x_record_layer_t *rl, const uint8_t *wire, si
             ++k;
         }
         size_t cons, olen, nrec;
+        const double t0 = getenv("XFER_DEBUG") != NULL ? now() : 0;
         const int rc = ptls_mi355x_record_layer_open(rl, wire + in, win, &cons, pt + got, cap - got, &olen, &nrec);
+        if (getenv("XFER_DEBUG") != NULL)
+            fprintf(stderr, "open window of %zu records at +%zu: %.1f us\n", k, in, (now() - t0) * 1e6);
         if (rc != 0 || cons != win || nrec != k)
             FAIL("layer open: rc %d, %zu of %zu bytes: %s", rc, cons, win, ptls_mi355x_record_layer_last_error());
         in += cons;
@@ -313,8 +319,8 @@ static void rapido_transfer(struct gpu_record_layer_cb *cb, ptls_t *s, ptls_t *c
     enum { REPS = 8 };
     double t_layer1 = 0, t_layer4 = 0, t_slot = 0, t_layer_recv = 0, t_slot_recv = 0;
     uint8_t *w2 = take(XFER + 64 * PTLS_MI355X_TLS_OVERHEAD + 64), *p2 = take(XFER + 64);
-    /* long-lived layers and AEADs, as a connection's (rep 0, untimed, creates their streams, staging and contexts);
-     * every rep restarts them at seq0, so each rep's output is the checked stream again */
+    /* long-lived layers and AEADs, as a connection's (set up by reserve; rep 0 untimed); every rep restarts them at
+     * seq0, so each rep's output is the checked stream again */
     ptls_mi355x_record_layer_t *txs[2], *rxs[2];
     for (int mode = 0; mode < 2; ++mode) {
         ptls_mi355x_record_layer_t *tx = txs[mode] = ptls_mi355x_record_layer_new(key, keylen, iv, seq0),
@@ -334,6 +340,10 @@ static void rapido_transfer(struct gpu_record_layer_cb *cb, ptls_t *s, ptls_t *c
             ptls_mi355x_record_layer_set_zero_copy_bytes(tx, 0);
             ptls_mi355x_record_layer_set_zero_copy_bytes(rx, 0);
         }
+        /* a connection's layers set up once (without this, each slot's first window pays ~3 ms of setup) */
+        if (ptls_mi355x_record_layer_reserve(tx, XWIN * (16384 + PTLS_MI355X_TLS_OVERHEAD), 1) != 0 ||
+            ptls_mi355x_record_layer_reserve(rx, XRECV * (16384 + PTLS_MI355X_TLS_OVERHEAD), 1) != 0)
+            FAIL("record_layer_reserve: %s", ptls_mi355x_record_layer_last_error());
     }
     /* the slot: ptls_send per record over a ptls_t whose traffic AEAD is the engine's (rapido today) */
     ptls_context_t ectx = {fill_random, &ptls_get_time};

@@ -77,6 +77,7 @@ EXPORTED_FUNCTIONS = (
     "ptls_mi355x_record_layer_flush", "ptls_mi355x_record_layer_set_coalesce", "ptls_mi355x_record_layer_launches",
     "ptls_mi355x_record_layer_cork",
     "ptls_mi355x_record_layer_set_direct_dma", "ptls_mi355x_tls_deliver_records", "ptls_mi355x_prepare_copies",
+    "ptls_mi355x_record_layer_reserve",
 )
 EXPORTED_OBJECTS = ("ptls_mi355x_aes128gcm", "ptls_mi355x_aes256gcm", "ptls_mi355x_aes128ctr",
                     "ptls_mi355x_aes256ctr", "ptls_mi355x_aes128ecb", "ptls_mi355x_aes256ecb")
@@ -203,6 +204,8 @@ def lib() -> C.CDLL:
             L.ptls_mi355x_record_layer_launches.restype = u64
             L.ptls_mi355x_record_layer_cork.argtypes = [vp, C.c_int]
             L.ptls_mi355x_record_layer_set_direct_dma.argtypes = [vp, C.c_int]
+            if hasattr(L, "ptls_mi355x_record_layer_reserve"):
+                L.ptls_mi355x_record_layer_reserve.argtypes = [vp, sz, sz]
         for name in ("ptls_mi355x_set_win16_records", "ptls_mi355x_set_split_records"):
             if hasattr(L, name):  # (absent from older builds used in A/B timing runs)
                 getattr(L, name).argtypes = [sz]
@@ -587,6 +590,11 @@ class RecordLayer:
         mode."""
         mode = on if on == RECORD_LAYER_DMA_IN else (1 if on else 0)
         return lib().ptls_mi355x_record_layer_set_direct_dma(self.handle, mode)
+
+    def reserve(self, window_bytes: int, windows_per_launch: int = 1) -> None:
+        """Sets up every launch slot now (stream, engine context, staging and device buffers for windows_per_launch
+        windows of window_bytes each) instead of at each slot's first window (ptls_mi355x_record_layer_reserve)."""
+        self._check(lib().ptls_mi355x_record_layer_reserve(self.handle, window_bytes, windows_per_launch), "reserve")
 
     def set_zero_copy_bytes(self, n: int) -> int:
         """Windows of at most n staged bytes run zero-copy on the pinned staging (0: DMA copies); -> previous."""

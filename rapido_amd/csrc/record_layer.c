@@ -441,8 +441,13 @@ int ptls_mi355x_record_layer_rekey(ptls_mi355x_record_layer_t *rl, const void *k
         memset(k, 0, sizeof(k));
         return rl_msg(ptls_mi355x_last_error());
     }
-    for (int i = 0; i < RL_SLOTS; ++i) { /* every slot's context holds the old key: the first gets the new one */
+    /* every slot's context holds the old key: slot 0 gets the new one, and the other slots that had a context get one
+     * too, now (a rekey keeps the layer's setup, ptls_mi355x_record_layer_reserve, instead of moving a key setup into
+     * each slot's next window) */
+    int had[RL_SLOTS];
+    for (int i = 0; i < RL_SLOTS; ++i) {
         rl_slot_t *s = &rl->slot[i];
+        had[i] = s->ctx != NULL;
         if (s->ctx != NULL) {
             if (s->stream != NULL)
                 RL_DEFER("rekey: slot synchronisation", hipStreamSynchronize(s->stream));
@@ -451,12 +456,35 @@ int ptls_mi355x_record_layer_rekey(ptls_mi355x_record_layer_t *rl, const void *k
         }
     }
     rl->slot[0].ctx = ctx;
+    for (int i = 1; i < RL_SLOTS; ++i)
+        if (had[i])
+            rl->slot[i].ctx = ptls_mi355x_aesgcm_new(k, key_size, 0); /* (NULL: created at the slot's next use) */
     memcpy(rl->key, k, key_size);
     memset(k, 0, sizeof(k));
     rl->key_size = key_size;
     memcpy(rl->iv, iv12, 12);
     rl->seq = rl->spec_seq = 0; /* a new traffic key starts at record 0 (setup_traffic_protection, lib/picotls.c:1217) */
     return 0;
+}
+
+int ptls_mi355x_record_layer_reserve(ptls_mi355x_record_layer_t *rl, size_t window_bytes, size_t windows_per_launch)
+{
+    if (window_bytes == 0 || windows_per_launch == 0 || windows_per_launch > RL_TICKETS)
+        return rl_msg("reserve: window bytes and 1..32 windows per launch");
+    /* the largest layout a launch of such windows takes (copy transport: descriptors, inputs, outputs, statuses, types,
+     * delivery parts, every piece 16-aligned), and its descriptors (an open parses up to inlen / 5 + 1) */
+    const size_t recs = window_bytes / 16384u + 2u;
+    const size_t need = windows_per_launch * (2u * window_bytes + recs * 128u) + 4096u;
+    for (int i = 0; i < RL_SLOTS; ++i) {
+        rl_slot_t *s = &rl->slot[i];
+        if (s->op.busy)
+            return rl_msg("reserve with windows outstanding");
+        if (slot_ready(rl, s) != 0 || reserve_stage(s, need) != 0 || reserve_device(s) != 0 ||
+            reserve_recs(s, windows_per_launch * (window_bytes / PTLS_MI355X_TLS_HEADER_SIZE + 1u)) != 0)
+            return -1;
+        s->copies_prepared = 1;
+    }
+    return ptls_mi355x_prepare_copies() == 0 ? 0 : rl_msg(ptls_mi355x_last_error());
 }
 
 int ptls_mi355x_record_layer_set_direct_dma(ptls_mi355x_record_layer_t *rl, int on)

@@ -550,3 +550,38 @@ def test_shared_registration_outlives_its_first_layer(gpu):
         ra.device_check()
         other.close()
     ra.device_check()
+
+
+@pytest.mark.parametrize("transport", ["direct", "copy"])
+def test_reserved_layer_across_a_rekey(gpu, transport):
+    """ptls_mi355x_record_layer_reserve sets up every launch slot before the first window (streams, contexts, staging
+    for rapido's windows); windows on all four slots, a rekey (every slot's context re-created under the new key), and
+    more windows -- every record against the oracle under its key and seq."""
+    rng = np.random.default_rng(1414)
+    key, key2 = rng.integers(0, 256, 16, dtype=np.uint8).tobytes(), rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+    iv, iv2 = rng.integers(0, 256, 12, dtype=np.uint8).tobytes(), rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    tx = ra.RecordLayer(key, iv, seq=9)
+    h = Host(transport, [tx], 1 << 23)
+    tx.reserve(16 * (16384 + ra.TLS_OVERHEAD), 1)
+    for k, v, s0 in ((key, iv, 9), (key2, iv2, 0)):
+        if k is key2:
+            tx.rekey(key2, iv2)
+            assert tx.seq == 0
+        wins_b = [[rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in rng.integers(1, 16385, 5)]
+                  for _ in range(6)]
+        wins = [[h.take(len(f), f) for f in w] for w in wins_b]
+        wants, s = [], s0
+        for w in wins_b:
+            want, s = oracle_window(k, v, s, w)
+            wants.append(want)
+        outs = [h.take(len(x) + 64) for x in wants]
+        tickets = []
+        for w, o in zip(wins, outs):
+            if len(tickets) == 4:
+                assert tx.wait(tickets.pop(0))[3] == 0
+            tickets.append(tx.seal_submit(w, o))
+        for t in tickets:
+            assert tx.wait(t)[3] == 0
+        for o, want in zip(outs, wants):
+            assert o[:len(want)].tobytes() == want
+    tx.close()
