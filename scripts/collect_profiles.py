@@ -73,7 +73,7 @@ def main(tag, label):
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, f"{label}_kernel_stats.csv"))
-    for w in ("16k", "16k-aes128", "ragged"):
+    for w in ("16k", "16k-aes128", "16k-max", "16k-max-aes128", "ragged"):
         p = os.path.join(src, f"trace_{w}", "run_kernel_stats.csv")
         if os.path.exists(p):
             shutil.copy(p, os.path.join(dst, f"{label}_kernel_stats_{w}.csv"))
@@ -135,7 +135,7 @@ def main(tag, label):
                 if line.strip().startswith("{"):
                     b = json.loads(line)
                     lines[b["config"]["workload"]] = b
-    name_of = {"1400": "trace", "16k": "trace_16k", "16k-aes128": "trace_16k-aes128", "ragged": "trace_ragged"}
+    name_of = {"1400": "trace", **{w: f"trace_{w}" for w in ("16k", "16k-aes128", "16k-max", "16k-max-aes128", "ragged")}}
     la = {}
     for w, d in name_of.items():
         p = os.path.join(src, d, "run_kernel_trace.csv")
@@ -156,7 +156,8 @@ def main(tag, label):
     with open(os.path.join(dst, f"{label}_launches.json"), "w") as f:
         json.dump(la, f, indent=1)
     hc = {}
-    for w, d in (("1400", "pmc_sq"), ("16k-aes128", "pmc_sq_16k-aes128")):
+    for w, d in (("1400", "pmc_sq"), ("16k-aes128", "pmc_sq_16k-aes128"),
+                 *((w, f"pmc_clk_{w}") for w in ("16k", "16k-max", "16k-max-aes128", "ragged"))):
         p = os.path.join(src, d, "run_counter_collection.csv")
         line = lines.get(WORKLOADS[w]["name"])
         if os.path.exists(p):
@@ -166,8 +167,11 @@ def main(tag, label):
                     continue  # microsecond kernels: GRBM_GUI_ACTIVE spans more than the dispatch, no clock to read
                 # the kernel's busy cycles over its UN-profiled launch time (the bench line's HIP events): the clock
                 # the chip holds in the benchmark itself; the profiled dispatches run slower (counter collection)
+                kt = la.get(w, {}).get("launches", {}).get(k)
                 if line is not None and line["roofline"]["kernel"] == k:
                     ghz, how = cyc / (line["roofline"]["launch_ms"] * 1e6), "GRBM_GUI_ACTIVE / 8 / bench launch_ms"
+                elif kt is not None:  # the other direction: its timed launches in the counter-free kernel trace
+                    ghz, how = cyc / (kt["timed_mean_ms"] * 1e6), "GRBM_GUI_ACTIVE / 8 / kernel-trace timed mean"
                 else:
                     ghz, how = ghz_prof, "GRBM_GUI_ACTIVE / 8 / profiled dispatch time"
                 hc[w][k] = {"ghz": round(ghz, 3), "ghz_profiled_dispatch": round(ghz_prof, 3),

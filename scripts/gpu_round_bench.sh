@@ -22,7 +22,11 @@ for w in 16k 16k-aes128 16k-max 16k-max-aes128 ragged; do
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_fetch_$w -o run --output-format csv -- python bench.py --workload $w --steps 2 --warmup 1 --no-cpu-baseline --no-e2e --no-workloads --check 0 --prewarm-ms 0 > $OUT/pmc_fetch_$w.log 2>&1
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/pmc_write_$w -o run --output-format csv -- python bench.py --workload $w --steps 2 --warmup 1 --no-cpu-baseline --no-e2e --no-workloads --check 0 --prewarm-ms 0 > $OUT/pmc_write_$w.log 2>&1
 done
+# GPU-busy cycles of the other workloads' kernels (profiles/held_clock.json: the clock their lds_roofline is priced at)
+for w in 16k 16k-max 16k-max-aes128 ragged; do
+  timeout -k 10 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_LDS_IDX_ACTIVE --kernel-trace -d $OUT/pmc_clk_$w -o run --output-format csv -- python bench.py --workload $w --steps 2 --warmup 1 --no-cpu-baseline --no-e2e --no-workloads --check 0 --prewarm-ms 0 > $OUT/pmc_clk_$w.log 2>&1
+done
 # rocprofv3 kernel-trace summaries of the other workloads (profiles/<label>_kernel_stats_<w>.csv)
-for w in 16k 16k-aes128 ragged; do
+for w in 16k 16k-aes128 16k-max 16k-max-aes128 ragged; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_$w -o run --output-format csv -- python bench.py --workload $w --steps 10 --warmup 2 --no-cpu-baseline --no-e2e --no-workloads > $OUT/trace_$w.log 2>&1
 done
