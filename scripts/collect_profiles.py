@@ -184,7 +184,7 @@ def main(tag, label):
     pmc = {}
     traffic = {}
     for k in fetch:
-        if "setup" in k:
+        if "setup" in k or "mi355x_gcm_" not in k:
             continue
         fb = fetch[k]["FETCH_SIZE"] * 1024 * 2
         wb = write.get(k, {}).get("WRITE_SIZE", 0.0) * 1024

@@ -1,0 +1,66 @@
+"""bench.py's roofline bookkeeping on CPU: the committed held-clock and PMC-traffic files name real workloads and the
+batch kernels those workloads run on, and lds_roofline prices the LDS model at the held clock (DESIGN.md section 3,
+"The LDS ceiling, pinned with counters"; section 5)."""
+import json
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNEL = re.compile(r"^mi355x_gcm_(seal|open)_aes(128|256)_k4$")
+
+
+def _load(name):
+    with open(os.path.join(ROOT, "profiles", name)) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("name", ["held_clock.json", "pmc_traffic.json"])
+def test_profile_files_name_workloads_and_their_kernels(name):
+    import bench
+    d = _load(name)
+    assert d
+    for w, kernels in d.items():
+        assert w in bench.WORKLOADS, w
+        bits = "128" if bench.WORKLOADS[w]["key"] == 16 else "256"
+        for k in kernels:
+            m = KERNEL.match(k)
+            assert m and m.group(2) == bits, (w, k)
+
+
+def test_held_clocks_are_plausible_and_sourced():
+    for w, kernels in _load("held_clock.json").items():
+        for k, v in kernels.items():
+            assert 1.0 < v["ghz"] <= 2.45, (w, k, v)
+            src = v["source"].split(" ")[0]
+            assert os.path.exists(os.path.join(ROOT, src)), (w, k, src)
+
+
+def test_every_bench_workload_has_a_held_clock():
+    import bench
+    d = _load("held_clock.json")
+    for w, wl in bench.WORKLOADS.items():
+        bits = "128" if wl["key"] == 16 else "256"
+        assert {f"mi355x_gcm_seal_aes{bits}_k4", f"mi355x_gcm_open_aes{bits}_k4"} <= set(d.get(w, {})), w
+
+
+def test_lds_roofline_prices_the_model_at_the_held_clock():
+    import bench
+    k = "mi355x_gcm_seal_aes128_k4"
+    ghz = _load("held_clock.json")["16k-aes128"][k]["ghz"]
+    nominal = 256 * 2.4 * 64 / 330 * 16  # GB/s of payload at 2.4 GHz: 330 LDS cycles per 64 blocks
+    r = bench.lds_roofline(k, 1000.0, "16k-aes128", 16, 133, 16, nominal, 256)
+    assert r["held_clock_ghz"] == ghz
+    assert r["peak"] == pytest.approx(256 * ghz * 64 / 330 * 16, rel=1e-3)
+    assert r["frac"] == pytest.approx(1000.0 / r["peak"], rel=1e-3)
+    assert r["frac_nominal_2p4ghz"] == pytest.approx(1000.0 / nominal, rel=1e-3)
+    none = bench.lds_roofline(k, 1000.0, "no-such-workload", 16, 133, 16, nominal, 256)
+    assert none["peak"] == pytest.approx(nominal, rel=1e-3) and "2.4 GHz" in none["held_clock_source"]
+
+
+def test_algorithmic_bytes_follow_survey_8d():
+    import bench
+    # 2845 B per 1400-B seal with a 5-B AAD (16-B descriptor + 8-B seq)
+    assert bench.algorithmic_bytes(1400, 1, 5, True) == 2845
+    assert bench.algorithmic_bytes(1400, 1, 5, False) == 1400 + 16 + 5 + 24 + 1400 + 4
