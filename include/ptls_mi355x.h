@@ -453,11 +453,12 @@ const char *ptls_mi355x_record_layer_last_error(void);
  * output) is copied into the layer's pinned, mapped staging, which the kernel reads and writes over PCIe (one
  * launch, one synchronisation); larger windows move by one H2D and one D2H DMA copy.  Results are identical. */
 /* registers host memory [base, base+len) that stays allocated (a connection's socket buffers) for direct calls
- * (hipHostRegister, mapped); up to 8 ranges per layer.  Layers share registrations process-wide: a range another
- * layer registered (the other direction of the connection sharing a buffer) is counted, and unmapped only when the
- * last layer holding it unregisters it or is freed.  A range the application registered itself is used as it is and
- * never unregistered here; it must stay registered while a layer uses it.  0, or -1
- * (ptls_mi355x_record_layer_last_error). */
+ * (hipHostRegister, mapped); up to 8 ranges per layer.  Layers share registrations process-wide: a range inside one
+ * a layer registered (the other direction of the connection sharing a buffer, or a part of it) is counted on that
+ * mapping, which is unmapped only when the last layer holding it unregisters it or is freed; a range that overlaps a
+ * registered one without lying inside it is refused (register the enclosing range first).  A range the application
+ * registered itself is used as it is and never unregistered here; it must stay registered while a layer uses it.  0,
+ * or -1 (ptls_mi355x_record_layer_last_error). */
 int ptls_mi355x_record_layer_register(ptls_mi355x_record_layer_t *rl, void *base, size_t len);
 /* unregisters a range given to ptls_mi355x_record_layer_register (by its base); 0 or -1.  The layer unregisters
  * its ranges when freed. */

@@ -65,10 +65,11 @@
 #define RL_STAGE_HEADROOM ((size_t)2 << 20)
 
 typedef struct {
-    uint8_t *base; /* host address as registered */
-    uint8_t *dev;  /* its device address */
+    uint8_t *base;   /* host address as registered */
+    uint8_t *dev;    /* its device address */
     size_t len;
-    int owned;     /* holds a reference on the process-wide entry (g_reg) of the range */
+    int owned;       /* holds a reference on the process-wide entry (g_reg) of the range that contains it */
+    uint8_t *shared; /* that entry's base */
 } rl_region_t;
 
 /* one layer's part of a window */
@@ -183,6 +184,7 @@ void ptls_mi355x_defer_error(const char *what, int err);
 static void op_discard(rl_op_t *op);
 static void op_release_layers(rl_op_t *op);
 static int rl_flush_n(ptls_mi355x_record_layer_t *rl, size_t n);
+static int overlaps(const void *a, size_t alen, const void *b, size_t blen);
 
 static size_t up16(size_t x) { return (x + 15) & ~(size_t)15; }
 
@@ -506,14 +508,15 @@ size_t ptls_mi355x_record_layer_set_zero_copy_bytes(ptls_mi355x_record_layer_t *
  * (hipHostRegister), the others share that mapping, and it is unmapped when the LAST of them lets go.  Two layers
  * share ranges whenever the two directions of a connection use the same socket buffers; with a per-layer "first one
  * owns it" rule the owner's free unmapped a range the other layer still ran windows on, and those kernels then
- * faulted on the unmapped host addresses.  A range the application registered itself (hipHostRegister answers
- * already-registered and the table does not hold it) is used and never unregistered here.
+ * faulted on the unmapped host addresses.  A range inside one mapped here shares that mapping (and counts on it); a
+ * range that overlaps one mapped here without lying inside it is refused, since only the mapped part would be reachable
+ * and the rest would fault.  A range the application registered itself (hipHostRegister answers already-registered and
+ * the table holds nothing over it) is used and never unregistered here.
  */
 typedef struct {
-    uint8_t *base, *dev;
+    uint8_t *base, *dev; /* mapped here (hipHostRegister) */
     size_t len;
-    int refs;  /* layers holding it */
-    int owned; /* mapped by this table (else the application's: never unmapped here) */
+    int refs; /* layer registrations inside it */
 } rl_shared_range_t;
 
 #define RL_MAX_SHARED 1024
@@ -530,6 +533,21 @@ static rl_shared_range_t *shared_range(const void *base)
     return NULL;
 }
 
+/* a table entry overlapping [base, base + len) -- one containing it if there is one -- or NULL (g_reg_mu held) */
+static rl_shared_range_t *shared_overlap(const uint8_t *base, size_t len)
+{
+    rl_shared_range_t *any = NULL;
+    for (size_t i = 0; i < g_nreg; ++i) {
+        rl_shared_range_t *r = &g_reg[i];
+        if (!overlaps(r->base, r->len, base, len))
+            continue;
+        if (base >= r->base && len <= r->len - (size_t)(base - r->base))
+            return r;
+        any = r;
+    }
+    return any;
+}
+
 int ptls_mi355x_record_layer_register(ptls_mi355x_record_layer_t *rl, void *base, size_t len)
 {
     if (rl->nreg == RL_MAX_REGIONS || base == NULL || len == 0)
@@ -538,14 +556,19 @@ int ptls_mi355x_record_layer_register(ptls_mi355x_record_layer_t *rl, void *base
         if (rl->reg[i].base == base)
             return rl_msg("range already registered with this layer");
     pthread_mutex_lock(&g_reg_mu);
-    rl_shared_range_t *sr = shared_range(base);
-    if (sr != NULL && sr->len >= len) { /* mapped already (by another layer): shared */
-        ++sr->refs;
-        rl->reg[rl->nreg++] = (rl_region_t){(uint8_t *)base, sr->dev, len, 1};
+    rl_shared_range_t *sr = shared_overlap((const uint8_t *)base, len);
+    if (sr != NULL) {
+        const size_t off = (size_t)((const uint8_t *)base - sr->base);
+        if ((const uint8_t *)base < sr->base || len > sr->len - off) {
+            pthread_mutex_unlock(&g_reg_mu);
+            return rl_msg("range overlaps a registered range without lying inside it (register the enclosing range)");
+        }
+        ++sr->refs; /* inside a range mapped here (by this or another layer): shared and counted */
+        rl->reg[rl->nreg++] = (rl_region_t){(uint8_t *)base, sr->dev + off, len, 1, sr->base};
         pthread_mutex_unlock(&g_reg_mu);
         return 0;
     }
-    if (sr == NULL && g_nreg == RL_MAX_SHARED) {
+    if (g_nreg == RL_MAX_SHARED) {
         pthread_mutex_unlock(&g_reg_mu);
         return rl_msg("too many registered ranges in the process");
     }
@@ -565,11 +588,11 @@ int ptls_mi355x_record_layer_register(ptls_mi355x_record_layer_t *rl, void *base
         pthread_mutex_unlock(&g_reg_mu);
         return rl_fail("hipHostGetDevicePointer", e);
     }
-    if (sr == NULL) {
-        g_reg[g_nreg++] = (rl_shared_range_t){(uint8_t *)base, dev, len, 1, owned};
-        rl->reg[rl->nreg++] = (rl_region_t){(uint8_t *)base, dev, len, 1};
-    } else { /* a longer range over a shorter one mapped here: the application's, or unmappable; not counted */
-        rl->reg[rl->nreg++] = (rl_region_t){(uint8_t *)base, dev, len, 0};
+    if (owned) {
+        g_reg[g_nreg++] = (rl_shared_range_t){(uint8_t *)base, dev, len, 1};
+        rl->reg[rl->nreg++] = (rl_region_t){(uint8_t *)base, dev, len, 1, (uint8_t *)base};
+    } else { /* the application's registration: used, not counted, never unmapped here */
+        rl->reg[rl->nreg++] = (rl_region_t){(uint8_t *)base, dev, len, 0, NULL};
     }
     pthread_mutex_unlock(&g_reg_mu);
     return 0;
@@ -588,10 +611,9 @@ int ptls_mi355x_record_layer_unregister(ptls_mi355x_record_layer_t *rl, void *ba
             hipError_t e = hipSuccess;
             if (rl->reg[i].owned) { /* holds a reference on the shared entry */
                 pthread_mutex_lock(&g_reg_mu);
-                rl_shared_range_t *sr = shared_range(base);
+                rl_shared_range_t *sr = shared_range(rl->reg[i].shared);
                 if (sr != NULL && --sr->refs == 0) {
-                    if (sr->owned)
-                        e = hipHostUnregister(base);
+                    e = hipHostUnregister(sr->base);
                     *sr = g_reg[--g_nreg];
                 }
                 pthread_mutex_unlock(&g_reg_mu);

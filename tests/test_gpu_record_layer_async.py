@@ -552,6 +552,45 @@ def test_shared_registration_outlives_its_first_layer(gpu):
     ra.device_check()
 
 
+def test_registration_inside_a_shared_range_and_partial_overlaps(gpu):
+    """A range inside one another layer mapped shares that mapping and counts on it: the enclosing range's layer is
+    freed first and the inner range's windows still run in place on it (the 1 MiB mapping stays while the inner range
+    holds it).  A range that overlaps a mapped one without lying inside it (only the mapped part would be reachable by
+    the kernels) is refused, before and after; once the last holder lets go the whole buffer registers."""
+    rng = np.random.default_rng(1515)
+    key, iv = rng.integers(0, 256, 16, dtype=np.uint8).tobytes(), rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    buf = page_buffer(1 << 21)
+    frags_b = [rng.integers(0, 256, 16384, dtype=np.uint8).tobytes() for _ in range(4)]
+    want, _ = oracle_window(key, iv, 0, frags_b)
+    outer, inner, other = ra.RecordLayer(key, iv), ra.RecordLayer(key, iv), ra.RecordLayer(key, iv)
+    outer.register(buf[: 1 << 20])
+    for bad in (buf[(1 << 20) - 4096:(1 << 20) + 4096], buf):  # straddles the end; encloses it
+        with pytest.raises(RuntimeError, match="overlaps a registered range"):
+            other.register(bad)
+    inner_buf = buf[1 << 18:(1 << 18) + (1 << 19)]
+    inner.register(inner_buf)
+    outer.close()  # the mapping stays: the inner registration counts on it
+    ra.device_check()
+    frags = []
+    for i, f in enumerate(frags_b):
+        v = inner_buf[i * 16384:(i + 1) * 16384]
+        v[:] = np.frombuffer(f, np.uint8)
+        frags.append(v)
+    wire = inner_buf[1 << 17:(1 << 17) + len(want)]
+    olen, n = inner.seal_into(frags, wire)
+    assert wire[:olen].tobytes() == want and n == 4
+    with pytest.raises(RuntimeError, match="overlaps a registered range"):
+        other.register(buf)  # the mapping kept for the inner range is still the enclosing 1 MiB one
+    other.register(buf[:1 << 20])  # inside it: shared
+    inner.close()
+    other.close()
+    ra.device_check()
+    last = ra.RecordLayer(key, iv)
+    last.register(buf)  # nothing mapped over it any more
+    last.close()
+    ra.device_check()
+
+
 @pytest.mark.parametrize("transport", ["direct", "copy"])
 def test_reserved_layer_across_a_rekey(gpu, transport):
     """ptls_mi355x_record_layer_reserve sets up every launch slot before the first window (streams, contexts, staging
