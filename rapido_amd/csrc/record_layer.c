@@ -174,7 +174,7 @@ struct rl_queued {
     uint8_t type; /* seal: the content type its records carry (a group never mixes types: rl_flush_n) */
 };
 
-static char rl_err[160];
+static _Thread_local char rl_err[160]; /* per thread, as the engine's (layers on different threads) */
 
 /* gcm_engine.hip: an error met where nothing can be returned (a free path) -- printed and kept for
  * ptls_mi355x_device_check, never dropped */

@@ -180,6 +180,21 @@ def test_async_stream_matches_oracle(gpu, transport):
             rng.integers(0, 256, 12, dtype=np.uint8).tobytes(), rng)
 
 
+def test_layers_on_concurrent_threads(gpu):
+    """A layer is used by one thread at a time (include/ptls_mi355x.h section 5); four threads stream windows through
+    their own layer pairs at once, one transport each (ctypes releases the GIL, so the calls overlap), sharing the
+    process-wide registration table, the copy warm-up and the device: every wire byte and plaintext against the
+    oracle."""
+    def one(t):
+        rng = np.random.default_rng(700 + t)
+        _stream(["direct", "direct_dma_in", "zero_copy", "copy"][t], 12, 4,
+                rng.integers(0, 256, 16 * (1 + t % 2), dtype=np.uint8).tobytes(),
+                rng.integers(0, 256, 12, dtype=np.uint8).tobytes(), rng)
+    with ThreadPoolExecutor(4) as ex:
+        for f in [ex.submit(one, t) for t in range(4)]:
+            f.result()
+
+
 @pytest.mark.parametrize("family", ["split", "window16", "batch"])
 def test_async_stream_families(gpu, family):
     rng = np.random.default_rng(65)
