@@ -214,6 +214,33 @@ def test_slot_zero_copy_and_copied(gpu, zero_copy):
         ra.set_slot_zero_copy_bytes(prev)
 
 
+def test_slot_contexts_on_concurrent_threads(gpu):
+    """picotls contexts are used by one thread each; a server runs one per connection on several threads.  Eight
+    threads seal and open through their own slot contexts at once (the calls share the device's staging under its
+    lock; ctypes releases the GIL, so they overlap), AES-128 and AES-256, every size class: the oracle's bytes."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    def one(t):
+        rng = np.random.default_rng(900 + t)
+        keylen = 16 if t % 2 == 0 else 32
+        algo = "aes128gcm" if keylen == 16 else "aes256gcm"
+        key, iv = rng.integers(0, 256, keylen, dtype=np.uint8).tobytes(), rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+        a, d = ra.aead_new_direct(algo, True, key, iv), ra.aead_new_direct(algo, False, key, iv)
+        for i in range(24):
+            n = int(rng.choice([0, 1, 15, 16, 17, 1400, 4097, 16384, 16401]))
+            pt = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+            aad = rng.integers(0, 256, int(rng.integers(0, 40)), dtype=np.uint8).tobytes()
+            ct = a.encrypt(pt, i, aad)
+            assert ct == oracle.seal(key, oracle.build_iv(iv, i), aad, pt), (t, i, n)
+            assert d.decrypt(ct, i, aad) == pt
+        a.free()
+        d.free()
+
+    with ThreadPoolExecutor(8) as ex:
+        for f in [ex.submit(one, t) for t in range(8)]:
+            f.result()
+
+
 @pytest.mark.parametrize("algo,keylen", [("aes128gcm", 16), ("aes256gcm", 32)])
 def test_slot_streaming_and_record_layer(gpu, algo, keylen):
     """The TLS record-layer call sequence (lib/picotls.c:630-643) and t/picotls.c:161-198."""
