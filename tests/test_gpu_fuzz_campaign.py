@@ -1,9 +1,10 @@
-"""A time-boxed random campaign over the AEAD batch API, against the CPU oracle (bit-exact): every case draws a fresh
-seed, a kernel family, K lanes per record, the key size, 1..300 records whose lengths mix every size class the walk
+"""A time-boxed random campaign over the AEAD batch API and the TLS framing API, against the CPU oracle (bit-exact):
+every case draws a fresh seed, a kernel family, K lanes per record, the key size, 1..300 records whose lengths mix every size class the walk
 treats differently (empty, under a block, TLS sizes, 16 KiB +- a block, up to 70 000 B), AAD lengths 0..300 at
 arbitrary byte offsets, records in place or not, and tampers with a few tags or ciphertext bytes before the open.
 Checked per record: the sealed bytes and tag against the oracle, the open's status, the plaintext of every verified
-record, and a zeroed output for every record that fails (fusion's open leaves nothing, lib/fusion.c:656-679).
+record, and a zeroed output for every record that fails (fusion's open leaves nothing, lib/fusion.c:656-679).  A
+third of the cases frame TLS 1.3 records instead (run_tls_case).
 
 RAPIDO_FUZZ_SECONDS sets the budget (default 20 s), RAPIDO_FUZZ_SEED the first case's seed (default fixed; "random"
 takes it from the clock); RAPIDO_FUZZ_LOG names a file that gets the campaign's summary as one JSON line.  The seed of
@@ -121,15 +122,106 @@ def run_case(seed, stats):
     stats["families"][family] = stats["families"].get(family, 0) + 1
 
 
+def conn_iv(iv: bytes, conn_id: int) -> bytes:
+    """rapido's derive_connection_aead_iv (lib/rapido.c:127-133): IV bytes 0..3 ^= BE32(connection_id)."""
+    return (int.from_bytes(iv[:4], "big") ^ conn_id).to_bytes(4, "big") + iv[4:]
+
+
+def run_tls_case(seed, stats):
+    """TLS 1.3 framing (include/ptls_mi355x.h section 4): random fragments and content types, one connection or several
+    (per-record connection ids, the _multi entry points), sealed in one launch against the oracle's record layer
+    (pinned to the reference ptls_send); then a received stream of those records, some re-sealed by the oracle with
+    padding, some tampered, opened in one launch against the oracle's ptls_receive model (status, type, plaintext,
+    nothing released by a failed record)."""
+    import torch
+    rng = np.random.default_rng(seed)
+    family = FAMILIES[int(rng.integers(0, len(FAMILIES)))]
+    keylen = int(rng.choice([16, 32]))
+    key = rng.integers(0, 256, keylen, dtype=np.uint8).tobytes()
+    iv = rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    n = int(rng.integers(1, 4)) if rng.random() < 0.2 else int(rng.integers(1, 201))
+    multi = bool(rng.random() < 0.4)
+    conns = rng.choice([0, 1, 7, int(rng.integers(0, 2 ** 32))], n).astype(np.uint32) if multi else np.zeros(n, np.uint32)
+    cls = rng.choice(len(LEN_CLASSES) - 1, n, p=LEN_WEIGHTS[:-1] / LEN_WEIGHTS[:-1].sum())
+    lens = [min(int(rng.integers(*LEN_CLASSES[c])), ra.TLS_MAX_FRAGMENT) for c in cls]
+    trecs = np.zeros(n, ra.TLS_RECORD_DTYPE)
+    off = woff = 0
+    for i, ln in enumerate(lens):
+        off += int(rng.integers(0, 32))
+        woff += int(rng.integers(0, 32))
+        trecs[i] = (off, woff, int(rng.integers(0, 2 ** 48)), ln, int(rng.choice([23, 23, 23, 22, 21])))
+        off += ln
+        woff += ln + ra.TLS_OVERHEAD
+    src = rng.integers(0, 256, off + 16, dtype=np.uint8)
+    ivs = [conn_iv(iv, int(c)) for c in conns]
+    with kernel_family(family, framing=True):
+        eng = ra.Engine(key)
+        d_src, d_recs = torch.from_numpy(src).cuda(), torch.from_numpy(trecs.view(np.uint8)).cuda()
+        d_conn = torch.from_numpy(conns.view(np.int32)).cuda()
+        d_wire = torch.zeros(woff + 16, dtype=torch.uint8, device="cuda")
+        eng.tls_seal_records(iv, d_recs.data_ptr(), n, d_src.data_ptr(), d_wire.data_ptr(),
+                             conn_ptr=d_conn.data_ptr() if multi else 0)
+        torch.cuda.synchronize()
+        wire = d_wire.cpu().numpy()
+        received, seqs = [], []
+        for i, t in enumerate(trecs):
+            frag = src[int(t["src"]):int(t["src"]) + int(t["len"])].tobytes()
+            want = oracle.tls_seal_record(key, ivs[i], int(t["seq"]), int(t["type"]), frag)
+            got = wire[int(t["dst"]):int(t["dst"]) + len(want)].tobytes()
+            assert got == want, f"seed {seed}: seal of record {i} (len {int(t['len'])}, {family}, multi {multi})"
+            u = rng.random()
+            if u < 0.1 and int(t["len"]) + 64 <= ra.TLS_MAX_FRAGMENT + 256:  # the peer padded it
+                got = oracle.tls_seal_record(key, ivs[i], int(t["seq"]), int(t["type"]), frag, int(rng.integers(1, 64)))
+            elif u < 0.13:  # damaged in flight: a ciphertext or tag byte
+                w = bytearray(got)
+                w[int(rng.integers(5, len(w)))] ^= 1 << int(rng.integers(0, 8))
+                got = bytes(w)
+            received.append(got)
+            seqs.append(int(t["seq"]))
+        buf = b"".join(received)
+        rc, orecs, used, _ = ra.tls_parse_records(buf, 0)
+        assert rc == 0 and len(orecs) == n and used == len(buf), f"seed {seed}: parse"
+        orecs["seq"] = seqs
+        d_buf, d_orecs = torch.from_numpy(np.frombuffer(buf, np.uint8).copy()).cuda(), torch.from_numpy(orecs.view(np.uint8)).cuda()
+        pt_size = int(orecs["dst"][-1]) + int(orecs["len"][-1]) + 16
+        d_pt = torch.zeros(pt_size, dtype=torch.uint8, device="cuda")
+        d_st = torch.zeros(n, dtype=torch.int32, device="cuda")
+        d_ty = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        eng.tls_open_records(iv, d_orecs.data_ptr(), n, d_buf.data_ptr(), d_pt.data_ptr(), d_st.data_ptr(),
+                             d_ty.data_ptr(), conn_ptr=d_conn.data_ptr() if multi else 0)
+        torch.cuda.synchronize()
+        pt, st, ty = d_pt.cpu().numpy(), d_st.cpu().numpy().view(np.uint32), d_ty.cpu().numpy()
+        bad = 0
+        for i, w in enumerate(received):
+            want = oracle.tls_open_record(key, ivs[i], seqs[i], w)
+            o = orecs[i]
+            where = f"seed {seed}: open of record {i} ({family}, multi {multi})"
+            if want == oracle.TLS_BAD_MAC:
+                bad += 1
+                assert st[i] == ra.TLS_BAD_RECORD_MAC, where
+                assert not pt[int(o["dst"]):int(o["dst"]) + max(int(o["len"]) - 16, 0)].any(), where + ": released"
+            elif want == oracle.TLS_NO_TYPE:
+                assert st[i] == ra.TLS_UNEXPECTED_MESSAGE, where
+            else:
+                assert st[i] == len(want[0]) and ty[i] == want[1], where + f": status {st[i]:#x} type {ty[i]}"
+                assert pt[int(o["dst"]):int(o["dst"]) + int(st[i])].tobytes() == want[0], where
+        eng.close()
+    stats["tls_cases"] += 1
+    stats["tls_records"] += n
+    stats["tls_refused"] += bad
+    stats["families"][family] = stats["families"].get(family, 0) + 1
+
+
 def test_fuzz_campaign(gpu):
     budget = float(os.environ.get("RAPIDO_FUZZ_SECONDS", "20"))
     seed = os.environ.get("RAPIDO_FUZZ_SEED", "20250")  # fixed by default (the suite's gate); "random": from the clock
     base = int(time.time()) & 0xFFFFFFF if seed == "random" else int(seed)
     stats = {"seed_base": base, "cases": 0, "records": 0, "payload_bytes": 0, "tampered": 0, "in_place": 0,
-             "families": {}}
+             "tls_cases": 0, "tls_records": 0, "tls_refused": 0, "families": {}}
     t0 = last = time.time()
     while time.time() - t0 < budget:
-        run_case(base + stats["cases"], stats)
+        seed = base + stats["cases"] + stats["tls_cases"]
+        (run_tls_case if seed % 3 == 2 else run_case)(seed, stats)
         if time.time() - last > 30:  # progress (a long campaign under a watchdog that wants output)
             last = time.time()
             print("progress", json.dumps(stats), flush=True)
