@@ -2050,16 +2050,22 @@ Fail:
     return nullptr;
 }
 
-int ptls_mi355x_aesgcm_release(ptls_mi355x_aesgcm_context_t *ctx)
+/* release (the caller gets the first error) or free (nothing to return it to: every error deferred, see defer) */
+static int context_release(ptls_mi355x_aesgcm_context_t *ctx, bool deferred)
 {
     if (ctx == nullptr)
         return 0;
     DeviceGuard guard(ctx->device);
     int rc = 0;
     auto chk = [&](const char *what, hipError_t e) {
-        if (e != hipSuccess && rc == 0)
+        if (e == hipSuccess)
+            return;
+        if (deferred)
+            defer(what, e);
+        else if (rc == 0)
             rc = fail(what, e);
-        defer(what, e);
+        else /* a later error of the same release: printed (the first one is returned) */
+            fprintf(stderr, "ptls_mi355x: %s: %s\n", what, hipGetErrorString(e));
     };
     /* launches on caller streams may still read the key image; a fault of any earlier work surfaces here */
     chk("context free: hipDeviceSynchronize", hipDeviceSynchronize());
@@ -2086,7 +2092,9 @@ int ptls_mi355x_aesgcm_release(ptls_mi355x_aesgcm_context_t *ctx)
     return rc;
 }
 
-void ptls_mi355x_aesgcm_free(ptls_mi355x_aesgcm_context_t *ctx) { (void)ptls_mi355x_aesgcm_release(ctx); }
+int ptls_mi355x_aesgcm_release(ptls_mi355x_aesgcm_context_t *ctx) { return context_release(ctx, false); }
+
+void ptls_mi355x_aesgcm_free(ptls_mi355x_aesgcm_context_t *ctx) { (void)context_release(ctx, true); }
 
 ptls_mi355x_aesgcm_context_t *ptls_mi355x_aesgcm_new_on(int device, const void *key, size_t key_size, size_t capacity)
 {
