@@ -214,6 +214,38 @@ def test_slot_zero_copy_and_copied(gpu, zero_copy):
         ra.set_slot_zero_copy_bytes(prev)
 
 
+@pytest.mark.parametrize("lanes", [1, 4, 8])
+def test_gcm_spec_vectors_in_a_batch(gpu, lanes):
+    """The GCM specification's test cases with 96-bit IVs (McGrew-Viega 1-4, AES-128, as cifra's testmodes.c; 13-16,
+    AES-256, tests/test_oracle.py) in one batch per key, and the AES-256 ones through the slot: tags and
+    ciphertext against the published values."""
+    from test_oracle import MV, MV256
+    prev = ra.set_lanes_per_record(lanes)
+    try:
+        for keyhex in sorted({v[0] for v in MV + MV256}):
+            cases = [v for v in MV + MV256 if v[0] == keyhex]
+            key = bytes.fromhex(keyhex)
+            eng = ra.Engine(key)
+            for _, pt, aad, iv, ct, tag in cases:  # one record per batch (the cases' IVs differ; the batch IV is static)
+                ptb, aadb = bytes.fromhex(pt), bytes.fromhex(aad)
+                recs = np.zeros(1, ra.RECORD_DTYPE)
+                recs[0] = (0, 0, 0, 0, len(ptb), len(aadb))
+                src = np.frombuffer(ptb + bytes(32), np.uint8).copy()
+                out, _ = run_batch(eng, True, bytes.fromhex(iv), recs, src, len(src), np.frombuffer(aadb + bytes(16), np.uint8).copy())
+                got = out[:len(ptb) + 16].tobytes().hex()
+                assert got.startswith(ct) and got.endswith(tag), (keyhex[:8], len(ptb))
+                back, st = run_batch(eng, False, bytes.fromhex(iv), recs, out, len(src), np.frombuffer(aadb + bytes(16), np.uint8).copy())
+                assert st[0] == len(ptb) and back[:len(ptb)].tobytes() == ptb
+            eng.close()
+    finally:
+        ra.set_lanes_per_record(prev)
+    for key, pt, aad, iv, ct, tag in MV256:
+        a = ra.aead_new_direct("aes256gcm", True, bytes.fromhex(key), bytes.fromhex(iv))
+        got = a.encrypt(bytes.fromhex(pt), 0, bytes.fromhex(aad)).hex()  # seq 0: the nonce is the IV itself
+        assert got.startswith(ct) and got.endswith(tag)
+        a.free()
+
+
 def test_slot_contexts_on_concurrent_threads(gpu):
     """picotls contexts are used by one thread each; a server runs one per connection on several threads.  Eight
     threads seal and open through their own slot contexts at once (the calls share the device's staging under its

@@ -77,6 +77,25 @@ MV = [  # McGrew-Viega GCM test cases 1-4, deps/cifra/src/testmodes.c:395-440 (A
 ]
 
 
+# AES-256 test cases 13-16 of the GCM specification (McGrew & Viega, "The Galois/Counter Mode of Operation",
+# Appendix B): not in the reference (cifra's list stops at AES-192); published known answers, which the oracle pinned
+# by the reference engine's own outputs reproduces.  (key, plaintext, aad, iv, ciphertext prefix, tag)
+MV256 = [
+    ("00" * 32, "", "", "00" * 12, "", "530f8afbc74536b9a963b4f1c4cb738b"),
+    ("00" * 32, "00" * 16, "", "00" * 12, "cea7403d4d606b6e074ec5d3baf39d18", "d0d1c8a799996bf0265b98b5d48ab919"),
+    ("feffe9928665731c6d6a8f9467308308" * 2, MV[2][1], "", "cafebabefacedbaddecaf888",
+     "522dc1f099567d07f47f37a32a84427d", "b094dac5d93471bdec1a502270e3cc6c"),
+    ("feffe9928665731c6d6a8f9467308308" * 2, MV[3][1], MV[3][2], "cafebabefacedbaddecaf888",
+     "522dc1f099567d07f47f37a32a84427d", "76fc6ece0f4e1768cddf8853bb2d551b"),
+]
+
+
+@pytest.mark.parametrize("key,pt,aad,iv,ct,tag", MV256)
+def test_gcm_spec_aes256(key, pt, aad, iv, ct, tag):
+    out = oracle.seal(bytes.fromhex(key), bytes.fromhex(iv), bytes.fromhex(aad), bytes.fromhex(pt)).hex()
+    assert out.startswith(ct) and out.endswith(tag) and len(out) == len(pt) + 32
+
+
 @pytest.mark.parametrize("key,pt,aad,iv,ct,tag", MV)
 def test_mcgrew_viega(key, pt, aad, iv, ct, tag):
     out = oracle.seal(bytes.fromhex(key), bytes.fromhex(iv), bytes.fromhex(aad), bytes.fromhex(pt))
