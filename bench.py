@@ -450,8 +450,8 @@ def measure(ra, wl_key, args, dev, rank, world, check):
     }
     for e in engs[1:]:
         e.close()
-    extra = dict(eng=eng, iv=iv, d_src=d_src, d_ct=d_ct, d_recs=d_recs, d_aad=d_aad, recs=recs, n=n,
-                 src_bytes=src_bytes, payload=payload, stream=stream, key=wl["key"])
+    extra = dict(eng=eng, iv=iv, d_src=d_src, d_ct=d_ct, d_pt=d_pt, d_st=d_st, d_recs=d_recs, d_aad=d_aad, recs=recs,
+                 n=n, src_bytes=src_bytes, payload=payload, stream=stream, key=wl["key"])
     return res, extra
 
 
@@ -565,10 +565,42 @@ def e2e_pcie(ra, extra, dev, steps):
     piped = (time.perf_counter() - t0) / reps
     if not torch.equal(h_dst[: int(ends[-1])], d_ct[: int(ends[-1])].cpu()):
         raise SystemExit("bench: pipelined PCIe seal differs from the device-resident seal -- results invalid")
+    # the receive side: the sealed records (h_dst) in, opened, plaintexts and statuses back into pinned host memory
+    d_pt, d_st = extra["d_pt"], extra["d_st"]
+    h_pt = torch.empty(extra["src_bytes"], dtype=torch.uint8, pin_memory=True)
+    h_st = torch.empty(n, dtype=torch.int32, pin_memory=True)
+
+    def pipelined_open():
+        for c in range(nchunk):
+            r0, r1 = int(bounds[c]), int(bounds[c + 1])
+            a, b = int(starts[r0]), int(ends[r1 - 1])
+            st = streams[c % 3]
+            with torch.cuda.stream(st):
+                d_ct[a:b].copy_(h_dst[a:b], non_blocking=True)
+                eng.open_batch(iv, d_recs.data_ptr() + r0 * DESC_BYTES, r1 - r0, d_ct.data_ptr(), d_pt.data_ptr(),
+                               d_aad.data_ptr(), d_st.data_ptr() + 4 * r0, st.cuda_stream)
+                h_pt[a:b].copy_(d_pt[a:b], non_blocking=True)
+                h_st[r0:r1].copy_(d_st[r0:r1], non_blocking=True)
+
+    pipelined_open()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        pipelined_open()
+    torch.cuda.synchronize(dev)
+    piped_open = (time.perf_counter() - t0) / reps
+    if not (h_st.numpy().view(np.uint32) == recs["len"]).all():
+        raise SystemExit("bench: pipelined PCIe open did not verify every record -- results invalid")
+    for i in np.linspace(0, n - 1, 64).astype(np.int64):  # plaintexts back in host memory
+        a, ln = int(starts[i]), int(recs["len"][i])
+        if not torch.equal(h_pt[a:a + ln], h_src[a:a + ln]):
+            raise SystemExit("bench: pipelined PCIe open returned other plaintext -- results invalid")
     return {"seal_gibps_serial": round(extra["payload"] / serial / GIB, 2),
             "seal_gibps_pipelined": round(extra["payload"] / piped / GIB, 2),
+            "open_gibps_pipelined": round(extra["payload"] / piped_open / GIB, 2),
             "note": "pinned host src -> H2D -> seal -> D2H -> pinned host dst; serial = one copy each way "
-                    "around one launch; pipelined = 16 chunks over 3 streams"}
+                    "around one launch; pipelined = 16 chunks over 3 streams; open: the sealed records in, "
+                    "plaintexts and statuses out, pipelined the same way"}
 
 
 def record_layer_stream(key_bytes: int = 16, nwin: int = 64, depth: int = 4, transport: str = "dma_in",
@@ -706,7 +738,8 @@ def main() -> None:
                 "rank_ms_per_step": res["rank_ms_per_step"], "seal_gibps": res["seal_gibps"],
                 "open_gibps": res["open_gibps"], "launch_ms": res["roofline"]["launch_ms"]}
         if e2e is not None:
-            mine["e2e_pcie"] = {k: e2e[k] for k in ("seal_gibps_serial", "seal_gibps_pipelined")}
+            mine["e2e_pcie"] = {k: e2e[k] for k in ("seal_gibps_serial", "seal_gibps_pipelined",
+                                                     "open_gibps_pipelined")}
         out["ranks"] = gather_rank_stats(mine)
         out["placement"] = [list(p) for p in placement]
         if e2e is not None:
