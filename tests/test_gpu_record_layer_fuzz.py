@@ -46,18 +46,27 @@ def record_spans(wire):
 
 def model_open(key, iv, seq, wire):
     """ptls_receive over a window: the complete application_data records in order, stopping at the first that fails
-    -> (alert, plaintext, consumed, records)"""
-    pt, cons, n = b"", 0, 0
-    for off, ln in record_spans(wire):
-        rec = wire[off:off + ln]
-        got = oracle.tls_open_record(key, iv, seq, rec)
+    -> (alert, plaintext, consumed, records).  A header is judged as soon as its 5 bytes are there: a length past
+    2^14 + 256 is DECODE_ERROR even before the record is complete (parse_record_header, lib/picotls.c:4243-4254); a
+    record of another outer type is left to picotls (open_record)."""
+    pt, cons, n, off = b"", 0, 0, 0
+    while off + 5 <= len(wire):
+        ln = int.from_bytes(wire[off + 3:off + 5], "big")
+        if wire[off] != 23:
+            break
+        if ln > 16640:
+            return 50, pt, cons, n
+        if off + 5 + ln > len(wire):  # incomplete: wait for more bytes
+            break
+        got = oracle.tls_open_record(key, iv, seq, wire[off:off + 5 + ln])
         if isinstance(got, int):  # TLS_BAD_MAC -> bad_record_mac, TLS_NO_TYPE -> unexpected_message
             return (20 if got == oracle.TLS_BAD_MAC else 10), pt, cons, n
         inner, ctype = got
         if ctype != 23:
             break
         pt += inner
-        cons += ln
+        cons += 5 + ln
+        off += 5 + ln
         n += 1
         seq += 1
     return 0, pt, cons, n
@@ -68,11 +77,43 @@ def draw_frags(rng, k):
     return [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in sizes]
 
 
+TRANSPORTS = ["direct", "direct_dma", "direct_dma_in", "zero_copy", "copy"]
+
+
 @pytest.mark.parametrize("case", range(24))
 def test_random_session(gpu, case):
-    rng = np.random.default_rng(1000 + case)
-    transport = ["direct", "direct_dma", "direct_dma_in", "zero_copy", "copy"][case % 5]
-    keylen = 16 if case % 3 else 32
+    random_session(np.random.default_rng(1000 + case), TRANSPORTS[case % 5], 16 if case % 3 else 32, f"case {case}")
+
+
+def test_record_layer_campaign(gpu):
+    """Time-boxed: random sessions as above, each with a fresh seed, transport and key size (RAPIDO_RL_FUZZ_SECONDS,
+    default 15 s; RAPIDO_FUZZ_SEED as in test_gpu_fuzz_campaign.py; RAPIDO_FUZZ_LOG gets a summary line)."""
+    import json
+    import os
+    import time
+    budget = float(os.environ.get("RAPIDO_RL_FUZZ_SECONDS", "15"))
+    seed = os.environ.get("RAPIDO_FUZZ_SEED", "31337")
+    base = int(time.time()) & 0xFFFFFFF if seed == "random" else int(seed)
+    stats = {"what": "record layer sessions", "seed_base": base, "sessions": 0, "transports": {}}
+    t0 = last = time.time()
+    while time.time() - t0 < budget:
+        rng = np.random.default_rng(base + stats["sessions"])
+        transport, keylen = TRANSPORTS[int(rng.integers(0, 5))], int(rng.choice([16, 32]))
+        random_session(rng, transport, keylen, f"seed {base + stats['sessions']}")
+        stats["sessions"] += 1
+        stats["transports"][transport] = stats["transports"].get(transport, 0) + 1
+        if time.time() - last > 30:
+            last = time.time()
+            print("progress", json.dumps(stats), flush=True)
+    stats["seconds"] = round(time.time() - t0, 1)
+    print(json.dumps(stats))
+    if os.environ.get("RAPIDO_FUZZ_LOG"):
+        with open(os.environ["RAPIDO_FUZZ_LOG"], "a") as f:
+            f.write(json.dumps(stats) + "\n")
+    assert stats["sessions"] > 0
+
+
+def random_session(rng, transport, keylen, case):
     key = rng.integers(0, 256, keylen, dtype=np.uint8).tobytes()
     iv = rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
     nconn = int(rng.integers(1, 4))
@@ -91,7 +132,7 @@ def test_random_session(gpu, case):
     wires = []
     for c, w, o, (wlen, n) in zip(order, windows_b, outs, got):
         want, wn, run_seq[c] = model_seal(key, conn_iv(iv, cids[c]), run_seq[c], w)
-        assert o[:wlen].tobytes() == want and n == wn, f"case {case} ({transport}): seal window of connection {c}"
+        assert o[:wlen].tobytes() == want and n == wn, f"{case} ({transport}): seal window of connection {c}"
         wires.append(want)
     assert [t.seq for t in tx] == run_seq
     # the receive side: damage some windows, open them all in one launch (staging) and model the outcome
@@ -111,20 +152,22 @@ def test_random_session(gpu, case):
     exp_seq, state = list(seqs), ["ok"] * nconn
     for c, w, r in zip(order, damaged, res):
         if state[c] == "stale":
-            assert r[0] == ra.RECORD_LAYER_STALE and r[3] == 0, f"case {case}: window behind a stop"
+            assert r[0] == ra.RECORD_LAYER_STALE and r[3] == 0, f"{case}: window behind a stop"
             continue
         if state[c] == "lost":
-            assert r[1] == b"" and r[3] == 0, f"case {case}: window behind a broken stream"
+            assert r[1] == b"" and r[3] == 0, f"{case}: window behind a broken stream"
             continue
         spans = record_spans(w)
-        hdr_ok = all(w[o] == 23 and w[o + 1:o + 3] == b"\x03\x03" and 17 <= ln - 5 <= 16640 for o, ln in spans)
-        if not hdr_ok:  # a flipped header bit: the layer's parser decides; only the delivered prefix is checked
+        # the parser reads a header's type and length; the legacy version bytes are neither checked nor authenticated
+        # (build_aad writes 03 03 itself, lib/picotls.c:621-628), so a flipped version bit leaves the stream intact
+        hdr_ok = all(w[o] == 23 and 17 <= ln - 5 <= 16640 for o, ln in spans)
+        if not hdr_ok:  # a flipped type or length bit: the layer's parser decides; only the delivered prefix is checked
             assert r[1] == model_open(key, conn_iv(iv, cids[c]), exp_seq[c], w[:r[2]])[1]
             exp_seq[c] += r[3]
             state[c] = "lost"
             continue
         want = model_open(key, conn_iv(iv, cids[c]), exp_seq[c], w)
-        assert r == want, f"case {case}: open window of connection {c}"
+        assert r == want, f"{case}: open window of connection {c}"
         exp_seq[c] += want[3]
         if want[3] < len(spans):
             state[c] = "stale"
