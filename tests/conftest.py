@@ -29,7 +29,9 @@ def _gpu_work_checked(request):
     device is synchronised, and any fault of the test's GPU work -- or an error a free path met -- fails THIS test.
     A fault is reported by whatever HIP call comes next; without this check the next test's first call takes the
     blame (round 4: an illegal address surfaced at the first H2D copy of an unrelated test).  A page fault is signalled
-    asynchronously, possibly after the kernel has completed, so the check runs twice, a moment apart."""
+    asynchronously, possibly after the kernel has completed (a faulting store does not stop its wave), so the check
+    runs twice, RAPIDO_FAULT_SETTLE_MS (default 20) apart: round 5 saw the round-4 report again at the same place
+    with the checks 3 ms apart, i.e. the report arrived later than that."""
     yield
     if request.node.get_closest_marker("gpu") is None:
         return
@@ -40,7 +42,7 @@ def _gpu_work_checked(request):
     nerr = len(ra.FINALIZER_ERRORS)
     gc.collect()
     ra.device_check()
-    time.sleep(0.003)
+    time.sleep(float(os.environ.get("RAPIDO_FAULT_SETTLE_MS", "20")) * 1e-3)
     ra.device_check()
     new = ra.FINALIZER_ERRORS[nerr:]
     if new:

@@ -86,17 +86,19 @@ def test_random_session(gpu, case):
 
 
 def test_record_layer_campaign(gpu):
-    """Time-boxed: random sessions as above, each with a fresh seed, transport and key size (RAPIDO_RL_FUZZ_SECONDS,
-    default 15 s; RAPIDO_FUZZ_SEED as in test_gpu_fuzz_campaign.py; RAPIDO_FUZZ_LOG gets a summary line)."""
+    """Random sessions as above, each with a fresh seed, transport and key size: 1000 from a fixed seed by default (the
+    same sessions on every box), or time-boxed with RAPIDO_RL_FUZZ_SECONDS (RAPIDO_FUZZ_SEED as in
+    test_gpu_fuzz_campaign.py; RAPIDO_FUZZ_LOG gets a summary line)."""
     import json
     import os
     import time
-    budget = float(os.environ.get("RAPIDO_RL_FUZZ_SECONDS", "15"))
+    timed = "RAPIDO_RL_FUZZ_SECONDS" in os.environ  # else the gate: 1000 sessions from the fixed seed on every box
+    budget = float(os.environ.get("RAPIDO_RL_FUZZ_SECONDS", "0"))
     seed = os.environ.get("RAPIDO_FUZZ_SEED", "31337")
     base = int(time.time()) & 0xFFFFFFF if seed == "random" else int(seed)
     stats = {"what": "record layer sessions", "seed_base": base, "sessions": 0, "transports": {}}
     t0 = last = time.time()
-    while time.time() - t0 < budget:
+    while (time.time() - t0 < budget) if timed else stats["sessions"] < 1000:
         rng = np.random.default_rng(base + stats["sessions"])
         transport, keylen = TRANSPORTS[int(rng.integers(0, 5))], int(rng.choice([16, 32]))
         random_session(rng, transport, keylen, f"seed {base + stats['sessions']}")
