@@ -171,3 +171,53 @@ def test_tls_records_at_guard_edges(guards, family, at):
             assert OUT.get(slot + 5, ln) == frag, (family, at, "in place", ln)
     eng.close()
     checked()
+
+
+@pytest.mark.parametrize("family", FAMILIES)
+@pytest.mark.parametrize("at", ["start", "end"])
+def test_tls_window_in_place_at_guard_edges(guards, family, at):
+    """test_gpu_tls.py::test_in_place's exact launch -- six records of 0..16384 bytes, back to back in one buffer, sealed
+    in ONE launch with each fragment 5 bytes into its slot (dst = src - 5), then opened in one launch where they lie
+    (dst = src + 5) -- with the buffer flush against the guard at either end.  The cases above put one record per
+    launch at the edges; this is the multi-record group (ten idle lanes, walks of 1 to 1026 steps) that preceded the
+    illegal-address report of rounds 4 and 5."""
+    lib, gs = guards
+    _, AUX, OUT = (Region(lib, g) for g in gs)
+    key, iv = bytes(range(16)), bytes(range(12))
+    lens = [0, 1, 16, 100, 1400, 16384]
+    slots = [ln + 22 for ln in lens]
+    base = np.cumsum([0] + slots[:-1]).astype(np.uint64)
+    total = int(sum(slots))
+    eng = ra.Engine(key)
+    with kernel_family(family, framing=True):
+        OUT.clear()
+        AUX.clear()
+        buf = np.zeros(total, np.uint8)
+        trecs = np.zeros(len(lens), ra.TLS_RECORD_DTYPE)
+        frags = []
+        for i, ln in enumerate(lens):
+            f = xorshift64star(20 + i, ln).tobytes()
+            frags.append(f)
+            buf[int(base[i]) + 5: int(base[i]) + 5 + ln] = np.frombuffer(f, np.uint8)
+            trecs[i] = (int(base[i]) + 5, int(base[i]), 50 + i, ln, 23)
+        arena = OUT.put(buf, at)  # the window's buffer flush against the edge (its last tag ends on it, or its
+        d_t = AUX.put(trecs.view(np.uint8), "end" if at == "start" else "start")  # first header starts on it)
+        eng.tls_seal_records(iv, d_t, len(lens), arena, arena)
+        checked()
+        wire = OUT.get(arena, total)
+        for i, ln in enumerate(lens):
+            b = int(base[i])
+            assert wire[b:b + ln + 22] == oracle.tls_seal_record(key, iv, 50 + i, 23, frags[i]), (family, at, ln)
+        orecs = trecs.copy()
+        orecs["src"], orecs["dst"], orecs["len"] = base, base + 5, np.array(lens) + 17
+        mid = AUX.base + AUX.len // 2
+        assert lib.guard_h2d(mid + 4096, orecs.ctypes.data, orecs.nbytes) == 0
+        eng.tls_open_records(iv, mid + 4096, len(lens), arena, arena, mid, mid + 64)
+        checked()
+        assert list(np.frombuffer(AUX.get(mid, 4 * len(lens)), np.uint32)) == lens
+        pt = OUT.get(arena, total)
+        for i, ln in enumerate(lens):
+            b = int(base[i]) + 5
+            assert pt[b:b + ln] == frags[i], (family, at, ln)
+    eng.close()
+    checked()
