@@ -1618,8 +1618,12 @@ static int ensure_stage(DeviceShared *d, size_t need)
     while (cap < need)
         cap *= 2;
     d->cap = 0; /* (nothing is left half-freed for a later call if a free below fails) */
-    if (d->d_stage)
+    if (d->d_stage) {
+        /* the last copied call's clear of the staging may still be queued on the device stream: it ends first (an
+         * explicit wait, not hipFree's implicit one) */
+        HIPCHK(hipStreamSynchronize(d->stream));
         HIPCHK(hipFree(d->d_stage));
+    }
     d->d_stage = nullptr;
     if (d->h_stage)
         HIPCHK(hipHostFree(d->h_stage));
@@ -1816,8 +1820,12 @@ static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void
         if (ctx_stream(ctx, stream) != 0)
             return -1;
         if (ctx->split_cap < n) {
-            if (ctx->d_split)
-                HIPCHK(hipFree(ctx->d_split)); /* synchronises the device: no launch still uses it */
+            if (ctx->d_split) {
+                /* split launches of this context may be on any stream: the device is idle before the buffer goes
+                 * (an explicit wait, not hipFree's implicit one) */
+                HIPCHK(hipDeviceSynchronize());
+                HIPCHK(hipFree(ctx->d_split));
+            }
             ctx->d_split = nullptr;
             ctx->split_cap = 0;
             ctx->split_ev_valid = false;
@@ -2072,7 +2080,7 @@ static int context_release(ptls_mi355x_aesgcm_context_t *ctx, bool deferred)
     if (ctx->d_ki) {
         /* clear key material, as ptls_fusion_aesgcm_free does; ordered before the free on the null stream */
         chk("context free: clearing the key image", hipMemsetAsync(ctx->d_ki, 0, sizeof(KeyImage), nullptr));
-        chk("context free: hipStreamSynchronize", hipStreamSynchronize(nullptr));
+        chk("context free: hipDeviceSynchronize", hipDeviceSynchronize());
         chk("context free: hipFree(key image)", hipFree(ctx->d_ki));
     }
     if (ctx->d_work)
