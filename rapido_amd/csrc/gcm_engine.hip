@@ -1424,25 +1424,26 @@ struct st_ptls_mi355x_aes_context {
 };
 
 static thread_local char g_err[256];
-static int g_lanes = 4;
+/* the tuning knobs below are process-wide and may be set from any thread: atomics, each read once per decision */
+static std::atomic<int> g_lanes{4};
 /* framing batches of at most this many records go to the window kernels (ptls_mi355x_set_tls_window_records) */
-static size_t g_window_records = 16384;
+static std::atomic<size_t> g_window_records{16384};
 /* AEAD batches (section 3) of at most this many records go to the window kernels (ptls_mi355x_set_aead_window_records):
  * the single-record slot calls and small batches, where 4 lanes per record would leave the GPU idle */
-static size_t g_aead_window_records = 2048; /* break-even of 1400-B records (scripts/window_bench.py aead_batches) */
+static std::atomic<size_t> g_aead_window_records{2048}; /* break-even of 1400-B records (scripts/window_bench.py aead_batches) */
 /* single-record slot calls staging at most this many bytes run zero-copy (ptls_mi355x_set_slot_zero_copy_bytes) */
-static size_t g_slot_zero_copy_bytes = 1u << 20;
+static std::atomic<size_t> g_slot_zero_copy_bytes{1u << 20};
 /* starting value of new contexts' work counters (ptls_mi355x_set_work_ticket_origin; tests the 2^32 wrap) */
-static uint32_t g_ticket_origin = 0u;
+static std::atomic<uint32_t> g_ticket_origin{0u};
 /* window batches of at most this many records use 32-position segments (ptls_mi355x_set_seg32_records;
  * SIZE_MAX = the device's CU count) */
-static size_t g_seg32_records = SIZE_MAX;
+static std::atomic<size_t> g_seg32_records{SIZE_MAX};
 /* window batches of at most this many records use the 16-lane single-record kernels (ptls_mi355x_set_win16_records;
  * SIZE_MAX = the device's CU count); they take precedence over the 32-position 8-lane ones */
-static size_t g_win16_records = SIZE_MAX;
+static std::atomic<size_t> g_win16_records{SIZE_MAX};
 /* window batches of at most this many records use the split kernels, SPLIT_MAXRUN workgroups per record
  * (ptls_mi355x_set_split_records; SIZE_MAX = CU count / SPLIT_MAXRUN); they take precedence over the others */
-static size_t g_split_records = SIZE_MAX;
+static std::atomic<size_t> g_split_records{SIZE_MAX};
 
 static int fail(const char *what, hipError_t e)
 {
@@ -1645,6 +1646,7 @@ struct LaunchPlan {
     win_kernel_t win = nullptr;
     split_kernel_t split = nullptr;
     uint32_t blocks = 0, threads = 0;
+    uint32_t k = 0; /* batch kernels: lanes per record (the work-ticket count of the launch follows it) */
 };
 
 #define KN(f) {#f, f}
@@ -1672,7 +1674,7 @@ static LaunchPlan plan_launch(bool seal, bool frame, uint32_t key_size, size_t n
 {
     LaunchPlan p;
     const int a256 = key_size == 32 ? 1 : 0, s = seal ? 1 : 0, f = frame ? 1 : 0;
-    if (n <= (frame ? g_window_records : g_aead_window_records)) {
+    if (n <= (frame ? g_window_records.load() : g_aead_window_records.load())) {
         static const WinEntry table[2][2][2][2] = {
             /* [frame][wide][seal][aes256] */
             {{{KN(mi355x_gcm_win_open_aes128), KN(mi355x_gcm_win_open_aes256)},
@@ -1701,7 +1703,9 @@ static LaunchPlan plan_launch(bool seal, bool frame, uint32_t key_size, size_t n
              {KN(mi355x_gcm_wins_seal_aes128), KN(mi355x_gcm_wins_seal_aes256)}},
             {{KN(mi355x_tls_wins_open_aes128), KN(mi355x_tls_wins_open_aes256)},
              {KN(mi355x_tls_wins_seal_aes128), KN(mi355x_tls_wins_seal_aes256)}}};
-        if (n <= (g_split_records == SIZE_MAX ? (size_t)num_cu / SPLIT_MAXRUN : g_split_records) &&
+        const size_t split_max = g_split_records.load(), win16_max = g_win16_records.load(),
+                     seg32_max = g_seg32_records.load();
+        if (n <= (split_max == SIZE_MAX ? (size_t)num_cu / SPLIT_MAXRUN : split_max) &&
             n <= 0xffffffffu / SPLIT_MAXRUN) {
             const SplitEntry &e = table_split[f][s][a256];
             p.name = e.name;
@@ -1712,8 +1716,8 @@ static LaunchPlan plan_launch(bool seal, bool frame, uint32_t key_size, size_t n
         }
         const bool wide = n > 15u * (uint64_t)num_cu; /* the wide groups (15 records) fill every CU */
         constexpr uint32_t per32 = (MI355X_WIN32_THREADS / 8u) / WIN_SEG32_MAXSEG; /* records per 32-position group */
-        const bool win16 = !wide && n <= (g_win16_records == SIZE_MAX ? (size_t)num_cu : g_win16_records);
-        const bool seg32 = !win16 && !wide && n <= (g_seg32_records == SIZE_MAX ? (size_t)per32 * num_cu : g_seg32_records);
+        const bool win16 = !wide && n <= (win16_max == SIZE_MAX ? (size_t)num_cu : win16_max);
+        const bool seg32 = !win16 && !wide && n <= (seg32_max == SIZE_MAX ? (size_t)per32 * num_cu : seg32_max);
         const WinEntry &e = win16 ? table16[f][s][a256] : seg32 ? table32[f][s][a256] : table[f][wide][s][a256];
         p.name = e.name;
         p.win = e.f;
@@ -1738,11 +1742,12 @@ static LaunchPlan plan_launch(bool seal, bool frame, uint32_t key_size, size_t n
     static const BatchEntry tls[2][2] = {/* [seal][aes256] */
                                          {KN(mi355x_tls_open_aes128_k4), KN(mi355x_tls_open_aes256_k4)},
                                          {KN(mi355x_tls_seal_aes128_k4), KN(mi355x_tls_seal_aes256_k4)}};
-    const int k = frame ? 4 : g_lanes;
+    const int k = frame ? 4 : g_lanes.load();
     const int lk = k == 1 ? 0 : k == 2 ? 1 : k == 4 ? 2 : 3;
     const BatchEntry &e = frame ? tls[s][a256] : gcm[s][a256][lk];
     p.name = e.name;
     p.batch = e.f;
+    p.k = (uint32_t)k;
     p.threads = WG_THREADS;
     const uint64_t ngroups = (n + (64 / k) - 1) / (64 / k), waves = WG_THREADS / 64;
     uint64_t blocks = (ngroups + waves - 1) / waves;
@@ -1859,7 +1864,7 @@ static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void
      * right after its previous launch, so two launches never share a counter at once.  The slot's base is
      * committed only once the launch has been accepted.
      */
-    const uint32_t k = frame ? 4u : (uint32_t)g_lanes;
+    const uint32_t k = p.k; /* the plan's: a concurrent ptls_mi355x_set_lanes_per_record does not split the two */
     const uint32_t ngroups = (uint32_t)((n + (64 / k) - 1) / (64 / k));
     const uint32_t wslot = ctx->work_next % WORK_SLOTS;
     uint32_t *work = ctx->d_work + wslot;
@@ -1925,60 +1930,44 @@ int ptls_mi355x_set_lanes_per_record(int k)
 {
     if (k != 1 && k != 2 && k != 4 && k != 8)
         return -1;
-    int prev = g_lanes;
-    g_lanes = k;
-    return prev;
+    return g_lanes.exchange(k);
 }
 
 int ptls_mi355x_get_lanes_per_record(void) { return g_lanes; }
 
 size_t ptls_mi355x_set_tls_window_records(size_t n)
 {
-    const size_t prev = g_window_records;
-    g_window_records = n;
-    return prev;
+    return g_window_records.exchange(n);
 }
 
 size_t ptls_mi355x_set_aead_window_records(size_t n)
 {
-    const size_t prev = g_aead_window_records;
-    g_aead_window_records = n;
-    return prev;
+    return g_aead_window_records.exchange(n);
 }
 
 size_t ptls_mi355x_set_split_records(size_t n)
 {
-    const size_t prev = g_split_records;
-    g_split_records = n;
-    return prev;
+    return g_split_records.exchange(n);
 }
 
 size_t ptls_mi355x_set_win16_records(size_t n)
 {
-    const size_t prev = g_win16_records;
-    g_win16_records = n;
-    return prev;
+    return g_win16_records.exchange(n);
 }
 
 size_t ptls_mi355x_set_seg32_records(size_t n)
 {
-    const size_t prev = g_seg32_records;
-    g_seg32_records = n;
-    return prev;
+    return g_seg32_records.exchange(n);
 }
 
 uint32_t ptls_mi355x_set_work_ticket_origin(uint32_t origin)
 {
-    const uint32_t prev = g_ticket_origin;
-    g_ticket_origin = origin;
-    return prev;
+    return g_ticket_origin.exchange(origin);
 }
 
 size_t ptls_mi355x_set_slot_zero_copy_bytes(size_t n)
 {
-    const size_t prev = g_slot_zero_copy_bytes;
-    g_slot_zero_copy_bytes = n;
-    return prev;
+    return g_slot_zero_copy_bytes.exchange(n);
 }
 
 int ptls_mi355x_batch_ghash_reads(int k)
@@ -2025,8 +2014,9 @@ ptls_mi355x_aesgcm_context_t *ptls_mi355x_aesgcm_new(const void *key, size_t key
         snprintf(g_err, sizeof(g_err), "context allocation: %s", hipGetErrorString(hipGetLastError()));
         goto Fail;
     }
-    for (uint32_t i = 0; i < WORK_SLOTS; ++i)
-        ctx->work_base[i] = g_ticket_origin;
+    ctx->work_base[0] = g_ticket_origin; /* (read once: the counters below start where the bases say) */
+    for (uint32_t i = 1; i < WORK_SLOTS; ++i)
+        ctx->work_base[i] = ctx->work_base[0];
     {
         /* the key goes through the shared pinned staging (zero-copy read by the setup kernel), cleared after */
         std::lock_guard<std::mutex> lk(d->mu);
@@ -2034,7 +2024,7 @@ ptls_mi355x_aesgcm_context_t *ptls_mi355x_aesgcm_new(const void *key, size_t key
             goto Fail;
         memcpy(d->h_stage, key, key_size);
         *(volatile int *)(d->h_stage + 64) = -2;
-        if (hipMemsetD32Async((hipDeviceptr_t)ctx->d_work, (int)g_ticket_origin, WORK_SLOTS, d->stream) != hipSuccess) {
+        if (hipMemsetD32Async((hipDeviceptr_t)ctx->d_work, (int)ctx->work_base[0], WORK_SLOTS, d->stream) != hipSuccess) {
             snprintf(g_err, sizeof(g_err), "work counters: %s", hipGetErrorString(hipGetLastError()));
             goto Fail;
         }
