@@ -2167,13 +2167,17 @@ GCM_HD uint32_t window_group_start(uint32_t g, uint32_t ns) { return g == 0u ? 0
  * GCM_READ(p, n): the walk is about to read bytes [p, p + n) of a record (or its AAD / descriptor).  Nothing in the
  * kernels; the CPU test suite's host model (tests/cpp/kernel_model.cpp, GCM_HOST_READ_CHECK) checks every such range
  * against the records' own bytes, so a read outside them -- a fault wherever a record ends at an unmapped page --
- * fails on the CPU, deterministically.
+ * fails on the CPU, deterministically.  GCM_WRITE(p, n), likewise for every store of the walk, against the records'
+ * output ranges: a stray store -- which need not stop its wave, and faults late, if at all -- fails there too.
  */
 #if defined(GCM_HOST_READ_CHECK) && !defined(__HIP_DEVICE_COMPILE__)
 extern "C" void gcm_host_read_check(const void *p, size_t n);
+extern "C" void gcm_host_write_check(const void *p, size_t n);
 #define GCM_READ(p, n) gcm_host_read_check((const void *)(p), (size_t)(n))
+#define GCM_WRITE(p, n) gcm_host_write_check((const void *)(p), (size_t)(n))
 #else
 #define GCM_READ(p, n) ((void)0)
+#define GCM_WRITE(p, n) ((void)0)
 #endif
 
 /* loads n (< 16) bytes zero-extended */
@@ -2204,6 +2208,7 @@ GCM_HD u32x4 load_partial(const uint8_t *p, uint32_t n)
 GCM_HD void store_partial(uint8_t *p, uint32_t n, u32x4 v)
 {
     /* loop-free (n < 16), mirror of load_partial */
+    GCM_WRITE(p, n);
     const uint32_t q = n >> 2, rem = n & 3u;
 #pragma unroll
     for (uint32_t d = 0; d < 3; ++d)
@@ -2428,16 +2433,17 @@ GCM_HD u32x4 lane_walk_seg(const uint8_t *lds, uint32_t lanesel, const uint32_t 
         if constexpr (PAIRST) {
             if ((t & 1u) == 0u) {
                 if (pend_c != 0xffffffffu) /* (a lane's payload blocks are consecutive steps: not reached) */
-                    *(u32x4_u *)(out + 16u * pend_c) = pend_v;
+                    GCM_WRITE(out + 16u * pend_c, 16), *(u32x4_u *)(out + 16u * pend_c) = pend_v;
                 pend_v = o;
                 pend_c = c;
                 return;
             }
             if (pend_c != 0xffffffffu) {
-                *(u32x4_u *)(out + 16u * pend_c) = pend_v;
+                GCM_WRITE(out + 16u * pend_c, 16), *(u32x4_u *)(out + 16u * pend_c) = pend_v;
                 pend_c = 0xffffffffu;
             }
         }
+        GCM_WRITE(out + 16u * c, 16);
 #if defined(__HIP_DEVICE_COMPILE__)
         if constexpr (NTST)
             __builtin_nontemporal_store(o, (u32x4_u *)(out + 16u * c));
@@ -2726,7 +2732,7 @@ Scale:
     GCM_WALK_STAMP(12);
     if constexpr (PAIRST) {
         if (pend_c != 0xffffffffu) /* a first half with no second half in this walk */
-            *(u32x4_u *)(out + 16u * pend_c) = pend_v;
+            GCM_WRITE(out + 16u * pend_c, 16), *(u32x4_u *)(out + 16u * pend_c) = pend_v;
     }
     /* scale the chain by H^(pad + g - q_last(j)) (make_walk) */
     if (LY::gh5) {

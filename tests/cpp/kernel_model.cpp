@@ -59,6 +59,40 @@ extern "C" uint64_t model_read_violations(uint64_t *first)
     return g_read_bad;
 }
 
+/* Write checking (GCM_WRITE): the same, for the walk's stores against the records' output ranges. */
+static std::vector<std::pair<uintptr_t, uintptr_t>> g_write_ok;
+static uint64_t g_write_bad = 0, g_write_first[2] = {0, 0};
+
+extern "C" void gcm_host_write_check(const void *p, size_t n)
+{
+    if (g_write_ok.empty() || n == 0)
+        return;
+    const uintptr_t a = (uintptr_t)p, b = a + n;
+    for (const auto &r : g_write_ok)
+        if (a >= r.first && b <= r.second)
+            return;
+    if (g_write_bad++ == 0) {
+        g_write_first[0] = a;
+        g_write_first[1] = n;
+    }
+}
+
+extern "C" void model_set_write_ranges(const uint64_t *lohi, size_t n)
+{
+    g_write_ok.clear();
+    for (size_t i = 0; i < n; ++i)
+        g_write_ok.emplace_back((uintptr_t)lohi[2 * i], (uintptr_t)lohi[2 * i + 1]);
+    g_write_bad = 0;
+    g_write_first[0] = g_write_first[1] = 0;
+}
+
+extern "C" uint64_t model_write_violations(uint64_t *first)
+{
+    first[0] = g_write_first[0];
+    first[1] = g_write_first[1];
+    return g_write_bad;
+}
+
 static constexpr AesTables kTabs{};
 
 /* lanes per 64-position segment of the window math: 8 (latency kernels) or 4 (wide kernels) */

@@ -221,3 +221,89 @@ def test_tls_window_in_place_at_guard_edges(guards, family, at):
             assert pt[b:b + ln] == frags[i], (family, at, ln)
     eng.close()
     checked()
+
+
+@pytest.mark.parametrize("family", FAMILIES)
+@pytest.mark.parametrize("at", ["start", "end"])
+def test_status_and_types_at_guard_edges(guards, family, at):
+    """The open's per-record outputs -- the status array and the TLS content types -- flush against a guard, and the
+    length order (open_batch_ordered) flush against the other edge: the cases above keep them mid-region.  Six records
+    (test_in_place's lengths) in one launch, one of them tampered, opened separately, in place, and with
+    OPEN_STOP_AT_FAILURE (its later statuses written as TLS_NOT_PROCESSED); a write one element past either end of the
+    arrays is a page fault here."""
+    lib, gs = guards
+    IN, AUX, OUT = (Region(lib, g) for g in gs)
+    key, iv = bytes(range(40, 56)), bytes(range(12))
+    lens = [0, 1, 16, 100, 1400, 16384]
+    n, bad = len(lens), 3
+    other = "end" if at == "start" else "start"
+    mid_in, mid_aux, mid_out = IN.base + 4096, AUX.base + AUX.len // 2, OUT.base + 4096
+    eng = ra.Engine(key)
+    with kernel_family(family, framing=True):
+        for r in (IN, AUX, OUT):
+            r.clear()
+        frags = [xorshift64star(60 + i, ln).tobytes() for i, ln in enumerate(lens)]
+        wires = [bytearray(oracle.tls_seal_record(key, iv, 9 + i, 23 if i % 2 else 22, f)) for i, f in enumerate(frags)]
+        wires[bad][-1] ^= 1
+        woff = np.cumsum([0] + [len(w) for w in wires[:-1]]).astype(np.uint64)
+        poff = np.cumsum([0] + [ln + 1 for ln in lens[:-1]]).astype(np.uint64)
+        wire = b"".join(bytes(w) for w in wires)
+        o = np.zeros(n, ra.TLS_RECORD_DTYPE)
+        o["src"], o["dst"], o["seq"], o["len"] = woff, poff, 9 + np.arange(n), np.array(lens) + 17
+        d_o = mid_aux
+        assert lib.guard_h2d(d_o, o.ctypes.data, o.nbytes) == 0
+        st, ty = AUX.addr(4 * n, at), OUT.addr(n, at)
+        want_ty = [23 if i % 2 else 22 for i in range(n)]
+        for flags in (0, ra.OPEN_STOP_AT_FAILURE):
+            for inplace in (False, True):
+                src = IN.put(wire, other) if inplace else mid_in
+                if not inplace:
+                    assert lib.guard_h2d(src, np.frombuffer(wire, np.uint8).ctypes.data, len(wire)) == 0
+                recs = o.copy()
+                if inplace:  # plaintext over each record's own header + ciphertext
+                    recs["dst"] = woff + 5
+                assert lib.guard_h2d(d_o, recs.ctypes.data, recs.nbytes) == 0
+                eng.tls_open_records(iv, d_o, n, src, src if inplace else mid_out, st, ty, flags=flags)
+                checked()
+                got = list(np.frombuffer(AUX.get(st, 4 * n), np.uint32))
+                want = [0xFFFFFFFF if i == bad else ra.TLS_NOT_PROCESSED if flags and i > bad else ln
+                        for i, ln in enumerate(lens)]
+                assert got == want, (family, at, flags, inplace)
+                types = OUT.get(ty, n)
+                for i in range(bad):
+                    assert types[i] == want_ty[i], (family, at, flags, inplace, i)
+                    d = int(recs["dst"][i])
+                    pt = IN.get(src + d, lens[i]) if inplace else OUT.get(mid_out + d, lens[i])
+                    assert pt == frags[i], (family, at, flags, inplace, i)
+    with kernel_family(family, framing=False):
+        for r in (IN, AUX, OUT):
+            r.clear()
+        pts = [xorshift64star(80 + i, ln).tobytes() for i, ln in enumerate(lens)]
+        aad = xorshift64star(99, 13).tobytes()
+        cts = [bytearray(oracle.seal(key, oracle.build_iv(iv, 5 + i), aad, p)) for i, p in enumerate(pts)]
+        cts[bad][0 if lens[bad] == 0 else -1] ^= 1
+        coff = np.cumsum([0] + [len(c) for c in cts[:-1]]).astype(np.uint64)
+        poff = np.cumsum([0] + lens[:-1]).astype(np.uint64)
+        recs = np.zeros(n, ra.RECORD_DTYPE)
+        recs["src"], recs["dst"], recs["seq"], recs["len"], recs["aadlen"] = coff, poff, 5 + np.arange(n), lens, 13
+        blob = b"".join(bytes(c) for c in cts)
+        assert lib.guard_h2d(mid_in, np.frombuffer(blob, np.uint8).ctypes.data, len(blob)) == 0
+        d_aad = mid_aux + 8192
+        assert lib.guard_h2d(d_aad, np.frombuffer(aad, np.uint8).ctypes.data, 13) == 0
+        assert lib.guard_h2d(mid_aux, recs.ctypes.data, recs.nbytes) == 0
+        st = AUX.addr(4 * n, at)
+        want = [0xFFFFFFFF if i == bad else ln for i, ln in enumerate(lens)]
+        eng.open_batch(iv, mid_aux, n, mid_in, mid_out, d_aad, st)
+        checked()
+        assert list(np.frombuffer(AUX.get(st, 4 * n), np.uint32)) == want, (family, at)
+        order = AUX.addr(4 * n, other)
+        eng.order_by_length(mid_aux, n, order)
+        checked()
+        eng.open_batch_ordered(iv, mid_aux, order, n, mid_in, mid_out, d_aad, st)
+        checked()
+        assert list(np.frombuffer(AUX.get(st, 4 * n), np.uint32)) == want, (family, at, "ordered")
+        for i in range(n):
+            if i != bad:
+                assert OUT.get(mid_out + int(poff[i]), lens[i]) == pts[i], (family, at, i)
+    eng.close()
+    checked()

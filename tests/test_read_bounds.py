@@ -1,8 +1,9 @@
-"""No kernel family reads outside a record (CPU, deterministic).
+"""No kernel family reads or writes outside a record (CPU, deterministic).
 
 The walk's reads (gcm_core.h: walk_load, load_partial, the hoisted AAD block -- every one passes GCM_READ) are checked
 by the host model against each record's own bytes: its input (plus the received tag for an open), its AAD, and the
-descriptor array the idle loads point at.  Records sit 48 bytes apart, so a read that strays past either end of a
+descriptor array the idle loads point at; the walk's stores (every one passes GCM_WRITE) against each record's own
+output.  Records sit 48 bytes apart, so a read that strays past either end of a
 record -- which faults on the GPU wherever that end is the edge of a mapped page -- lands in a gap and is counted.
 Every family the GPU suites route batches to (conftest.FAMILIES: the batch kernels at K = 1, 2, 4, 8, the window
 kernels with 4 / 8 lanes and 64- / 32-position segments, the 16-lane and split kernels) is run seal and open, AEAD and
@@ -30,6 +31,9 @@ def model():
     lib.model_set_read_ranges.argtypes = [vp, C.c_size_t]
     lib.model_read_violations.argtypes = [vp]
     lib.model_read_violations.restype = C.c_uint64
+    lib.model_set_write_ranges.argtypes = [vp, C.c_size_t]
+    lib.model_write_violations.argtypes = [vp]
+    lib.model_write_violations.restype = C.c_uint64
     lib.model_batch.argtypes = [C.c_int, C.c_int, vp, C.c_size_t, vp, vp, C.c_size_t, vp, vp, vp, vp]
     lib.model_batch_window.argtypes = [C.c_int, vp, C.c_size_t, vp, vp, C.c_size_t, vp, vp, vp, vp]
     lib.model_batch_win16.argtypes = [C.c_int, C.c_int, vp, C.c_size_t, vp, vp, C.c_size_t, vp, vp, vp, vp]
@@ -37,24 +41,33 @@ def model():
     lib.model_tls_window.argtypes = [C.c_int, vp, C.c_size_t, vp, vp, C.c_size_t, vp, vp, vp, vp, vp]
     yield lib
     lib.model_set_read_ranges(None, 0)
+    lib.model_set_write_ranges(None, 0)
 
 
 class Checked:
-    """Sets the allowed ranges for one model call and asserts no read fell outside them."""
+    """Sets the allowed read (and, given, write) ranges for one model call and asserts no access fell outside them."""
 
-    def __init__(self, lib, ranges):
+    def __init__(self, lib, ranges, writes=None):
         self.lib, self.ranges = lib, np.array(ranges, dtype=np.uint64).reshape(-1, 2)
+        self.writes = None if writes is None else np.array(writes, dtype=np.uint64).reshape(-1, 2)
 
     def __enter__(self):
         self.lib.model_set_read_ranges(self.ranges.ctypes.data, len(self.ranges))
+        if self.writes is not None:
+            self.lib.model_set_write_ranges(self.writes.ctypes.data, len(self.writes))
 
     def __exit__(self, *exc):
-        first = (C.c_uint64 * 2)()
+        first, wfirst = (C.c_uint64 * 2)(), (C.c_uint64 * 2)()
         bad = self.lib.model_read_violations(first)
+        wbad = self.lib.model_write_violations(wfirst)
         self.lib.model_set_read_ranges(None, 0)
+        self.lib.model_set_write_ranges(None, 0)
         if exc[0] is None:
             near = [(int(lo), int(hi)) for lo, hi in self.ranges if lo - 64 <= first[0] <= hi + 64]
             assert bad == 0, f"{bad} reads outside the records; first {first[1]} B at {first[0]:#x}, near {near}"
+            if self.writes is not None:
+                near = [(int(lo), int(hi)) for lo, hi in self.writes if lo - 64 <= wfirst[0] <= hi + 64]
+                assert wbad == 0, f"{wbad} writes outside the records; first {wfirst[1]} B at {wfirst[0]:#x}, near {near}"
 
 
 def aead_layout(lens, aads):
@@ -77,6 +90,11 @@ def aead_ranges(recs, src, aad, is_open):
         a0 = aad.ctypes.data + int(x["aad"])
         r.append((a0, a0 + int(x["aadlen"])))
     return r
+
+
+def out_ranges(base, offs, lens):
+    """Each record's output bytes [base + off, base + off + len)"""
+    return [(base.ctypes.data + int(o), base.ctypes.data + int(o) + int(n)) for o, n in zip(offs, lens)]
 
 
 def call_aead(lib, fam, is_seal, key, iv, recs, src, dst, aad, st):
@@ -103,7 +121,7 @@ def test_aead_walk_reads_stay_inside_records(model, fam):
     key, iv = bytes(range(16)), bytes(range(40, 52))
     ct = np.zeros_like(src)
     st = np.zeros(len(recs), np.uint32)
-    with Checked(model, aead_ranges(recs, src, aad, False)):
+    with Checked(model, aead_ranges(recs, src, aad, False), out_ranges(ct, recs["dst"], recs["len"] + 16)):
         assert call_aead(model, fam, True, key, iv, recs, src, ct, aad, st) == 0
     want = np.zeros_like(src)
     oracle.batch(True, key, iv, recs, src, want, aad)
@@ -111,7 +129,7 @@ def test_aead_walk_reads_stay_inside_records(model, fam):
         a, n = int(x["dst"]), int(x["len"])
         assert ct[a:a + n + 16].tobytes() == want[a:a + n + 16].tobytes(), n
     pt = np.zeros_like(src)
-    with Checked(model, aead_ranges(recs, ct, aad, True)):
+    with Checked(model, aead_ranges(recs, ct, aad, True), out_ranges(pt, recs["dst"], recs["len"])):
         assert call_aead(model, fam, False, key, iv, recs, ct, pt, aad, st) == 0
     assert (st == recs["len"]).all()
 
@@ -155,7 +173,7 @@ def test_tls_walk_reads_stay_inside_records(model, fam):
 
     ranges = [(t.ctypes.data, t.ctypes.data + t.nbytes)] + \
              [(src.ctypes.data + int(x["src"]), src.ctypes.data + int(x["src"]) + int(x["len"])) for x in t]
-    with Checked(model, ranges):
+    with Checked(model, ranges, out_ranges(wire, t["dst"], t["len"].astype(np.int64) + 22)):
         assert call(True, t, src, wire) == 0
     for x in t:
         frag = src[int(x["src"]): int(x["src"]) + int(x["len"])].tobytes()
@@ -167,7 +185,7 @@ def test_tls_walk_reads_stay_inside_records(model, fam):
     pt = np.zeros(int(o["dst"][-1]) + int(t["len"][-1]) + 1 + GAP, np.uint8)
     ranges = [(o.ctypes.data, o.ctypes.data + o.nbytes)] + \
              [(wire.ctypes.data + int(x["src"]) + 5, wire.ctypes.data + int(x["src"]) + 5 + int(x["len"])) for x in o]
-    with Checked(model, ranges):
+    with Checked(model, ranges, out_ranges(pt, o["dst"], o["len"].astype(np.int64) - 16)):
         assert call(False, o, wire, pt) == 0
     assert (st == t["len"]).all() and (ty == t["type"]).all()
 
@@ -183,4 +201,18 @@ def test_checker_catches_an_over_read(model):
     ranges[2] = (ranges[2][0], ranges[2][1] - 1)  # record 0's input, one byte short
     with pytest.raises(AssertionError, match="reads outside the records"):
         with Checked(model, ranges):
+            call_aead(model, 4, True, bytes(16), bytes(12), recs, src, out, aad, st)
+
+
+def test_checker_catches_a_stray_write(model):
+    """The write checker itself: an output range one byte short of what the walk stores is reported."""
+    recs, nsrc, naad = aead_layout([100, 1400], [5, 13])
+    src = np.zeros(nsrc, np.uint8)
+    aad = np.zeros(naad, np.uint8)
+    out = np.zeros_like(src)
+    st = np.zeros(2, np.uint32)
+    writes = out_ranges(out, recs["dst"], recs["len"])
+    writes[1] = (writes[1][0], writes[1][1] - 1)  # record 1's ciphertext, one byte short
+    with pytest.raises(AssertionError, match="writes outside the records"):
+        with Checked(model, aead_ranges(recs, src, aad, False), writes):
             call_aead(model, 4, True, bytes(16), bytes(12), recs, src, out, aad, st)
