@@ -115,30 +115,73 @@ extern "C" int model_set_window_lanes(int kw)
     return prev;
 }
 
+/*
+ * One wave of the batch kernels (batch_body, gcm_engine.hip): R = 64 / K records side by side, every lane walking to
+ * the wave's longest walk (Tmax), the fast-path steps those every lane can take (an idle slot -- past the batch's
+ * end, or a record the kernel does not walk -- leaves none), loads issued GCM_BATCH_PF = 3 steps ahead with the
+ * descriptor array as the idle lanes' load address.  part[s] = the XOR of record s's K lane results.
+ */
+template <int NR, int K, bool SEAL, bool FRAME>
+static void run_wave(const KeyImage *ki, const uint8_t *lds, const Record *rec, const bool *valid, const uint32_t (*iv)[3],
+                     const uint32_t *ctype, const uint8_t *src, uint8_t *dst, const uint8_t *aad, const uint8_t *descs,
+                     u32x4 *part)
+{
+    constexpr uint32_t R = 64u / (uint32_t)K;
+    uint32_t Tmax = 0u, f_lo = 0xffffffffu, f_hi = 0u;
+    for (uint32_t s = 0; s < R; ++s) {
+        const uint32_t plen = FRAME && SEAL ? rec[s].len + 1u : rec[s].len;
+        const Walk wk = make_walk(plen, FRAME ? 5u : rec[s].aadlen, K, walk_out16(dst + rec[s].dst));
+        for (uint32_t j = 0; j < (uint32_t)K; ++j) {
+            uint32_t lo = 0xffffffffu, hi = 0u;
+            if (valid[s])
+                walk_interior(wk, j, K, rec[s].len, lo, hi);
+            f_lo = f_lo > lo ? f_lo : lo;
+            f_hi = f_hi < hi ? f_hi : hi;
+        }
+        if (valid[s] && wk.T > Tmax)
+            Tmax = wk.T;
+    }
+    for (uint32_t s = 0; s < R; ++s) {
+        part[s] = u32x4{0, 0, 0, 0};
+        for (uint32_t j = 0; j < (uint32_t)K; ++j)
+            part[s] ^= lane_walk<NR, K, SEAL, FRAME, Layout<K>, 3>(lds, 4u * ((s * K + j) & 31u) | 0x10000u, ki->rk, j,
+                                                                   rec[s], valid[s], Tmax, iv[s][0], iv[s][1], iv[s][2],
+                                                                   src, dst, aad, descs, ctype[s], nullptr, 0u, nullptr,
+                                                                   f_lo, f_hi);
+    }
+}
+
 template <int NR, int K, bool SEAL>
 static void run(const KeyImage *ki, const uint8_t *lds, const uint8_t *static_iv, const Record *recs, size_t n,
                 const uint8_t *src, uint8_t *dst, const uint8_t *aad, uint32_t *status)
 {
+    constexpr uint32_t R = 64u / (uint32_t)K;
     uint32_t iv0, iv1, iv2;
     memcpy(&iv0, static_iv, 4);
     memcpy(&iv1, static_iv + 4, 4);
     memcpy(&iv2, static_iv + 8, 4);
-    for (size_t i = 0; i < n; ++i) {
-        const Record &r = recs[i];
-        Walk wk = make_walk(r.len, r.aadlen, K, walk_out16(dst + r.dst));
-        uint32_t n1 = iv1 ^ bswap32((uint32_t)(r.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)r.seq);
-        u32x4 tag = {0, 0, 0, 0};
-        for (uint32_t j = 0; j < (uint32_t)K; ++j) {
-            uint32_t f_lo, f_hi; /* the lane's own interior steps: the fast path wherever a wave could take it */
-            walk_interior(wk, j, K, r.len, f_lo, f_hi);
-            tag ^= lane_walk<NR, K, SEAL>(lds, 4u * (j & 31u) | 0x10000u, ki->rk, j, r, true, wk.T, iv0, n1, n2, src, dst,
-                                          aad, (const uint8_t *)recs, 0u, nullptr, 0u, nullptr, f_lo, f_hi);
+    for (size_t g = 0; g < n; g += R) {
+        Record rec[R];
+        bool valid[R];
+        uint32_t iv[R][3], ctype[R];
+        u32x4 part[R];
+        for (uint32_t s = 0; s < R; ++s) {
+            valid[s] = g + s < n;
+            rec[s] = valid[s] ? recs[g + s] : Record{0, 0, 0, 0, 0, 0};
+            iv[s][0] = iv0;
+            iv[s][1] = iv1 ^ bswap32((uint32_t)(rec[s].seq >> 32));
+            iv[s][2] = iv2 ^ bswap32((uint32_t)rec[s].seq);
+            ctype[s] = 0u;
         }
-        if (SEAL) {
-            memcpy(dst + r.dst + r.len, &tag, 16);
-        } else {
-            const u32x4 d = tag; /* computed ^ received (lane_walk) */
-            status[i] = (d[0] | d[1] | d[2] | d[3]) ? 0xffffffffu : r.len;
+        run_wave<NR, K, SEAL, false>(ki, lds, rec, valid, iv, ctype, src, dst, aad, (const uint8_t *)recs, part);
+        for (uint32_t s = 0; s < R && g + s < n; ++s) {
+            const Record &r = rec[s];
+            if (SEAL) {
+                memcpy(dst + r.dst + r.len, &part[s], 16);
+            } else {
+                const u32x4 d = part[s]; /* computed ^ received (lane_walk) */
+                status[g + s] = (d[0] | d[1] | d[2] | d[3]) ? 0xffffffffu : r.len;
+            }
         }
     }
 }
@@ -180,60 +223,68 @@ static u32x4 model_window_join(const uint8_t *lds, u32x4 *parts, uint32_t ns)
     return acc;
 }
 
-/* the FRAME walk (TLS 1.3 record framing) with the framing kernels' prologue/epilogue, K = 4 */
+/* the FRAME walk (TLS 1.3 record framing) with the framing kernels' prologue/epilogue, K = 4, a wave of 16 records
+ * at a time (run_wave) */
 template <int NR, bool SEAL>
 static void run_tls(const KeyImage *ki, const uint8_t *lds, const uint8_t *static_iv, const TlsRecord *trecs, size_t n,
                     const uint8_t *src, uint8_t *dst, uint32_t *status, uint8_t *types, const uint32_t *conn)
 {
     constexpr int K = 4;
+    constexpr uint32_t R = 64u / K;
     uint32_t iv0, iv1, iv2;
     memcpy(&iv0, static_iv, 4);
     memcpy(&iv1, static_iv + 4, 4);
     memcpy(&iv2, static_iv + 8, 4);
-    for (size_t i = 0; i < n; ++i) {
-        const TlsRecord &t = trecs[i];
-        Record r = {0, 0, 0, t.seq, 0, 5};
-        if (SEAL) {
-            r.src = t.src;
-            r.dst = t.dst + 5;
-            r.len = t.len;
-        } else {
-            if (t.len < 16) {
+    for (size_t g = 0; g < n; g += R) {
+        Record rec[R];
+        bool valid[R];
+        uint32_t iv[R][3], ctype[R];
+        u32x4 part[R];
+        for (uint32_t s = 0; s < R; ++s) {
+            const bool in = g + s < n;
+            const TlsRecord t = in ? trecs[g + s] : TlsRecord{0, 0, 0, 0, 0};
+            Record r = {0, 0, 0, t.seq, 0, 5};
+            if (SEAL) { /* header at t.dst, ciphertext after it; a fragment above 2^14 is not walked */
+                r.src = t.src;
+                r.dst = t.dst + 5;
+                r.len = t.len;
+                valid[s] = in && t.len <= 16384u;
+            } else { /* shorter than a tag: bad_record_mac without a walk */
+                r.src = t.src + 5;
+                r.dst = t.dst;
+                r.len = t.len >= 16u ? t.len - 16u : 0u;
+                valid[s] = in && t.len >= 16u;
+            }
+            rec[s] = in ? r : Record{0, 0, 0, 0, 0, 0};
+            iv[s][0] = conn != nullptr && in ? iv0 ^ bswap32(conn[g + s]) : iv0; /* rapido's per-connection IV */
+            iv[s][1] = iv1 ^ bswap32((uint32_t)(rec[s].seq >> 32));
+            iv[s][2] = iv2 ^ bswap32((uint32_t)rec[s].seq);
+            ctype[s] = t.type;
+        }
+        run_wave<NR, K, SEAL, true>(ki, lds, rec, valid, iv, ctype, src, dst, nullptr, (const uint8_t *)trecs, part);
+        for (uint32_t s = 0; s < R && g + s < n; ++s) {
+            const size_t i = g + s;
+            const Record &r = rec[s];
+            const u32x4 tag = part[s];
+            const uint32_t plen = SEAL ? r.len + 1 : r.len;
+            if (SEAL) {
+                if (!valid[s])
+                    continue;
+                memcpy(dst + r.dst + plen, &tag, 16);
+                const uint32_t reclen = plen + 16;
+                const uint8_t hdr[5] = {23, 3, 3, (uint8_t)(reclen >> 8), (uint8_t)reclen};
+                memcpy(dst + trecs[i].dst, hdr, 5);
+            } else if (!valid[s] || (tag[0] | tag[1] | tag[2] | tag[3])) {
                 status[i] = 0xffffffffu;
                 types[i] = 0;
-                continue;
+                memset(dst + r.dst, 0, plen);
+            } else {
+                uint32_t m = plen;
+                while (m != 0 && dst[r.dst + m - 1] == 0)
+                    --m;
+                status[i] = m ? m - 1 : 0xfffffffeu;
+                types[i] = m ? dst[r.dst + m - 1] : 0;
             }
-            r.src = t.src + 5;
-            r.dst = t.dst;
-            r.len = t.len - 16;
-        }
-        const uint32_t plen = SEAL ? r.len + 1 : r.len;
-        Walk wk = make_walk(plen, 5, K, walk_out16(dst + r.dst));
-        uint32_t n1 = iv1 ^ bswap32((uint32_t)(r.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)r.seq);
-        const uint32_t n0 = conn ? iv0 ^ bswap32(conn[i]) : iv0; /* rapido's per-connection IV */
-        u32x4 tag = {0, 0, 0, 0};
-        for (uint32_t j = 0; j < (uint32_t)K; ++j) {
-            uint32_t f_lo, f_hi;
-            walk_interior(wk, j, K, r.len, f_lo, f_hi);
-            tag ^= lane_walk<NR, K, SEAL, true>(lds, 4u * (j & 31u) | 0x10000u, ki->rk, j, r, true, wk.T, n0, n1, n2, src,
-                                                dst, nullptr, (const uint8_t *)trecs, t.type, nullptr, 0u, nullptr, f_lo,
-                                                f_hi);
-        }
-        if (SEAL) {
-            memcpy(dst + r.dst + plen, &tag, 16);
-            const uint32_t reclen = plen + 16;
-            const uint8_t hdr[5] = {23, 3, 3, (uint8_t)(reclen >> 8), (uint8_t)reclen};
-            memcpy(dst + t.dst, hdr, 5);
-        } else if (tag[0] | tag[1] | tag[2] | tag[3]) {
-            status[i] = 0xffffffffu;
-            types[i] = 0;
-            memset(dst + r.dst, 0, plen);
-        } else {
-            uint32_t m = plen;
-            while (m != 0 && dst[r.dst + m - 1] == 0)
-                --m;
-            status[i] = m ? m - 1 : 0xfffffffeu;
-            types[i] = m ? dst[r.dst + m - 1] : 0;
         }
     }
 }

@@ -365,11 +365,13 @@ def test_model_tls_multi_connection_window(model, window):
         assert bytes(wire[int(t["dst"]): int(t["dst"]) + len(want)]) == want
     orecs = trecs.copy()
     orecs["src"], orecs["len"] = trecs["dst"], trecs["len"] + 17
-    orecs["dst"] = trecs["src"]
-    pt = np.zeros_like(src)
+    orecs["dst"] = trecs["src"] + np.arange(len(trecs), dtype=np.uint64)  # slots of len + 1 (fragment + type)
+    pt = np.zeros(off + len(trecs) + 16, np.uint8)
     st, ty = run_tls(model, False, key, iv, orecs, wire, pt, conn=conn, window=window)
     assert (st[: len(trecs)] == trecs["len"]).all() and (ty[: len(trecs)] == 23).all()
-    assert bytes(pt[:off]) == bytes(src[:off])
+    for t, o in zip(trecs, orecs):
+        n, d, s0 = int(t["len"]), int(o["dst"]), int(t["src"])
+        assert bytes(pt[d:d + n]) == bytes(src[s0:s0 + n])
     # a record opened under another connection's IV fails
     wrong = conn.copy()
     wrong[3] ^= 1
