@@ -61,7 +61,7 @@ def gpu(engine_lib):
 
 # the kernel families every parity test runs on (rapido_amd/csrc/gcm_engine.hip plan_launch): the window kernels
 # with 64-position segments, with 32-position segments (8 lanes, 4 steps), with 32-position segments and 16 lanes
-# (2 steps), the split kernels (runs of 16 such segments on separate workgroups), and the batch kernels (K lanes per
+# (2 steps), the split kernels (runs of 8 such segments on separate workgroups), and the batch kernels (K lanes per
 # record)
 FAMILIES = ["window", "window32", "window16", "split", "batch"]
 

@@ -432,9 +432,9 @@ extern "C" int model_batch_window(int is_seal, const uint8_t *key, size_t keylen
  * The 16-lane latency kernels (window_body with LayoutWin16) and the split kernels (split_body, LayoutSplit) for AEAD
  * records: 32-position segments walked by 16 lanes (2 steps; lane scaling H^(16 - j) as H^8 x H^(8 - j) for j < 8).
  * win16 joins the segments as window_body does with SEG = 32 (groups of 4 with H^32, pairs of groups with H^128, the
- * chain of pairs with H^256); split cuts them into runs of 16 aligned to the record's end, joins each run (groups of
- * 4 with H^32, the chain of groups with H^128), scales it by H^(512 m) and XORs the runs.  Records of more than
- * 33 (win16) / 48 (split) segments are walked whole by 16 lanes.
+ * chain of pairs with H^256); split cuts them into runs of SPLIT_RUNSEG = 8 aligned to the record's end, joins each
+ * run (groups of 4 with H^32, the two groups chained with H^128), scales it by H^(256 m) and XORs the runs.  Records
+ * of more than 33 (win16) / 40 (split) segments are walked whole by 16 lanes.
  */
 template <int NR, bool SEAL, bool SPLIT>
 static void run_win16(const KeyImage *ki, uint8_t *lds, uint8_t *lds_m2, const uint8_t *static_iv, const Record *recs,
