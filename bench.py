@@ -128,6 +128,85 @@ def algorithmic_bytes(lengths_sum: int, n: int, aad_sum: int, seal: bool) -> int
 
 
 # ------------------------------------------------------------------------------------------- CPU baseline ----
+class ClockSampler:
+    """The chip's gfx clock and socket power while a region runs, measured in THIS run: amdsmi's GPU metrics
+    (`current_gfxclks`, one value per XCD, and `current_socket_power`; the same source as torch.cuda.clock_rate on
+    ROCm) sampled every `period` seconds on a thread that never touches HIP.  The firmware refreshes them about every
+    20-30 ms (scripts/probe_amdsmi_clock.py, profiles/r05zk_amdsmi_clock.json).  Off, with the reason, when amdsmi or
+    the device's metrics are unavailable."""
+
+    _init = None  # amdsmi initialised once per process (None: not tried; else the error string or "")
+
+    def __init__(self, dev, period: float = 0.004):
+        import threading
+        self.samples, self.err, self.h, self.period = [], None, None, period
+        self._stop = threading.Event()
+        self._thread = None
+        try:
+            import amdsmi
+            import torch
+            if ClockSampler._init is None:
+                try:
+                    amdsmi.amdsmi_init()
+                    ClockSampler._init = ""
+                except Exception as e:  # noqa: BLE001 -- reported in the line
+                    ClockSampler._init = f"amdsmi_init: {type(e).__name__}: {e}"
+            if ClockSampler._init:
+                raise RuntimeError(ClockSampler._init)
+            pr = torch.cuda.get_device_properties(dev)
+            bdf = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+            self.h = amdsmi.amdsmi_get_processor_handle_from_bdf(bdf)
+            self._amdsmi = amdsmi
+            self.read()  # fails here, not on the thread, if the metrics are unreadable
+        except Exception as e:  # noqa: BLE001 -- reported in the line
+            self.err = f"{type(e).__name__}: {e}"
+            self.h = None
+
+    def read(self):
+        m = self._amdsmi.amdsmi_get_gpu_metrics_info(self.h)
+        clks = [c for c in m.get("current_gfxclks") or [] if isinstance(c, (int, float))]
+        if not clks and isinstance(m.get("current_gfxclk"), (int, float)):
+            clks = [m["current_gfxclk"]]
+        pw = m.get("current_socket_power")
+        return (sum(clks) / len(clks) if clks else None, pw if isinstance(pw, (int, float)) else None)
+
+    def _run(self):
+        while not self._stop.is_set():
+            try:
+                mhz, w = self.read()
+            except Exception:  # noqa: BLE001 -- a missed sample
+                mhz, w = None, None
+            self.samples.append((time.perf_counter(), mhz, w))
+            self._stop.wait(self.period)
+
+    def __enter__(self):
+        import threading
+        if self.h is not None:
+            self._thread = threading.Thread(target=self._run, daemon=True)
+            self._thread.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        if self._thread is not None:
+            self._thread.join()
+
+    def summary(self, t_from: float, t_to: float) -> dict:
+        """Medians over the samples taken in [t_from, t_to] (perf_counter seconds)."""
+        import statistics
+        if self.h is None:
+            return {"source": None, "error": self.err}
+        sel = [(c, w) for t, c, w in self.samples if t_from <= t <= t_to and c is not None]
+        if not sel:
+            return {"source": None, "error": "no sample in the window"}
+        clk = [c for c, _ in sel]
+        pw = [w for _, w in sel if w is not None]
+        return {"gfx_mhz_median": round(statistics.median(clk), 1), "gfx_mhz_min": round(min(clk), 1),
+                "gfx_mhz_max": round(max(clk), 1), "socket_power_w_median": statistics.median(pw) if pw else None,
+                "samples": len(sel), "window_ms": round((t_to - t_from) * 1e3, 1),
+                "source": "amdsmi current_gfxclks (mean of the XCDs) and current_socket_power, sampled in this run"}
+
+
 def _cgroup_cpus():
     """CPUs' worth of the cgroup v2 quota (cpu.max), or None when unlimited."""
     try:
@@ -328,6 +407,8 @@ def measure(ra, wl_key, args, dev, rank, world, check):
 
     # untimed pre-warm: the power manager takes ~10-20 ms of load to raise the clock (the first launches of a run are
     # up to 35% slower, profiles/r03zc_launches.json), so steps run for prewarm_ms before the W warmup steps
+    sampler = ClockSampler(dev)
+    sampler.__enter__()
     t_pre, n_pre = time.perf_counter(), 0
     while (time.perf_counter() - t_pre) * 1e3 < args.prewarm_ms:
         step()
@@ -350,8 +431,13 @@ def measure(ra, wl_key, args, dev, rank, world, check):
     join(ev_join)
     ev_t1.record(streams[0])
     torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
+    t_end = time.perf_counter()
+    sampler.__exit__(None, None, None)
+    elapsed = t_end - t0
     elapsed_rank = elapsed
+    # the clock under this load: the timed region, widened back into the steady pre-warm to hold several of the
+    # firmware's 20-30 ms metric refreshes when the region is short
+    live_clock = sampler.summary(max(t_pre + 0.2 * (t0 - t_pre), t0 - 0.25), t_end)
     if world > 1:
         dist.barrier()
         elapsed = max_over_ranks(elapsed, dev)
@@ -446,7 +532,8 @@ def measure(ra, wl_key, args, dev, rank, world, check):
                                 "algorithmic_bytes_per_step": seal_b + open_b, "region_ms": round(region_ms, 4),
                                 "note": "every launch of the timed region (seal + open, all chunks) over its HIP-event "
                                         "time"}},
-        "lds_roofline": lds_roofline(kname, dom_payload, wl_key, wl["key"], b32_reads, b128_reads, lds_nominal, ncu),
+        "lds_roofline": lds_roofline(kname, dom_payload, wl_key, wl["key"], b32_reads, b128_reads, lds_nominal, ncu,
+                                     live_clock),
     }
     for e in engs[1:]:
         e.close()
@@ -455,13 +542,13 @@ def measure(ra, wl_key, args, dev, rank, world, check):
     return res, extra
 
 
-def lds_roofline(kname, achieved, wl_key, key, b32_reads, b128_reads, nominal, ncu):
+def lds_roofline(kname, achieved, wl_key, key, b32_reads, b128_reads, nominal, ncu, live=None):
     """The LDS bound of the batch kernel.  The ceiling is the LDS array busy every cycle: b32_reads x 2 + b128_reads x 4
     array cycles per 64 blocks per CU (MI355X_MICROARCH.md LDS table), which the counters confirm exactly --
     SQ_LDS_IDX_ACTIVE per 64 blocks is 330.0 / 458.0 for the AES-128 / AES-256 read mix alone and 333 / 461 in the
-    kernels (profiles/r05e_lds_ceiling.json).  Priced at the clock the chip holds under the kernel
-    (profiles/held_clock.json: GRBM_GUI_ACTIVE / 8 over the dispatch time of the builder's PMC pass), beside the
-    nominal 2.4 GHz."""
+    kernels (profiles/r05e_lds_ceiling.json).  Priced at the clock the chip holds under the kernel in THIS run (`live`:
+    amdsmi, ClockSampler), beside the builder's counter-derived figure for the same workload (profiles/held_clock.json:
+    GRBM_GUI_ACTIVE / 8 over the kernel's dispatch time) and the nominal 2.4 GHz."""
     cyc = 2.0 * b32_reads + 4.0 * b128_reads
     r = {"bound": "lds", "kernel": kname, "achieved": round(achieved, 1), "unit": "GB/s payload",
          "model": f"{b32_reads} ds_read_b32 + {b128_reads} ds_read_b128 per 16-B block: {cyc:.0f} LDS-array cycles per 64 "
@@ -476,10 +563,20 @@ def lds_roofline(kname, achieved, wl_key, key, b32_reads, b128_reads, nominal, n
             held = json.load(open(hpath)).get(wl_key, {}).get(kname)
         except ValueError:
             held = None
+    def peak_at(ghz):
+        return ncu * ghz * 1e9 / (cyc / 64.0) * 16 / 1e9
+
     if held:
-        peak = ncu * held["ghz"] * 1e9 / (cyc / 64.0) * 16 / 1e9
-        r.update({"peak": round(peak, 1), "frac": round(achieved / peak, 4), "held_clock_ghz": held["ghz"],
-                  "held_clock_source": held["source"]})
+        r["pmc_clock"] = {"ghz": held["ghz"], "peak": round(peak_at(held["ghz"]), 1),
+                          "frac": round(achieved / peak_at(held["ghz"]), 4), "source": held["source"]}
+    if live and live.get("gfx_mhz_median"):
+        ghz = live["gfx_mhz_median"] / 1e3
+        r.update({"peak": round(peak_at(ghz), 1), "frac": round(achieved / peak_at(ghz), 4),
+                  "held_clock_ghz": round(ghz, 3), "held_clock_source": "live: measured in this run",
+                  "live_clock": live})
+    elif held:
+        r.update({"peak": r["pmc_clock"]["peak"], "frac": r["pmc_clock"]["frac"], "held_clock_ghz": held["ghz"],
+                  "held_clock_source": held["source"] + " (no live clock: " + str((live or {}).get("error")) + ")"})
     else:
         r.update({"peak": round(nominal, 1), "frac": round(achieved / nominal, 4),
                   "held_clock_source": "none for this kernel and workload: priced at 2.4 GHz"})

@@ -64,3 +64,29 @@ def test_algorithmic_bytes_follow_survey_8d():
     # 2845 B per 1400-B seal with a 5-B AAD (16-B descriptor + 8-B seq)
     assert bench.algorithmic_bytes(1400, 1, 5, True) == 2845
     assert bench.algorithmic_bytes(1400, 1, 5, False) == 1400 + 16 + 5 + 24 + 1400 + 4
+
+
+def test_lds_roofline_prefers_the_live_clock():
+    """A clock measured in the run (ClockSampler) prices the model; the builder's counter clock stays beside it."""
+    import bench
+    k = "mi355x_gcm_seal_aes128_k4"
+    nominal = 256 * 2.4 * 64 / 330 * 16
+    live = {"gfx_mhz_median": 1913.0, "samples": 40, "source": "amdsmi"}
+    r = bench.lds_roofline(k, 1000.0, "16k-aes128", 16, 133, 16, nominal, 256, live)
+    assert r["held_clock_ghz"] == pytest.approx(1.913)
+    assert r["peak"] == pytest.approx(256 * 1.913 * 64 / 330 * 16, rel=1e-3)
+    assert r["live_clock"] is live and r["held_clock_source"].startswith("live")
+    assert r["pmc_clock"]["ghz"] == _load("held_clock.json")["16k-aes128"][k]["ghz"]
+    off = bench.lds_roofline(k, 1000.0, "16k-aes128", 16, 133, 16, nominal, 256, {"error": "no amdsmi"})
+    assert off["frac"] == off["pmc_clock"]["frac"] and "no amdsmi" in off["held_clock_source"]
+
+
+def test_clock_sampler_reports_why_it_is_off():
+    """Without a GPU the sampler never raises: it is off, says why, and its summary carries the reason."""
+    import bench
+    s = bench.ClockSampler(0)
+    with s:
+        pass
+    summ = s.summary(0.0, 1e12)
+    if s.h is None:
+        assert s.err and summ["source"] is None and summ["error"]
