@@ -133,7 +133,7 @@ class ClockSampler:
     (`current_gfxclks`, one value per XCD, and `current_socket_power`; the same source as torch.cuda.clock_rate on
     ROCm) sampled every `period` seconds on a thread that never touches HIP.  The firmware refreshes them about every
     20-30 ms (scripts/probe_amdsmi_clock.py, profiles/r05zk_amdsmi_clock.json).  Off, with the reason, when amdsmi or
-    the device's metrics are unavailable."""
+    the device's metrics are unavailable, or with RAPIDO_BENCH_NO_CLOCK=1."""
 
     _init = None  # amdsmi initialised once per process (None: not tried; else the error string or "")
 
@@ -143,6 +143,8 @@ class ClockSampler:
         self._stop = threading.Event()
         self._thread = None
         try:
+            if os.environ.get("RAPIDO_BENCH_NO_CLOCK") == "1":
+                raise RuntimeError("disabled (RAPIDO_BENCH_NO_CLOCK=1)")
             import amdsmi
             import torch
             if ClockSampler._init is None:
