@@ -307,3 +307,57 @@ def test_status_and_types_at_guard_edges(guards, family, at):
                 assert OUT.get(mid_out + int(poff[i]), lens[i]) == pts[i], (family, at, i)
     eng.close()
     checked()
+
+
+@pytest.mark.parametrize("at", ["start", "end"])
+def test_delivery_at_guard_edges(guards, at):
+    """The delivery kernel (ptls_mi355x_tls_deliver_records, handle_input's receive loop on the device) writing each
+    part's plaintexts back to back into an `out` flush against a guard, with a capacity of exactly what it should
+    take: part A delivers all its records (one of 0 bytes, one of 16 KiB), part B stops before a tampered record and
+    part C (any_type) takes one handshake record.  Its outputs, not only its inputs, meet the guard."""
+    import torch
+    lib, gs = guards
+    IN, AUX, OUT = (Region(lib, g) for g in gs)
+    key, iv = bytes(range(7, 23)), bytes(range(30, 42))
+    lens = [100, 16384, 1, 777, 0, 300, 4096, 50, 60, 200]
+    types = [23] * 9 + [22]
+    bad = 7
+    n = len(lens)
+    eng = ra.Engine(key)
+    for r in (IN, AUX, OUT):
+        r.clear()
+    frags = [xorshift64star(500 + i, ln).tobytes() for i, ln in enumerate(lens)]
+    wires = [bytearray(oracle.tls_seal_record(key, iv, 3 + i, types[i], f)) for i, f in enumerate(frags)]
+    wires[bad][-1] ^= 1
+    woff = np.cumsum([0] + [len(w) for w in wires[:-1]]).astype(np.uint64)
+    soff = np.cumsum([0] + [(ln + 1 + 15) // 16 * 16 for ln in lens[:-1]]).astype(np.uint64)  # 16-aligned slots
+    wire = b"".join(bytes(w) for w in wires)
+    d_wire = torch.from_numpy(np.frombuffer(wire, np.uint8).copy()).cuda()
+    d_slots = torch.zeros(int(soff[-1]) + lens[-1] + 17, dtype=torch.uint8, device="cuda")
+    o = np.zeros(n, ra.TLS_RECORD_DTYPE)
+    o["src"], o["dst"], o["seq"], o["len"] = woff, soff, 3 + np.arange(n), np.array(lens) + 17
+    mid = AUX.base + AUX.len // 2
+    d_o, st, ty, d_parts = mid, mid - 4096, mid - 2048, mid + 4096
+    assert lib.guard_h2d(d_o, o.ctypes.data, o.nbytes) == 0
+    eng.tls_open_records(iv, d_o, n, d_wire.data_ptr(), d_slots.data_ptr(), st, ty)
+    checked()
+    assert list(np.frombuffer(AUX.get(st, 4 * n), np.uint32)) == [0xFFFFFFFF if i == bad else ln
+                                                                    for i, ln in enumerate(lens)]
+    want_a = b"".join(frags[0:5])
+    want_b = b"".join(frags[5:bad])
+    want_c = frags[9]
+    other = "end" if at == "start" else "start"
+    out_a, out_b = OUT.addr(len(want_a), at), OUT.addr(len(want_b), other)
+    out_c = IN.addr(len(want_c), at)
+    parts = np.zeros(3, ra.TLS_DELIVER_DTYPE)
+    parts[0] = (d_slots.data_ptr(), out_a, len(want_a), 0, 5, 0, 0)
+    parts[1] = (d_slots.data_ptr(), out_b, len(want_b), 5, 4, 0, 0)
+    parts[2] = (d_slots.data_ptr(), out_c, len(want_c), 9, 1, 1, 0)
+    assert lib.guard_h2d(d_parts, parts.ctypes.data, parts.nbytes) == 0
+    assert ra.lib().ptls_mi355x_tls_deliver_records(eng.handle, d_o, st, ty, d_parts, 3, 5, None) == 0, ra.last_error()
+    checked()
+    assert OUT.get(out_a, len(want_a)) == want_a, at
+    assert OUT.get(out_b, len(want_b)) == want_b, at
+    assert IN.get(out_c, len(want_c)) == want_c, at
+    eng.close()
+    checked()
