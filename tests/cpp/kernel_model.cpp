@@ -404,7 +404,7 @@ extern "C" int model_batch_window(int is_seal, const uint8_t *key, size_t keylen
                                   const Record *recs, size_t n, const uint8_t *src, uint8_t *dst, const uint8_t *aad,
                                   uint32_t *status)
 {
-    KeyImage *ki = (KeyImage *)aligned_alloc(64, sizeof(KeyImage));
+    KeyImage *ki = (KeyImage *)aligned_alloc(64, (sizeof(KeyImage) + 63) & ~(size_t)63) /* (a multiple of the alignment) */;
     uint8_t *lds = (uint8_t *)aligned_alloc(256, 160u * 1024u);
     if (build_key_image(kTabs.sbox, key, (uint32_t)keylen, ki) != 0) {
         free(ki);
@@ -520,7 +520,7 @@ extern "C" int model_batch_win16(int is_seal, int split, const uint8_t *key, siz
                                  const Record *recs, size_t n, const uint8_t *src, uint8_t *dst, const uint8_t *aad,
                                  uint32_t *status)
 {
-    KeyImage *ki = (KeyImage *)aligned_alloc(64, sizeof(KeyImage));
+    KeyImage *ki = (KeyImage *)aligned_alloc(64, (sizeof(KeyImage) + 63) & ~(size_t)63) /* (a multiple of the alignment) */;
     uint8_t *lds = (uint8_t *)aligned_alloc(256, 160u * 1024u), *lds2 = (uint8_t *)aligned_alloc(256, 160u * 1024u);
     if (build_key_image(kTabs.sbox, key, (uint32_t)keylen, ki) != 0) {
         free(ki);
@@ -553,7 +553,7 @@ extern "C" int model_tls_window(int is_seal, const uint8_t *key, size_t keylen, 
                                 const TlsRecord *trecs, size_t n, const uint8_t *src, uint8_t *dst, uint32_t *status,
                                 uint8_t *types, const uint32_t *conn)
 {
-    KeyImage *ki = (KeyImage *)aligned_alloc(64, sizeof(KeyImage));
+    KeyImage *ki = (KeyImage *)aligned_alloc(64, (sizeof(KeyImage) + 63) & ~(size_t)63) /* (a multiple of the alignment) */;
     uint8_t *lds = (uint8_t *)aligned_alloc(256, 160u * 1024u);
     if (build_key_image(kTabs.sbox, key, (uint32_t)keylen, ki) != 0) {
         free(ki);
@@ -581,7 +581,7 @@ extern "C" int model_tls_batch(int is_seal, const uint8_t *key, size_t keylen, c
                                const TlsRecord *trecs, size_t n, const uint8_t *src, uint8_t *dst, uint32_t *status,
                                uint8_t *types, const uint32_t *conn)
 {
-    KeyImage *ki = (KeyImage *)aligned_alloc(64, sizeof(KeyImage));
+    KeyImage *ki = (KeyImage *)aligned_alloc(64, (sizeof(KeyImage) + 63) & ~(size_t)63) /* (a multiple of the alignment) */;
     uint8_t *lds = (uint8_t *)aligned_alloc(256, 160u * 1024u);
     if (build_key_image(kTabs.sbox, key, (uint32_t)keylen, ki) != 0) {
         free(ki);
@@ -604,7 +604,7 @@ extern "C" int model_batch(int is_seal, int K, const uint8_t *key, size_t keylen
                            const Record *recs, size_t n, const uint8_t *src, uint8_t *dst, const uint8_t *aad,
                            uint32_t *status)
 {
-    KeyImage *ki = (KeyImage *)aligned_alloc(64, sizeof(KeyImage));
+    KeyImage *ki = (KeyImage *)aligned_alloc(64, (sizeof(KeyImage) + 63) & ~(size_t)63) /* (a multiple of the alignment) */;
     uint8_t *lds = (uint8_t *)aligned_alloc(256, 160u * 1024u);
     if (build_key_image(kTabs.sbox, key, (uint32_t)keylen, ki) != 0) {
         free(ki);
@@ -635,7 +635,7 @@ extern "C" int model_batch(int is_seal, int K, const uint8_t *key, size_t keylen
  */
 extern "C" int model_gh8_mul(const uint8_t *key, size_t keylen, const uint8_t *x, size_t nx, uint8_t *out)
 {
-    KeyImage *ki = (KeyImage *)aligned_alloc(64, sizeof(KeyImage));
+    KeyImage *ki = (KeyImage *)aligned_alloc(64, (sizeof(KeyImage) + 63) & ~(size_t)63) /* (a multiple of the alignment) */;
     uint8_t *lds = (uint8_t *)aligned_alloc(256, 160u * 1024u);
     if (build_key_image(kTabs.sbox, key, (uint32_t)keylen, ki) != 0) {
         free(ki);
@@ -677,7 +677,7 @@ extern "C" size_t model_key_image_size(void) { return sizeof(KeyImage); }
  */
 extern "C" int model_bs_keystream(const uint8_t *key, size_t keylen, const uint8_t *nonce12, uint32_t ctr0, uint8_t *out)
 {
-    KeyImage *ki = (KeyImage *)aligned_alloc(64, sizeof(KeyImage));
+    KeyImage *ki = (KeyImage *)aligned_alloc(64, (sizeof(KeyImage) + 63) & ~(size_t)63) /* (a multiple of the alignment) */;
     uint8_t *kp = (uint8_t *)aligned_alloc(256, KEYPLANE_BYTES);
     if (build_key_image(kTabs.sbox, key, (uint32_t)keylen, ki) != 0) {
         free(ki);
