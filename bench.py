@@ -835,7 +835,9 @@ def main() -> None:
         mine = {"rank": rank, "host": socket.gethostname(), "device": dev_index,
                 "device_name": torch.cuda.get_device_name(dev), "rank_gibps": res["rank_gibps"],
                 "rank_ms_per_step": res["rank_ms_per_step"], "seal_gibps": res["seal_gibps"],
-                "open_gibps": res["open_gibps"], "launch_ms": res["roofline"]["launch_ms"]}
+                "open_gibps": res["open_gibps"], "launch_ms": res["roofline"]["launch_ms"],
+                "gfx_mhz": res["lds_roofline"].get("live_clock", {}).get("gfx_mhz_median"),
+                "socket_power_w": res["lds_roofline"].get("live_clock", {}).get("socket_power_w_median")}
         if e2e is not None:
             mine["e2e_pcie"] = {k: e2e[k] for k in ("seal_gibps_serial", "seal_gibps_pipelined",
                                                      "open_gibps_pipelined")}
