@@ -103,8 +103,9 @@ def check_device_map(dev_index: int, same_device_ok: bool, device_count: int):
 
 RANK_KEYS = ("rank", "host", "device", "device_name", "rank_gibps", "rank_ms_per_step", "seal_gibps", "open_gibps",
              "launch_ms")
-# optional per-rank figures carried when present: each GPU's own PCIe-inclusive rate (north_star: PCIe is per GPU)
-RANK_OPTIONAL_KEYS = ("e2e_pcie",)
+# optional per-rank figures carried when present: each GPU's own PCIe-inclusive rate (north_star: PCIe is per GPU), and
+# the gfx clock and socket power sampled under its timed steps (ClockSampler: why one GPU of a node lags another)
+RANK_OPTIONAL_KEYS = ("e2e_pcie", "gfx_mhz", "socket_power_w")
 
 
 def gather_rank_stats(mine: dict):

@@ -122,7 +122,8 @@ def _line_worker(rank, world, port, q, dev_index, same_ok):
     ranks = bench.gather_rank_stats({"rank": rank, "host": "h", "device": dev_index(rank), "device_name": "gfx950",
                                      "rank_gibps": 100.0 + rank, "rank_ms_per_step": 2.0 - rank, "seal_gibps": 1.0,
                                      "open_gibps": 2.0, "launch_ms": 1.5,
-                                     "e2e_pcie": {"seal_gibps_serial": 20.0 + rank, "seal_gibps_pipelined": 30.0 + rank}})
+                                     "e2e_pcie": {"seal_gibps_serial": 20.0 + rank, "seal_gibps_pipelined": 30.0 + rank},
+                                     "gfx_mhz": 2000.0 + rank, "socket_power_w": 1200 + rank})
     q.put((rank, placement, ranks))
     dist.destroy_process_group()
 
@@ -155,7 +156,8 @@ def test_bench_line_per_rank_figures():
     for rank, placement, ranks in _run_line(_dev_per_rank, False):
         assert [p[1] for p in placement] == [0, 1]
         assert [r["rank"] for r in ranks] == [0, 1] and [r["device"] for r in ranks] == [0, 1]
-        assert all(set(r) == set(bench.RANK_KEYS) | {"e2e_pcie"} for r in ranks)
+        assert all(set(r) == set(bench.RANK_KEYS) | {"e2e_pcie", "gfx_mhz", "socket_power_w"} for r in ranks)
+        assert [r["gfx_mhz"] for r in ranks] == [2000.0, 2001.0]  # each GPU's sampled clock rides with its rank
         assert [r["rank_gibps"] for r in ranks] == [100.0, 101.0]
         # each GPU's own PCIe-inclusive rate rides with its rank (north_star: PCIe is per GPU)
         assert [r["e2e_pcie"]["seal_gibps_pipelined"] for r in ranks] == [30.0, 31.0]
