@@ -105,7 +105,106 @@ RANK_KEYS = ("rank", "host", "device", "device_name", "rank_gibps", "rank_ms_per
              "launch_ms")
 # optional per-rank figures carried when present: each GPU's own PCIe-inclusive rate (north_star: PCIe is per GPU), and
 # the gfx clock and socket power sampled under its timed steps (ClockSampler: why one GPU of a node lags another)
-RANK_OPTIONAL_KEYS = ("e2e_pcie", "gfx_mhz", "socket_power_w")
+RANK_OPTIONAL_KEYS = ("e2e_pcie", "gfx_mhz", "socket_power_w", "numa_node", "cpus", "pci_bus_id", "error")
+
+
+def parse_cpulist(text: str) -> list:
+    """The CPUs of a sysfs cpulist ("0-3,8,10-11")."""
+    cpus = []
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        lo, _, hi = part.partition("-")
+        cpus.extend(range(int(lo), int(hi or lo) + 1))
+    return cpus
+
+
+def cpulist(cpus) -> str:
+    """The compact cpulist form of a CPU set (the inverse of parse_cpulist)."""
+    out, run = [], []
+    for c in sorted(set(cpus)):
+        if run and c == run[-1] + 1:
+            run.append(c)
+            continue
+        if run:
+            out.append(f"{run[0]}-{run[-1]}" if len(run) > 1 else str(run[0]))
+        run = [c]
+    if run:
+        out.append(f"{run[0]}-{run[-1]}" if len(run) > 1 else str(run[0]))
+    return ",".join(out)
+
+
+def hip_pci_bus_id(dev_index: int):
+    """The GPU's PCI address ("0000:c1:00.0") from hipDeviceGetPCIBusId, or None."""
+    import ctypes
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+        buf = ctypes.create_string_buffer(64)
+        if hip.hipDeviceGetPCIBusId(buf, 64, dev_index) != 0:
+            return None
+        return buf.value.decode().lower()
+    except OSError:
+        return None
+
+
+def place_rank(dev_index: int, bus_id=None, sysfs: str = "/sys/bus/pci/devices") -> dict:
+    """Puts this rank's host work on its GPU's NUMA node (north_star's per-GPU pinned hipMemcpyAsync
+    rate): the node from the GPU's PCI address (sysfs numa_node), the process pinned to that node's CPUs (local_cpulist)
+    within the CPUs it may use, and later allocations preferring the node's memory (set_mempolicy MPOL_PREFERRED), so the
+    pinned staging and e2e_pcie buffers, touched first after this, are node-local.  Returns the fields every rank's line
+    carries; a field that could not be had is None (never a guess)."""
+    bus_id = bus_id if bus_id is not None else hip_pci_bus_id(dev_index)
+    out = {"pci_bus_id": bus_id, "numa_node": None, "cpus": None, "pinned": False, "mempolicy": None}
+    if not bus_id:
+        return out
+    base = os.path.join(sysfs, bus_id)
+    try:
+        node = int(open(os.path.join(base, "numa_node")).read().strip())
+    except (OSError, ValueError):
+        return out
+    out["numa_node"] = node if node >= 0 else None  # -1: the platform reports no node
+    try:
+        local = set(parse_cpulist(open(os.path.join(base, "local_cpulist")).read()))
+    except OSError:
+        local = set()
+    allowed = os.sched_getaffinity(0)
+    cpus = sorted(local & allowed)
+    if cpus:
+        os.sched_setaffinity(0, cpus)
+        out["pinned"] = True
+        out["cpus"] = cpulist(cpus)
+    else:
+        out["cpus"] = cpulist(allowed)  # the node's CPUs are not ours to use: left as it was, and said so
+    if out["numa_node"] is not None:
+        out["mempolicy"] = _prefer_node(out["numa_node"])
+    return out
+
+
+def _prefer_node(node: int) -> str:
+    """set_mempolicy(MPOL_PREFERRED, {node}) for this process's later allocations (x86-64 syscall 238)."""
+    import ctypes
+    if node >= 64:
+        return "node beyond the mask"
+    try:
+        libc = ctypes.CDLL(None, use_errno=True)
+        mask = ctypes.c_ulong(1 << node)
+        rc = libc.syscall(238, 1, ctypes.byref(mask), 65)  # (MPOL_PREFERRED, nodemask, maxnode)
+        return "preferred" if rc == 0 else f"errno {ctypes.get_errno()}"
+    except OSError as e:  # pragma: no cover - libc is always there
+        return str(e)
+
+
+class RankFailure(Exception):
+    """A rank's own verification failed: reported to every rank with the per-rank figures, then every rank exits."""
+
+
+def fail_together(mine_error):
+    """Every rank learns whether any rank failed (all_gather_object), so no rank waits in a later collective for one
+    that has left: returns the per-rank errors (None where a rank passed)."""
+    import torch.distributed as dist
+    errs = [None] * dist.get_world_size()
+    dist.all_gather_object(errs, mine_error)
+    return errs
 
 
 def gather_rank_stats(mine: dict):
@@ -796,8 +895,22 @@ def main() -> None:
     ra.require_gpu()
     if args.lanes:
         ra.set_lanes_per_record(args.lanes)
+    # this rank's host work on its GPU's NUMA node, before the measured path allocates and touches host buffers
+    host_place = place_rank(dev.index if dev.index is not None else 0)
 
-    res, extra = measure(ra, args.workload, args, dev, rank, world, args.check)
+    # At N > 1 a rank whose own verification fails (SystemExit) does not leave alone: its error is gathered with every
+    # other rank's (fail_together) before any later collective, and all ranks exit together.
+    my_error = None
+    try:
+        res, extra = measure(ra, args.workload, args, dev, rank, world, args.check)
+    except SystemExit as e:
+        if world == 1:
+            raise
+        my_error, res, extra = str(e), None, None
+    if world > 1:  # every rank, at the same point: learn whether any rank failed
+        errs = fail_together(my_error)
+        if any(errs):
+            raise SystemExit(f"bench: rank(s) failed: {[(r, m) for r, m in enumerate(errs) if m]}")
     out = {
         "metric": METRIC,
         "value": res["value"],
@@ -825,20 +938,31 @@ def main() -> None:
         "build_id_matches_sources": ra.build_id() == ra.source_build_id(),
     }
     out["device_count"] = device_count
+    out["host_placement"] = host_place
     if world == 1 and not args.no_e2e:
         out["window_latency"] = window_latency(ra, extra, dev)
     e2e = None
     if not args.no_e2e:  # every rank at N > 1: each GPU's own link, all ranks at once (after the timed steps)
-        e2e = e2e_pcie(ra, extra, dev, args.steps)
+        try:
+            e2e = e2e_pcie(ra, extra, dev, args.steps)
+        except SystemExit as e:
+            if world == 1:
+                raise
+            my_error = str(e)
         out["e2e_pcie"] = e2e
     if world > 1:
+        errs = fail_together(my_error)
+        if any(errs):
+            raise SystemExit(f"bench: rank(s) failed: {[(r, m) for r, m in enumerate(errs) if m]}")
         import socket
         mine = {"rank": rank, "host": socket.gethostname(), "device": dev_index,
                 "device_name": torch.cuda.get_device_name(dev), "rank_gibps": res["rank_gibps"],
                 "rank_ms_per_step": res["rank_ms_per_step"], "seal_gibps": res["seal_gibps"],
                 "open_gibps": res["open_gibps"], "launch_ms": res["roofline"]["launch_ms"],
                 "gfx_mhz": res["lds_roofline"].get("live_clock", {}).get("gfx_mhz_median"),
-                "socket_power_w": res["lds_roofline"].get("live_clock", {}).get("socket_power_w_median")}
+                "socket_power_w": res["lds_roofline"].get("live_clock", {}).get("socket_power_w_median"),
+                "numa_node": host_place["numa_node"], "cpus": host_place["cpus"],
+                "pci_bus_id": host_place["pci_bus_id"]}
         if e2e is not None:
             mine["e2e_pcie"] = {k: e2e[k] for k in ("seal_gibps_serial", "seal_gibps_pipelined",
                                                      "open_gibps_pipelined")}

@@ -206,6 +206,25 @@ int ptls_mi355x_open_batch_ordered(ptls_mi355x_aesgcm_context_t *ctx, const void
                                    const ptls_mi355x_record_t *recs, const uint32_t *order, size_t n, const uint8_t *src,
                                    uint8_t *dst, const uint8_t *aad, uint32_t *status, void *stream);
 
+/*
+ * Multi-key batches: the records of many sessions -- each with its own traffic key and static IV (a rapido server's
+ * connections, include/rapido.h:147, lib/rapido.c:135-200) -- in ONE launch.  ctxs[k] (k < nkeys) is the context of key
+ * k and static_ivs its 12-byte IV at static_ivs + 12 k (host memory); key_idx (n device uint32) the key of each record.
+ * Every context must live on ctxs[0]'s device and have its key size; ctxs[0] leads the launch (its scratch holds the key
+ * table and the by-key sort, which run on `stream` before the kernel).  Results are those of one single-key call per
+ * key.  A record whose key index is >= nkeys is not processed: seal writes nothing, open reports status 0xffffffff with
+ * its output untouched (never a record under another key).  Up to a fifth of the CUs' records run on the split window
+ * kernels, up to one record per CU on the 16-lane window kernels (each workgroup on its record's key), larger batches
+ * on the batch kernels, whose workgroups take one key at a time and move between keys as their groups run out (DESIGN.md
+ * section 3, "Multi-key batches").  The context's (and the key table's) upload is skipped when the keys repeat.
+ */
+int ptls_mi355x_seal_batch_multikey(ptls_mi355x_aesgcm_context_t *const *ctxs, const void *static_ivs, size_t nkeys,
+                                    const ptls_mi355x_record_t *recs, const uint32_t *key_idx, size_t n,
+                                    const uint8_t *src, uint8_t *dst, const uint8_t *aad, void *stream);
+int ptls_mi355x_open_batch_multikey(ptls_mi355x_aesgcm_context_t *const *ctxs, const void *static_ivs, size_t nkeys,
+                                    const ptls_mi355x_record_t *recs, const uint32_t *key_idx, size_t n,
+                                    const uint8_t *src, uint8_t *dst, const uint8_t *aad, uint32_t *status, void *stream);
+
 /* ======================================================================================
  * 4. TLS 1.3 record framing in the batch.  The framing of picotls's
  *    record layer done by the kernel, so a send window / recv() window of records is ONE launch
@@ -353,14 +372,17 @@ void ptls_mi355x_record_layer_set_seq(ptls_mi355x_record_layer_t *rl, uint64_t s
 #define PTLS_MI355X_RECORD_LAYER_KEY_UPDATE 1
 int ptls_mi355x_record_layer_seal(ptls_mi355x_record_layer_t *rl, const ptls_mi355x_iovec_t *frags, size_t nfrags,
                                   uint8_t type, void *out, size_t capacity, size_t *outlen, size_t *nrecords);
-/* The send windows of several connections of one session in ONE launch: layers[l] seals frags[l][0..nfrags[l]) into
- * out[l] (capacity[l]) exactly as ptls_mi355x_record_layer_seal would, outlen[l] / nrecords[l] its results, each
- * layer's seq advanced.  The layers must share the key and IV bytes 4..11: rapido's connections of a session, whose
- * IVs differ by the connection id in bytes 0..3 (derive_connection_aead_iv, lib/rapido.c:123-133); the kernel applies
- * each record's difference (ptls_mi355x_tls_seal_records_multi).  Runs on layers[0]'s stream and staging; direct when
- * every fragment and output lies in a range registered with any of the layers.  0, or -1: a capacity or a layer with
- * another key or IV (nothing written, no seq advanced), or an engine error (as for ptls_mi355x_record_layer_seal: seq
- * stays past records whose launch was accepted). */
+/* The send windows of several connections -- of one session or of many -- in ONE launch: layers[l] seals
+ * frags[l][0..nfrags[l]) into out[l] (capacity[l]) exactly as ptls_mi355x_record_layer_seal would, outlen[l] /
+ * nrecords[l] its results, each layer's seq advanced.  Layers sharing the key and IV bytes 4..11 are the connections of
+ * one session, whose IVs differ by the connection id in bytes 0..3 (derive_connection_aead_iv, lib/rapido.c:123-133);
+ * the kernel applies each record's difference (ptls_mi355x_tls_seal_records_multi).  Layers of different sessions (a
+ * server's many connections, each session with its own traffic key, include/rapido.h:147) go into the same launch as
+ * a multi-key batch (ptls_mi355x_tls_seal_records_multikey): a session's key is the context of its first layer.  All
+ * layers must have one key size.  Runs on layers[0]'s stream and staging; direct when every fragment and output lies
+ * in a range registered with any of the layers.  0, or -1: a capacity or another key size (nothing written, no seq
+ * advanced), or an engine error (as for ptls_mi355x_record_layer_seal: seq stays past records whose launch was
+ * accepted). */
 int ptls_mi355x_record_layer_seal_multi(ptls_mi355x_record_layer_t *const *layers, size_t nlayers,
                                         const ptls_mi355x_iovec_t *const *frags, const size_t *nfrags, uint8_t type,
                                         void *const *out, const size_t *capacity, size_t *outlen, size_t *nrecords);
@@ -376,8 +398,8 @@ int ptls_mi355x_record_layer_open(ptls_mi355x_record_layer_t *rl, const void *in
 /* The receive windows of several connections of one session in ONE launch: layers[l] opens in[l][0..inlen[l]) into
  * out[l] (capacity[l]) exactly as ptls_mi355x_record_layer_open would; alerts[l] is what that call would have
  * returned (0, a TLS alert, or -1 for out[l] too small for its first record), consumed[l] / outlen[l] / nrecords[l]
- * its results.  Same session rule and stream as ptls_mi355x_record_layer_seal_multi.  0, or -1 (engine error: nothing
- * consumed, no seq advanced). */
+ * its results.  Layers of one or of many sessions, grouped and launched as in ptls_mi355x_record_layer_seal_multi, on
+ * the same stream.  0, or -1 (engine error: nothing consumed, no seq advanced). */
 int ptls_mi355x_record_layer_open_multi(ptls_mi355x_record_layer_t *const *layers, size_t nlayers, const void *const *in,
                                         const size_t *inlen, size_t *consumed, void *const *out, const size_t *capacity,
                                         size_t *outlen, size_t *nrecords, int *alerts);
@@ -481,10 +503,27 @@ int ptls_mi355x_prepare_copies(void);
  * `windows_per_launch` windows of up to `window_bytes` each (the wire or fragment bytes of one window), and the HIP
  * copy path (ptls_mi355x_prepare_copies).  A fresh layer's first window on each slot otherwise costs ~3 ms of setup
  * (DESIGN.md section 2); a connection calls this once, after creating its layers.  0, or -1 (windows outstanding, or
- * an allocation failed). */
+ * an allocation failed).  The staging's per-record space (descriptors, statuses, types, 128 B a record) is sized for
+ * windows of full-size records (16 KiB fragments, as rapido sends them); the descriptor arrays for the most records
+ * an open can parse (window_bytes / 5 + 1).  A window of many small records -- more than window_bytes / 16384 + 2 --
+ * still grows a slot's staging once, at its first such window (a one-time stall of ~1-3 ms). */
 int ptls_mi355x_record_layer_reserve(ptls_mi355x_record_layer_t *rl, size_t window_bytes, size_t windows_per_launch);
 /* zero-copy limit in bytes (default 4 MiB; 0 = always DMA copies); returns the previous value */
 size_t ptls_mi355x_record_layer_set_zero_copy_bytes(ptls_mi355x_record_layer_t *rl, size_t n);
+
+/*
+ * Multi-key framing (section 3's multi-key batches over section 4's records): the windows of many sessions in one launch,
+ * key_idx[i] selecting record i's key and IV, conn_ids[i] (may be NULL) its rapido connection id within that session.
+ * With PTLS_MI355X_OPEN_STOP_AT_FAILURE a connection is a (key, connection id) pair: consecutive records of one.
+ */
+int ptls_mi355x_tls_seal_records_multikey(ptls_mi355x_aesgcm_context_t *const *ctxs, const void *static_ivs, size_t nkeys,
+                                          const ptls_mi355x_tls_record_t *recs, const uint32_t *key_idx,
+                                          const uint32_t *conn_ids, size_t n, const uint8_t *src, uint8_t *dst,
+                                          void *stream);
+int ptls_mi355x_tls_open_records_multikey(ptls_mi355x_aesgcm_context_t *const *ctxs, const void *static_ivs, size_t nkeys,
+                                          const ptls_mi355x_tls_record_t *recs, const uint32_t *key_idx,
+                                          const uint32_t *conn_ids, size_t n, const uint8_t *src, uint8_t *dst,
+                                          uint32_t *status, uint8_t *types, int flags, void *stream);
 
 /* ---- tuning / introspection ---- */
 /* lanes per record used by the batch kernels (1, 2, 4 or 8; default 4); returns the previous value, or -1 */
@@ -537,12 +576,44 @@ uint32_t ptls_mi355x_set_work_ticket_origin(uint32_t origin);
 /* name of the kernel symbol a launch of n records with these parameters uses on the current device (framing:
  * the section-4 entry points) -- the same selection launch_batch makes (for profiling and reports) */
 const char *ptls_mi355x_kernel_name(int is_seal, size_t key_size, size_t n, int framing);
+/* the same for a multi-key launch (the ptls_mi355x_*_multikey entry points) */
+const char *ptls_mi355x_kernel_name_multikey(int is_seal, size_t key_size, size_t n, int framing);
 /* LDS table reads (ds_read_b128) per 16-byte block of the batch kernels' GHASH Horner multiply at k lanes per record:
  * 16 with the 8-bit latin tables (k = 4), 32 with the nibble tables; -1 for an invalid k
  * (for the LDS roofline in reports) */
 int ptls_mi355x_batch_ghash_reads(int k);
 /* last HIP error string seen by the engine ("" if none) */
 const char *ptls_mi355x_last_error(void);
+
+/* ---- fault attribution (rapido_amd/csrc/fault_journal.c) ---- */
+/*
+ * Registers an observer for the GPU's memory-fault events (hsa_amd_register_system_event_handler) and keeps a journal
+ * of the engine's last 256 device events: every launch (kernel, stream, grid, pointer arguments with their extents
+ * where known), every device allocation and free, every host registration, every device check.  On a fault the
+ * handler writes the faulting virtual address, the fault reasons and the journal (ranges holding the address marked)
+ * to stderr and appends it to `path` (NULL: stderr only).  It only observes: HIP's own handling of the fault (the
+ * sticky hipErrorIllegalAddress) is unchanged.  Call it before the first HIP call where possible.  Returns 0, or the
+ * HSA status of hsa_init / the registration (e.g. no GPU).  Calling it again only changes `path`.
+ */
+int ptls_mi355x_fault_journal_install(const char *path);
+int ptls_mi355x_fault_journal_installed(void);
+/* memory-fault events the handler has received */
+unsigned long ptls_mi355x_fault_journal_faults(void);
+/* writes the report the handler writes, for a fault at `va` (diagnostics: a report on demand, and its test) */
+void ptls_mi355x_fault_journal_report(uint64_t va, uint32_t reason_mask);
+/* records a device memory event over [p, p + len) in the journal (the engine's own allocations are recorded) */
+void ptls_mi355x_fault_journal_note(const char *what, const void *p, size_t len);
+
+/* ---- slot error accounting and test hooks ---- */
+/* engine errors the AEAD slot's do_decrypt failed closed on: the record was refused as a bad MAC (SIZE_MAX) and its
+ * output zeroed, the process kept running (aead_slot.c; do_encrypt has no error return and aborts) */
+unsigned long ptls_mi355x_slot_engine_errors(void);
+/* test hook: AEAD slot contexts set up while `on` get no engine context, so every engine call of theirs fails (the
+ * engine-error path without a GPU).  Returns the previous setting.  Not for production use. */
+int ptls_mi355x_test_slot_without_engine(int on);
+/* test hook: the next n single-record engine calls (the slot's encrypt / decrypt) fail as a GPU error would.  Returns
+ * the previous count.  Not for production use. */
+unsigned ptls_mi355x_test_inject_engine_errors(unsigned n);
 /*
  * Build provenance: the first 16 hex digits of SHA-256 over the library's sources (rapido_amd/csrc/ and this header,
  * in name order, each as "<name>\0<bytes>"), fixed when the library was built (rapido_amd/build.py).  Equal to

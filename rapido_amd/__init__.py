@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import weakref
 
 try:  # load torch's bundled HIP runtime first: same SONAME, so one runtime serves both
     import torch as _torch  # noqa: F401
@@ -77,7 +78,11 @@ EXPORTED_FUNCTIONS = (
     "ptls_mi355x_record_layer_flush", "ptls_mi355x_record_layer_set_coalesce", "ptls_mi355x_record_layer_launches",
     "ptls_mi355x_record_layer_cork",
     "ptls_mi355x_record_layer_set_direct_dma", "ptls_mi355x_tls_deliver_records", "ptls_mi355x_prepare_copies",
-    "ptls_mi355x_record_layer_reserve",
+    "ptls_mi355x_record_layer_reserve", "ptls_mi355x_fault_journal_install", "ptls_mi355x_fault_journal_installed",
+    "ptls_mi355x_fault_journal_faults", "ptls_mi355x_fault_journal_report", "ptls_mi355x_fault_journal_note",
+    "ptls_mi355x_slot_engine_errors", "ptls_mi355x_test_slot_without_engine", "ptls_mi355x_test_inject_engine_errors",
+    "ptls_mi355x_seal_batch_multikey", "ptls_mi355x_open_batch_multikey", "ptls_mi355x_tls_seal_records_multikey",
+    "ptls_mi355x_tls_open_records_multikey", "ptls_mi355x_kernel_name_multikey",
 )
 EXPORTED_OBJECTS = ("ptls_mi355x_aes128gcm", "ptls_mi355x_aes256gcm", "ptls_mi355x_aes128ctr",
                     "ptls_mi355x_aes256ctr", "ptls_mi355x_aes128ecb", "ptls_mi355x_aes256ecb")
@@ -226,8 +231,48 @@ def lib() -> C.CDLL:
         L.ptls_mi355x_tls_parse_records.argtypes = [vp, sz, u64, C.POINTER(u64), u64, vp, sz, C.POINTER(sz),
                                                     C.POINTER(sz)]
         L.ptls_mi355x_tls_parse_records.restype = C.c_int
+        if hasattr(L, "ptls_mi355x_fault_journal_install"):
+            L.ptls_mi355x_fault_journal_install.argtypes = [C.c_char_p]
+            L.ptls_mi355x_fault_journal_faults.restype = C.c_ulong
+            L.ptls_mi355x_fault_journal_report.argtypes = [u64, C.c_uint32]
+            L.ptls_mi355x_fault_journal_note.argtypes = [C.c_char_p, vp, sz]
+            L.ptls_mi355x_slot_engine_errors.restype = C.c_ulong
+            L.ptls_mi355x_test_slot_without_engine.argtypes = [C.c_int]
+            L.ptls_mi355x_test_inject_engine_errors.argtypes = [C.c_uint]
+            L.ptls_mi355x_test_inject_engine_errors.restype = C.c_uint
+        if hasattr(L, "ptls_mi355x_seal_batch_multikey"):
+            L.ptls_mi355x_seal_batch_multikey.argtypes = [vp, vp, sz, vp, vp, sz, vp, vp, vp, vp]
+            L.ptls_mi355x_open_batch_multikey.argtypes = [vp, vp, sz, vp, vp, sz, vp, vp, vp, vp, vp]
+            L.ptls_mi355x_tls_seal_records_multikey.argtypes = [vp, vp, sz, vp, vp, vp, sz, vp, vp, vp]
+            L.ptls_mi355x_tls_open_records_multikey.argtypes = [vp, vp, sz, vp, vp, vp, sz, vp, vp, vp, vp, C.c_int, vp]
+            L.ptls_mi355x_kernel_name_multikey.argtypes = [C.c_int, sz, sz, C.c_int]
+            L.ptls_mi355x_kernel_name_multikey.restype = C.c_char_p
+            global FAULT_JOURNAL_STATUS
+            if os.environ.get("RAPIDO_FAULT_JOURNAL", "1") != "0":
+                # before the first HIP call of the process where possible (tests/conftest.py sets the path)
+                path = os.environ.get("RAPIDO_FAULT_LOG")
+                FAULT_JOURNAL_STATUS = L.ptls_mi355x_fault_journal_install(path.encode() if path else None)
         _lib = L
     return _lib
+
+
+#: status of the fault journal's installation at load (0: the memory-fault observer is registered; else the HSA status,
+#: e.g. no GPU in this process; None: not attempted).  See include/ptls_mi355x.h "fault attribution".
+FAULT_JOURNAL_STATUS = None
+
+
+def fault_journal_report(va: int, reason_mask: int = 1) -> None:
+    """Writes the fault journal's report for a fault at `va` (what the memory-fault handler writes; diagnostics)."""
+    lib().ptls_mi355x_fault_journal_report(va, reason_mask)
+
+
+def fault_journal_note(what: bytes, ptr: int, length: int) -> None:
+    lib().ptls_mi355x_fault_journal_note(what, ptr, length)
+
+
+def fault_journal_faults() -> int:
+    """Memory-fault events the journal's handler has received in this process."""
+    return int(lib().ptls_mi355x_fault_journal_faults())
 
 
 def last_error() -> str:
@@ -241,8 +286,11 @@ def device_check() -> None:
         raise RuntimeError("device check: " + last_error())
 
 
-#: errors raised by close() inside a finalizer (__del__ cannot raise): reported, and collected for the test suite
+#: errors raised by close() inside a finalizer (__del__ cannot raise): reported, and collected for the test suite (the
+#: most recent FINALIZER_ERRORS_KEEP; FINALIZER_ERROR_COUNT counts them all)
 FINALIZER_ERRORS: list = []
+FINALIZER_ERRORS_KEEP = 256
+FINALIZER_ERROR_COUNT = 0
 
 
 def _finalize(obj, method: str = "close") -> None:
@@ -251,7 +299,11 @@ def _finalize(obj, method: str = "close") -> None:
         getattr(obj, method)()
     except Exception as e:  # noqa: BLE001 - __del__ must not raise; report instead
         msg = f"{type(obj).__name__}.__del__: {e}"
+        global FINALIZER_ERROR_COUNT
+        FINALIZER_ERROR_COUNT += 1
         FINALIZER_ERRORS.append(msg)
+        if len(FINALIZER_ERRORS) > FINALIZER_ERRORS_KEEP:  # a long-running process keeps only the recent ones
+            del FINALIZER_ERRORS[: len(FINALIZER_ERRORS) - FINALIZER_ERRORS_KEEP]
         import sys
         print("rapido_amd: " + msg, file=sys.stderr)
 
@@ -389,8 +441,13 @@ def cipher_new(name: str, is_enc: bool, key: bytes) -> Cipher:
 
 
 # ------------------------------------------------------------------ direct + batch API -----
+#: every Engine not yet closed (tests/conftest.py closes the ones a test leaves open, before its device check)
+LIVE_ENGINES: "weakref.WeakSet" = weakref.WeakSet()
+
+
 class Engine:
-    """ptls_mi355x_aesgcm_context_t: the device-resident key image + batch launches."""
+    """ptls_mi355x_aesgcm_context_t: the device-resident key image + batch launches.  close() (or a with-block) releases
+    it deterministically; the finalizer is the fallback."""
 
     def __init__(self, key: bytes, capacity: int = 16384, device: int | None = None):
         """device: the HIP ordinal to create the context on (ptls_mi355x_aesgcm_new_on); None: the current device."""
@@ -404,13 +461,23 @@ class Engine:
             self.handle = lib().ptls_mi355x_aesgcm_new_on(device, _cbuf(key), len(key), capacity)
         if not self.handle:
             raise RuntimeError("ptls_mi355x_aesgcm_new failed: " + last_error())
+        LIVE_ENGINES.add(self)
+
+    def __enter__(self) -> "Engine":
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.close()
 
     def close(self) -> None:
         """ptls_mi355x_aesgcm_release: waits for the context's launches, clears and frees its key image; raises if
         that met an error (an asynchronous fault of earlier GPU work surfaces at its synchronisation)."""
         if self.handle:
             h, self.handle = self.handle, None
-            if lib().ptls_mi355x_aesgcm_release(h):
+            L = lib()
+            if not hasattr(L, "ptls_mi355x_aesgcm_release"):  # older builds (A/B timing runs): free reports nothing
+                L.ptls_mi355x_aesgcm_free(h)
+            elif L.ptls_mi355x_aesgcm_release(h):
                 raise RuntimeError("ptls_mi355x_aesgcm_release: " + last_error())
 
     def __del__(self):
@@ -485,6 +552,51 @@ class Engine:
         if lib().ptls_mi355x_tls_open_records_ex(self.handle, _cbuf(static_iv), recs_ptr, conn_ptr or None, n,
                                                  src_ptr, dst_ptr, status_ptr, types_ptr, flags, stream or None):
             raise RuntimeError("tls_open_records failed: " + last_error())
+
+
+# ------------------------------------------------------------------ multi-key batches -----
+# The records of many sessions in one launch (include/ptls_mi355x.h, "Multi-key batches"): engines[k] and static_ivs[k]
+# are key k's context and IV, key_idx_ptr a device uint32 array of each record's key.
+class MultiKey:
+    """The contexts and IVs of a multi-key launch, marshalled once (a server re-sends its sessions' batches)."""
+
+    def __init__(self, engines, static_ivs):
+        if len(engines) != len(static_ivs) or not engines:
+            raise ValueError("one static IV per engine, at least one")
+        self.engines = list(engines)  # kept alive while the launches may run
+        self.ctxs = (C.c_void_p * len(engines))(*[e.handle for e in engines])
+        self.ivs = C.create_string_buffer(b"".join(bytes(iv) for iv in static_ivs), 12 * len(engines))
+        if any(len(iv) != 12 for iv in static_ivs):
+            raise ValueError("static IVs are 12 bytes")
+
+    def __len__(self) -> int:
+        return len(self.engines)
+
+    def seal_batch(self, recs_ptr, key_idx_ptr, n, src_ptr, dst_ptr, aad_ptr, stream: int = 0) -> None:
+        if lib().ptls_mi355x_seal_batch_multikey(self.ctxs, self.ivs, len(self), recs_ptr, key_idx_ptr, n, src_ptr,
+                                                 dst_ptr, aad_ptr, stream or None):
+            raise RuntimeError("seal_batch_multikey failed: " + last_error())
+
+    def open_batch(self, recs_ptr, key_idx_ptr, n, src_ptr, dst_ptr, aad_ptr, status_ptr, stream: int = 0) -> None:
+        if lib().ptls_mi355x_open_batch_multikey(self.ctxs, self.ivs, len(self), recs_ptr, key_idx_ptr, n, src_ptr,
+                                                 dst_ptr, aad_ptr, status_ptr, stream or None):
+            raise RuntimeError("open_batch_multikey failed: " + last_error())
+
+    def tls_seal_records(self, recs_ptr, key_idx_ptr, n, src_ptr, dst_ptr, stream: int = 0, conn_ptr: int = 0) -> None:
+        if lib().ptls_mi355x_tls_seal_records_multikey(self.ctxs, self.ivs, len(self), recs_ptr, key_idx_ptr,
+                                                       conn_ptr or None, n, src_ptr, dst_ptr, stream or None):
+            raise RuntimeError("tls_seal_records_multikey failed: " + last_error())
+
+    def tls_open_records(self, recs_ptr, key_idx_ptr, n, src_ptr, dst_ptr, status_ptr, types_ptr, stream: int = 0,
+                         conn_ptr: int = 0, flags: int = 0) -> None:
+        if lib().ptls_mi355x_tls_open_records_multikey(self.ctxs, self.ivs, len(self), recs_ptr, key_idx_ptr,
+                                                       conn_ptr or None, n, src_ptr, dst_ptr, status_ptr, types_ptr,
+                                                       flags, stream or None):
+            raise RuntimeError("tls_open_records_multikey failed: " + last_error())
+
+
+def kernel_name_multikey(is_seal: bool, key_size: int, n: int, framing: bool) -> str:
+    return lib().ptls_mi355x_kernel_name_multikey(int(is_seal), key_size, n, int(framing)).decode()
 
 
 def prepare_copies() -> None:

@@ -1,7 +1,8 @@
 """Builds the MI355X engine library in-tree (no JIT cache, so the .so travels with the repo).
 
     rapido_amd/_lib/libptls_mi355x.so  <- csrc/gcm_engine.hip (hipcc, --offload-arch=gfx950)
-                                         + csrc/aead_slot.c, csrc/tls_records.c, csrc/record_layer.c (host C, gcc)
+                                         + csrc/aead_slot.c, csrc/tls_records.c, csrc/record_layer.c,
+                                           csrc/fault_journal.c (host C, gcc; the last against libhsa-runtime64)
                                          + a generated build-id object (ptls_mi355x_build_id)
     tests/cpp/_build/libkernel_model.so <- tests/cpp/kernel_model.cpp (host clang++, test only)
     tests/cpp/_build/libguard_alloc.so  <- tests/cpp/guard_alloc.c (gcc against libamdhip64: guard-paged device
@@ -76,7 +77,7 @@ def _run(cmd, verbose):
     return r
 
 
-C_SRCS = [os.path.join(CSRC, f) for f in ("aead_slot.c", "tls_records.c", "record_layer.c")]
+C_SRCS = [os.path.join(CSRC, f) for f in ("aead_slot.c", "tls_records.c", "record_layer.c", "fault_journal.c")]
 ROCM_INCLUDE = "/opt/rocm/include"
 C_OBJS = [os.path.join(OBJDIR, os.path.basename(f)[:-2] + ".o") for f in C_SRCS]
 C_FLAGS = ["-std=gnu99", "-O2", "-g", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter", "-D__HIP_PLATFORM_AMD__",
@@ -114,7 +115,8 @@ def build_engine(verbose: bool = False, force: bool = False) -> str:
     if force or _newer(LIB, [hip_obj] + C_OBJS):
         if os.path.exists(STAMP):
             os.remove(STAMP)
-        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, hip_obj, bid_obj] + C_OBJS, verbose)
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, hip_obj, bid_obj] + C_OBJS +
+             ["-L/opt/rocm/lib", "-lhsa-runtime64"], verbose)
         with open(STAMP, "w") as f:
             f.write(bid + "\n")
     return LIB

@@ -11,10 +11,14 @@
  *   ecb cipher            (NULL in fusion, lib/fusion.c:990) -> struct mi355x_ecb (t/picotls.c:266-307)
  * Every AES/GHASH computation is done by the HIP engine (gcm_engine.hip); this file only
  * keeps per-context state (static IV, streaming buffer) and maps picotls' arguments onto
- * the engine's record descriptor.  A GPU failure inside a void slot entry point aborts with
- * a message: the slot ABI has no error return for do_encrypt, and silently emitting wrong
- * ciphertext is not an option.
+ * the engine's record descriptor.  A GPU failure inside a void slot entry point (do_encrypt,
+ * the streaming trio, the ciphers) aborts with a message: those ABI entries have no error
+ * return, and silently emitting wrong ciphertext is not an option.  do_decrypt has one: an
+ * engine error there fails closed -- the output is zeroed and SIZE_MAX returned, which picotls
+ * turns into PTLS_ALERT_BAD_RECORD_MAC (lib/picotls.c:645-654) -- so one GPU fault ends the
+ * connection it hit, not the process serving every connection.
  */
+#include <stdatomic.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -40,6 +44,21 @@ static void engine_abort(const char *what)
 {
     fprintf(stderr, "ptls_mi355x: %s failed: %s\n", what, ptls_mi355x_last_error());
     abort();
+}
+
+/* engine errors the slot's decrypt failed closed on (ptls_mi355x_slot_engine_errors) */
+static atomic_ulong g_slot_errors;
+/* test hook (ptls_mi355x_test_slot_without_engine): slot contexts set up while it is on get no engine context */
+static atomic_int g_test_no_engine;
+
+unsigned long ptls_mi355x_slot_engine_errors(void)
+{
+    return atomic_load(&g_slot_errors);
+}
+
+int ptls_mi355x_test_slot_without_engine(int on)
+{
+    return atomic_exchange(&g_test_no_engine, on != 0);
 }
 
 /* ------------------------------------------------------------------------ AES-CTR ------ */
@@ -233,9 +252,22 @@ static size_t aead_do_decrypt(ptls_aead_context_t *_ctx, void *output, const voi
         return SIZE_MAX;
     size_t enclen = inlen - MI355X_TAG_SIZE;
     build_nonce(ctx, seq, nonce);
-    int ok = ptls_mi355x_aesgcm_decrypt(ctx->engine, output, input, enclen, nonce, aad, aadlen, (const uint8_t *)input + enclen);
-    if (ok < 0)
-        engine_abort("open");
+    int ok = ctx->engine != NULL ? ptls_mi355x_aesgcm_decrypt(ctx->engine, output, input, enclen, nonce, aad, aadlen,
+                                                              (const uint8_t *)input + enclen)
+                                 : -1;
+    if (ok < 0) {
+        /*
+         * Fail closed: nothing of the record is released (the output is zeroed, in place or not) and the record is
+         * refused as a bad MAC.  picotls raises PTLS_ALERT_BAD_RECORD_MAC for it and does not advance the receive
+         * sequence (lib/picotls.c:645-654, include/picotls.h:1354-1358); the error is printed and counted.
+         */
+        if (enclen != 0)
+            memset(output, 0, enclen);
+        atomic_fetch_add(&g_slot_errors, 1);
+        fprintf(stderr, "ptls_mi355x: open failed closed (record refused as a bad MAC): %s\n",
+                ctx->engine != NULL ? ptls_mi355x_last_error() : "no engine context");
+        return SIZE_MAX;
+    }
     return ok ? enclen : SIZE_MAX;
 }
 
@@ -308,6 +340,10 @@ static int aesgcm_setup(ptls_aead_context_t *_ctx, int is_enc, const void *key, 
     ctx->s_buf = ctx->s_aad = NULL;
     ctx->s_len = ctx->s_cap = ctx->s_aadlen = ctx->s_aadcap = 0;
 
+    if (atomic_load(&g_test_no_engine)) { /* test hook: a context whose every engine call fails */
+        ctx->engine = NULL;
+        return 0;
+    }
     if ((ctx->engine = ptls_mi355x_aesgcm_new(key, key_size, 1500)) == NULL)
         return PTLS_ERROR_LIBRARY;
     return 0;

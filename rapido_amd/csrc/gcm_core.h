@@ -1950,6 +1950,39 @@ GCM_HD void fill_lds(uint8_t *lds, const uint32_t *t0, const KeyImage *ki, uint3
     }
 }
 
+/*
+ * fill_lds split for the multi-key batch kernels (the GH8 layout, Layout<4>): the key-independent AES image once per
+ * workgroup, and a key's GHASH tables (the GH8 table of H^4, the nibble tables of H^4..H^1) at every key change.
+ */
+GCM_HD void fill_lds_aes(uint8_t *lds, const uint32_t *t0, uint32_t K, uint32_t tid, uint32_t nthr)
+{
+    const uint32_t aes_base = 0x10000u, aes_bytes = 0x10000u;
+    (void)K;
+    for (uint32_t i = tid; i < aes_bytes / 16; i += nthr) {
+        const uint32_t off = i * 16, x = (off >> 8) & 0xffu;
+        uint32_t v = t0[x];
+        if (off & 128u)
+            v = rotl32(v, 8); /* image A: T0 | T1 */
+        *(u32x4 *)(lds + aes_base + off) = u32x4{v, v, v, v};
+    }
+}
+
+GCM_HD void fill_lds_key(uint8_t *lds, const KeyImage *ki, uint32_t tid, uint32_t nthr)
+{
+    for (uint32_t i = tid; i < GH8_BYTES / 16u; i += nthr) {
+        const uint32_t e = i >> 4, p = i & 15u;
+        const u32x4 lo = *(const u32x4 *)ki->gh[3][2u * p][e & 15u];
+        const u32x4 hi = *(const u32x4 *)ki->gh[3][2u * p + 1u][e >> 4];
+        *(u32x4 *)(lds + 16u * i) = lo ^ hi;
+    }
+    const uint32_t gh_base = 0x20000u, nvec = 4u * (GH_TABLE_BYTES / 16);
+    for (uint32_t i = tid; i < nvec; i += nthr) {
+        const uint32_t slot = i / (GH_TABLE_BYTES / 16), within = i % (GH_TABLE_BYTES / 16);
+        const u32x4 *srcv = (const u32x4 *)ki->gh[3u - slot];
+        *(u32x4 *)(lds + gh_base + slot * GH_TABLE_BYTES + within * 16) = srcv[within];
+    }
+}
+
 /* ------------------------------------------------------------------ window kernels --------- */
 
 /*

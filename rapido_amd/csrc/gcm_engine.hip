@@ -50,7 +50,11 @@ __device__ uint64_t g_win_times[32];
 #define SPLIT_STAMP_LAST(i) ((void)0)
 #endif
 #include "gcm_core.h"
+#include "fault_journal.h"
 #include "../../include/ptls_mi355x.h"
+
+/* a device memory event in the fault journal (fault_journal.c) */
+#define JNOTE(what, p, len) ptls_mi355x_fault_journal_note(what, (const void *)(p), (size_t)(len))
 
 using namespace mi355x;
 
@@ -179,29 +183,54 @@ static_assert(sizeof(TlsRecord) == sizeof(ptls_mi355x_tls_record_t), "descriptor
 #ifndef GCM_FAST_STEP
 #define GCM_FAST_STEP 1 /* batch kernels: interior steps on lane_walk's fast path (scalar branch, no per-lane flags) */
 #endif
-template <int NR, int K, bool SEAL, bool FRAME>
+/*
+ * Multi-key batches (MK): one key of the launch (ptls_mi355x_seal_batch_multikey).  The prep kernels (mi355x_mk_*) fill
+ * `first` / `end` -- the key's records are order[first .. end), order sorted by key -- and zero the key's group counter.
+ */
+struct MkKey {
+    const KeyImage *ki;
+    uint32_t iv0, iv1, iv2; /* the key's static IV (LE dwords) */
+    uint32_t first, end, pad_;
+};
+static_assert(sizeof(MkKey) == 32, "multi-key table entry");
+constexpr uint32_t MK_NONE = 0xffffffffu;
+
+/* the launch's key table and the workgroups' phase state (MK kernels) */
+struct MkLaunch {
+    const MkKey *keys;
+    uint32_t nkeys;
+    uint32_t *ctr;    /* per key: record groups handed out (zeroed by the prep) */
+    uint32_t *wg_key; /* per workgroup: the key of its current phase (the workgroup's broadcast slot) */
+};
+
+template <int NR, int K, bool SEAL, bool FRAME, bool MK = false>
 __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2,
                                                const void *__restrict__ descs, const uint32_t *__restrict__ order,
                                                uint32_t nrecs, const uint8_t *src, uint8_t *dst,
                                                const uint8_t *__restrict__ aad, uint32_t *__restrict__ status,
                                                uint8_t *__restrict__ types, uint32_t *__restrict__ work,
-                                               uint32_t work_base, const uint32_t *__restrict__ conn)
+                                               uint32_t work_base, const uint32_t *__restrict__ conn,
+                                               MkLaunch mk = MkLaunch{nullptr, 0u, nullptr, nullptr})
 {
     static_assert(K <= MAX_KERNEL_K, "LDS holds at most MAX_KERNEL_K GHASH tables");
+    static_assert(!MK || Layout<K>::gh8, "multi-key batches run the GH8 layout (K = 4)");
     __shared__ __attribute__((aligned(16))) uint8_t lds[Layout<K>::total];
     constexpr uint32_t R = 64 / K; /* records per wave step */
     const Record *__restrict__ recs = (const Record *)descs;
     const TlsRecord *__restrict__ trecs = (const TlsRecord *)descs;
 
-    fill_lds(lds, c_tabs.t0, ki, K, threadIdx.x, blockDim.x);
-
     uint32_t rk[4 * (NR + 1)], kr[4 * (NR + 1)];
+    if constexpr (!MK) {
+        fill_lds(lds, c_tabs.t0, ki, K, threadIdx.x, blockDim.x);
 #pragma unroll
-    for (int i = 0; i < 4 * (NR + 1); ++i) {
-        rk[i] = ki->rk[i];
-        kr[i] = rotl32(rk[i], 16); /* GH8 layout: the round keys of aes_round_tt2k_asm (wave-uniform) */
+        for (int i = 0; i < 4 * (NR + 1); ++i) {
+            rk[i] = ki->rk[i];
+            kr[i] = rotl32(rk[i], 16); /* GH8 layout: the round keys of aes_round_tt2k_asm (wave-uniform) */
+        }
+        __syncthreads();
+    } else {
+        fill_lds_aes(lds, c_tabs.t0, K, threadIdx.x, blockDim.x); /* the key-independent AES image, once */
     }
-    __syncthreads();
 
     const uint32_t lane = threadIdx.x & 63u;
 #if GCM_LANE_MAJOR
@@ -238,29 +267,8 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
         __builtin_amdgcn_s_sleep(127);
 #endif
 
-    /*
-     * Record groups (64/K records) are handed out dynamically: one returning atomic per group
-     * (MI355X_MICROARCH.md "dequeue": ~1 us under load, against ~100 us of work per group).
-     * With `order` sorted by length (ptls_mi355x_order_by_length) this is longest-first
-     * scheduling, and each group holds records of similar length.
-     */
-#if GCM_STATIC_GROUPS /* measurement builds: group k of wave w is w + k * (waves in the grid), no atomic */
-    const uint32_t wave_id = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), nwaves = gridDim.x * (blockDim.x >> 6);
-    for (uint32_t gs = wave_id;; gs += nwaves) {
-        const uint32_t g = __builtin_amdgcn_readfirstlane(gs);
-        (void)work;
-        (void)work_base;
-#else
-    for (;;) {
-        uint32_t g = 0;
-        if (lane == 0)
-            g = atomicAdd(work, 1u) - work_base; /* tickets of this launch start at work_base (mod 2^32) */
-        g = (uint32_t)__shfl((int)g, 0, 64);
-#endif
-        if (g >= ngroups)
-            break;
-        const uint32_t idx = g * R + slot;
-        const bool in_batch = idx < nrecs;
+    /* one record group: lane (j, slot) walks record order[idx] (idx itself without an order) if in_batch */
+    auto run_group = [&](uint32_t idx, bool in_batch, uint32_t iv0, uint32_t iv1, uint32_t iv2) {
         const uint32_t r = in_batch ? (order ? order[idx] : idx) : 0u;
         Record rec = {0, 0, 0, 0, 0, 0};
         uint32_t ctype = 0u;
@@ -396,6 +404,102 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
                 status[r] = found;
                 types[r] = (uint8_t)ty;
             }
+        }
+    };
+
+    if constexpr (!MK) {
+    /*
+     * Record groups (64/K records) are handed out dynamically: one returning atomic per group
+     * (MI355X_MICROARCH.md "dequeue": ~1 us under load, against ~100 us of work per group).
+     * With `order` sorted by length (ptls_mi355x_order_by_length) this is longest-first
+     * scheduling, and each group holds records of similar length.
+     */
+#if GCM_STATIC_GROUPS /* measurement builds: group k of wave w is w + k * (waves in the grid), no atomic */
+    const uint32_t wave_id = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), nwaves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t gs = wave_id;; gs += nwaves) {
+        const uint32_t g = __builtin_amdgcn_readfirstlane(gs);
+        (void)work;
+        (void)work_base;
+#else
+    for (;;) {
+        uint32_t g = 0;
+        if (lane == 0)
+            g = atomicAdd(work, 1u) - work_base; /* tickets of this launch start at work_base (mod 2^32) */
+        g = (uint32_t)__shfl((int)g, 0, 64);
+#endif
+        if (g >= ngroups)
+            break;
+        const uint32_t idx = g * R + slot;
+        run_group(idx, idx < nrecs, iv0, iv1, iv2);
+    }
+    } else {
+        /*
+         * Multi-key phases.  The LDS holds one key's GHASH tables, shared by the workgroup's 16 waves, so a workgroup
+         * works on one key at a time: its waves take that key's record groups from the key's counter, exactly as the
+         * single-key kernels do from theirs, and when the key has none left the workgroup meets at a barrier, wave 0
+         * picks the next key with groups left (starting from where this workgroup is, so the workgroups spread over the
+         * keys), and the tables are refilled only if the key changed.  Barriers happen only at key changes: with 64
+         * keys over 256 CUs a workgroup sees a handful.  The records of key k are order[first_k .. first_k + count_k).
+         */
+        uint32_t cur = MK_NONE, kk = (uint32_t)(((uint64_t)blockIdx.x * mk.nkeys) / gridDim.x);
+        for (;;) {
+            if (threadIdx.x < 64u) {
+                uint32_t pick = MK_NONE;
+                for (uint32_t b = 0; b < mk.nkeys && pick == MK_NONE; b += 64u) {
+                    const uint32_t t = b + lane;
+                    bool left = false;
+                    uint32_t kx = 0u;
+                    if (t < mk.nkeys) {
+                        kx = kk + t < mk.nkeys ? kk + t : kk + t - mk.nkeys;
+                        const uint32_t ng = (mk.keys[kx].end - mk.keys[kx].first + R - 1u) / R;
+                        left = __hip_atomic_load(mk.ctr + kx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ng;
+                    }
+                    const uint64_t m = __ballot(left);
+                    if (m != 0ull)
+                        pick = (uint32_t)__shfl((int)kx, (int)__builtin_ctzll(m), 64);
+                }
+                if (lane == 0u)
+                    __hip_atomic_store(mk.wg_key + blockIdx.x, pick, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __threadfence(); /* the pick is in L2 before the barrier: the other waves read it there (agent scope) */
+            __syncthreads();
+            const uint32_t k = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(mk.wg_key + blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            if (k == MK_NONE)
+                break; /* uniform over the workgroup */
+            /* the key's fields are wave-uniform: SGPRs, as the single-key kernels' arguments are (the round keys must be,
+             * for the asm rounds) */
+            const MkKey *kp = mk.keys + k;
+            const KeyImage *kki = (const KeyImage *)(uintptr_t)(((uint64_t)__builtin_amdgcn_readfirstlane(
+                                                                     (uint32_t)((uintptr_t)kp->ki >> 32)) << 32) |
+                                                                 __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)kp->ki));
+            const uint32_t kfirst = __builtin_amdgcn_readfirstlane(kp->first),
+                           count = __builtin_amdgcn_readfirstlane(kp->end) - kfirst;
+            const uint32_t kiv0 = __builtin_amdgcn_readfirstlane(kp->iv0), kiv1 = __builtin_amdgcn_readfirstlane(kp->iv1),
+                           kiv2 = __builtin_amdgcn_readfirstlane(kp->iv2);
+            if (k != cur) { /* every wave is past the previous phase (the barrier at its end): the LDS is free */
+                fill_lds_key(lds, kki, threadIdx.x, blockDim.x);
+                cur = k;
+            }
+#pragma unroll
+            for (int i = 0; i < 4 * (NR + 1); ++i) {
+                rk[i] = __builtin_amdgcn_readfirstlane(kki->rk[i]);
+                kr[i] = rotl32(rk[i], 16);
+            }
+            __syncthreads();
+            const uint32_t ng = (count + R - 1u) / R;
+            for (;;) {
+                uint32_t g = 0;
+                if (lane == 0)
+                    g = atomicAdd(mk.ctr + k, 1u);
+                g = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)g, 0, 64));
+                if (g >= ng)
+                    break;
+                const uint32_t pos = g * R + slot;
+                run_group(kfirst + pos, pos < count, kiv0, kiv1, kiv2);
+            }
+            kk = k;
+            __syncthreads(); /* every wave is done with this key's tables */
         }
     }
 }
@@ -942,6 +1046,40 @@ MI355X_GCM_KERNEL_F(mi355x_tls_seal_aes256_k4, 14, 4, true, true)
 MI355X_GCM_KERNEL_F(mi355x_tls_open_aes128_k4, 10, 4, false, true)
 MI355X_GCM_KERNEL_F(mi355x_tls_open_aes256_k4, 14, 4, false, true)
 
+/* multi-key batches (K = 4, GH8): the records of many keys in one launch, `order` sorted by key (gcm_batch_body MK) */
+#define MI355X_GCM_KERNEL_MK(NAME, NR, SEAL, FRAME)                                                                    \
+    extern "C" __global__ __launch_bounds__(WG_THREADS) void NAME(                                                     \
+        const MkKey *__restrict__ keys, uint32_t nkeys, uint32_t *__restrict__ ctr, uint32_t *__restrict__ wg_key,     \
+        const void *__restrict__ descs, const uint32_t *__restrict__ order, uint32_t nrecs, const uint8_t *src,        \
+        uint8_t *dst, const uint8_t *__restrict__ aad, uint32_t *__restrict__ st, uint8_t *__restrict__ types,         \
+        const uint32_t *__restrict__ conn)                                                                             \
+    {                                                                                                                  \
+        gcm_batch_body<NR, 4, SEAL, FRAME, true>(nullptr, 0u, 0u, 0u, descs, order, nrecs, src, dst, aad, st, types,   \
+                                                 nullptr, 0u, conn, MkLaunch{keys, nkeys, ctr, wg_key});               \
+    }
+MI355X_GCM_KERNEL_MK(mi355x_gcm_seal_aes128_k4_mk, 10, true, false)
+MI355X_GCM_KERNEL_MK(mi355x_gcm_seal_aes256_k4_mk, 14, true, false)
+MI355X_GCM_KERNEL_MK(mi355x_gcm_open_aes128_k4_mk, 10, false, false)
+MI355X_GCM_KERNEL_MK(mi355x_gcm_open_aes256_k4_mk, 14, false, false)
+MI355X_GCM_KERNEL_MK(mi355x_tls_seal_aes128_k4_mk, 10, true, true)
+MI355X_GCM_KERNEL_MK(mi355x_tls_seal_aes256_k4_mk, 14, true, true)
+MI355X_GCM_KERNEL_MK(mi355x_tls_open_aes128_k4_mk, 10, false, true)
+MI355X_GCM_KERNEL_MK(mi355x_tls_open_aes256_k4_mk, 14, false, true)
+
+/*
+ * A multi-key record whose key index is out of range is not processed: seal writes nothing, open reports it as failing
+ * (status 0xffffffff, type 0) with its output untouched -- never a record under another session's key.
+ */
+template <bool FRAME>
+__device__ __forceinline__ void mk_reject(uint32_t r, uint32_t *__restrict__ st, uint8_t *__restrict__ types)
+{
+    if (st != nullptr) {
+        st[r] = 0xffffffffu;
+        if (FRAME && types != nullptr)
+            types[r] = 0u;
+    }
+}
+
 #define MI355X_WIN_KERNEL(NAME, NR, SEAL, FRAME, THREADS, KW)                                                              \
     extern "C" __global__ __launch_bounds__(THREADS) void NAME(                                                        \
         const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2, const void *__restrict__ descs,     \
@@ -994,6 +1132,35 @@ MI355X_WIN16_KERNEL(mi355x_gcm_win16_seal_aes256, 14, true, false)
 MI355X_WIN16_KERNEL(mi355x_gcm_win16_open_aes128, 10, false, false)
 MI355X_WIN16_KERNEL(mi355x_gcm_win16_open_aes256, 14, false, false)
 
+/* multi-key 16-lane kernels: one record per workgroup (grid = records), its key from its key index */
+#define MI355X_WIN16_KERNEL_MK(NAME, NR, SEAL, FRAME)                                                                  \
+    extern "C" __global__ __launch_bounds__(576) void NAME(                                                            \
+        const MkKey *__restrict__ keys, uint32_t nkeys, const uint32_t *__restrict__ key_idx,                          \
+        const void *__restrict__ descs, uint32_t nrecs, const uint8_t *src, uint8_t *dst,                              \
+        const uint8_t *__restrict__ aad, uint32_t *__restrict__ st, uint8_t *__restrict__ types,                       \
+        const uint32_t *__restrict__ conn, const u32x4 *__restrict__ win_aes)                                          \
+    {                                                                                                                  \
+        const uint32_t r = blockIdx.x, k = r < nrecs ? key_idx[r] : 0u;                                                \
+        if (r >= nrecs)                                                                                                \
+            return;                                                                                                    \
+        if (k >= nkeys) {                                                                                              \
+            if (!SEAL && threadIdx.x == 0u)                                                                            \
+                mk_reject<FRAME>(r, st, types);                                                                        \
+            return;                                                                                                    \
+        }                                                                                                              \
+        const MkKey key = keys[k];                                                                                     \
+        window_body<NR, SEAL, FRAME, 576, 16, 32, LayoutWin16>(key.ki, key.iv0, key.iv1, key.iv2, descs, nrecs, src,   \
+                                                               dst, aad, st, types, conn, win_aes);                    \
+    }
+MI355X_WIN16_KERNEL_MK(mi355x_tls_win16_seal_aes128_mk, 10, true, true)
+MI355X_WIN16_KERNEL_MK(mi355x_tls_win16_seal_aes256_mk, 14, true, true)
+MI355X_WIN16_KERNEL_MK(mi355x_tls_win16_open_aes128_mk, 10, false, true)
+MI355X_WIN16_KERNEL_MK(mi355x_tls_win16_open_aes256_mk, 14, false, true)
+MI355X_WIN16_KERNEL_MK(mi355x_gcm_win16_seal_aes128_mk, 10, true, false)
+MI355X_WIN16_KERNEL_MK(mi355x_gcm_win16_seal_aes256_mk, 14, true, false)
+MI355X_WIN16_KERNEL_MK(mi355x_gcm_win16_open_aes128_mk, 10, false, false)
+MI355X_WIN16_KERNEL_MK(mi355x_gcm_win16_open_aes256_mk, 14, false, false)
+
 /*
  * Split window kernels (split_body): SPLIT_MAXRUN 128-thread workgroups per record, each walking one run of 8
  * segments on its own CU; partials and arrival tickets in the context's split buffer.
@@ -1017,6 +1184,37 @@ MI355X_SPLIT_KERNEL(mi355x_gcm_wins_seal_aes128, 10, true, false)
 MI355X_SPLIT_KERNEL(mi355x_gcm_wins_seal_aes256, 14, true, false)
 MI355X_SPLIT_KERNEL(mi355x_gcm_wins_open_aes128, 10, false, false)
 MI355X_SPLIT_KERNEL(mi355x_gcm_wins_open_aes256, 14, false, false)
+
+/* multi-key split kernels: each record's key from its key index (a workgroup walks one run of one record) */
+#define MI355X_SPLIT_KERNEL_MK(NAME, NR, SEAL, FRAME)                                                                  \
+    extern "C" __global__ __launch_bounds__(SPLIT_THREADS) void NAME(                                                  \
+        const MkKey *__restrict__ keys, uint32_t nkeys, const uint32_t *__restrict__ key_idx,                          \
+        const void *__restrict__ descs, uint32_t nrecs, const uint8_t *src, uint8_t *dst,                              \
+        const uint8_t *__restrict__ aad, uint32_t *__restrict__ st, uint8_t *__restrict__ types,                       \
+        const uint32_t *__restrict__ conn, const u32x4 *__restrict__ win_aes, u32x4 *__restrict__ partials,             \
+        uint32_t *__restrict__ tickets)                                                                                \
+    {                                                                                                                  \
+        __shared__ __attribute__((aligned(16))) uint8_t lds[LayoutSplit::bytes];                                       \
+        const uint32_t r = blockIdx.x / SPLIT_MAXRUN, k = r < nrecs ? key_idx[r] : 0u;                                 \
+        if (r >= nrecs)                                                                                                \
+            return;                                                                                                    \
+        if (k >= nkeys) {                                                                                              \
+            if (!SEAL && blockIdx.x % SPLIT_MAXRUN == 0u && threadIdx.x == 0u)                                         \
+                mk_reject<FRAME>(r, st, types);                                                                        \
+            return;                                                                                                    \
+        }                                                                                                              \
+        const MkKey key = keys[k];                                                                                     \
+        split_body<NR, SEAL, FRAME>(key.ki, key.iv0, key.iv1, key.iv2, descs, nrecs, src, dst, aad, st, types, conn,   \
+                                    win_aes, partials, tickets, lds, r, blockIdx.x % SPLIT_MAXRUN);                    \
+    }
+MI355X_SPLIT_KERNEL_MK(mi355x_tls_wins_seal_aes128_mk, 10, true, true)
+MI355X_SPLIT_KERNEL_MK(mi355x_tls_wins_seal_aes256_mk, 14, true, true)
+MI355X_SPLIT_KERNEL_MK(mi355x_tls_wins_open_aes128_mk, 10, false, true)
+MI355X_SPLIT_KERNEL_MK(mi355x_tls_wins_open_aes256_mk, 14, false, true)
+MI355X_SPLIT_KERNEL_MK(mi355x_gcm_wins_seal_aes128_mk, 10, true, false)
+MI355X_SPLIT_KERNEL_MK(mi355x_gcm_wins_seal_aes256_mk, 14, true, false)
+MI355X_SPLIT_KERNEL_MK(mi355x_gcm_wins_open_aes128_mk, 10, false, false)
+MI355X_SPLIT_KERNEL_MK(mi355x_gcm_wins_open_aes256_mk, 14, false, false)
 
 /* the AES rows of the window image (window_image_vec, v < 4096), once per device: the 16-lane kernels copy them */
 extern "C" __global__ void mi355x_win_aes_image(u32x4 *out)
@@ -1356,6 +1554,61 @@ extern "C" __global__ void mi355x_sort_keys(const Record *__restrict__ recs, uin
     }
 }
 
+/* ---- multi-key prep (ptls_mi355x_*_multikey): records sorted by key, each key's range in the key table ---- */
+/* sort input: the record's key index (out of range -> nkeys, sorted after every key) and its descriptor index */
+extern "C" __global__ void mi355x_mk_keys(const uint32_t *__restrict__ key_idx, uint32_t n, uint32_t nkeys,
+                                          uint32_t *__restrict__ keys, uint32_t *__restrict__ vals)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const uint32_t k = key_idx[i];
+        keys[i] = k < nkeys ? k : nkeys;
+        vals[i] = i;
+    }
+}
+
+/* every key's range empty and its group counter zero (before mi355x_mk_bounds) */
+extern "C" __global__ void mi355x_mk_reset(MkKey *__restrict__ keys, uint32_t nkeys, uint32_t *__restrict__ ctr)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < nkeys) {
+        keys[k].first = 0u;
+        keys[k].end = 0u;
+        ctr[k] = 0u;
+    }
+}
+
+/* each key's range [first, end) in the sorted order; an out-of-range key's record fails an open (mk_reject) */
+extern "C" __global__ void mi355x_mk_bounds(const uint32_t *__restrict__ sorted, const uint32_t *__restrict__ order,
+                                            uint32_t n, uint32_t nkeys, MkKey *__restrict__ keys,
+                                            uint32_t *__restrict__ st, uint8_t *__restrict__ types, uint32_t frame)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint32_t k = sorted[i];
+    if (k >= nkeys) {
+        if (frame)
+            mk_reject<true>(order[i], st, types);
+        else
+            mk_reject<false>(order[i], st, types);
+        return;
+    }
+    if (i == 0u || sorted[i - 1u] != k)
+        keys[k].first = i;
+    if (i + 1u == n || sorted[i + 1u] != k)
+        keys[k].end = i + 1u;
+}
+
+/* stop-at-failure segments of a multi-key open: a connection is (key, connection id) */
+extern "C" __global__ void mi355x_mk_segkeys(const uint32_t *__restrict__ key_idx, const uint32_t *__restrict__ conn,
+                                             uint32_t n, uint64_t *__restrict__ out)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n)
+        out[i] = (uint64_t)key_idx[i] << 32 | (conn != nullptr ? conn[i] : 0u);
+}
+
 /* ================================================================== host side ============ */
 
 typedef void (*batch_kernel_t)(const KeyImage *, uint32_t, uint32_t, uint32_t, const void *, const uint32_t *, uint32_t,
@@ -1413,6 +1666,13 @@ struct st_ptls_mi355x_aesgcm_context {
     bool work_ev_valid[WORK_SLOTS];
     hipEvent_t split_ev, scratch_ev;
     bool split_ev_valid, scratch_ev_valid;
+    /* multi-key launches led by this context: the key table last uploaded (pinned host copy), where it went, and the
+     * event after its upload (the host copy is rewritten only once that copy is done) */
+    MkKey *mk_host;
+    size_t mk_cap, mk_n;
+    const void *mk_dev;
+    hipEvent_t mk_ev;
+    bool mk_ev_valid;
 };
 
 struct st_ptls_mi355x_aes_context {
@@ -1457,7 +1717,8 @@ static int fail(const char *what, hipError_t e)
  * ptls_mi355x_device_check, and never dropped, so the next unrelated call is not the one blamed for it.
  */
 static std::mutex g_deferred_mu;
-static char g_deferred[256];
+constexpr int MAX_DEVICES = 64;
+static char g_deferred[MAX_DEVICES][256]; /* per device ordinal: the first error deferred on it since its last check */
 
 extern "C" void ptls_mi355x_defer_error(const char *what, int err)
 {
@@ -1465,9 +1726,12 @@ extern "C" void ptls_mi355x_defer_error(const char *what, int err)
         return;
     const char *msg = hipGetErrorString((hipError_t)err);
     fprintf(stderr, "ptls_mi355x: %s: %s\n", what, msg);
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEVICES)
+        dev = 0; /* (the free paths run with the context's device current: DeviceGuard) */
     std::lock_guard<std::mutex> lk(g_deferred_mu);
-    if (g_deferred[0] == 0)
-        snprintf(g_deferred, sizeof(g_deferred), "%s: %s", what, msg);
+    if (g_deferred[dev][0] == 0)
+        snprintf(g_deferred[dev], sizeof(g_deferred[dev]), "%s: %s", what, msg);
 }
 
 static void defer(const char *what, hipError_t e) { ptls_mi355x_defer_error(what, (int)e); }
@@ -1618,22 +1882,28 @@ static int ensure_stage(DeviceShared *d, size_t need)
     size_t cap = d->cap ? d->cap : 4096;
     while (cap < need)
         cap *= 2;
+    const size_t cap_old = d->cap;
     d->cap = 0; /* (nothing is left half-freed for a later call if a free below fails) */
     if (d->d_stage) {
         /* the last copied call's clear of the staging may still be queued on the device stream: it ends first (an
          * explicit wait, not hipFree's implicit one) */
         HIPCHK(hipStreamSynchronize(d->stream));
+        JNOTE("hipFree shared staging", d->d_stage, cap_old);
         HIPCHK(hipFree(d->d_stage));
     }
     d->d_stage = nullptr;
-    if (d->h_stage)
+    if (d->h_stage) {
+        JNOTE("hipHostFree shared staging", d->h_stage_dev, cap_old);
         HIPCHK(hipHostFree(d->h_stage));
+    }
     d->h_stage = nullptr;
     d->h_stage_dev = nullptr;
     HIPCHK(hipMalloc(&d->d_stage, cap));
     /* coherent: the GPU's zero-copy reads never see stale cache lines of a previous call */
     HIPCHK(hipHostMalloc(&d->h_stage, cap, hipHostMallocMapped | hipHostMallocCoherent));
     HIPCHK(hipHostGetDevicePointer((void **)&d->h_stage_dev, d->h_stage, 0));
+    JNOTE("hipMalloc shared staging", d->d_stage, cap);
+    JNOTE("hipHostMalloc shared staging (device view)", d->h_stage_dev, cap);
     d->cap = cap;
     return 0;
 }
@@ -1806,6 +2076,55 @@ static int res_used(ptls_mi355x_aesgcm_context_t *ctx, hipEvent_t *ev, bool *val
     return 0;
 }
 
+/* the journal entry of a record launch (fault_journal.c): every pointer argument, with its extent where it is known */
+static void journal_records_launch(const char *kernel, hipStream_t stream, uint32_t blocks, uint32_t threads, size_t n,
+                                   const void *ki, const void *recs, bool frame, const uint32_t *order, const uint8_t *src,
+                                   const uint8_t *dst, const uint8_t *aad, const uint32_t *status, const uint8_t *types,
+                                   const uint32_t *conn, const void *extra, size_t extra_len)
+{
+    const ptls_mi355x_journal_arg_t a[8] = {
+        {"keyimg", ki, sizeof(KeyImage)},
+        {"descs", recs, (uint64_t)n * (frame ? sizeof(TlsRecord) : sizeof(Record))},
+        {"src", src, 0},
+        {"dst", dst, 0},
+        {"aad", aad, 0},
+        {"status", status, status ? (uint64_t)n * 4u : 0u},
+        {order ? "order" : conn ? "conn" : "types", order ? (const void *)order : conn ? (const void *)conn : types,
+         (uint64_t)n * (order || conn ? 4u : 1u)},
+        {"work", extra, extra_len}};
+    ptls_mi355x_journal_launch(kernel, stream, blocks, threads, n, a, 8);
+}
+
+/* the split kernels' partials and tickets for n records, for a launch on `stream` (ordered after the last split launch) */
+static int ensure_split(ptls_mi355x_aesgcm_context_t *ctx, size_t n, hipStream_t stream, uint32_t **tickets)
+{
+    if (ctx_stream(ctx, stream) != 0)
+        return -1;
+    if (ctx->split_cap < n) {
+        if (ctx->d_split) {
+            /* split launches of this context may be on any stream: the device is idle before the buffer goes
+             * (an explicit wait, not hipFree's implicit one) */
+            HIPCHK(hipDeviceSynchronize());
+            JNOTE("hipFree split buffer", ctx->d_split, ctx->split_cap * (SPLIT_PSLOTS * sizeof(u32x4) + sizeof(uint32_t)));
+            HIPCHK(hipFree(ctx->d_split));
+        }
+        ctx->d_split = nullptr;
+        ctx->split_cap = 0;
+        ctx->split_ev_valid = false;
+        const size_t cap = split_cap_for(n);
+        HIPCHK(hipMalloc(&ctx->d_split, cap * (SPLIT_PSLOTS * sizeof(u32x4) + sizeof(uint32_t))));
+        JNOTE("hipMalloc split buffer", ctx->d_split, cap * (SPLIT_PSLOTS * sizeof(u32x4) + sizeof(uint32_t)));
+        HIPCHK(hipMemsetAsync((uint8_t *)ctx->d_split + cap * SPLIT_PSLOTS * sizeof(u32x4), 0, cap * sizeof(uint32_t),
+                              stream));
+        ctx->split_cap = cap;
+    }
+    /* the tickets are shared: order after the previous split launch */
+    if (res_wait(ctx, ctx->split_ev, ctx->split_ev_valid, stream) != 0)
+        return -1;
+    *tickets = (uint32_t *)((uint8_t *)ctx->d_split + ctx->split_cap * SPLIT_PSLOTS * sizeof(u32x4));
+    return 0;
+}
+
 static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void *static_iv12, const void *recs,
                         const uint32_t *order, size_t n, const uint8_t *src, uint8_t *dst, const uint8_t *aad,
                         uint32_t *status, hipStream_t stream, bool frame = false, uint8_t *types = nullptr,
@@ -1822,28 +2141,11 @@ static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void
     DeviceGuard guard(ctx->device);
     if (p.split != nullptr) {
         /* partials and tickets for n records (tickets are zero between launches: each record's last run resets its) */
-        if (ctx_stream(ctx, stream) != 0)
+        uint32_t *tickets = nullptr;
+        if (ensure_split(ctx, n, stream, &tickets) != 0)
             return -1;
-        if (ctx->split_cap < n) {
-            if (ctx->d_split) {
-                /* split launches of this context may be on any stream: the device is idle before the buffer goes
-                 * (an explicit wait, not hipFree's implicit one) */
-                HIPCHK(hipDeviceSynchronize());
-                HIPCHK(hipFree(ctx->d_split));
-            }
-            ctx->d_split = nullptr;
-            ctx->split_cap = 0;
-            ctx->split_ev_valid = false;
-            const size_t cap = split_cap_for(n);
-            HIPCHK(hipMalloc(&ctx->d_split, cap * (SPLIT_PSLOTS * sizeof(u32x4) + sizeof(uint32_t))));
-            HIPCHK(hipMemsetAsync((uint8_t *)ctx->d_split + cap * SPLIT_PSLOTS * sizeof(u32x4), 0, cap * sizeof(uint32_t),
-                                  stream));
-            ctx->split_cap = cap;
-        }
-        /* the tickets are shared: order after the previous split launch */
-        if (res_wait(ctx, ctx->split_ev, ctx->split_ev_valid, stream) != 0)
-            return -1;
-        uint32_t *tickets = (uint32_t *)((uint8_t *)ctx->d_split + ctx->split_cap * SPLIT_PSLOTS * sizeof(u32x4));
+        journal_records_launch(p.name, stream, p.blocks, p.threads, n, ctx->d_ki, recs, frame, order, src, dst, aad, status,
+                               types, conn, ctx->d_split, ctx->split_cap * (SPLIT_PSLOTS * sizeof(u32x4) + sizeof(uint32_t)));
         hipLaunchKernelGGL(p.split, dim3(p.blocks), dim3(p.threads), 0, stream, ctx->d_ki, le32(iv), le32(iv + 4),
                            le32(iv + 8), recs, (uint32_t)n, src, dst, aad, status, types, conn,
                            (const u32x4 *)ctx->shared->d_win_aes, ctx->d_split, tickets);
@@ -1851,6 +2153,8 @@ static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void
         return res_used(ctx, &ctx->split_ev, &ctx->split_ev_valid, stream);
     }
     if (p.win != nullptr) {
+        journal_records_launch(p.name, stream, p.blocks, p.threads, n, ctx->d_ki, recs, frame, order, src, dst, aad, status,
+                               types, conn, ctx->shared->d_win_aes, 0x10000);
         hipLaunchKernelGGL(p.win, dim3(p.blocks), dim3(p.threads), 0, stream, ctx->d_ki, le32(iv), le32(iv + 4),
                            le32(iv + 8), recs, (uint32_t)n, src, dst, aad, status, types, conn,
                            (const u32x4 *)ctx->shared->d_win_aes);
@@ -1871,6 +2175,8 @@ static int launch_batch(ptls_mi355x_aesgcm_context_t *ctx, bool seal, const void
     const uint32_t work_base = ctx->work_base[wslot];
     if (ctx_stream(ctx, stream) != 0 || res_wait(ctx, ctx->work_ev[wslot], ctx->work_ev_valid[wslot], stream) != 0)
         return -1;
+    journal_records_launch(p.name, stream, p.blocks, p.threads, n, ctx->d_ki, recs, frame, order, src, dst, aad, status,
+                           types, conn, work, 4);
     hipLaunchKernelGGL(p.batch, dim3(p.blocks), dim3(p.threads), 0, stream, ctx->d_ki, le32(iv), le32(iv + 4),
                        le32(iv + 8), recs, order, (uint32_t)n, src, dst, aad, status, types, work, work_base, conn);
     HIPCHK(hipGetLastError());
@@ -1895,12 +2201,14 @@ static int ensure_scratch(ptls_mi355x_aesgcm_context_t *ctx, size_t need, hipStr
         return 0;
     if (ctx->d_scratch) {
         HIPCHK(hipStreamSynchronize(stream)); /* the last use (ordered before this stream's queue above) is done */
+        JNOTE("hipFree scratch", ctx->d_scratch, ctx->scratch_cap);
         HIPCHK(hipFree(ctx->d_scratch));
     }
     ctx->d_scratch = nullptr;
     need = need < 2 * ctx->scratch_cap ? 2 * ctx->scratch_cap : need; /* (doubling: few growths, each a sync) */
     ctx->scratch_cap = 0;
     HIPCHK(hipMalloc(&ctx->d_scratch, need));
+    JNOTE("hipMalloc scratch", ctx->d_scratch, need);
     ctx->scratch_cap = need;
     return 0;
 }
@@ -2014,6 +2322,8 @@ ptls_mi355x_aesgcm_context_t *ptls_mi355x_aesgcm_new(const void *key, size_t key
         snprintf(g_err, sizeof(g_err), "context allocation: %s", hipGetErrorString(hipGetLastError()));
         goto Fail;
     }
+    JNOTE("hipMalloc key image", ctx->d_ki, sizeof(KeyImage));
+    JNOTE("hipMalloc work counters", ctx->d_work, WORK_SLOTS * sizeof(uint32_t));
     ctx->work_base[0] = g_ticket_origin; /* (read once: the counters below start where the bases say) */
     for (uint32_t i = 1; i < WORK_SLOTS; ++i)
         ctx->work_base[i] = ctx->work_base[0];
@@ -2071,14 +2381,21 @@ static int context_release(ptls_mi355x_aesgcm_context_t *ctx, bool deferred)
         /* clear key material, as ptls_fusion_aesgcm_free does; ordered before the free on the null stream */
         chk("context free: clearing the key image", hipMemsetAsync(ctx->d_ki, 0, sizeof(KeyImage), nullptr));
         chk("context free: hipDeviceSynchronize", hipDeviceSynchronize());
+        JNOTE("hipFree key image", ctx->d_ki, sizeof(KeyImage));
         chk("context free: hipFree(key image)", hipFree(ctx->d_ki));
     }
-    if (ctx->d_work)
+    if (ctx->d_work) {
+        JNOTE("hipFree work counters", ctx->d_work, WORK_SLOTS * sizeof(uint32_t));
         chk("context free: hipFree(work counters)", hipFree(ctx->d_work));
-    if (ctx->d_scratch)
+    }
+    if (ctx->d_scratch) {
+        JNOTE("hipFree scratch", ctx->d_scratch, ctx->scratch_cap);
         chk("context free: hipFree(scratch)", hipFree(ctx->d_scratch));
-    if (ctx->d_split)
+    }
+    if (ctx->d_split) {
+        JNOTE("hipFree split buffer", ctx->d_split, ctx->split_cap * (SPLIT_PSLOTS * sizeof(u32x4) + sizeof(uint32_t)));
         chk("context free: hipFree(split buffer)", hipFree(ctx->d_split));
+    }
     for (uint32_t i = 0; i < WORK_SLOTS; ++i)
         if (ctx->work_ev[i])
             chk("context free: hipEventDestroy", hipEventDestroy(ctx->work_ev[i]));
@@ -2086,6 +2403,10 @@ static int context_release(ptls_mi355x_aesgcm_context_t *ctx, bool deferred)
         chk("context free: hipEventDestroy", hipEventDestroy(ctx->split_ev));
     if (ctx->scratch_ev)
         chk("context free: hipEventDestroy", hipEventDestroy(ctx->scratch_ev));
+    if (ctx->mk_ev)
+        chk("context free: hipEventDestroy", hipEventDestroy(ctx->mk_ev));
+    if (ctx->mk_host)
+        chk("context free: hipHostFree(key table)", hipHostFree(ctx->mk_host));
     free(ctx);
     return rc;
 }
@@ -2116,14 +2437,34 @@ ptls_mi355x_aesgcm_context_t *ptls_mi355x_aesgcm_new_on(int device, const void *
 
 int ptls_mi355x_device_check(void)
 {
+    /*
+     * The current device's deferred error comes first, read and cleared before any HIP call: a sticky fault makes
+     * every call fail, and an error a free path met earlier must be reported by this check, not left queued for a
+     * later one.  (A fault with no deferred error is then named by the first HIP call below.)
+     */
     int dev = 0;
-    HIPCHK(hipGetDevice(&dev));
+    const hipError_t g = hipGetDevice(&dev);
+    if (g != hipSuccess || dev < 0 || dev >= MAX_DEVICES)
+        dev = 0;
+    char deferred[256];
+    {
+        std::lock_guard<std::mutex> lk(g_deferred_mu);
+        snprintf(deferred, sizeof(deferred), "%s", g_deferred[dev]);
+        g_deferred[dev][0] = 0;
+    }
+    if (g != hipSuccess) {
+        JNOTE("device check: hipGetDevice failed", nullptr, 0);
+        if (deferred[0] != 0)
+            snprintf(g_err, sizeof(g_err), "%s (then hipGetDevice: %s)", deferred, hipGetErrorString(g));
+        else
+            fail("hipGetDevice(&dev)", g);
+        return -1;
+    }
     const hipError_t s = hipDeviceSynchronize();
     const hipError_t l = hipGetLastError();
-    std::lock_guard<std::mutex> lk(g_deferred_mu);
-    if (g_deferred[0] != 0) {
-        snprintf(g_err, sizeof(g_err), "%s", g_deferred);
-        g_deferred[0] = 0;
+    JNOTE(s == hipSuccess && l == hipSuccess && deferred[0] == 0 ? "device check: ok" : "device check: error", nullptr, 0);
+    if (deferred[0] != 0) {
+        snprintf(g_err, sizeof(g_err), "%s", deferred);
         return -1;
     }
     if (s != hipSuccess)
@@ -2287,6 +2628,286 @@ int ptls_mi355x_order_by_length(ptls_mi355x_aesgcm_context_t *ctx, const ptls_mi
     return scratch_done(ctx, stream);
 }
 
+/* ------------------------------------------------------------------ multi-key batches ----- */
+
+/*
+ * The key table of a multi-key launch led by ctx, in its scratch at `dev`: uploaded from a pinned host copy only when
+ * the keys, their IVs or the table's place changed (a caller that sends its sessions' batches again pays nothing).
+ */
+static int mk_upload(ptls_mi355x_aesgcm_context_t *ctx, ptls_mi355x_aesgcm_context_t *const *ctxs, const uint8_t *ivs,
+                     size_t nkeys, void *dev, hipStream_t stream)
+{
+    bool same = ctx->mk_dev == dev && ctx->mk_n == nkeys && ctx->mk_host != nullptr;
+    for (size_t k = 0; same && k < nkeys; ++k)
+        same = ctx->mk_host[k].ki == ctxs[k]->d_ki && ctx->mk_host[k].iv0 == le32(ivs + 12 * k) &&
+               ctx->mk_host[k].iv1 == le32(ivs + 12 * k + 4) && ctx->mk_host[k].iv2 == le32(ivs + 12 * k + 8);
+    if (same)
+        return 0;
+    if (ctx->mk_ev_valid) /* the previous upload has read the pinned copy */
+        HIPCHK(hipEventSynchronize(ctx->mk_ev));
+    if (ctx->mk_cap < nkeys) {
+        if (ctx->mk_host)
+            HIPCHK(hipHostFree(ctx->mk_host));
+        ctx->mk_host = nullptr;
+        ctx->mk_cap = 0;
+        HIPCHK(hipHostMalloc((void **)&ctx->mk_host, nkeys * sizeof(MkKey), hipHostMallocDefault));
+        ctx->mk_cap = nkeys;
+    }
+    for (size_t k = 0; k < nkeys; ++k)
+        ctx->mk_host[k] = MkKey{ctxs[k]->d_ki, le32(ivs + 12 * k), le32(ivs + 12 * k + 4), le32(ivs + 12 * k + 8), 0u, 0u, 0u};
+    ctx->mk_n = 0;
+    ctx->mk_dev = nullptr;
+    HIPCHK(hipMemcpyAsync(dev, ctx->mk_host, nkeys * sizeof(MkKey), hipMemcpyHostToDevice, stream));
+    if (ctx->mk_ev == nullptr)
+        HIPCHK(hipEventCreateWithFlags(&ctx->mk_ev, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(ctx->mk_ev, stream));
+    ctx->mk_ev_valid = true;
+    ctx->mk_n = nkeys;
+    ctx->mk_dev = dev;
+    return 0;
+}
+
+/* the kernel family of a multi-key batch of n records (the same selection setters as plan_launch) */
+enum MkFamily { MK_SPLIT, MK_WIN16, MK_BATCH };
+static MkFamily mk_family(bool frame, size_t n, int num_cu)
+{
+    if (n <= (frame ? g_window_records.load() : g_aead_window_records.load())) {
+        const size_t split_max = g_split_records.load(), win16_max = g_win16_records.load();
+        if (n <= (split_max == SIZE_MAX ? (size_t)num_cu / SPLIT_MAXRUN : split_max) && n <= 0xffffffffu / SPLIT_MAXRUN)
+            return MK_SPLIT;
+        if (n <= (win16_max == SIZE_MAX ? (size_t)num_cu : win16_max))
+            return MK_WIN16;
+    }
+    return MK_BATCH;
+}
+
+static const char *mk_kernel_name(bool seal, bool frame, uint32_t key_size, size_t n, int num_cu)
+{
+    static const char *names[3][2][2][2] = {
+        /* [family][frame][seal][aes256] */
+        {{{"mi355x_gcm_wins_open_aes128_mk", "mi355x_gcm_wins_open_aes256_mk"},
+          {"mi355x_gcm_wins_seal_aes128_mk", "mi355x_gcm_wins_seal_aes256_mk"}},
+         {{"mi355x_tls_wins_open_aes128_mk", "mi355x_tls_wins_open_aes256_mk"},
+          {"mi355x_tls_wins_seal_aes128_mk", "mi355x_tls_wins_seal_aes256_mk"}}},
+        {{{"mi355x_gcm_win16_open_aes128_mk", "mi355x_gcm_win16_open_aes256_mk"},
+          {"mi355x_gcm_win16_seal_aes128_mk", "mi355x_gcm_win16_seal_aes256_mk"}},
+         {{"mi355x_tls_win16_open_aes128_mk", "mi355x_tls_win16_open_aes256_mk"},
+          {"mi355x_tls_win16_seal_aes128_mk", "mi355x_tls_win16_seal_aes256_mk"}}},
+        {{{"mi355x_gcm_open_aes128_k4_mk", "mi355x_gcm_open_aes256_k4_mk"},
+          {"mi355x_gcm_seal_aes128_k4_mk", "mi355x_gcm_seal_aes256_k4_mk"}},
+         {{"mi355x_tls_open_aes128_k4_mk", "mi355x_tls_open_aes256_k4_mk"},
+          {"mi355x_tls_seal_aes128_k4_mk", "mi355x_tls_seal_aes256_k4_mk"}}}};
+    return names[mk_family(frame, n, num_cu)][frame][seal][key_size == 32];
+}
+
+typedef void (*mk_batch_kernel_t)(const MkKey *, uint32_t, uint32_t *, uint32_t *, const void *, const uint32_t *, uint32_t,
+                                  const uint8_t *, uint8_t *, const uint8_t *, uint32_t *, uint8_t *, const uint32_t *);
+typedef void (*mk_split_kernel_t)(const MkKey *, uint32_t, const uint32_t *, const void *, uint32_t, const uint8_t *,
+                                  uint8_t *, const uint8_t *, uint32_t *, uint8_t *, const uint32_t *, const u32x4 *, u32x4 *,
+                                  uint32_t *);
+typedef void (*mk_win16_kernel_t)(const MkKey *, uint32_t, const uint32_t *, const void *, uint32_t, const uint8_t *,
+                                  uint8_t *, const uint8_t *, uint32_t *, uint8_t *, const uint32_t *, const u32x4 *);
+
+/*
+ * One launch over the records of nkeys keys (contexts ctxs[k], static IVs ivs[12 k ..]); record i uses key key_idx[i].
+ * ctxs[0] leads: its scratch holds the key table, the counters and the sort, its split buffer the split kernels' state.
+ *  - up to a fifth of the CUs' records: the split kernels, each workgroup on its record's key;
+ *  - up to one record per CU: the 16-lane kernels, likewise;
+ *  - above: the batch kernels' multi-key phases, over the records sorted by key (a stable device radix sort on the key
+ *    index, then each key's range, both on `stream` before the launch).
+ * Every key must be on ctxs[0]'s device with its key size.  A record whose key index is >= nkeys is not processed
+ * (open: status 0xffffffff).
+ */
+static int launch_multikey(ptls_mi355x_aesgcm_context_t *const *ctxs, const void *static_ivs, size_t nkeys, bool seal,
+                           bool frame, const void *recs, const uint32_t *key_idx, const uint32_t *conn, size_t n,
+                           const uint8_t *src, uint8_t *dst, const uint8_t *aad, uint32_t *status, uint8_t *types,
+                           hipStream_t stream)
+{
+    if (n == 0)
+        return 0;
+    if (ctxs == nullptr || nkeys == 0 || nkeys > (1u << 24) || static_ivs == nullptr || key_idx == nullptr) {
+        snprintf(g_err, sizeof(g_err), "multi-key batch: contexts, IVs and key indices are required (1..2^24 keys)");
+        return -1;
+    }
+    if (n > 0xffffffffull) {
+        snprintf(g_err, sizeof(g_err), "batch of %zu records exceeds 2^32-1", n);
+        return -1;
+    }
+    ptls_mi355x_aesgcm_context_t *ctx = ctxs[0];
+    for (size_t k = 0; k < nkeys; ++k)
+        if (ctxs[k] == nullptr || ctxs[k]->device != ctx->device || ctxs[k]->key_size != ctx->key_size) {
+            snprintf(g_err, sizeof(g_err), "multi-key batch: key %zu is %s", k,
+                     ctxs[k] == nullptr ? "NULL" : "on another device or of another key size");
+            return -1;
+        }
+    DeviceGuard guard(ctx->device);
+    const bool a256 = ctx->key_size == 32;
+    const MkFamily fam = mk_family(frame, n, ctx->num_cu);
+    const uint32_t grid = (uint32_t)ctx->num_cu;
+    /* scratch: key table | counters | broadcast slots | sort keys in, out | values in | order | sort temp */
+    const size_t a_tab = (nkeys * sizeof(MkKey) + 255) & ~(size_t)255, a_ctr = (nkeys * 4 + 255) & ~(size_t)255,
+                 a_wg = ((size_t)grid * 4 + 255) & ~(size_t)255, arr = fam == MK_BATCH ? (n * 4 + 255) & ~(size_t)255 : 0;
+    size_t temp = 0;
+    uint32_t bits = 1;
+    while (bits < 32 && (1ull << bits) <= nkeys) /* keys 0..nkeys (nkeys: out of range) */
+        ++bits;
+    if (fam == MK_BATCH)
+        HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                                  (uint32_t *)nullptr, (uint32_t *)nullptr, (int)n, 0, (int)bits, stream));
+    const size_t need = a_tab + a_ctr + a_wg + 4 * arr + temp;
+    if (ensure_scratch(ctx, need, stream) != 0)
+        return -1;
+    uint8_t *base = (uint8_t *)ctx->d_scratch;
+    MkKey *tab = (MkKey *)base;
+    uint32_t *ctr = (uint32_t *)(base + a_tab), *wg = (uint32_t *)(base + a_tab + a_ctr);
+    uint8_t *sb = base + a_tab + a_ctr + a_wg;
+    uint32_t *keys_in = (uint32_t *)sb, *keys_out = (uint32_t *)(sb + arr), *vals_in = (uint32_t *)(sb + 2 * arr),
+             *order = (uint32_t *)(sb + 3 * arr);
+    if (mk_upload(ctx, ctxs, (const uint8_t *)static_ivs, nkeys, tab, stream) != 0)
+        return -1;
+    const char *name = mk_kernel_name(seal, frame, ctx->key_size, n, ctx->num_cu);
+    if (fam == MK_SPLIT) {
+        static const mk_split_kernel_t ks[2][2][2] = {
+            {{mi355x_gcm_wins_open_aes128_mk, mi355x_gcm_wins_open_aes256_mk},
+             {mi355x_gcm_wins_seal_aes128_mk, mi355x_gcm_wins_seal_aes256_mk}},
+            {{mi355x_tls_wins_open_aes128_mk, mi355x_tls_wins_open_aes256_mk},
+             {mi355x_tls_wins_seal_aes128_mk, mi355x_tls_wins_seal_aes256_mk}}};
+        uint32_t *tickets = nullptr;
+        if (ensure_split(ctx, n, stream, &tickets) != 0)
+            return -1;
+        journal_records_launch(name, stream, (uint32_t)(n * SPLIT_MAXRUN), SPLIT_THREADS, n, tab, recs, frame, key_idx, src,
+                               dst, aad, status, types, conn, ctx->d_split,
+                               ctx->split_cap * (SPLIT_PSLOTS * sizeof(u32x4) + sizeof(uint32_t)));
+        hipLaunchKernelGGL(ks[frame][seal][a256], dim3((uint32_t)(n * SPLIT_MAXRUN)), dim3(SPLIT_THREADS), 0, stream, tab,
+                           (uint32_t)nkeys, key_idx, recs, (uint32_t)n, src, dst, aad, status, types, conn,
+                           (const u32x4 *)ctx->shared->d_win_aes, ctx->d_split, tickets);
+        HIPCHK(hipGetLastError());
+        if (res_used(ctx, &ctx->split_ev, &ctx->split_ev_valid, stream) != 0)
+            return -1;
+        return scratch_done(ctx, stream);
+    }
+    if (fam == MK_WIN16) {
+        static const mk_win16_kernel_t kw[2][2][2] = {
+            {{mi355x_gcm_win16_open_aes128_mk, mi355x_gcm_win16_open_aes256_mk},
+             {mi355x_gcm_win16_seal_aes128_mk, mi355x_gcm_win16_seal_aes256_mk}},
+            {{mi355x_tls_win16_open_aes128_mk, mi355x_tls_win16_open_aes256_mk},
+             {mi355x_tls_win16_seal_aes128_mk, mi355x_tls_win16_seal_aes256_mk}}};
+        journal_records_launch(name, stream, (uint32_t)n, 576, n, tab, recs, frame, key_idx, src, dst, aad, status, types,
+                               conn, ctx->shared->d_win_aes, 0x10000);
+        hipLaunchKernelGGL(kw[frame][seal][a256], dim3((uint32_t)n), dim3(576), 0, stream, tab, (uint32_t)nkeys, key_idx,
+                           recs, (uint32_t)n, src, dst, aad, status, types, conn, (const u32x4 *)ctx->shared->d_win_aes);
+        HIPCHK(hipGetLastError());
+        return scratch_done(ctx, stream);
+    }
+    static const mk_batch_kernel_t kb[2][2][2] = {
+        {{mi355x_gcm_open_aes128_k4_mk, mi355x_gcm_open_aes256_k4_mk},
+         {mi355x_gcm_seal_aes128_k4_mk, mi355x_gcm_seal_aes256_k4_mk}},
+        {{mi355x_tls_open_aes128_k4_mk, mi355x_tls_open_aes256_k4_mk},
+         {mi355x_tls_seal_aes128_k4_mk, mi355x_tls_seal_aes256_k4_mk}}};
+    const unsigned g = (unsigned)((n + 255) / 256), gk = (unsigned)((nkeys + 255) / 256);
+    hipLaunchKernelGGL(mi355x_mk_keys, dim3(g), dim3(256), 0, stream, key_idx, (uint32_t)n, (uint32_t)nkeys, keys_in, vals_in);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(sb + 4 * arr, temp, keys_in, keys_out, vals_in, order, (int)n, 0, (int)bits,
+                                              stream));
+    hipLaunchKernelGGL(mi355x_mk_reset, dim3(gk), dim3(256), 0, stream, tab, (uint32_t)nkeys, ctr);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(mi355x_mk_bounds, dim3(g), dim3(256), 0, stream, keys_out, order, (uint32_t)n, (uint32_t)nkeys, tab,
+                       seal ? nullptr : status, seal ? nullptr : types, frame ? 1u : 0u);
+    HIPCHK(hipGetLastError());
+    /* groups: at most n / 16 + nkeys (each key's last group partial); a CU's worth of waves per workgroup */
+    const uint64_t groups = n / 16 + nkeys, blocks = (groups + 15) / 16;
+    const uint32_t nb = (uint32_t)(blocks < grid ? blocks : grid);
+    journal_records_launch(name, stream, nb, WG_THREADS, n, tab, recs, frame, order, src, dst, aad, status, types, conn, ctr,
+                           nkeys * 4);
+    hipLaunchKernelGGL(kb[frame][seal][a256], dim3(nb), dim3(WG_THREADS), 0, stream, tab, (uint32_t)nkeys, ctr, wg, recs,
+                       order, (uint32_t)n, src, dst, aad, status, types, conn);
+    HIPCHK(hipGetLastError());
+    return scratch_done(ctx, stream);
+}
+
+int ptls_mi355x_seal_batch_multikey(ptls_mi355x_aesgcm_context_t *const *ctxs, const void *static_ivs, size_t nkeys,
+                                    const ptls_mi355x_record_t *recs, const uint32_t *key_idx, size_t n,
+                                    const uint8_t *src, uint8_t *dst, const uint8_t *aad, void *stream)
+{
+    return launch_multikey(ctxs, static_ivs, nkeys, true, false, recs, key_idx, nullptr, n, src, dst, aad, nullptr, nullptr,
+                           (hipStream_t)stream);
+}
+
+int ptls_mi355x_open_batch_multikey(ptls_mi355x_aesgcm_context_t *const *ctxs, const void *static_ivs, size_t nkeys,
+                                    const ptls_mi355x_record_t *recs, const uint32_t *key_idx, size_t n,
+                                    const uint8_t *src, uint8_t *dst, const uint8_t *aad, uint32_t *status, void *stream)
+{
+    if (n != 0 && status == nullptr) {
+        snprintf(g_err, sizeof(g_err), "open_batch_multikey needs status");
+        return -1;
+    }
+    return launch_multikey(ctxs, static_ivs, nkeys, false, false, recs, key_idx, nullptr, n, src, dst, aad, status, nullptr,
+                           (hipStream_t)stream);
+}
+
+int ptls_mi355x_tls_seal_records_multikey(ptls_mi355x_aesgcm_context_t *const *ctxs, const void *static_ivs, size_t nkeys,
+                                          const ptls_mi355x_tls_record_t *recs, const uint32_t *key_idx,
+                                          const uint32_t *conn_ids, size_t n, const uint8_t *src, uint8_t *dst,
+                                          void *stream)
+{
+    return launch_multikey(ctxs, static_ivs, nkeys, true, true, recs, key_idx, conn_ids, n, src, dst, nullptr, nullptr,
+                           nullptr, (hipStream_t)stream);
+}
+
+int ptls_mi355x_tls_open_records_multikey(ptls_mi355x_aesgcm_context_t *const *ctxs, const void *static_ivs, size_t nkeys,
+                                          const ptls_mi355x_tls_record_t *recs, const uint32_t *key_idx,
+                                          const uint32_t *conn_ids, size_t n, const uint8_t *src, uint8_t *dst,
+                                          uint32_t *status, uint8_t *types, int flags, void *stream_)
+{
+    if (n != 0 && (status == nullptr || types == nullptr)) {
+        snprintf(g_err, sizeof(g_err), "tls_open_records_multikey needs status and types");
+        return -1;
+    }
+    if ((flags & ~PTLS_MI355X_OPEN_STOP_AT_FAILURE) != 0) {
+        snprintf(g_err, sizeof(g_err), "unknown flags %#x", flags);
+        return -1;
+    }
+    hipStream_t stream = (hipStream_t)stream_;
+    if (launch_multikey(ctxs, static_ivs, nkeys, false, true, recs, key_idx, conn_ids, n, src, dst, nullptr, status, types,
+                        stream) != 0)
+        return -1;
+    if (n == 0 || !(flags & PTLS_MI355X_OPEN_STOP_AT_FAILURE))
+        return 0;
+    /* stop at each connection's first failure; a connection is (key, connection id): consecutive records of one */
+    ptls_mi355x_aesgcm_context_t *ctx = ctxs[0];
+    DeviceGuard guard(ctx->device);
+    size_t temp = 0;
+    HIPCHK(hipcub::DeviceScan::InclusiveScanByKey(nullptr, temp, (uint64_t *)nullptr, (uint32_t *)nullptr,
+                                                  (uint32_t *)nullptr, hipcub::Min(), (uint32_t)n, hipcub::Equality(),
+                                                  stream));
+    const size_t arr = ((n * sizeof(uint32_t)) + 255) & ~(size_t)255, arr64 = ((n * sizeof(uint64_t)) + 255) & ~(size_t)255;
+    if (ensure_scratch(ctx, 2 * arr + arr64 + temp, stream) != 0)
+        return -1;
+    uint8_t *base = (uint8_t *)ctx->d_scratch;
+    uint32_t *pos = (uint32_t *)base, *first = (uint32_t *)(base + arr);
+    uint64_t *seg = (uint64_t *)(base + 2 * arr);
+    const unsigned g = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(mi355x_mk_segkeys, dim3(g), dim3(256), 0, stream, key_idx, conn_ids, (uint32_t)n, seg);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(mi355x_tls_fail_pos, dim3(g), dim3(256), 0, stream, status, (uint32_t)n, pos);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipcub::DeviceScan::InclusiveScanByKey(base + 2 * arr + arr64, temp, seg, pos, first, hipcub::Min(), (uint32_t)n,
+                                                  hipcub::Equality(), stream));
+    hipLaunchKernelGGL(mi355x_tls_truncate, dim3(g), dim3(256), 0, stream, (const TlsRecord *)recs, (uint32_t)n, first, dst,
+                       status, types);
+    HIPCHK(hipGetLastError());
+    ctx->mk_dev = nullptr; /* the scan wrote over the key table's place: upload it again next time */
+    return scratch_done(ctx, stream);
+}
+
+const char *ptls_mi355x_kernel_name_multikey(int is_seal, size_t key_size, size_t n, int framing)
+{
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        ncu = 256;
+    return mk_kernel_name(is_seal != 0, framing != 0, key_size == 32 ? 32u : 16u, n, ncu);
+}
+
 /*
  * Single record in host memory (the slot calls), on the device's shared stream and staging.  Stage layout
  * (device and pinned host alike):
@@ -2308,13 +2929,29 @@ static int finish_single(DeviceShared *d, bool seal, void *output, size_t inlen,
     return st == (uint32_t)inlen ? 1 : 0;
 }
 
+/* test hook (ptls_mi355x_test_inject_engine_errors): the next n single-record calls fail as a GPU error would */
+static std::atomic<unsigned> g_inject_errors{0u};
+
+static int single_record_staged(ptls_mi355x_aesgcm_context_t *ctx, DeviceShared *d, bool seal, void *output,
+                                const void *input, size_t inlen, const void *nonce12, const void *aad, size_t aadlen,
+                                const void *tag, size_t off_aad, size_t off_data, size_t off_status, size_t total);
+
 static int single_record(ptls_mi355x_aesgcm_context_t *ctx, bool seal, void *output, const void *input, size_t inlen,
                          const void *nonce12, const void *aad, size_t aadlen, const void *tag)
 {
+    if (ctx == nullptr) {
+        snprintf(g_err, sizeof(g_err), "no engine context");
+        return -1;
+    }
     if (inlen > 0xffffffffu || aadlen > 0xffffffffu) {
         snprintf(g_err, sizeof(g_err), "record too large");
         return -1;
     }
+    for (unsigned n = g_inject_errors.load(); n != 0u;)
+        if (g_inject_errors.compare_exchange_weak(n, n - 1u)) {
+            snprintf(g_err, sizeof(g_err), "injected engine error (ptls_mi355x_test_inject_engine_errors)");
+            return -1;
+        }
     DeviceGuard guard(ctx->device);
     DeviceShared *d = ctx->shared;
     std::lock_guard<std::mutex> lk(d->mu);
@@ -2322,6 +2959,17 @@ static int single_record(ptls_mi355x_aesgcm_context_t *ctx, bool seal, void *out
     const size_t total = off_status + 16;
     if (ensure_stage(d, total) != 0)
         return -1;
+    const int rc = single_record_staged(ctx, d, seal, output, input, inlen, nonce12, aad, aadlen, tag, off_aad, off_data,
+                                        off_status, total);
+    if (rc < 0) /* a failed call leaves nothing of the record in the pinned staging */
+        memset(d->h_stage, 0, total);
+    return rc;
+}
+
+static int single_record_staged(ptls_mi355x_aesgcm_context_t *ctx, DeviceShared *d, bool seal, void *output,
+                                const void *input, size_t inlen, const void *nonce12, const void *aad, size_t aadlen,
+                                const void *tag, size_t off_aad, size_t off_data, size_t off_status, size_t total)
+{
     Record rec = {off_data, off_data, off_aad, 0, (uint32_t)inlen, (uint32_t)aadlen};
     memcpy(d->h_stage, &rec, sizeof(rec));
     if (aadlen)
@@ -2356,6 +3004,8 @@ static int single_record(ptls_mi355x_aesgcm_context_t *ctx, bool seal, void *out
         HIPCHK(hipMemsetAsync(d->d_stage, 0, total, d->stream)); /* nothing of the record stays on the device */
     return finish_single(d, seal, output, inlen, off_data, off_status, total);
 }
+
+unsigned ptls_mi355x_test_inject_engine_errors(unsigned n) { return g_inject_errors.exchange(n); }
 
 int ptls_mi355x_aesgcm_encrypt(ptls_mi355x_aesgcm_context_t *ctx, void *output, const void *input, size_t inlen,
                                const void *nonce12, const void *aad, size_t aadlen)

@@ -53,6 +53,7 @@
 #include <pthread.h>
 #include <hip/hip_runtime_api.h>
 #include "../../include/ptls_mi355x.h"
+#include "fault_journal.h"
 
 #define RL_MAX_REGIONS 8
 #define RL_ZERO_COPY_DEFAULT ((size_t)4 << 20)
@@ -112,6 +113,17 @@ typedef struct {
     size_t nrec, off_src, srcbytes, off_dst, dstbytes, off_st, off_ty, off_dp, max_part;
     rl_copy_t *h2d, *d2h; /* dma: registered host ranges <-> the slot's device buffer */
     size_t nh2d, nd2h;
+    /*
+     * Sessions (op_sessions): the op's layers grouped by session -- key and IV bytes 4..11 (a rapido session's
+     * connections differ only in IV bytes 0..3, lib/rapido.c:127-133).  One session: the single-key launch, each record
+     * carrying its connection's IV difference.  Several: a multi-key launch (ptls_mi355x_tls_*_records_multikey), each
+     * record also carrying its session's index, the key of session k being its first layer's context.
+     */
+    size_t nsess;
+    ptls_mi355x_aesgcm_context_t **sess_ctx; /* per session */
+    uint8_t *sess_iv;                        /* per session: its first layer's IV */
+    uint32_t *sess_of;                       /* per layer: its session */
+    size_t off_kidx;                         /* nsess > 1: the per-record session indices in the staging layout */
 } rl_op_t;
 
 typedef struct {
@@ -257,6 +269,7 @@ static int reserve_stage(rl_slot_t *s, size_t bytes)
     hipError_t e;
     if (s->h_buf != NULL) {
         memset(s->h_buf, 0, s->cap);
+        ptls_mi355x_fault_journal_note("record layer: hipHostFree staging (device view)", s->h_dev, s->cap);
         const hipError_t ef = hipHostFree(s->h_buf);
         s->h_buf = s->h_dev = NULL;
         s->cap = 0;
@@ -270,6 +283,7 @@ static int reserve_stage(rl_slot_t *s, size_t bytes)
         return rl_fail("hipHostMalloc", e);
     if ((e = hipHostGetDevicePointer((void **)&s->h_dev, s->h_buf, 0)) != hipSuccess)
         return rl_fail("hipHostGetDevicePointer", e);
+    ptls_mi355x_fault_journal_note("record layer: hipHostMalloc staging (device view)", s->h_dev, c);
     s->cap = c;
     if (rl_trace_on())
         fprintf(stderr, "record layer: slot %p staging grown to %zu B\n", (void *)s, c);
@@ -285,6 +299,7 @@ static int reserve_device(rl_slot_t *s)
         hipError_t ef = hipMemsetAsync(s->d_buf, 0, s->d_cap, s->stream);
         if (ef == hipSuccess)
             ef = hipStreamSynchronize(s->stream);
+        ptls_mi355x_fault_journal_note("record layer: hipFree device buffer", s->d_buf, s->d_cap);
         const hipError_t ef2 = hipFree(s->d_buf);
         s->d_buf = NULL;
         s->d_cap = 0;
@@ -295,6 +310,7 @@ static int reserve_device(rl_slot_t *s)
     s->d_cap = 0;
     if ((e = hipMalloc((void **)&s->d_buf, s->cap)) != hipSuccess)
         return rl_fail("hipMalloc", e);
+    ptls_mi355x_fault_journal_note("record layer: hipMalloc device buffer", s->d_buf, s->cap);
     s->d_cap = s->cap;
     if (rl_trace_on())
         fprintf(stderr, "record layer: slot %p device buffer grown to %zu B\n", (void *)s, s->cap);
@@ -329,12 +345,14 @@ static void slot_release(rl_slot_t *s)
     if (s->d_buf != NULL) { /* cleared on the slot's stream, before that stream goes */
         RL_DEFER("clearing the device buffer", hipMemsetAsync(s->d_buf, 0, s->d_cap, s->stream));
         RL_DEFER("slot synchronisation", hipStreamSynchronize(s->stream));
+        ptls_mi355x_fault_journal_note("record layer: hipFree device buffer", s->d_buf, s->d_cap);
         RL_DEFER("hipFree (device buffer)", hipFree(s->d_buf));
     }
     if (s->stream != NULL)
         RL_DEFER("hipStreamDestroy", hipStreamDestroy(s->stream));
     if (s->h_buf != NULL) {
         memset(s->h_buf, 0, s->cap); /* plaintexts passed through the staging */
+        ptls_mi355x_fault_journal_note("record layer: hipHostFree staging (device view)", s->h_dev, s->cap);
         RL_DEFER("hipHostFree (staging)", hipHostFree(s->h_buf));
     }
     free(s->recs);
@@ -473,8 +491,10 @@ int ptls_mi355x_record_layer_reserve(ptls_mi355x_record_layer_t *rl, size_t wind
 {
     if (window_bytes == 0 || windows_per_launch == 0 || windows_per_launch > RL_TICKETS)
         return rl_msg("reserve: window bytes and 1..32 windows per launch");
-    /* the largest layout a launch of such windows takes (copy transport: descriptors, inputs, outputs, statuses, types,
-     * delivery parts, every piece 16-aligned), and its descriptors (an open parses up to inlen / 5 + 1) */
+    /* the largest layout a launch of such windows of full-size records takes (copy transport: descriptors, inputs,
+     * outputs, statuses, types, delivery parts, every piece 16-aligned), and its descriptors (an open parses up to
+     * inlen / 5 + 1).  Staging for the per-record pieces of windows of many small records is not reserved: 128 B a
+     * record at the parse bound would be ~6x the window bytes (include/ptls_mi355x.h) */
     const size_t recs = window_bytes / 16384u + 2u;
     const size_t need = windows_per_launch * (2u * window_bytes + recs * 128u) + 4096u;
     for (int i = 0; i < RL_SLOTS; ++i) {
@@ -588,6 +608,9 @@ int ptls_mi355x_record_layer_register(ptls_mi355x_record_layer_t *rl, void *base
         pthread_mutex_unlock(&g_reg_mu);
         return rl_fail("hipHostGetDevicePointer", e);
     }
+    ptls_mi355x_fault_journal_note(owned ? "record layer: hipHostRegister (device view)"
+                                         : "record layer: application-registered range (device view)",
+                                   dev, len);
     if (owned) {
         g_reg[g_nreg++] = (rl_shared_range_t){(uint8_t *)base, dev, len, 1};
         rl->reg[rl->nreg++] = (rl_region_t){(uint8_t *)base, dev, len, 1, (uint8_t *)base};
@@ -613,6 +636,7 @@ int ptls_mi355x_record_layer_unregister(ptls_mi355x_record_layer_t *rl, void *ba
                 pthread_mutex_lock(&g_reg_mu);
                 rl_shared_range_t *sr = shared_range(rl->reg[i].shared);
                 if (sr != NULL && --sr->refs == 0) {
+                    ptls_mi355x_fault_journal_note("record layer: hipHostUnregister (device view)", sr->dev, sr->len);
                     e = hipHostUnregister(sr->base);
                     *sr = g_reg[--g_nreg];
                 }
@@ -644,19 +668,61 @@ static int overlaps(const void *a, size_t alen, const void *b, size_t blen)
 
 static uint32_t be32(const uint8_t *b) { return (uint32_t)b[0] << 24 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 8 | b[3]; }
 
-/* the layers of one launch share the key and IV bytes 4..11 (the connections of a session) */
-static int same_session(ptls_mi355x_record_layer_t *const *layers, size_t nlayers)
+/* the layers of one launch share the key size (a launch runs the AES-128 or the AES-256 kernels) */
+static int same_key_size(ptls_mi355x_record_layer_t *const *layers, size_t nlayers)
 {
-    const ptls_mi355x_record_layer_t *rl = layers[0];
-    for (size_t l = 1; l < nlayers; ++l) {
-        const ptls_mi355x_record_layer_t *x = layers[l];
-        if (x->key_size != rl->key_size || memcmp(x->key, rl->key, rl->key_size) != 0 ||
-            memcmp(x->iv + 4, rl->iv + 4, 8) != 0) {
-            snprintf(rl_err, sizeof(rl_err), "record layer: layer %zu has another key or IV bytes 4..11", l);
+    for (size_t l = 1; l < nlayers; ++l)
+        if (layers[l]->key_size != layers[0]->key_size) {
+            snprintf(rl_err, sizeof(rl_err), "record layer: layer %zu has another key size", l);
             return 0;
         }
-    }
     return 1;
+}
+
+/* the connections of one session share the key and IV bytes 4..11 (lib/rapido.c:127-133) */
+static int same_session(const ptls_mi355x_record_layer_t *a, const ptls_mi355x_record_layer_t *b)
+{
+    return a->key_size == b->key_size && memcmp(a->key, b->key, a->key_size) == 0 && memcmp(a->iv + 4, b->iv + 4, 8) == 0;
+}
+
+/*
+ * Groups the op's layers by session (rl_op_t): session 0 is layers[0]'s, led by the launch slot's context; another
+ * session's key is its first layer's own slot-0 context (created here if need be).  That layer counts the launch in
+ * flight like every layer it names, so its context is not rekeyed or freed under it.
+ */
+static int op_sessions(rl_slot_t *s)
+{
+    rl_op_t *op = &s->op;
+    const size_t n = op->nlayers;
+    uint8_t *mem = calloc(1, n * (sizeof(void *) + 12 + sizeof(uint32_t) + sizeof(void *)));
+    if (mem == NULL)
+        return rl_msg("out of memory");
+    op->sess_ctx = (ptls_mi355x_aesgcm_context_t **)mem;
+    ptls_mi355x_record_layer_t **lead = (ptls_mi355x_record_layer_t **)(mem + n * sizeof(void *));
+    op->sess_iv = mem + 2 * n * sizeof(void *);
+    op->sess_of = (uint32_t *)(op->sess_iv + 12 * n);
+    op->nsess = 0;
+    for (size_t l = 0; l < n; ++l) {
+        ptls_mi355x_record_layer_t *x = op->layers[l];
+        size_t k = 0;
+        while (k < op->nsess && !same_session(lead[k], x))
+            ++k;
+        if (k == op->nsess) {
+            ptls_mi355x_aesgcm_context_t *c = s->ctx;
+            if (k != 0) {
+                rl_slot_t *xs = &x->slot[0];
+                if (slot_ready(x, xs) != 0)
+                    return -1;
+                c = xs->ctx;
+            }
+            lead[k] = x;
+            op->sess_ctx[k] = c;
+            memcpy(op->sess_iv + 12 * k, x->iv, 12);
+            ++op->nsess;
+        }
+        op->sess_of[l] = (uint32_t)k;
+    }
+    return 0;
 }
 
 /* a new op on layers[0]'s next launch slot: its arrays allocated, NULL when every slot is in flight or on error */
@@ -698,6 +764,7 @@ static void op_discard(rl_op_t *op)
 {
     free(op->h2d);
     free(op->layers);
+    free(op->sess_ctx);
     memset(op, 0, sizeof(*op));
 }
 
@@ -792,6 +859,7 @@ static int op_launch(rl_slot_t *s, const uint8_t *src_base, uint8_t *dst_base)
     const uint8_t *src = op->dma_in ? s->d_buf + op->off_src : mapped ? src_base : base + op->off_src;
     uint8_t *dst = op->deliver ? s->d_buf + op->off_dst : mapped ? dst_base : base + op->off_dst;
     const uint32_t *conn = op->nlayers > 1 ? (const uint32_t *)(base + up16(op->nrec * sizeof(ptls_mi355x_tls_record_t))) : NULL;
+    const uint32_t *kidx = op->nsess > 1 ? (const uint32_t *)(base + op->off_kidx) : NULL;
     hipError_t e;
     int rc;
     /* the runtime's one-time copy setup, before the first copy rather than inside some later window's */
@@ -816,7 +884,15 @@ static int op_launch(rl_slot_t *s, const uint8_t *src_base, uint8_t *dst_base)
             rl_slow("an input H2D", t0);
     }
     t0 = tr ? rl_now() : 0;
-    if (op->is_seal)
+    if (kidx != NULL && op->is_seal) /* several sessions: one multi-key launch */
+        rc = ptls_mi355x_tls_seal_records_multikey(op->sess_ctx, op->sess_iv, op->nsess,
+                                                   (const ptls_mi355x_tls_record_t *)base, kidx, conn, op->nrec, src, dst,
+                                                   s->stream);
+    else if (kidx != NULL)
+        rc = ptls_mi355x_tls_open_records_multikey(op->sess_ctx, op->sess_iv, op->nsess,
+                                                   (const ptls_mi355x_tls_record_t *)base, kidx, conn, op->nrec, src, dst,
+                                                   (uint32_t *)(base + op->off_st), base + op->off_ty, 0, s->stream);
+    else if (op->is_seal)
         rc = ptls_mi355x_tls_seal_records_multi(s->ctx, op->layers[0]->iv, (const ptls_mi355x_tls_record_t *)base, conn,
                                                 op->nrec, src, dst, s->stream);
     else /* every record verified independently; the stop at a connection's first failure is the host loop in wait */
@@ -946,8 +1022,11 @@ static int seal_build(rl_slot_t *s, ptls_mi355x_record_layer_t *const *layers, s
     op->direct = direct;
     op->dma = dma;
     op->dma_in = dma_in;
+    if (op_sessions(s) != 0)
+        goto Fail;
     const size_t off_conn = up16(nrec * sizeof(ptls_mi355x_tls_record_t));
-    op->off_src = off_conn + (nlayers > 1 ? up16(nrec * 4) : 0);
+    op->off_kidx = off_conn + (nlayers > 1 ? up16(nrec * 4) : 0);
+    op->off_src = op->off_kidx + (op->nsess > 1 ? up16(nrec * 4) : 0);
     op->srcbytes = packed || dma_in ? srcbytes : 0;
     op->off_dst = op->off_src + up16(op->srcbytes);
     op->dstbytes = packed ? wire : 0;
@@ -958,7 +1037,7 @@ static int seal_build(rl_slot_t *s, ptls_mi355x_record_layer_t *const *layers, s
         goto Fail;
     /* descriptors (offsets relative to the src / dst bases), the per-record IV differences and, unless direct, the
      * fragments back to back */
-    uint32_t *conn = (uint32_t *)(s->h_buf + off_conn);
+    uint32_t *conn = (uint32_t *)(s->h_buf + off_conn), *kidx = (uint32_t *)(s->h_buf + op->off_kidx);
     size_t k = 0, src_off = 0, dst_off = 0;
     for (size_t l = 0; l < nlayers; ++l) {
         rl_part_t *p = &op->part[l];
@@ -967,7 +1046,8 @@ static int seal_build(rl_slot_t *s, ptls_mi355x_record_layer_t *const *layers, s
             dst_off = (size_t)(dev_addr_any(layers, nlayers, out[l], p->wire) - dst_base);
         if (dma && p->wire != 0) /* the layer's wire records, back to the caller's output in one copy */
             op->d2h[op->nd2h++] = (rl_copy_t){out[l], s->d_buf + op->off_dst + dst_off, p->wire};
-        const uint32_t cid = be32(layers[l]->iv) ^ be32(layers[0]->iv); /* BE32(cid) ^ IV[0..3] of layer 0 = layer l's */
+        /* BE32(cid) ^ IV[0..3] of its session's first layer = layer l's */
+        const uint32_t sess = op->sess_of[l], cid = be32(layers[l]->iv) ^ be32(op->sess_iv + 12 * sess);
         const size_t k0 = k;
         for (size_t f = 0; f < p->nfrags; ++f) {
             const ptls_mi355x_iovec_t *fr = &frags[l][f];
@@ -987,6 +1067,9 @@ static int seal_build(rl_slot_t *s, ptls_mi355x_record_layer_t *const *layers, s
         if (nlayers > 1)
             for (size_t i = k0; i < k; ++i)
                 conn[i] = cid;
+        if (op->nsess > 1)
+            for (size_t i = k0; i < k; ++i)
+                kidx[i] = sess;
     }
     memcpy(s->h_buf, s->recs, nrec * sizeof(ptls_mi355x_tls_record_t));
     if (op_launch(s, src_base, dst_base) != 0) {
@@ -1093,8 +1176,11 @@ static int open_build(rl_slot_t *s, ptls_mi355x_record_layer_t *const *layers, s
     op->deliver = deliver;
     op->dma_in = dma_in;
     op->max_part = max_part;
+    if (op_sessions(s) != 0)
+        goto Fail;
     const size_t off_conn = up16(nrec * sizeof(ptls_mi355x_tls_record_t));
-    op->off_src = off_conn + (nlayers > 1 ? up16(nrec * 4) : 0);
+    op->off_kidx = off_conn + (nlayers > 1 ? up16(nrec * 4) : 0);
+    op->off_src = op->off_kidx + (op->nsess > 1 ? up16(nrec * 4) : 0);
     op->srcbytes = packed || dma_in ? srcbytes : 0;
     op->off_dst = op->off_src + op->srcbytes;
     op->dstbytes = packed ? ptbytes : deliver ? slots16 : 0;
@@ -1107,7 +1193,7 @@ static int open_build(rl_slot_t *s, ptls_mi355x_record_layer_t *const *layers, s
         ((dma || dma_in) && op_copies(op, nlayers) != 0))
         goto Fail;
     ptls_mi355x_tls_deliver_t *dp = (ptls_mi355x_tls_deliver_t *)(s->h_buf + op->off_dp);
-    uint32_t *conn = (uint32_t *)(s->h_buf + off_conn);
+    uint32_t *conn = (uint32_t *)(s->h_buf + off_conn), *kidx = (uint32_t *)(s->h_buf + op->off_kidx);
     for (size_t l = 0, so = 0, dso = 0; l < nlayers; ++l) {
         rl_part_t *p = &op->part[l];
         if (deliver)
@@ -1148,12 +1234,14 @@ static int open_build(rl_slot_t *s, ptls_mi355x_record_layer_t *const *layers, s
             so += up16(p->cons);
             dso += up16(p->ptbytes);
         }
-        const uint32_t cid = be32(layers[l]->iv) ^ be32(layers[0]->iv);
+        const uint32_t sess = op->sess_of[l], cid = be32(layers[l]->iv) ^ be32(op->sess_iv + 12 * sess);
         for (size_t i = p->k0; i < p->k0 + p->n; ++i) {
             s->recs[i].src += p->src_add;
             s->recs[i].dst += p->dst_add;
             if (nlayers > 1)
                 conn[i] = cid;
+            if (op->nsess > 1)
+                kidx[i] = sess;
         }
     }
     memcpy(s->h_buf, s->recs, nrec * sizeof(ptls_mi355x_tls_record_t));
@@ -1413,7 +1501,7 @@ static rl_slot_t *submit_begin(ptls_mi355x_record_layer_t *const *layers, size_t
         rl_msg("no layers");
         return NULL;
     }
-    if (!same_session(layers, nlayers))
+    if (!same_key_size(layers, nlayers))
         return NULL;
     for (size_t l = 0; l < nlayers; ++l)
         if (layers[l]->nqueued != 0 && rl_flush(layers[l]) != 0)

@@ -103,7 +103,8 @@ def build():
         src = os.path.join(srcdir, "gcm_engine.hip")
         subprocess.run([b.HIPCC, f"--offload-arch={b.ARCH}", "-O3", "-std=c++17", "-fPIC", "-I" + b.CSRC, *flags, "-c",
                         src, "-o", obj], check=True)
-        subprocess.run([b.HIPCC, f"--offload-arch={b.ARCH}", "-shared", "-fPIC", "-o", so, obj] + b.C_OBJS, check=True)
+        subprocess.run([b.HIPCC, f"--offload-arch={b.ARCH}", "-shared", "-fPIC", "-o", so, obj] + b.C_OBJS +
+                       ["-L/opt/rocm/lib", "-lhsa-runtime64"], check=True)
         print("built", so)
 
 

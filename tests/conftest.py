@@ -8,6 +8,26 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+# where the engine's fault journal (rapido_amd/csrc/fault_journal.c) appends its report if the GPU signals a memory
+# fault: read after every GPU test (below), and merged back from the GPU box with the rest of gpurun_out/
+FAULT_LOG = os.environ.setdefault("RAPIDO_FAULT_LOG", os.path.join(ROOT, "gpurun_out", "fault_journal.log"))
+
+
+def _fault_log_size() -> int:
+    try:
+        return os.path.getsize(FAULT_LOG)
+    except OSError:
+        return 0
+
+
+def _fault_log_since(offset: int) -> str:
+    try:
+        with open(FAULT_LOG, "rb") as f:
+            f.seek(offset)
+            return f.read().decode(errors="replace")
+    except OSError:
+        return ""
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU; run with -m gpu")
@@ -32,21 +52,37 @@ def _gpu_work_checked(request):
     asynchronously, possibly after the kernel has completed (a faulting store does not stop its wave), so the check
     runs twice, RAPIDO_FAULT_SETTLE_MS (default 20) apart: round 5 saw the round-4 report again at the same place
     with the checks 3 ms apart, i.e. the report arrived later than that."""
+    gpu = request.node.get_closest_marker("gpu") is not None
+    if gpu:
+        os.makedirs(os.path.dirname(FAULT_LOG), exist_ok=True)
+    log0 = _fault_log_size()
+    import rapido_amd as ra
+    engines0 = set(id(e) for e in ra.LIVE_ENGINES)
     yield
-    if request.node.get_closest_marker("gpu") is None:
+    if not gpu:
         return
     import gc
     import time
 
-    import rapido_amd as ra
-    nerr = len(ra.FINALIZER_ERRORS)
+    nerr = ra.FINALIZER_ERROR_COUNT
+    # engines the test left open are released here, explicitly and in creation-independent order, before the checks
+    # (not at some later garbage collection): each release synchronises and reports, so an error is this test's
+    for eng in [e for e in list(ra.LIVE_ENGINES) if id(e) not in engines0]:
+        eng.close()
     gc.collect()
-    ra.device_check()
-    time.sleep(float(os.environ.get("RAPIDO_FAULT_SETTLE_MS", "20")) * 1e-3)
-    ra.device_check()
-    new = ra.FINALIZER_ERRORS[nerr:]
-    if new:
-        pytest.fail("finalizer errors: " + "; ".join(new))
+    try:
+        ra.device_check()
+        time.sleep(float(os.environ.get("RAPIDO_FAULT_SETTLE_MS", "20")) * 1e-3)
+        ra.device_check()
+    except RuntimeError as e:
+        # the journal's report, if the handler wrote one, names the faulting address and the launches around it
+        raise RuntimeError(f"{e}\n{_fault_log_since(log0)}") from None
+    report = _fault_log_since(log0)
+    if report:
+        pytest.fail("the GPU signalled a memory fault during this test (fault journal):\n" + report)
+    k = ra.FINALIZER_ERROR_COUNT - nerr
+    if k:
+        pytest.fail("finalizer errors: " + "; ".join(ra.FINALIZER_ERRORS[-k:]))
 
 
 @pytest.fixture(scope="session")

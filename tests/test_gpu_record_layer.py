@@ -231,13 +231,62 @@ def test_seal_multi_session_windows(family, transport, keylen):
     for lr, c, s, w, (wire, n) in zip(layers, cids, seqs, windows, got):
         want, end = oracle_window(key, conn_iv(iv, c), s, w)
         assert wire == want and n == end - s and lr.seq == end
-    # a layer with another key: refused, nothing advanced
+    # a layer of another session (another key) joins the same launch as a multi-key batch: its records are its own
+    # ptls_send output under its key (round 6; it used to be refused)
     other = layer(transport, bytes(keylen), conn_iv(iv, 1), seq=9)
+    before = [lr.seq for lr in layers[:2]]
+    got = ra.record_layer_seal_multi(layers[:2] + [other], windows[:2] + [[b"x" * 10]])
+    for lr, c, s, w, (wire, n) in zip(layers[:2], cids[:2], before, windows[:2], got[:2]):
+        want, end = oracle_window(key, conn_iv(iv, c), s, w)
+        assert wire == want and n == end - s and lr.seq == end
+    assert got[2] == (oracle_window(bytes(keylen), conn_iv(iv, 1), 9, [b"x" * 10])[0], 1) and other.seq == 10
+    # a layer of another key size cannot share a launch: refused, nothing advanced
+    odd = layer(transport, bytes(48 - keylen), conn_iv(iv, 1), seq=9)
     before = [lr.seq for lr in layers]
-    with pytest.raises(RuntimeError):
-        ra.record_layer_seal_multi(layers[:2] + [other], windows[:2] + [[b"x" * 10]])
-    assert [lr.seq for lr in layers] == before and other.seq == 9
-    for lr in layers + [other]:
+    with pytest.raises(RuntimeError, match="another key size"):
+        ra.record_layer_seal_multi(layers[:2] + [odd], windows[:2] + [[b"x" * 10]])
+    assert [lr.seq for lr in layers] == before and odd.seq == 9
+    for lr in layers + [other, odd]:
+        lr.close()
+
+
+@pytest.mark.parametrize("nsess", [2, 16])
+def test_windows_of_many_sessions_in_one_launch(family, transport, nsess):
+    """A server's connections of many sessions -- each session its own traffic key and IV, each connection its own
+    IV bytes 0..3 -- sealed in ONE launch (a multi-key batch): every connection's wire bytes are
+    its own ptls_send output; then the same windows, one tampered, opened in ONE launch: every connection gets what
+    its own ptls_receive would deliver."""
+    rng = np.random.default_rng(900 + nsess)
+    keylen = 16 if nsess == 2 else 32
+    keys = [rng.integers(0, 256, keylen, dtype=np.uint8).tobytes() for _ in range(nsess)]
+    ivs = [rng.integers(0, 256, 12, dtype=np.uint8).tobytes() for _ in range(nsess)]
+    conns = [(s, c) for s in range(nsess) for c in ((0, 5) if s % 3 == 0 else (1,))]
+    rng.shuffle(conns)
+    seqs = [int(x) for x in rng.integers(0, 1000, len(conns))]
+    tx = [layer(transport, keys[s], conn_iv(ivs[s], c), seq=q) for (s, c), q in zip(conns, seqs)]
+    windows = [[rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in rng.integers(0, 16385, k)]
+               for k in rng.integers(0, 5, len(conns))]
+    windows[0] = [rng.integers(0, 256, 1000, dtype=np.uint8).tobytes(), rng.integers(0, 256, 77, dtype=np.uint8).tobytes()]
+    got = ra.record_layer_seal_multi(tx, windows)
+    wires = []
+    for lr, (s, c), q, w, (wire, n) in zip(tx, conns, seqs, windows, got):
+        want, end = oracle_window(keys[s], conn_iv(ivs[s], c), q, w)
+        assert wire == want and n == end - q and lr.seq == end, (s, c)
+        wires.append(wire)
+    rx = [layer(transport, keys[s], conn_iv(ivs[s], c), seq=q) for (s, c), q in zip(conns, seqs)]
+    hit = 0
+    bad = bytearray(wires[hit])
+    first = 5 + len(windows[hit][0]) + 17
+    bad[first + 5] ^= 8  # the second record's first ciphertext byte
+    wires[hit] = bytes(bad)
+    res = ra.record_layer_open_multi(rx, wires)
+    for i, (lr, w, (alert, pt, cons, n)) in enumerate(zip(rx, windows, res)):
+        if i == hit:
+            assert (alert, pt, cons, n) == (20, w[0], first, 1) and lr.seq == seqs[i] + 1
+        else:
+            nrec = len([f for f in w if f])  # (an empty fragment makes no record)
+            assert alert == 0 and pt == b"".join(w) and cons == len(wires[i]) and n == nrec, i
+    for lr in tx + rx:
         lr.close()
 
 

@@ -87,7 +87,8 @@ def test_receive_matches_reference_ptls_receive(gpu, i):
     key, iv, wire = bytes.fromhex(c["key"]), bytes.fromhex(c["iv"]), bytes.fromhex(c["wire"])
     rc, orecs, used, _ = ra.tls_parse_records(wire, c["seq"])
     assert rc == 0 and len(orecs) == 1
-    pt, st, ty = open_(ra.Engine(key), iv, orecs, np.frombuffer(wire, np.uint8), int(orecs[0]["len"]))
+    with ra.Engine(key) as eng:
+        pt, st, ty = open_(eng, iv, orecs, np.frombuffer(wire, np.uint8), int(orecs[0]["len"]))
     if c["rc"] == 20:
         assert st[0] == ra.TLS_BAD_RECORD_MAC and not pt.any()
     elif c["rc"] == 10:
@@ -146,8 +147,8 @@ def test_open_padding_tamper_short(gpu):
     rc, orecs, used, _ = ra.tls_parse_records(buf, 0)
     assert rc == 0 and len(orecs) == len(wires) and used == len(buf)
     orecs["seq"] = seqs
-    pt, st, ty = open_(ra.Engine(key), iv, orecs, np.frombuffer(buf, np.uint8),
-                       int(orecs["dst"][-1]) + int(orecs["len"][-1]))
+    with ra.Engine(key) as eng:
+        pt, st, ty = open_(eng, iv, orecs, np.frombuffer(buf, np.uint8), int(orecs["dst"][-1]) + int(orecs["len"][-1]))
     for i, w in enumerate(wires):
         want = oracle.tls_open_record(key, iv, seqs[i], w)
         o = orecs[i]
@@ -216,6 +217,7 @@ def test_in_place(gpu):
     orecs = trecs.copy()
     orecs["src"], orecs["dst"], orecs["len"] = base, base + 5, np.array(lens) + 17
     pt, st, ty = open_(eng, iv, orecs, wire, 0, inplace=True)
+    eng.close()  # explicitly, after its launches' results are read back (not at a later collection)
     assert list(st[: len(lens)]) == lens
     for i, ln in enumerate(lens):
         assert pt[base[i] + 5: base[i] + 5 + ln].tobytes() == frags[i]

@@ -216,3 +216,66 @@ def test_contexts_on_each_present_device(gpu):
     with pytest.raises(RuntimeError, match=f"device ordinal {n} is not present"):
         ra.Engine(key, device=n)
     assert torch.cuda.current_device() == cur
+
+
+def _place_worker(rank, world, port, q, sysfs):
+    """bench.place_rank on gloo, world size 2: each rank's GPU (a fake PCI address per rank in a fake sysfs tree) on
+    its own NUMA node; the rank pins itself to that node's CPUs and the fields ride in its line (gather_rank_stats)."""
+    import torch.distributed as dist
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    place = bench.place_rank(rank, bus_id=f"0000:0{rank + 1}:00.0", sysfs=sysfs)
+    mine = {"rank": rank, "host": "h", "device": rank, "device_name": "gfx950", "rank_gibps": 1.0,
+            "rank_ms_per_step": 1.0, "seal_gibps": 1.0, "open_gibps": 1.0, "launch_ms": 1.0,
+            "numa_node": place["numa_node"], "cpus": place["cpus"], "pci_bus_id": place["pci_bus_id"]}
+    ranks = bench.gather_rank_stats(mine)
+    errs = bench.fail_together("verification failed" if rank == 1 else None)
+    q.put((rank, place, sorted(os.sched_getaffinity(0)), ranks, errs))
+    dist.destroy_process_group()
+
+
+def test_ranks_placed_on_their_gpus_numa_nodes(tmp_path):
+    """every rank's host work sits on its GPU's NUMA node (PCI address -> numa_node ->
+    local_cpulist), its line carries numa_node / cpus / pci_bus_id, and a rank's failure reaches every rank."""
+    allowed = sorted(os.sched_getaffinity(0))
+    if len(allowed) < 2:
+        pytest.skip("needs two CPUs")
+    half = len(allowed) // 2
+    nodes = [allowed[:half], allowed[half:]]
+    import bench
+    for r in range(2):
+        d = tmp_path / f"0000:0{r + 1}:00.0"
+        d.mkdir()
+        (d / "numa_node").write_text(f"{r}\n")
+        (d / "local_cpulist").write_text(bench.cpulist(nodes[r]) + "\n")
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_place_worker, args=(r, world, port, q, str(tmp_path))) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, place, affinity, ranks, errs in res:
+        assert place["numa_node"] == rank and place["pinned"] and affinity == nodes[rank]
+        assert place["cpus"] == bench.cpulist(nodes[rank])
+        assert [r["numa_node"] for r in ranks] == [0, 1]
+        assert [r["cpus"] for r in ranks] == [bench.cpulist(n) for n in nodes]
+        assert [r["pci_bus_id"] for r in ranks] == ["0000:01:00.0", "0000:02:00.0"]
+        assert errs == [None, "verification failed"]  # every rank learns that rank 1 failed
+
+
+def test_placement_without_a_numa_node_is_reported_not_guessed(tmp_path):
+    import bench
+    d = tmp_path / "0000:09:00.0"
+    d.mkdir()
+    (d / "numa_node").write_text("-1\n")
+    before = os.sched_getaffinity(0)
+    place = bench.place_rank(0, bus_id="0000:09:00.0", sysfs=str(tmp_path))
+    assert place["numa_node"] is None and not place["pinned"] and os.sched_getaffinity(0) == before
+    assert bench.place_rank(0, bus_id="0000:0a:00.0", sysfs=str(tmp_path))["numa_node"] is None  # no such device
+    assert bench.parse_cpulist("0-3,8,10-11") == [0, 1, 2, 3, 8, 10, 11]
+    assert bench.cpulist([0, 1, 2, 3, 8, 10, 11]) == "0-3,8,10-11"
