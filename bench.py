@@ -56,9 +56,13 @@ WORKLOADS = {
     "16k-max-aes128": dict(name="AES-128-GCM seal+open, 256K x 16385 B TLS-max records", key=16, n=1 << 18,
                            length=16385),
     "ragged": dict(name="AES-128-GCM seal+open, 1M records U{64..16384} B", key=16, n=1 << 20, length=None),
+    # multi-key batches (SURVEY.md 8(d) "K distinct keys with a per-record key index"): a server's 64 sessions, each
+    # record of a random session, one launch each way (the launch's by-key sort inside the timed step)
+    "1400-mk64": dict(name="AES-128-GCM seal+open, 1M x 1400 B TLS records of 64 sessions (per-record key index)",
+                      key=16, n=1 << 20, length=1400, keys=64),
 }
 # the single-GPU configs measured beside `value` at N=1: the north-star config first
-SIDE_WORKLOADS = "16k-aes128,16k,ragged"
+SIDE_WORKLOADS = "16k-aes128,16k,ragged,1400-mk64"
 
 CPU_BENCH = os.path.join(ROOT, "oracle", "_ref", "ref_fusion_bench")
 PTLSBENCH = os.path.join(ROOT, "oracle", "_ref", "ptlsbench")
@@ -451,6 +455,14 @@ def measure(ra, wl_key, args, dev, rank, world, check):
     key = bytes(range(wl["key"]))
     iv = bytes(range(0xA0, 0xAC))
     eng = ra.Engine(key)
+    mk = d_kidx = None
+    if wl.get("keys"):  # one context and IV per session; every record of a random session
+        nk = wl["keys"]
+        mk_engines = [eng] + [ra.Engine(bytes((b + 7 * k) & 0xFF for b in range(wl["key"]))) for k in range(1, nk)]
+        mk = ra.MultiKey(mk_engines, [bytes((b + k) & 0xFF for b in range(0xA0, 0xAC)) for k in range(nk)])
+        d_kidx = torch.from_numpy(rng.integers(0, nk, n).astype(np.int32)).to(dev)
+        if args.pipeline != 1:
+            raise SystemExit("bench: the multi-key workload runs one launch each way (--pipeline 1)")
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
     ragged = wl["length"] is None
@@ -469,7 +481,11 @@ def measure(ra, wl_key, args, dev, rank, world, check):
 
     def seal_chunk(e, s, r0, cnt):
         rp = d_recs.data_ptr() + r0 * DESC_BYTES
-        if ragged:
+        if mk is not None:  # every session's records in one launch; the by-key device sort in the step, shared with open
+            mk.order_by_key(d_kidx.data_ptr() + 4 * r0, cnt, d_order.data_ptr() + 4 * r0, s)
+            mk.seal_batch_ordered(rp, d_kidx.data_ptr() + 4 * r0, d_order.data_ptr() + 4 * r0, cnt, d_src.data_ptr(),
+                                  d_ct.data_ptr(), d_aad.data_ptr(), s)
+        elif ragged:
             # length-binned, longest-first schedule; the device sort is inside the timed step
             e.order_by_length(rp, cnt, d_order.data_ptr() + 4 * r0, s)
             e.seal_batch_ordered(iv, rp, d_order.data_ptr() + 4 * r0, cnt, d_src.data_ptr(), d_ct.data_ptr(),
@@ -479,7 +495,10 @@ def measure(ra, wl_key, args, dev, rank, world, check):
 
     def open_chunk(e, s, r0, cnt):
         rp = d_recs.data_ptr() + r0 * DESC_BYTES
-        if ragged:
+        if mk is not None:
+            mk.open_batch_ordered(rp, d_kidx.data_ptr() + 4 * r0, d_order.data_ptr() + 4 * r0, cnt, d_ct.data_ptr(),
+                                  d_pt.data_ptr(), d_aad.data_ptr(), d_st.data_ptr() + 4 * r0, s)
+        elif ragged:
             e.open_batch_ordered(iv, rp, d_order.data_ptr() + 4 * r0, cnt, d_ct.data_ptr(), d_pt.data_ptr(),
                                  d_aad.data_ptr(), d_st.data_ptr() + 4 * r0, s)
         else:
@@ -585,8 +604,9 @@ def measure(ra, wl_key, args, dev, rank, world, check):
     # the whole timed region: every launch's algorithmic bytes over the region's HIP-event time (with chunks > 1 the
     # launches overlap at their ends)
     achieved_region = (seal_b + open_b) * args.steps / (region_ms * 1e-3) / 1e9
-    kname = ra.kernel_name(dom_is_seal, wl["key"], n)
-    chunk_kernels = sorted({ra.kernel_name(s, wl["key"], r1 - r0) for s in (True, False) for _, r0, r1 in chunks})
+    kname_of = ra.kernel_name if mk is None else (lambda s_, k_, n_: ra.kernel_name_multikey(s_, k_, n_, False))
+    kname = kname_of(dom_is_seal, wl["key"], n)
+    chunk_kernels = sorted({kname_of(s, wl["key"], r1 - r0) for s in (True, False) for _, r0, r1 in chunks})
 
     # HBM bytes per launch from PMC counters: rocprofv3 cannot run inside this process, so this is the builder's
     # counter pass of the same workload and kernel (scripts/collect_profiles.py), labelled as such in the line
@@ -639,6 +659,13 @@ def measure(ra, wl_key, args, dev, rank, world, check):
     }
     for e in engs[1:]:
         e.close()
+    if mk is not None:
+        res["sessions"] = {"keys": len(mk), "records_per_key": n // len(mk), "assignment": "uniform random per record",
+                           "note": "one launch each way over every session's records (ptls_mi355x_*_batch_multikey_"
+                                   "ordered); the by-key device sort (ptls_mi355x_order_by_key) runs once per step, "
+                                   "in the timed step, as the ragged workload's length sort does"}
+        for e in mk.engines[1:]:
+            e.close()
     extra = dict(eng=eng, iv=iv, d_src=d_src, d_ct=d_ct, d_pt=d_pt, d_st=d_st, d_recs=d_recs, d_aad=d_aad, recs=recs,
                  n=n, src_bytes=src_bytes, payload=payload, stream=stream, key=wl["key"])
     return res, extra

@@ -224,6 +224,21 @@ int ptls_mi355x_seal_batch_multikey(ptls_mi355x_aesgcm_context_t *const *ctxs, c
 int ptls_mi355x_open_batch_multikey(ptls_mi355x_aesgcm_context_t *const *ctxs, const void *static_ivs, size_t nkeys,
                                     const ptls_mi355x_record_t *recs, const uint32_t *key_idx, size_t n,
                                     const uint8_t *src, uint8_t *dst, const uint8_t *aad, uint32_t *status, void *stream);
+/* The by-key sort once for several launches over the same records (a batch's seal and open): ptls_mi355x_order_by_key
+ * fills `order` (n device uint32) with the descriptor indices grouped by key index, keys ascending, out-of-range
+ * indices last (within a key the order is unspecified: a device counting sort), on ctx's scratch and `stream`; the
+ * _ordered launches take it instead of grouping.  The order must be one of ptls_mi355x_order_by_key's for these key
+ * indices. */
+int ptls_mi355x_order_by_key(ptls_mi355x_aesgcm_context_t *ctx, const uint32_t *key_idx, size_t n, size_t nkeys,
+                             uint32_t *order, void *stream);
+int ptls_mi355x_seal_batch_multikey_ordered(ptls_mi355x_aesgcm_context_t *const *ctxs, const void *static_ivs,
+                                            size_t nkeys, const ptls_mi355x_record_t *recs, const uint32_t *key_idx,
+                                            const uint32_t *order, size_t n, const uint8_t *src, uint8_t *dst,
+                                            const uint8_t *aad, void *stream);
+int ptls_mi355x_open_batch_multikey_ordered(ptls_mi355x_aesgcm_context_t *const *ctxs, const void *static_ivs,
+                                            size_t nkeys, const ptls_mi355x_record_t *recs, const uint32_t *key_idx,
+                                            const uint32_t *order, size_t n, const uint8_t *src, uint8_t *dst,
+                                            const uint8_t *aad, uint32_t *status, void *stream);
 
 /* ======================================================================================
  * 4. TLS 1.3 record framing in the batch.  The framing of picotls's

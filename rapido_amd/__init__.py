@@ -82,7 +82,8 @@ EXPORTED_FUNCTIONS = (
     "ptls_mi355x_fault_journal_faults", "ptls_mi355x_fault_journal_report", "ptls_mi355x_fault_journal_note",
     "ptls_mi355x_slot_engine_errors", "ptls_mi355x_test_slot_without_engine", "ptls_mi355x_test_inject_engine_errors",
     "ptls_mi355x_seal_batch_multikey", "ptls_mi355x_open_batch_multikey", "ptls_mi355x_tls_seal_records_multikey",
-    "ptls_mi355x_tls_open_records_multikey", "ptls_mi355x_kernel_name_multikey",
+    "ptls_mi355x_tls_open_records_multikey", "ptls_mi355x_kernel_name_multikey", "ptls_mi355x_order_by_key",
+    "ptls_mi355x_seal_batch_multikey_ordered", "ptls_mi355x_open_batch_multikey_ordered",
 )
 EXPORTED_OBJECTS = ("ptls_mi355x_aes128gcm", "ptls_mi355x_aes256gcm", "ptls_mi355x_aes128ctr",
                     "ptls_mi355x_aes256ctr", "ptls_mi355x_aes128ecb", "ptls_mi355x_aes256ecb")
@@ -247,6 +248,9 @@ def lib() -> C.CDLL:
             L.ptls_mi355x_tls_open_records_multikey.argtypes = [vp, vp, sz, vp, vp, vp, sz, vp, vp, vp, vp, C.c_int, vp]
             L.ptls_mi355x_kernel_name_multikey.argtypes = [C.c_int, sz, sz, C.c_int]
             L.ptls_mi355x_kernel_name_multikey.restype = C.c_char_p
+            L.ptls_mi355x_order_by_key.argtypes = [vp, vp, sz, sz, vp, vp]
+            L.ptls_mi355x_seal_batch_multikey_ordered.argtypes = [vp, vp, sz, vp, vp, vp, sz, vp, vp, vp, vp]
+            L.ptls_mi355x_open_batch_multikey_ordered.argtypes = [vp, vp, sz, vp, vp, vp, sz, vp, vp, vp, vp, vp]
             global FAULT_JOURNAL_STATUS
             if os.environ.get("RAPIDO_FAULT_JOURNAL", "1") != "0":
                 # before the first HIP call of the process where possible (tests/conftest.py sets the path)
@@ -581,6 +585,22 @@ class MultiKey:
         if lib().ptls_mi355x_open_batch_multikey(self.ctxs, self.ivs, len(self), recs_ptr, key_idx_ptr, n, src_ptr,
                                                  dst_ptr, aad_ptr, status_ptr, stream or None):
             raise RuntimeError("open_batch_multikey failed: " + last_error())
+
+    def order_by_key(self, key_idx_ptr, n, order_ptr, stream: int = 0) -> None:
+        """The records sorted by key once, for several _ordered launches (ptls_mi355x_order_by_key)."""
+        if lib().ptls_mi355x_order_by_key(self.ctxs[0], key_idx_ptr, n, len(self), order_ptr, stream or None):
+            raise RuntimeError("order_by_key failed: " + last_error())
+
+    def seal_batch_ordered(self, recs_ptr, key_idx_ptr, order_ptr, n, src_ptr, dst_ptr, aad_ptr, stream: int = 0):
+        if lib().ptls_mi355x_seal_batch_multikey_ordered(self.ctxs, self.ivs, len(self), recs_ptr, key_idx_ptr, order_ptr,
+                                                         n, src_ptr, dst_ptr, aad_ptr, stream or None):
+            raise RuntimeError("seal_batch_multikey_ordered failed: " + last_error())
+
+    def open_batch_ordered(self, recs_ptr, key_idx_ptr, order_ptr, n, src_ptr, dst_ptr, aad_ptr, status_ptr,
+                           stream: int = 0):
+        if lib().ptls_mi355x_open_batch_multikey_ordered(self.ctxs, self.ivs, len(self), recs_ptr, key_idx_ptr, order_ptr,
+                                                         n, src_ptr, dst_ptr, aad_ptr, status_ptr, stream or None):
+            raise RuntimeError("open_batch_multikey_ordered failed: " + last_error())
 
     def tls_seal_records(self, recs_ptr, key_idx_ptr, n, src_ptr, dst_ptr, stream: int = 0, conn_ptr: int = 0) -> None:
         if lib().ptls_mi355x_tls_seal_records_multikey(self.ctxs, self.ivs, len(self), recs_ptr, key_idx_ptr,

@@ -203,34 +203,29 @@ struct MkLaunch {
     uint32_t *wg_key; /* per workgroup: the key of its current phase (the workgroup's broadcast slot) */
 };
 
-template <int NR, int K, bool SEAL, bool FRAME, bool MK = false>
+template <int NR, int K, bool SEAL, bool FRAME>
 __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, uint32_t iv0, uint32_t iv1, uint32_t iv2,
                                                const void *__restrict__ descs, const uint32_t *__restrict__ order,
                                                uint32_t nrecs, const uint8_t *src, uint8_t *dst,
                                                const uint8_t *__restrict__ aad, uint32_t *__restrict__ status,
                                                uint8_t *__restrict__ types, uint32_t *__restrict__ work,
-                                               uint32_t work_base, const uint32_t *__restrict__ conn,
-                                               MkLaunch mk = MkLaunch{nullptr, 0u, nullptr, nullptr})
+                                               uint32_t work_base, const uint32_t *__restrict__ conn)
 {
     static_assert(K <= MAX_KERNEL_K, "LDS holds at most MAX_KERNEL_K GHASH tables");
-    static_assert(!MK || Layout<K>::gh8, "multi-key batches run the GH8 layout (K = 4)");
     __shared__ __attribute__((aligned(16))) uint8_t lds[Layout<K>::total];
     constexpr uint32_t R = 64 / K; /* records per wave step */
     const Record *__restrict__ recs = (const Record *)descs;
     const TlsRecord *__restrict__ trecs = (const TlsRecord *)descs;
 
+    fill_lds(lds, c_tabs.t0, ki, K, threadIdx.x, blockDim.x);
+
     uint32_t rk[4 * (NR + 1)], kr[4 * (NR + 1)];
-    if constexpr (!MK) {
-        fill_lds(lds, c_tabs.t0, ki, K, threadIdx.x, blockDim.x);
 #pragma unroll
-        for (int i = 0; i < 4 * (NR + 1); ++i) {
-            rk[i] = ki->rk[i];
-            kr[i] = rotl32(rk[i], 16); /* GH8 layout: the round keys of aes_round_tt2k_asm (wave-uniform) */
-        }
-        __syncthreads();
-    } else {
-        fill_lds_aes(lds, c_tabs.t0, K, threadIdx.x, blockDim.x); /* the key-independent AES image, once */
+    for (int i = 0; i < 4 * (NR + 1); ++i) {
+        rk[i] = ki->rk[i];
+        kr[i] = rotl32(rk[i], 16); /* GH8 layout: the round keys of aes_round_tt2k_asm (wave-uniform) */
     }
+    __syncthreads();
 
     const uint32_t lane = threadIdx.x & 63u;
 #if GCM_LANE_MAJOR
@@ -266,6 +261,200 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
     for (uint32_t i = 0, n = (threadIdx.x >> 8) * (uint32_t)GCM_STAGGER; i < n; ++i)
         __builtin_amdgcn_s_sleep(127);
 #endif
+
+    /*
+     * Record groups (64/K records) are handed out dynamically: one returning atomic per group
+     * (MI355X_MICROARCH.md "dequeue": ~1 us under load, against ~100 us of work per group).
+     * With `order` sorted by length (ptls_mi355x_order_by_length) this is longest-first
+     * scheduling, and each group holds records of similar length.
+     */
+#if GCM_STATIC_GROUPS /* measurement builds: group k of wave w is w + k * (waves in the grid), no atomic */
+    const uint32_t wave_id = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), nwaves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t gs = wave_id;; gs += nwaves) {
+        const uint32_t g = __builtin_amdgcn_readfirstlane(gs);
+        (void)work;
+        (void)work_base;
+#else
+    for (;;) {
+        uint32_t g = 0;
+        if (lane == 0)
+            g = atomicAdd(work, 1u) - work_base; /* tickets of this launch start at work_base (mod 2^32) */
+        g = (uint32_t)__shfl((int)g, 0, 64);
+#endif
+        if (g >= ngroups)
+            break;
+        const uint32_t idx = g * R + slot;
+        const bool in_batch = idx < nrecs;
+        const uint32_t r = in_batch ? (order ? order[idx] : idx) : 0u;
+        Record rec = {0, 0, 0, 0, 0, 0};
+        uint32_t ctype = 0u;
+        bool valid = in_batch;
+        if (FRAME) {
+            if (in_batch) {
+                const TlsRecord t = trecs[r];
+                rec.seq = t.seq;
+                rec.aadlen = 5u;
+                if (SEAL) { /* header at t.dst, ciphertext after it */
+                    rec.src = t.src;
+                    rec.dst = t.dst + 5u;
+                    rec.len = t.len;
+                    ctype = t.type;
+                    valid = t.len <= PTLS_MI355X_TLS_MAX_FRAGMENT; /* larger: not a TLS record, nothing written */
+                } else { /* header at t.src; length field = ciphertext + tag */
+                    rec.src = t.src + 5u;
+                    rec.dst = t.dst;
+                    rec.len = t.len >= 16u ? t.len - 16u : 0u;
+                    valid = t.len >= 16u; /* shorter: bad_record_mac without a walk (aead_do_decrypt) */
+                }
+            }
+        } else if (in_batch) {
+            rec = recs[r];
+        }
+        const uint32_t plen = FRAME && SEAL ? rec.len + 1u : rec.len;
+        const Walk wk = make_walk(plen, rec.aadlen, K, walk_out16(dst + rec.dst));
+        uint32_t Tmax = valid ? wk.T : 0u;
+        /* the steps in which every lane of the wave holds a whole payload block (walk_interior): lane_walk's fast path */
+        uint32_t f_lo = 0xffffffffu, f_hi = 0u;
+        if (GCM_FAST_STEP && valid)
+            walk_interior(wk, j, K, rec.len, f_lo, f_hi);
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            Tmax = max(Tmax, shfl_xor_u32(Tmax, o));
+            f_lo = max(f_lo, shfl_xor_u32(f_lo, o));
+            f_hi = min(f_hi, shfl_xor_u32(f_hi, o));
+        }
+        f_lo = __builtin_amdgcn_readfirstlane(f_lo);
+        f_hi = __builtin_amdgcn_readfirstlane(f_hi);
+#if GCM_UNIFORM_TMAX
+        Tmax = __builtin_amdgcn_readfirstlane(Tmax); /* the walk's trip tests on the scalar unit */
+#endif
+
+        const uint32_t n1 = iv1 ^ bswap32((uint32_t)(rec.seq >> 32)), n2 = iv2 ^ bswap32((uint32_t)rec.seq);
+        /* per-connection IV (rapido derive_connection_aead_iv, lib/rapido.c:127-133): IV bytes 0..3 ^= BE32(id) */
+        const uint32_t n0 = conn != nullptr && in_batch ? iv0 ^ bswap32(conn[r]) : iv0;
+        /* 16 always-readable bytes for idle prefetch slots: the first descriptor (>= 32 B, nrecs >= 1) */
+        const uint8_t *dummy = (const uint8_t *)descs;
+        u32x4 part = lane_walk<NR, K, SEAL, FRAME, Layout<K>, GCM_BATCH_PF>(lds, lanesel, rk, j, rec, valid, Tmax, n0, n1,
+                                                                           n2, src, dst, aad, dummy, ctype, nullptr, 0u, kr,
+                                                                           f_lo, f_hi);
+        if (GCM_LANE_MAJOR && GCM_PASS_LANES && K == 4) {
+            part ^= shfl_xor_u32x4(part, 4);
+            part ^= shfl_xor_u32x4(part, 32);
+        } else {
+#pragma unroll
+            for (int o = GCM_LANE_MAJOR ? (int)R : 1; o < (GCM_LANE_MAJOR ? 64 : K); o <<= 1)
+                part ^= shfl_xor_u32x4(part, o);
+        }
+
+        if (SEAL) {
+            if (j == 0 && valid) {
+                *(u32x4_u *)(dst + rec.dst + plen) = part;
+                if (FRAME) { /* record header 17 03 03 BE16(plen + 16) (buffer_push_record, lib/picotls.c:658-662) */
+                    const uint32_t reclen = plen + 16u;
+                    store_partial(dst + rec.dst - 5u, 5u, u32x4{0x00030317u | ((reclen >> 8) & 0xffu) << 24, reclen & 0xffu,
+                                                             0u, 0u});
+                }
+            }
+        } else {
+            /* part = computed tag ^ received tag (lane_walk) */
+            const bool bad = in_batch && (!valid || (part[0] | part[1] | part[2] | part[3]) != 0u);
+            if (j == 0 && in_batch && !FRAME)
+                status[r] = bad ? 0xffffffffu : rec.len;
+            if (bad) {
+                /*
+                 * Failed open: do not release plaintext (fusion leaves it, lib/fusion.c:656-679).
+                 * Rare path: the descriptor is re-read through an opaque pointer so the walk does
+                 * not keep dst/len alive in registers for it.
+                 */
+                uint64_t odst;
+                uint32_t olen;
+                if (FRAME) {
+                    const TlsRecord *tp = trecs + r;
+                    asm volatile("" : "+v"(tp));
+                    const TlsRecord again = *tp;
+                    odst = again.dst;
+                    olen = again.len >= 16u ? again.len - 16u : 0u;
+                    if (j == 0) {
+                        status[r] = 0xffffffffu; /* PTLS_ALERT_BAD_RECORD_MAC */
+                        types[r] = 0u;
+                    }
+                } else {
+                    const Record *rp = recs + r;
+                    asm volatile("" : "+v"(rp));
+                    const Record again = *rp;
+                    odst = again.dst;
+                    olen = again.len;
+                }
+                uint8_t *out = dst + odst;
+                for (uint32_t off = 16u * j; off < olen; off += 16u * K) {
+                    uint32_t n = olen - off;
+                    u32x4 z = {0u, 0u, 0u, 0u};
+                    if (n >= 16)
+                        *(u32x4_u *)(out + off) = z;
+                    else
+                        store_partial(out + off, n, z);
+                }
+            } else if (FRAME && in_batch && j == 0) {
+                /*
+                 * Verified record: skip the zero padding and pop the content type
+                 * (handle_input_tls13, lib/picotls.c:4784-4791), reading back the plaintext the
+                 * record's K lanes have just stored (made visible to this lane by the fence).
+                 */
+                __threadfence_block();
+                const uint8_t *pt = dst + rec.dst;
+                uint32_t n = plen, found = 0xfffffffeu; /* PTLS_ALERT_UNEXPECTED_MESSAGE if all zero */
+                uint32_t ty = 0u;
+                while (n != 0u && found == 0xfffffffeu) {
+                    const uint32_t base = n >= 16u ? n - 16u : 0u;
+                    const u32x4 v = n >= 16u ? *(const u32x4_u *)(pt + base) : load_partial(pt, n);
+#pragma unroll
+                    for (int d = 3; d >= 0; --d) {
+                        if (found == 0xfffffffeu && v[d] != 0u) {
+                            const uint32_t b = (31u - (uint32_t)__builtin_clz(v[d])) >> 3; /* highest nonzero byte */
+                            found = base + 4u * (uint32_t)d + b;
+                            ty = (v[d] >> (8u * b)) & 0xffu;
+                        }
+                    }
+                    n = base;
+                }
+                status[r] = found;
+                types[r] = (uint8_t)ty;
+            }
+        }
+    }
+}
+
+/*
+ * Multi-key batch kernels: gcm_batch_body's record walk in key phases (below).  The single-key body above is kept as
+ * it was -- expressed through the shared group lambda it compiled to a slightly different hot loop, 1% slower seal at
+ * 1400 B on one box (profiles/r06c_ablate.txt) -- so the group body is written twice; tests/test_gpu_multikey.py
+ * checks this one against the oracle and against single-key launches.
+ */
+template <int NR, int K, bool SEAL, bool FRAME>
+__device__ __forceinline__ void gcm_batch_body_mk(const void *__restrict__ descs, const uint32_t *__restrict__ order,
+                                                  uint32_t nrecs, const uint8_t *src, uint8_t *dst,
+                                                  const uint8_t *__restrict__ aad, uint32_t *__restrict__ status,
+                                                  uint8_t *__restrict__ types, const uint32_t *__restrict__ conn,
+                                                  MkLaunch mk)
+{
+    static_assert(Layout<K>::gh8, "multi-key batches run the GH8 layout (K = 4)");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[Layout<K>::total];
+    constexpr uint32_t R = 64 / K; /* records per wave step */
+    const Record *__restrict__ recs = (const Record *)descs;
+    const TlsRecord *__restrict__ trecs = (const TlsRecord *)descs;
+
+    uint32_t rk[4 * (NR + 1)], kr[4 * (NR + 1)];
+    fill_lds_aes(lds, c_tabs.t0, K, threadIdx.x, blockDim.x); /* the key-independent AES image, once */
+
+    const uint32_t lane = threadIdx.x & 63u;
+#if GCM_LANE_MAJOR /* the lanes of a record as in gcm_batch_body */
+    const uint32_t q = (lane & 31u) >> 2;
+    const uint32_t j = GCM_PASS_LANES && K == 4 ? 2u * (lane >> 5) + ((0x96u >> q) & 1u) : lane / R;
+    const uint32_t slot = GCM_PASS_LANES && K == 4 ? 4u * (q >> 1) + (lane & 3u) : lane % R;
+#else
+    const uint32_t j = lane % K, slot = lane / K;
+#endif
+    const uint32_t lanesel = (lane & 31u) * 4u | 0x10000u; /* bank + image-B select (gcm_core.h) */
 
     /* one record group: lane (j, slot) walks record order[idx] (idx itself without an order) if in_batch */
     auto run_group = [&](uint32_t idx, bool in_batch, uint32_t iv0, uint32_t iv1, uint32_t iv2) {
@@ -407,32 +596,7 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
         }
     };
 
-    if constexpr (!MK) {
-    /*
-     * Record groups (64/K records) are handed out dynamically: one returning atomic per group
-     * (MI355X_MICROARCH.md "dequeue": ~1 us under load, against ~100 us of work per group).
-     * With `order` sorted by length (ptls_mi355x_order_by_length) this is longest-first
-     * scheduling, and each group holds records of similar length.
-     */
-#if GCM_STATIC_GROUPS /* measurement builds: group k of wave w is w + k * (waves in the grid), no atomic */
-    const uint32_t wave_id = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), nwaves = gridDim.x * (blockDim.x >> 6);
-    for (uint32_t gs = wave_id;; gs += nwaves) {
-        const uint32_t g = __builtin_amdgcn_readfirstlane(gs);
-        (void)work;
-        (void)work_base;
-#else
-    for (;;) {
-        uint32_t g = 0;
-        if (lane == 0)
-            g = atomicAdd(work, 1u) - work_base; /* tickets of this launch start at work_base (mod 2^32) */
-        g = (uint32_t)__shfl((int)g, 0, 64);
-#endif
-        if (g >= ngroups)
-            break;
-        const uint32_t idx = g * R + slot;
-        run_group(idx, idx < nrecs, iv0, iv1, iv2);
-    }
-    } else {
+    {
         /*
          * Multi-key phases.  The LDS holds one key's GHASH tables, shared by the workgroup's 16 waves, so a workgroup
          * works on one key at a time: its waves take that key's record groups from the key's counter, exactly as the
@@ -461,7 +625,13 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
                 if (lane == 0u)
                     __hip_atomic_store(mk.wg_key + blockIdx.x, pick, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            __threadfence(); /* the pick is in L2 before the barrier: the other waves read it there (agent scope) */
+            /*
+             * The pick reaches L2 before the barrier (a workgroup fence: wave 0 waits for its store), and the other waves
+             * read it from L2 (agent-scope atomic loads bypass the CU's L1).  An agent-scope __threadfence() here wrote
+             * back and invalidated L2 (buffer_wbl2 / buffer_inv sc1) at every phase of every workgroup: a one-key batch
+             * on these kernels ran 13% slower than on the single-key ones (profiles/r06e_mk_layout_probe.txt).
+             */
+            __threadfence_block();
             __syncthreads();
             const uint32_t k = __builtin_amdgcn_readfirstlane(
                 __hip_atomic_load(mk.wg_key + blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -470,9 +640,11 @@ __device__ __forceinline__ void gcm_batch_body(const KeyImage *__restrict__ ki, 
             /* the key's fields are wave-uniform: SGPRs, as the single-key kernels' arguments are (the round keys must be,
              * for the asm rounds) */
             const MkKey *kp = mk.keys + k;
-            const KeyImage *kki = (const KeyImage *)(uintptr_t)(((uint64_t)__builtin_amdgcn_readfirstlane(
-                                                                     (uint32_t)((uintptr_t)kp->ki >> 32)) << 32) |
-                                                                 __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)kp->ki));
+            /* (readfirstlane returns int: each half widened as uint32_t, or a low half >= 2^31 would sign-extend over
+             * the high half -- the first report of the fault journal) */
+            const uint64_t ki_lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)kp->ki),
+                           ki_hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)kp->ki >> 32));
+            const KeyImage *kki = (const KeyImage *)(uintptr_t)(ki_hi << 32 | ki_lo);
             const uint32_t kfirst = __builtin_amdgcn_readfirstlane(kp->first),
                            count = __builtin_amdgcn_readfirstlane(kp->end) - kfirst;
             const uint32_t kiv0 = __builtin_amdgcn_readfirstlane(kp->iv0), kiv1 = __builtin_amdgcn_readfirstlane(kp->iv1),
@@ -1046,7 +1218,7 @@ MI355X_GCM_KERNEL_F(mi355x_tls_seal_aes256_k4, 14, 4, true, true)
 MI355X_GCM_KERNEL_F(mi355x_tls_open_aes128_k4, 10, 4, false, true)
 MI355X_GCM_KERNEL_F(mi355x_tls_open_aes256_k4, 14, 4, false, true)
 
-/* multi-key batches (K = 4, GH8): the records of many keys in one launch, `order` sorted by key (gcm_batch_body MK) */
+/* multi-key batches (K = 4, GH8): the records of many keys in one launch, `order` sorted by key (gcm_batch_body_mk) */
 #define MI355X_GCM_KERNEL_MK(NAME, NR, SEAL, FRAME)                                                                    \
     extern "C" __global__ __launch_bounds__(WG_THREADS) void NAME(                                                     \
         const MkKey *__restrict__ keys, uint32_t nkeys, uint32_t *__restrict__ ctr, uint32_t *__restrict__ wg_key,     \
@@ -1054,8 +1226,8 @@ MI355X_GCM_KERNEL_F(mi355x_tls_open_aes256_k4, 14, 4, false, true)
         uint8_t *dst, const uint8_t *__restrict__ aad, uint32_t *__restrict__ st, uint8_t *__restrict__ types,         \
         const uint32_t *__restrict__ conn)                                                                             \
     {                                                                                                                  \
-        gcm_batch_body<NR, 4, SEAL, FRAME, true>(nullptr, 0u, 0u, 0u, descs, order, nrecs, src, dst, aad, st, types,   \
-                                                 nullptr, 0u, conn, MkLaunch{keys, nkeys, ctr, wg_key});               \
+        gcm_batch_body_mk<NR, 4, SEAL, FRAME>(descs, order, nrecs, src, dst, aad, st, types, conn,                    \
+                                              MkLaunch{keys, nkeys, ctr, wg_key});                                     \
     }
 MI355X_GCM_KERNEL_MK(mi355x_gcm_seal_aes128_k4_mk, 10, true, false)
 MI355X_GCM_KERNEL_MK(mi355x_gcm_seal_aes256_k4_mk, 14, true, false)
@@ -1567,6 +1739,59 @@ extern "C" __global__ void mi355x_mk_keys(const uint32_t *__restrict__ key_idx, 
     }
 }
 
+/*
+ * Grouping by key as a counting sort (nkeys + 1 buckets up to MK_LDS_BUCKETS, the last for out-of-range indices): each
+ * workgroup counts its MK_PER_BLOCK records' keys in LDS and adds them to the global counts; an exclusive scan gives
+ * each key's first position; each workgroup counts again, reserves its run of every key with one global atomic, and
+ * places its records by LDS atomics.  Not stable (within a key the order is the atomics'), which a multi-key launch does
+ * not need.  (hipcub's radix sort took ~82 us for 1 M keys of 7 bits: a block sort and ten merge passes.)
+ */
+constexpr uint32_t MK_LDS_BUCKETS = 8192, MK_PER_BLOCK = 4096;
+
+extern "C" __global__ __launch_bounds__(1024) void mi355x_mk_count(const uint32_t *__restrict__ key_idx, uint32_t n,
+                                                                   uint32_t nkeys, uint32_t *__restrict__ counts)
+{
+    __shared__ uint32_t h[MK_LDS_BUCKETS];
+    const uint32_t nb = nkeys + 1u;
+    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x)
+        h[b] = 0u;
+    __syncthreads();
+    const uint32_t i0 = blockIdx.x * MK_PER_BLOCK, i1 = min(n, i0 + MK_PER_BLOCK);
+    for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+        const uint32_t k = key_idx[i];
+        atomicAdd(&h[k < nkeys ? k : nkeys], 1u);
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x)
+        if (h[b] != 0u)
+            atomicAdd(counts + b, h[b]);
+}
+
+extern "C" __global__ __launch_bounds__(1024) void mi355x_mk_scatter(const uint32_t *__restrict__ key_idx, uint32_t n,
+                                                                     uint32_t nkeys, uint32_t *__restrict__ cursor,
+                                                                     uint32_t *__restrict__ order)
+{
+    __shared__ uint32_t h[MK_LDS_BUCKETS];
+    const uint32_t nb = nkeys + 1u;
+    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x)
+        h[b] = 0u;
+    __syncthreads();
+    const uint32_t i0 = blockIdx.x * MK_PER_BLOCK, i1 = min(n, i0 + MK_PER_BLOCK);
+    for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+        const uint32_t k = key_idx[i];
+        atomicAdd(&h[k < nkeys ? k : nkeys], 1u);
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) /* this block's run of key b: one global atomic */
+        if (h[b] != 0u)
+            h[b] = atomicAdd(cursor + b, h[b]);
+    __syncthreads();
+    for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+        const uint32_t k = key_idx[i];
+        order[atomicAdd(&h[k < nkeys ? k : nkeys], 1u)] = i;
+    }
+}
+
 /* every key's range empty and its group counter zero (before mi355x_mk_bounds) */
 extern "C" __global__ void mi355x_mk_reset(MkKey *__restrict__ keys, uint32_t nkeys, uint32_t *__restrict__ ctr)
 {
@@ -1579,14 +1804,24 @@ extern "C" __global__ void mi355x_mk_reset(MkKey *__restrict__ keys, uint32_t nk
 }
 
 /* each key's range [first, end) in the sorted order; an out-of-range key's record fails an open (mk_reject) */
-extern "C" __global__ void mi355x_mk_bounds(const uint32_t *__restrict__ sorted, const uint32_t *__restrict__ order,
-                                            uint32_t n, uint32_t nkeys, MkKey *__restrict__ keys,
-                                            uint32_t *__restrict__ st, uint8_t *__restrict__ types, uint32_t frame)
+__device__ __forceinline__ uint32_t mk_sorted_key(const uint32_t *sorted, const uint32_t *key_idx, const uint32_t *order,
+                                                  uint32_t i, uint32_t nkeys)
+{
+    if (sorted != nullptr)
+        return sorted[i];
+    const uint32_t k = key_idx[order[i]]; /* a caller's order (ptls_mi355x_order_by_key) */
+    return k < nkeys ? k : nkeys;
+}
+
+extern "C" __global__ void mi355x_mk_bounds(const uint32_t *__restrict__ sorted, const uint32_t *__restrict__ key_idx,
+                                            const uint32_t *__restrict__ order, uint32_t n, uint32_t nkeys,
+                                            MkKey *__restrict__ keys, uint32_t *__restrict__ st,
+                                            uint8_t *__restrict__ types, uint32_t frame)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n)
         return;
-    const uint32_t k = sorted[i];
+    const uint32_t k = mk_sorted_key(sorted, key_idx, order, i, nkeys);
     if (k >= nkeys) {
         if (frame)
             mk_reject<true>(order[i], st, types);
@@ -1594,9 +1829,9 @@ extern "C" __global__ void mi355x_mk_bounds(const uint32_t *__restrict__ sorted,
             mk_reject<false>(order[i], st, types);
         return;
     }
-    if (i == 0u || sorted[i - 1u] != k)
+    if (i == 0u || mk_sorted_key(sorted, key_idx, order, i - 1u, nkeys) != k)
         keys[k].first = i;
-    if (i + 1u == n || sorted[i + 1u] != k)
+    if (i + 1u == n || mk_sorted_key(sorted, key_idx, order, i + 1u, nkeys) != k)
         keys[k].end = i + 1u;
 }
 
@@ -2667,6 +2902,69 @@ static int mk_upload(ptls_mi355x_aesgcm_context_t *ctx, ptls_mi355x_aesgcm_conte
     return 0;
 }
 
+/*
+ * The records grouped by key into `order` on `stream` (mi355x_mk_count / _scatter; hipcub's radix sort above
+ * MK_LDS_BUCKETS - 1 keys), in the scratch `work` of mk_group_bytes(n, nkeys) bytes.
+ */
+static size_t mk_group_bytes(size_t n, size_t nkeys)
+{
+    const size_t arr = (n * 4 + 255) & ~(size_t)255;
+    if (nkeys + 1 <= MK_LDS_BUCKETS) { /* counts, cursors, the scan's workspace */
+        size_t temp = 0;
+        (void)hipcub::DeviceScan::ExclusiveSum(nullptr, temp, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)(nkeys + 1),
+                                               (hipStream_t)0);
+        return 2 * (((nkeys + 1) * 4 + 255) & ~(size_t)255) + temp;
+    }
+    uint32_t bits = 1;
+    while (bits < 32 && (1ull << bits) <= nkeys)
+        ++bits;
+    size_t temp = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                             (uint32_t *)nullptr, (int)n, 0, (int)bits, (hipStream_t)0);
+    return 3 * arr + temp;
+}
+
+static int mk_group(const uint32_t *key_idx, size_t n, size_t nkeys, uint32_t *order, uint8_t *work, hipStream_t stream)
+{
+    if (nkeys + 1 <= MK_LDS_BUCKETS) {
+        const size_t ab = ((nkeys + 1) * 4 + 255) & ~(size_t)255;
+        uint32_t *counts = (uint32_t *)work, *cursor = (uint32_t *)(work + ab);
+        size_t temp = 0; /* (the scan's workspace lives after the cursors: mk_group_bytes) */
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, temp, counts, cursor, (int)(nkeys + 1), stream));
+        const unsigned blocks = (unsigned)((n + MK_PER_BLOCK - 1) / MK_PER_BLOCK);
+        HIPCHK(hipMemsetAsync(counts, 0, (nkeys + 1) * 4, stream));
+        hipLaunchKernelGGL(mi355x_mk_count, dim3(blocks), dim3(1024), 0, stream, key_idx, (uint32_t)n, (uint32_t)nkeys,
+                           counts);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(work + 2 * ab, temp, counts, cursor, (int)(nkeys + 1), stream));
+        hipLaunchKernelGGL(mi355x_mk_scatter, dim3(blocks), dim3(1024), 0, stream, key_idx, (uint32_t)n, (uint32_t)nkeys,
+                           cursor, order);
+        HIPCHK(hipGetLastError());
+        return 0;
+    }
+    const size_t arr = (n * 4 + 255) & ~(size_t)255;
+    uint32_t bits = 1;
+    while (bits < 32 && (1ull << bits) <= nkeys)
+        ++bits;
+    size_t temp = 0;
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                              (uint32_t *)nullptr, (int)n, 0, (int)bits, stream));
+    uint32_t *keys_in = (uint32_t *)work, *keys_out = (uint32_t *)(work + arr), *vals_in = (uint32_t *)(work + 2 * arr);
+    hipLaunchKernelGGL(mi355x_mk_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, key_idx, (uint32_t)n,
+                       (uint32_t)nkeys, keys_in, vals_in);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(work + 3 * arr, temp, keys_in, keys_out, vals_in, order, (int)n, 0, (int)bits,
+                                              stream));
+    return 0;
+}
+
+/* bytes of a multi-key launch's scratch before its sort arrays: the key table, the group counters, the broadcast slots */
+static size_t mk_prefix(size_t nkeys, int num_cu)
+{
+    return ((nkeys * sizeof(MkKey) + 255) & ~(size_t)255) + ((nkeys * 4 + 255) & ~(size_t)255) +
+           (((size_t)num_cu * 4 + 255) & ~(size_t)255);
+}
+
 /* the kernel family of a multi-key batch of n records (the same selection setters as plan_launch) */
 enum MkFamily { MK_SPLIT, MK_WIN16, MK_BATCH };
 static MkFamily mk_family(bool frame, size_t n, int num_cu)
@@ -2721,7 +3019,7 @@ typedef void (*mk_win16_kernel_t)(const MkKey *, uint32_t, const uint32_t *, con
 static int launch_multikey(ptls_mi355x_aesgcm_context_t *const *ctxs, const void *static_ivs, size_t nkeys, bool seal,
                            bool frame, const void *recs, const uint32_t *key_idx, const uint32_t *conn, size_t n,
                            const uint8_t *src, uint8_t *dst, const uint8_t *aad, uint32_t *status, uint8_t *types,
-                           hipStream_t stream)
+                           hipStream_t stream, const uint32_t *given_order = nullptr)
 {
     if (n == 0)
         return 0;
@@ -2744,25 +3042,19 @@ static int launch_multikey(ptls_mi355x_aesgcm_context_t *const *ctxs, const void
     const bool a256 = ctx->key_size == 32;
     const MkFamily fam = mk_family(frame, n, ctx->num_cu);
     const uint32_t grid = (uint32_t)ctx->num_cu;
-    /* scratch: key table | counters | broadcast slots | sort keys in, out | values in | order | sort temp */
+    /* scratch: key table | counters | broadcast slots (mk_prefix) | sort keys in, out | values in | order | sort temp */
     const size_t a_tab = (nkeys * sizeof(MkKey) + 255) & ~(size_t)255, a_ctr = (nkeys * 4 + 255) & ~(size_t)255,
-                 a_wg = ((size_t)grid * 4 + 255) & ~(size_t)255, arr = fam == MK_BATCH ? (n * 4 + 255) & ~(size_t)255 : 0;
-    size_t temp = 0;
-    uint32_t bits = 1;
-    while (bits < 32 && (1ull << bits) <= nkeys) /* keys 0..nkeys (nkeys: out of range) */
-        ++bits;
-    if (fam == MK_BATCH)
-        HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                                  (uint32_t *)nullptr, (uint32_t *)nullptr, (int)n, 0, (int)bits, stream));
-    const size_t need = a_tab + a_ctr + a_wg + 4 * arr + temp;
+                 a_wg = ((size_t)grid * 4 + 255) & ~(size_t)255,
+                 arr = fam == MK_BATCH && given_order == nullptr ? (n * 4 + 255) & ~(size_t)255 : 0;
+    const size_t gbytes = arr != 0 ? mk_group_bytes(n, nkeys) : 0;
+    const size_t need = a_tab + a_ctr + a_wg + arr + gbytes;
     if (ensure_scratch(ctx, need, stream) != 0)
         return -1;
     uint8_t *base = (uint8_t *)ctx->d_scratch;
     MkKey *tab = (MkKey *)base;
     uint32_t *ctr = (uint32_t *)(base + a_tab), *wg = (uint32_t *)(base + a_tab + a_ctr);
     uint8_t *sb = base + a_tab + a_ctr + a_wg;
-    uint32_t *keys_in = (uint32_t *)sb, *keys_out = (uint32_t *)(sb + arr), *vals_in = (uint32_t *)(sb + 2 * arr),
-             *order = (uint32_t *)(sb + 3 * arr);
+    uint32_t *order = (uint32_t *)sb; /* the records grouped by key, then the grouping's workspace */
     if (mk_upload(ctx, ctxs, (const uint8_t *)static_ivs, nkeys, tab, stream) != 0)
         return -1;
     const char *name = mk_kernel_name(seal, frame, ctx->key_size, n, ctx->num_cu);
@@ -2805,14 +3097,16 @@ static int launch_multikey(ptls_mi355x_aesgcm_context_t *const *ctxs, const void
         {{mi355x_tls_open_aes128_k4_mk, mi355x_tls_open_aes256_k4_mk},
          {mi355x_tls_seal_aes128_k4_mk, mi355x_tls_seal_aes256_k4_mk}}};
     const unsigned g = (unsigned)((n + 255) / 256), gk = (unsigned)((nkeys + 255) / 256);
-    hipLaunchKernelGGL(mi355x_mk_keys, dim3(g), dim3(256), 0, stream, key_idx, (uint32_t)n, (uint32_t)nkeys, keys_in, vals_in);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipcub::DeviceRadixSort::SortPairs(sb + 4 * arr, temp, keys_in, keys_out, vals_in, order, (int)n, 0, (int)bits,
-                                              stream));
+    if (given_order == nullptr) { /* the records grouped by key here */
+        if (mk_group(key_idx, n, nkeys, order, sb + arr, stream) != 0)
+            return -1;
+    } else { /* the caller's order (ptls_mi355x_order_by_key), e.g. shared by a batch's seal and open */
+        order = (uint32_t *)given_order;
+    }
     hipLaunchKernelGGL(mi355x_mk_reset, dim3(gk), dim3(256), 0, stream, tab, (uint32_t)nkeys, ctr);
     HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(mi355x_mk_bounds, dim3(g), dim3(256), 0, stream, keys_out, order, (uint32_t)n, (uint32_t)nkeys, tab,
-                       seal ? nullptr : status, seal ? nullptr : types, frame ? 1u : 0u);
+    hipLaunchKernelGGL(mi355x_mk_bounds, dim3(g), dim3(256), 0, stream, nullptr, key_idx, order, (uint32_t)n,
+                       (uint32_t)nkeys, tab, seal ? nullptr : status, seal ? nullptr : types, frame ? 1u : 0u);
     HIPCHK(hipGetLastError());
     /* groups: at most n / 16 + nkeys (each key's last group partial); a CU's worth of waves per workgroup */
     const uint64_t groups = n / 16 + nkeys, blocks = (groups + 15) / 16;
@@ -2898,6 +3192,52 @@ int ptls_mi355x_tls_open_records_multikey(ptls_mi355x_aesgcm_context_t *const *c
     HIPCHK(hipGetLastError());
     ctx->mk_dev = nullptr; /* the scan wrote over the key table's place: upload it again next time */
     return scratch_done(ctx, stream);
+}
+
+int ptls_mi355x_order_by_key(ptls_mi355x_aesgcm_context_t *ctx, const uint32_t *key_idx, size_t n, size_t nkeys,
+                             uint32_t *order, void *stream_)
+{
+    if (n == 0)
+        return 0;
+    if (n > 0x7fffffffull || nkeys == 0 || nkeys > (1u << 24) || key_idx == nullptr || order == nullptr) {
+        snprintf(g_err, sizeof(g_err), "order_by_key: key indices, an order array, 1..2^24 keys, under 2^31 records");
+        return -1;
+    }
+    DeviceGuard guard(ctx->device);
+    hipStream_t stream = (hipStream_t)stream_;
+    /* behind the place a multi-key launch led by ctx keeps its key table, counters and slots: those survive the sort */
+    const size_t pre = mk_prefix(nkeys, ctx->num_cu);
+    if (ensure_scratch(ctx, pre + mk_group_bytes(n, nkeys), stream) != 0)
+        return -1;
+    if (mk_group(key_idx, n, nkeys, order, (uint8_t *)ctx->d_scratch + pre, stream) != 0)
+        return -1;
+    return scratch_done(ctx, stream);
+}
+
+int ptls_mi355x_seal_batch_multikey_ordered(ptls_mi355x_aesgcm_context_t *const *ctxs, const void *static_ivs,
+                                            size_t nkeys, const ptls_mi355x_record_t *recs, const uint32_t *key_idx,
+                                            const uint32_t *order, size_t n, const uint8_t *src, uint8_t *dst,
+                                            const uint8_t *aad, void *stream)
+{
+    if (n != 0 && order == nullptr) {
+        snprintf(g_err, sizeof(g_err), "seal_batch_multikey_ordered needs the order (ptls_mi355x_order_by_key)");
+        return -1;
+    }
+    return launch_multikey(ctxs, static_ivs, nkeys, true, false, recs, key_idx, nullptr, n, src, dst, aad, nullptr, nullptr,
+                           (hipStream_t)stream, order);
+}
+
+int ptls_mi355x_open_batch_multikey_ordered(ptls_mi355x_aesgcm_context_t *const *ctxs, const void *static_ivs,
+                                            size_t nkeys, const ptls_mi355x_record_t *recs, const uint32_t *key_idx,
+                                            const uint32_t *order, size_t n, const uint8_t *src, uint8_t *dst,
+                                            const uint8_t *aad, uint32_t *status, void *stream)
+{
+    if (n != 0 && (order == nullptr || status == nullptr)) {
+        snprintf(g_err, sizeof(g_err), "open_batch_multikey_ordered needs the order and status");
+        return -1;
+    }
+    return launch_multikey(ctxs, static_ivs, nkeys, false, false, recs, key_idx, nullptr, n, src, dst, aad, status, nullptr,
+                           (hipStream_t)stream, order);
 }
 
 const char *ptls_mi355x_kernel_name_multikey(int is_seal, size_t key_size, size_t n, int framing)

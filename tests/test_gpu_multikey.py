@@ -232,6 +232,48 @@ def test_multikey_matches_single_key_launches(gpu):
         e.close()
 
 
+def test_multikey_ordered_launches_share_one_sort(gpu):
+    """ptls_mi355x_order_by_key once, then the _ordered seal and open over it: the bytes of the sorting launches, and an
+    out-of-range key index sorted last and refused (batch kernels, 32 keys, AES-256)."""
+    import torch
+    rng = np.random.default_rng(31)
+    nkeys, n = 32, 2500
+    keys, ivs = sessions(rng, nkeys, 32)
+    engines = [ra.Engine(k) for k in keys]
+    mk = ra.MultiKey(engines, ivs)
+    recs, src, aad = aead_batch(rng, n, 1500)
+    kidx = rng.integers(0, nkeys, n).astype(np.uint32)
+    kidx[77] = nkeys + 1
+    d_recs, d_src, d_aad, d_k = dev(recs.view(np.uint8)), dev(src), dev(aad), dev(kidx.view(np.int32))
+    d_order = torch.zeros(n, dtype=torch.int32, device="cuda")
+    mk.order_by_key(d_k.data_ptr(), n, d_order.data_ptr())
+    d_a = torch.zeros(len(src) + 16, dtype=torch.uint8, device="cuda")
+    d_b = torch.zeros_like(d_a)
+    mk.seal_batch_ordered(d_recs.data_ptr(), d_k.data_ptr(), d_order.data_ptr(), n, d_src.data_ptr(), d_a.data_ptr(),
+                          d_aad.data_ptr())
+    mk.seal_batch(d_recs.data_ptr(), d_k.data_ptr(), n, d_src.data_ptr(), d_b.data_ptr(), d_aad.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(d_a, d_b)
+    order = d_order.cpu().numpy().view(np.uint32)
+    assert sorted(order.tolist()) == list(range(n)) and order[-1] == 77  # a permutation, the stray key last
+    sk = np.minimum(kidx[order], nkeys)
+    assert (np.diff(sk.astype(np.int64)) >= 0).all()
+    d_pt = torch.zeros_like(d_a)
+    d_st = torch.zeros(n, dtype=torch.int32, device="cuda")
+    mk.open_batch_ordered(d_recs.data_ptr(), d_k.data_ptr(), d_order.data_ptr(), n, d_a.data_ptr(), d_pt.data_ptr(),
+                          d_aad.data_ptr(), d_st.data_ptr())
+    torch.cuda.synchronize()
+    st, pt = d_st.cpu().numpy().view(np.uint32), d_pt.cpu().numpy()
+    for i, r in enumerate(recs):
+        a, ln = int(r["dst"]), int(r["len"])
+        if i == 77:
+            assert st[i] == 0xFFFFFFFF
+        else:
+            assert st[i] == ln and bytes(pt[a:a + ln]) == bytes(src[int(r["src"]): int(r["src"]) + ln]), i
+    for e in engines:
+        e.close()
+
+
 def test_multikey_argument_errors(gpu):
     import torch
     e16, e32 = ra.Engine(bytes(16)), ra.Engine(bytes(32))
