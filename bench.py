@@ -684,6 +684,10 @@ def lds_roofline(kname, achieved, wl_key, key, b32_reads, b128_reads, nominal, n
                   f"blocks per CU",
          "ceiling_source": "the LDS array busy every cycle; SQ_LDS_IDX_ACTIVE per 64 blocks equals the model (probe "
                            "330.0 / 458.0, kernels 333 / 461: profiles/r05e_lds_ceiling.json)",
+         "frac_meaning": "LDS-array BUSY fraction (achieved / the array busy every cycle at the clock held), not a fraction "
+                         "of a demonstrated peak: the highest busy fraction any kernel or probe reached is 0.87-0.91 "
+                         "(SQ_LDS_IDX_ACTIVE, profiles/r05e_lds_ceiling.json and the r05x counter pass), so 1.0 has not "
+                         "been shown attainable (DESIGN.md section 3, ceiling table)",
          "peak_nominal_2p4ghz": round(nominal, 1), "frac_nominal_2p4ghz": round(achieved / nominal, 4)}
     held = None
     hpath = os.path.join(ROOT, "profiles", "held_clock.json")

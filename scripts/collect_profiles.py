@@ -71,7 +71,7 @@ def held_cycles(counter_csv, warmup):
     return out
 
 
-SIDE = ("16k", "16k-aes128", "16k-max", "16k-max-aes128", "ragged")
+SIDE = ("16k", "16k-aes128", "16k-max", "16k-max-aes128", "ragged", "1400-mk64")
 
 
 def bench_lines(src):
@@ -196,7 +196,7 @@ def main(tag, label):
     allt["1400"] = traffic
     # other workloads: FETCH / WRITE passes only (scripts/gpu_round_bench.sh)
     others = {}
-    for w in ("16k", "16k-aes128", "16k-max", "16k-max-aes128", "ragged"):
+    for w in SIDE:
         fp = os.path.join(src, f"pmc_fetch_{w}", "run_counter_collection.csv")
         wp = os.path.join(src, f"pmc_write_{w}", "run_counter_collection.csv")
         if not (os.path.exists(fp) and os.path.exists(wp)):

@@ -8,7 +8,7 @@ import re
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = re.compile(r"^mi355x_gcm_(seal|open)_aes(128|256)_k4$")
+KERNEL = re.compile(r"^mi355x_gcm_(seal|open)_aes(128|256)_k4(_mk)?$")  # _mk: the multi-key batch kernels
 
 
 def _load(name):
@@ -42,7 +42,8 @@ def test_every_bench_workload_has_a_held_clock():
     d = _load("held_clock.json")
     for w, wl in bench.WORKLOADS.items():
         bits = "128" if wl["key"] == 16 else "256"
-        assert {f"mi355x_gcm_seal_aes{bits}_k4", f"mi355x_gcm_open_aes{bits}_k4"} <= set(d.get(w, {})), w
+        mk = "_mk" if wl.get("keys") else ""  # a multi-key workload runs the multi-key batch kernels
+        assert {f"mi355x_gcm_seal_aes{bits}_k4{mk}", f"mi355x_gcm_open_aes{bits}_k4{mk}"} <= set(d.get(w, {})), w
 
 
 def test_lds_roofline_prices_the_model_at_the_held_clock():
