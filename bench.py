@@ -426,6 +426,7 @@ def cpu_baseline(main_key: int, main_length: int) -> dict:
 # ------------------------------------------------------------------------------------------- GPU workload ----
 def measure(ra, wl_key, args, dev, rank, world, check):
     """Times one workload: K steps (seal + open of the whole batch) after W warmups; -> result dict."""
+    from rapido_amd.hostmem import to_cpu, to_gpu  # pinned copies (rapido_amd/hostmem.py)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -449,8 +450,8 @@ def measure(ra, wl_key, args, dev, rank, world, check):
     d_src = torch.randint(0, 256, (src_bytes,), dtype=torch.uint8, device=dev, generator=gen)
     d_ct = torch.zeros_like(d_src)
     d_pt = torch.zeros_like(d_src)
-    d_recs = torch.from_numpy(recs.view(np.uint8)).to(dev)
-    d_aad = torch.from_numpy(aad).to(dev)
+    d_recs = to_gpu(recs.view(np.uint8), dev)
+    d_aad = to_gpu(aad, dev)
     d_st = torch.zeros(n, dtype=torch.int32, device=dev)
     key = bytes(range(wl["key"]))
     iv = bytes(range(0xA0, 0xAC))
@@ -460,7 +461,7 @@ def measure(ra, wl_key, args, dev, rank, world, check):
         nk = wl["keys"]
         mk_engines = [eng] + [ra.Engine(bytes((b + 7 * k) & 0xFF for b in range(wl["key"]))) for k in range(1, nk)]
         mk = ra.MultiKey(mk_engines, [bytes((b + k) & 0xFF for b in range(0xA0, 0xAC)) for k in range(nk)])
-        d_kidx = torch.from_numpy(rng.integers(0, nk, n).astype(np.int32)).to(dev)
+        d_kidx = to_gpu(rng.integers(0, nk, n).astype(np.int32), dev)
         if args.pipeline != 1:
             raise SystemExit("bench: the multi-key workload runs one launch each way (--pipeline 1)")
     stream = torch.cuda.current_stream(dev)
@@ -583,7 +584,7 @@ def measure(ra, wl_key, args, dev, rank, world, check):
 
     # correctness after timing: every status verifies and sampled records open back to their plaintext (parity with
     # the reference engine is the test suite's job: tests/test_gpu_*.py against oracle/ and its pinned fixtures)
-    st = d_st.cpu().numpy().view(np.uint32)
+    st = to_cpu(d_st).view(np.uint32)
     if not (st == recs["len"]).all():
         raise SystemExit(f"bench: open status mismatch ({wl_key}) -- results invalid")
     if check and rank == 0:
@@ -719,6 +720,7 @@ def lds_roofline(kname, achieved, wl_key, key, b32_reads, b128_reads, nominal, n
 def window_latency(ra, extra, dev):
     """Latency side (not `value`): one rapido send window, 16 x 16 KiB records framed in one launch on the
     window kernels, device-resident, back-to-back launches timed with HIP events."""
+    from rapido_amd.hostmem import to_gpu  # pinned copies (rapido_amd/hostmem.py)
     import numpy as np
     import torch
     WIN, FRAG = 16, 16384
@@ -728,7 +730,7 @@ def window_latency(ra, extra, dev):
     t["dst"] = np.arange(WIN, dtype=np.uint64) * (FRAG + 22)
     t["seq"] = np.arange(WIN, dtype=np.uint64)
     t["len"], t["type"] = FRAG, 23
-    d_t = torch.from_numpy(t.view(np.uint8)).to(dev)
+    d_t = to_gpu(t.view(np.uint8), dev)
     d_wire = torch.zeros(WIN * (FRAG + 22), dtype=torch.uint8, device=dev)
 
     def window():

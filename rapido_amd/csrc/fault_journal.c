@@ -12,6 +12,12 @@
  * writes the faulting virtual address, the fault reasons and the journal (each range that holds the address marked)
  * to stderr and to the file given at install.  The handler only observes: it returns HSA_STATUS_ERROR, so the
  * runtime's handling (HIP's) is what decides the outcome, as without it.
+ *
+ * The report also says what the faulting address IS at the moment of the fault: what the runtime knows of it and of
+ * the byte before its page (hsa_amd_pointer_info: an HSA allocation, a locked / registered host range and its extent,
+ * or unknown), the /proc/self/maps line that holds it (device memory, the heap, an anonymous mapping, nothing), and
+ * the tables other parts of the library keep (the record layer's host registrations, via
+ * ptls_mi355x_fault_journal_add_dumper) -- so a fault on memory the engine never launched on still names its owner.
  */
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
@@ -43,6 +49,9 @@ static struct event g_ring[RING];
 static uint64_t g_next; /* events recorded (under g_mu) */
 static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
 static char g_path[512];
+#define DUMPERS 4
+static ptls_mi355x_journal_dumper_t g_dumpers[DUMPERS];
+static atomic_int g_ndumpers;
 static atomic_ulong g_faults;
 static atomic_int g_installed;
 
@@ -125,6 +134,73 @@ static const char *hit(const ptls_mi355x_journal_arg_t *a, uint64_t va)
     return va >= p && va - p < (1ull << 30) ? "   <== faulting address within 1 GiB past this base" : "";
 }
 
+static const char *pointer_type(hsa_amd_pointer_type_t t)
+{
+    switch (t) {
+    case HSA_EXT_POINTER_TYPE_UNKNOWN: return "unknown to the runtime";
+    case HSA_EXT_POINTER_TYPE_HSA: return "HSA allocation (device memory or hipHostMalloc)";
+    case HSA_EXT_POINTER_TYPE_LOCKED: return "locked host range (hipHostRegister, or a runtime pin of pageable memory)";
+    case HSA_EXT_POINTER_TYPE_GRAPHICS: return "graphics interop";
+    case HSA_EXT_POINTER_TYPE_IPC: return "IPC import";
+    case HSA_EXT_POINTER_TYPE_RESERVED_ADDR: return "reserved address range (virtual memory API)";
+    case HSA_EXT_POINTER_TYPE_HSA_VMEM: return "virtual memory API allocation";
+    default: return "?";
+    }
+}
+
+/* what the runtime knows of an address now */
+static void describe_pointer(FILE *f, const char *label, uint64_t a)
+{
+    hsa_amd_pointer_info_t info;
+    memset(&info, 0, sizeof(info));
+    info.size = sizeof(info);
+    const hsa_status_t st = hsa_amd_pointer_info((const void *)(uintptr_t)a, &info, NULL, NULL, NULL);
+    if (st != HSA_STATUS_SUCCESS) {
+        fprintf(f, "  %s 0x%llx: hsa_amd_pointer_info status %d\n", label, (unsigned long long)a, (int)st);
+        return;
+    }
+    if (info.type == HSA_EXT_POINTER_TYPE_UNKNOWN) {
+        fprintf(f, "  %s 0x%llx: %s\n", label, (unsigned long long)a, pointer_type(info.type));
+        return;
+    }
+    fprintf(f, "  %s 0x%llx: %s, host base %p, agent base %p, %llu bytes (ends at 0x%llx)\n", label,
+            (unsigned long long)a, pointer_type(info.type), info.hostBaseAddress, info.agentBaseAddress,
+            (unsigned long long)info.sizeInBytes,
+            (unsigned long long)((uintptr_t)info.hostBaseAddress + info.sizeInBytes));
+}
+
+/* the process mappings around an address (/proc/self/maps: the line holding it, and the one before) */
+static void describe_mapping(FILE *f, uint64_t va)
+{
+    FILE *m = fopen("/proc/self/maps", "r");
+    if (m == NULL) {
+        fprintf(f, "  /proc/self/maps: unreadable\n");
+        return;
+    }
+    char line[512], prev[512] = "";
+    int found = 0;
+    while (fgets(line, sizeof(line), m) != NULL) {
+        unsigned long long lo = 0, hi = 0;
+        if (sscanf(line, "%llx-%llx", &lo, &hi) != 2)
+            continue;
+        if (va < lo) {
+            fprintf(f, "  maps: 0x%llx is in no mapping; around it:\n    %s    %s", (unsigned long long)va,
+                    prev[0] ? prev : "(none)\n", line);
+            found = 1;
+            break;
+        }
+        if (va < hi) {
+            fprintf(f, "  maps: %s", line);
+            found = 1;
+            break;
+        }
+        snprintf(prev, sizeof(prev), "%s", line);
+    }
+    if (!found)
+        fprintf(f, "  maps: 0x%llx is above every mapping\n", (unsigned long long)va);
+    fclose(m);
+}
+
 static void write_report(FILE *f, uint64_t va, uint32_t mask, uint64_t agent, uint64_t t_fault)
 {
     char rbuf[256];
@@ -132,6 +208,14 @@ static void write_report(FILE *f, uint64_t va, uint32_t mask, uint64_t agent, ui
                " t=%llu ns ===\n",
             (unsigned long long)va, mask, reasons(mask, rbuf, sizeof(rbuf)), (unsigned long long)agent, (int)getpid(),
             (unsigned long long)t_fault);
+    fprintf(f, "the faulting address now:\n");
+    describe_pointer(f, "fault VA", va);
+    describe_pointer(f, "byte before its page", (va & ~4095ull) - 1);
+    describe_mapping(f, va);
+    const int nd = atomic_load(&g_ndumpers);
+    for (int i = 0; i < nd && i < DUMPERS; ++i)
+        if (g_dumpers[i] != NULL)
+            g_dumpers[i](f, va);
     /* a snapshot under the lock when it can be had (the faulting thread may hold it: then read as it is) */
     const int locked = pthread_mutex_trylock(&g_mu) == 0;
     const uint64_t end = g_next, start = end > RING ? end - RING : 0;
@@ -200,6 +284,20 @@ int ptls_mi355x_fault_journal_install(const char *path)
         return (int)st;
     atomic_store(&g_installed, 1);
     return 0;
+}
+
+void ptls_mi355x_fault_journal_add_dumper(ptls_mi355x_journal_dumper_t fn)
+{
+    pthread_mutex_lock(&g_mu);
+    const int n = atomic_load(&g_ndumpers);
+    int have = 0;
+    for (int i = 0; i < n; ++i)
+        have |= g_dumpers[i] == fn;
+    if (!have && n < DUMPERS) {
+        g_dumpers[n] = fn;
+        atomic_store(&g_ndumpers, n + 1);
+    }
+    pthread_mutex_unlock(&g_mu);
 }
 
 int ptls_mi355x_fault_journal_installed(void)

@@ -7,6 +7,7 @@
 
 #include <stddef.h>
 #include <stdint.h>
+#include <stdio.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -27,6 +28,11 @@ void ptls_mi355x_journal_launch(const char *kernel, const void *stream, uint32_t
 
 /* a device memory event (allocation, free, host registration, device check) over [p, p + len) */
 void ptls_mi355x_fault_journal_note(const char *what, const void *p, size_t len);
+
+/* a table printed in every fault report (e.g. the record layer's host registrations); it must not block: called from
+ * the runtime's event thread while other threads may hold the library's locks */
+typedef void (*ptls_mi355x_journal_dumper_t)(FILE *f, uint64_t va);
+void ptls_mi355x_fault_journal_add_dumper(ptls_mi355x_journal_dumper_t fn);
 
 #ifdef __cplusplus
 }

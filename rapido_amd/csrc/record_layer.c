@@ -568,8 +568,27 @@ static rl_shared_range_t *shared_overlap(const uint8_t *base, size_t len)
     return any;
 }
 
+/* the fault report's view of the table (fault_journal.c): never blocks, since a thread may hold g_reg_mu */
+static void rl_dump_registrations(FILE *f, uint64_t va)
+{
+    if (pthread_mutex_trylock(&g_reg_mu) != 0) {
+        fprintf(f, "  record layer registrations: table busy (held by another thread)\n");
+        return;
+    }
+    fprintf(f, "  record layer registrations: %zu range(s) mapped by the layers\n", g_nreg);
+    for (size_t i = 0; i < g_nreg; ++i) {
+        const uint64_t b = (uint64_t)(uintptr_t)g_reg[i].base, d = (uint64_t)(uintptr_t)g_reg[i].dev;
+        const int in = (va >= b && va - b < g_reg[i].len) || (va >= d && va - d < g_reg[i].len);
+        const int next = va >= b + g_reg[i].len && va - (b + g_reg[i].len) < 4096;
+        fprintf(f, "    host %p dev %p + %zu, %d ref(s)%s\n", (void *)g_reg[i].base, (void *)g_reg[i].dev, g_reg[i].len,
+                g_reg[i].refs, in ? "   <== HOLDS THE FAULTING ADDRESS" : next ? "   <== the fault is the page after it" : "");
+    }
+    pthread_mutex_unlock(&g_reg_mu);
+}
+
 int ptls_mi355x_record_layer_register(ptls_mi355x_record_layer_t *rl, void *base, size_t len)
 {
+    ptls_mi355x_fault_journal_add_dumper(rl_dump_registrations);
     if (rl->nreg == RL_MAX_REGIONS || base == NULL || len == 0)
         return rl_msg(base == NULL || len == 0 ? "empty range" : "too many ranges");
     for (size_t i = 0; i < rl->nreg; ++i)

@@ -42,6 +42,27 @@ def test_fault_journal_report_marks_the_range_holding_the_address(engine_lib, tm
     assert text.rstrip().endswith("=== end of fault journal ===")
 
 
+def test_fault_report_says_what_the_address_is(engine_lib, tmp_path):
+    """The report describes the faulting address as it is at the fault: the runtime's view of it and of the byte
+    before its page (hsa_amd_pointer_info; here, without a GPU, its status), and the /proc/self/maps line holding it
+    -- an address in no mapping is reported as such, with its neighbours."""
+    import numpy as np
+    log = str(tmp_path / "fault.log")
+    host = np.zeros(1 << 20, np.uint8)
+    _with_report_path(log)
+    try:
+        ra.fault_journal_report(host.ctypes.data + 8192, 0x1)
+        ra.fault_journal_report(0x10, 0x1)  # below every mapping
+        text = open(log).read()
+    finally:
+        _with_report_path(os.environ["RAPIDO_FAULT_LOG"])
+    first, second = text.split("=== end of fault journal ===")[:2]
+    assert "the faulting address now:" in first and "fault VA 0x" in first and "byte before its page" in first
+    maps = [ln for ln in first.splitlines() if ln.strip().startswith("maps:")]
+    assert len(maps) == 1 and "rw" in maps[0], first  # the array's own (writable) mapping
+    assert "is in no mapping" in second, second
+
+
 def test_fault_journal_keeps_the_last_256_events(engine_lib, tmp_path):
     log = str(tmp_path / "fault.log")
     _with_report_path(log)

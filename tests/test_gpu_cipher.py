@@ -8,6 +8,7 @@ import oracle
 import rapido_amd as ra
 from conftest import FAMILIES, kernel_family
 from rapido_amd import records
+from rapido_amd.hostmem import to_cpu, to_gpu
 
 pytestmark = pytest.mark.gpu
 
@@ -58,11 +59,11 @@ def test_aes_context_device_batch(gpu, keylen):
     n = 1 << 20
     data = rng.integers(0, 256, 16 * n, dtype=np.uint8)
     ks = ra.AesKeys(key)
-    d_in = torch.from_numpy(data).cuda()
+    d_in = to_gpu(data)
     d_out = torch.zeros_like(d_in)
     ks.ecb_batch(d_out.data_ptr(), d_in.data_ptr(), n, encrypt=True)
     torch.cuda.synchronize()
-    ct = d_out.cpu().numpy()
+    ct = to_cpu(d_out)
     # the oracle is byte-serial: check a spread sample of blocks, plus the round trip of the whole buffer
     idx = np.unique(np.concatenate([[0, 1, n - 1], rng.integers(0, n, 2000)]))
     for i in idx:
@@ -106,7 +107,7 @@ def test_parallel_key_setup_all_tables(gpu, keylen):
     want = np.zeros_like(src)
     oracle.batch(True, key, iv, recs, src, want, aad)
     eng = ra.Engine(key)
-    d_recs, d_src, d_aad = (torch.from_numpy(a).cuda() for a in (recs.view(np.uint8), src, aad))
+    d_recs, d_src, d_aad = (to_gpu(a) for a in (recs.view(np.uint8), src, aad))
     configs = [("batch", k) for k in (1, 2, 4, 8)] + [(f, 4) for f in FAMILIES if f != "batch"]
     for family, k in configs:
         prev_k = ra.set_lanes_per_record(k)
@@ -117,7 +118,7 @@ def test_parallel_key_setup_all_tables(gpu, keylen):
                 torch.cuda.synchronize()
         finally:
             ra.set_lanes_per_record(prev_k)
-        got = d_dst.cpu().numpy()
+        got = to_cpu(d_dst)
         for r in recs:
             a, n = int(r["dst"]), int(r["len"]) + 16
             assert np.array_equal(got[a:a + n], want[a:a + n]), (family, k, int(r["len"]))
@@ -167,7 +168,7 @@ def test_work_slots_reused_across_streams(gpu):
     want = np.zeros_like(src)
     oracle.batch(True, key, iv, recs, src, want, np.zeros(1, np.uint8))
     eng = ra.Engine(key)
-    d_recs, d_src = torch.from_numpy(recs.view(np.uint8)).cuda(), torch.from_numpy(src).cuda()
+    d_recs, d_src = to_gpu(recs.view(np.uint8)), to_gpu(src)
     d_aad = torch.zeros(1, dtype=torch.uint8, device="cuda")
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
     outs = [torch.zeros_like(d_src) for _ in range(8)]
@@ -178,7 +179,7 @@ def test_work_slots_reused_across_streams(gpu):
         eng.seal_batch(iv, d_recs.data_ptr(), n, d_src.data_ptr(), out.data_ptr(), d_aad.data_ptr(), s.cuda_stream)
     torch.cuda.synchronize()
     for out in outs:
-        assert np.array_equal(out.cpu().numpy(), want)
+        assert np.array_equal(to_cpu(out), want)
     eng.close()
 
 
@@ -196,7 +197,7 @@ def test_shared_resources_across_destroyed_streams(gpu):
     want = np.zeros_like(src)
     oracle.batch(True, key, iv, recs, src, want, np.zeros(1, np.uint8))
     eng = ra.Engine(key)
-    d_recs, d_src = torch.from_numpy(recs.view(np.uint8)).cuda(), torch.from_numpy(src).cuda()
+    d_recs, d_src = to_gpu(recs.view(np.uint8)), to_gpu(src)
     d_aad = torch.zeros(1, dtype=torch.uint8, device="cuda")
     d_order = torch.zeros(n, dtype=torch.int32, device="cuda")
     outs = [torch.zeros_like(d_src) for _ in range(4)]
@@ -209,5 +210,5 @@ def test_shared_resources_across_destroyed_streams(gpu):
         del s
     torch.cuda.synchronize()
     for out in outs:
-        assert np.array_equal(out.cpu().numpy(), want)
+        assert np.array_equal(to_cpu(out), want)
     eng.close()

@@ -19,6 +19,7 @@ import pytest
 import oracle
 import rapido_amd as ra
 from rapido_amd import records
+from rapido_amd.hostmem import to_cpu, to_gpu
 
 pytestmark = pytest.mark.gpu
 
@@ -49,8 +50,8 @@ def test_full_size_round_trip(gpu, name, keylen, n, length):
     gen.manual_seed(77)
     d_src = torch.randint(0, 256, (src_bytes,), dtype=torch.uint8, device=dev, generator=gen)
     d_ct = torch.zeros_like(d_src)
-    d_recs = torch.from_numpy(recs.view(np.uint8)).to(dev)
-    d_aad = torch.from_numpy(aad).to(dev)
+    d_recs = to_gpu(recs.view(np.uint8), dev)
+    d_aad = to_gpu(aad, dev)
     d_st = torch.zeros(n, dtype=torch.int32, device=dev)
     d_order = torch.zeros(n, dtype=torch.int32, device=dev)
     eng = ra.Engine(key)
@@ -72,15 +73,15 @@ def test_full_size_round_trip(gpu, name, keylen, n, length):
         else:
             eng.open_batch(iv, d_recs.data_ptr(), n, src.data_ptr(), dst.data_ptr(), d_aad.data_ptr(), d_st.data_ptr())
         torch.cuda.synchronize()
-        return d_st.cpu().numpy().view(np.uint32)
+        return to_cpu(d_st).view(np.uint32)
 
     seal(d_ct)
     d_pt = torch.zeros_like(d_src)
     st = open_(d_ct, d_pt)
     assert (st == recs["len"]).all()
     # the payload bytes of every record round-trip (slot padding is not written by open)
-    starts = torch.from_numpy(recs["src"].astype(np.int64)).to(dev)
-    lens = torch.from_numpy(recs["len"].astype(np.int64)).to(dev)
+    starts = to_gpu(recs["src"].astype(np.int64), dev)
+    lens = to_gpu(recs["len"].astype(np.int64), dev)
     mark = torch.zeros(src_bytes + 1, dtype=torch.int32, device=dev)
     mark.index_add_(0, starts, torch.ones_like(starts, dtype=torch.int32))
     mark.index_add_(0, starts + lens, -torch.ones_like(starts, dtype=torch.int32))
@@ -99,8 +100,8 @@ def test_full_size_round_trip(gpu, name, keylen, n, length):
     got = np.zeros_like(sub_src)
     for k, i in enumerate(sample):
         a, ln, o = int(recs[i]["src"]), int(ln_s[k]), int(offs[k])
-        sub_src[o: o + ln] = d_src[a: a + ln].cpu().numpy()
-        got[o: o + ln + 16] = d_ct[a: a + ln + 16].cpu().numpy()
+        sub_src[o: o + ln] = to_cpu(d_src[a: a + ln])
+        got[o: o + ln + 16] = to_cpu(d_ct[a: a + ln + 16])
     sub_aad = np.concatenate([aad[int(r["aad"]): int(r["aad"]) + 5] for r in sub])
     sub["src"] = offs.astype(np.uint64)
     sub["dst"] = offs.astype(np.uint64)
@@ -158,8 +159,8 @@ def test_configs4_sharded_batch_equals_whole(gpu):
     d_src = torch.randint(0, 256, (src_bytes,), dtype=torch.uint8, device=dev, generator=gen)
     d_whole = torch.zeros_like(d_src)
     d_shard = torch.zeros_like(d_src)
-    d_recs = torch.from_numpy(recs.view(np.uint8)).to(dev)
-    d_aad = torch.from_numpy(aad).to(dev)
+    d_recs = to_gpu(recs.view(np.uint8), dev)
+    d_aad = to_gpu(aad, dev)
     dsize = recs.dtype.itemsize
     whole = ra.Engine(key)
     whole.seal_batch(iv, d_recs.data_ptr(), n, d_src.data_ptr(), d_whole.data_ptr(), d_aad.data_ptr())
@@ -179,14 +180,14 @@ def test_configs4_sharded_batch_equals_whole(gpu):
         eng.open_batch(iv, d_recs.data_ptr() + first * dsize, cnt, d_shard.data_ptr(), d_pt.data_ptr(),
                        d_aad.data_ptr(), d_st.data_ptr() + 4 * first, s.cuda_stream)
     torch.cuda.synchronize(dev)
-    assert (d_st.cpu().numpy().view(np.uint32) == 1400).all()
+    assert (to_cpu(d_st).view(np.uint32) == 1400).all()
     # one sampled record of every shard is bit-exact against the oracle
     for r in range(world):
         i = r * per + int(np.random.default_rng(r).integers(0, per))
         a = int(recs[i]["src"])
         want = oracle.seal(key, oracle.build_iv(iv, i), aad[int(recs[i]["aad"]): int(recs[i]["aad"]) + 5].tobytes(),
-                           d_src[a: a + 1400].cpu().numpy().tobytes())
-        assert d_shard[a: a + 1416].cpu().numpy().tobytes() == want
+                           to_cpu(d_src[a: a + 1400]).tobytes())
+        assert to_cpu(d_shard[a: a + 1416]).tobytes() == want
     for eng, _ in ranks:
         eng.close()
     whole.close()

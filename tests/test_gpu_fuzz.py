@@ -13,6 +13,7 @@ import oracle
 import rapido_amd as ra
 from conftest import FAMILIES, kernel_family
 from rapido_amd import RECORD_DTYPE
+from rapido_amd.hostmem import to_cpu, to_gpu
 
 pytestmark = pytest.mark.gpu
 
@@ -47,9 +48,9 @@ def test_fuzz_seal_open(gpu, family, lanes, keylen):
     try:
         with kernel_family(family, framing=False):
             eng = ra.Engine(key)
-            d_recs = torch.from_numpy(recs.view(np.uint8)).cuda()
-            d_src = torch.from_numpy(src).cuda()
-            d_aad = torch.from_numpy(aad).cuda()
+            d_recs = to_gpu(recs.view(np.uint8))
+            d_src = to_gpu(src)
+            d_aad = to_gpu(aad)
             d_ct = torch.zeros_like(d_src)
             d_pt = torch.zeros_like(d_src)
             d_st = torch.zeros(len(recs), dtype=torch.int32, device="cuda")
@@ -57,7 +58,7 @@ def test_fuzz_seal_open(gpu, family, lanes, keylen):
             eng.open_batch(iv, d_recs.data_ptr(), len(recs), d_ct.data_ptr(), d_pt.data_ptr(), d_aad.data_ptr(),
                            d_st.data_ptr())
             torch.cuda.synchronize()
-            ct, pt, st = d_ct.cpu().numpy(), d_pt.cpu().numpy(), d_st.cpu().numpy().view(np.uint32)
+            ct, pt, st = to_cpu(d_ct), to_cpu(d_pt), to_cpu(d_st).view(np.uint32)
             want = np.zeros_like(src)
             oracle.batch(True, key, iv, recs, src, want, aad)
             for i, r in enumerate(recs):

@@ -20,6 +20,7 @@ import oracle
 import rapido_amd as ra
 from conftest import FAMILIES, kernel_family
 from rapido_amd import RECORD_DTYPE
+from rapido_amd.hostmem import to_cpu, to_gpu
 
 pytestmark = pytest.mark.gpu
 
@@ -69,14 +70,14 @@ def run_case(seed, stats):
         with kernel_family(family, framing=False):
             eng = ra.Engine(key)
             dev = "cuda"
-            d_recs = torch.from_numpy(recs.view(np.uint8)).to(dev)
-            d_aad = torch.from_numpy(aad).to(dev)
-            d_src = torch.from_numpy(src).to(dev)
+            d_recs = to_gpu(recs.view(np.uint8), dev)
+            d_aad = to_gpu(aad, dev)
+            d_src = to_gpu(src, dev)
             d_ct = d_src.clone() if inplace else torch.zeros_like(d_src)
             eng.seal_batch(iv, d_recs.data_ptr(), n, (d_ct if inplace else d_src).data_ptr(), d_ct.data_ptr(),
                            d_aad.data_ptr())
             torch.cuda.synchronize()
-            ct = d_ct.cpu().numpy()
+            ct = to_cpu(d_ct)
             for i, r in enumerate(recs):
                 a, ln = int(r["dst"]), int(r["len"])
                 assert bytes(ct[a:a + ln + 16]) == bytes(want[a:a + ln + 16]), \
@@ -86,21 +87,21 @@ def run_case(seed, stats):
                 a, ln = int(recs[i]["dst"]), int(recs[i]["len"])
                 pos = a + ln + int(rng.integers(0, 16)) if ln == 0 or rng.random() < 0.5 else a + int(rng.integers(0, ln))
                 ct[pos] ^= 1 << int(rng.integers(0, 8))
-            d_in = torch.from_numpy(ct).to(dev)
+            d_in = to_gpu(ct, dev)
             if inplace:  # open in place: the ciphertext arena is the output, records at their seal offsets
                 open_recs = recs.copy()
                 open_recs["src"] = open_recs["dst"]
-                d_orecs = torch.from_numpy(open_recs.view(np.uint8)).to(dev)
+                d_orecs = to_gpu(open_recs.view(np.uint8), dev)
                 d_pt = d_in
             else:
                 open_recs = recs.copy()
                 open_recs["src"], open_recs["dst"] = recs["dst"], recs["src"]
-                d_orecs = torch.from_numpy(open_recs.view(np.uint8)).to(dev)
+                d_orecs = to_gpu(open_recs.view(np.uint8), dev)
                 d_pt = torch.zeros_like(d_src)
             d_st = torch.zeros(n, dtype=torch.int32, device=dev)
             eng.open_batch(iv, d_orecs.data_ptr(), n, d_in.data_ptr(), d_pt.data_ptr(), d_aad.data_ptr(), d_st.data_ptr())
             torch.cuda.synchronize()
-            pt, st = d_pt.cpu().numpy(), d_st.cpu().numpy().view(np.uint32)
+            pt, st = to_cpu(d_pt), to_cpu(d_st).view(np.uint32)
             bad = set(int(i) for i in tamper)
             for i, r in enumerate(open_recs):
                 a, ln = int(r["dst"]), int(r["len"])
@@ -156,13 +157,13 @@ def run_tls_case(seed, stats):
     ivs = [conn_iv(iv, int(c)) for c in conns]
     with kernel_family(family, framing=True):
         eng = ra.Engine(key)
-        d_src, d_recs = torch.from_numpy(src).cuda(), torch.from_numpy(trecs.view(np.uint8)).cuda()
-        d_conn = torch.from_numpy(conns.view(np.int32)).cuda()
+        d_src, d_recs = to_gpu(src), to_gpu(trecs.view(np.uint8))
+        d_conn = to_gpu(conns.view(np.int32))
         d_wire = torch.zeros(woff + 16, dtype=torch.uint8, device="cuda")
         eng.tls_seal_records(iv, d_recs.data_ptr(), n, d_src.data_ptr(), d_wire.data_ptr(),
                              conn_ptr=d_conn.data_ptr() if multi else 0)
         torch.cuda.synchronize()
-        wire = d_wire.cpu().numpy()
+        wire = to_cpu(d_wire)
         received, seqs = [], []
         for i, t in enumerate(trecs):
             frag = src[int(t["src"]):int(t["src"]) + int(t["len"])].tobytes()
@@ -182,7 +183,7 @@ def run_tls_case(seed, stats):
         rc, orecs, used, _ = ra.tls_parse_records(buf, 0)
         assert rc == 0 and len(orecs) == n and used == len(buf), f"seed {seed}: parse"
         orecs["seq"] = seqs
-        d_buf, d_orecs = torch.from_numpy(np.frombuffer(buf, np.uint8).copy()).cuda(), torch.from_numpy(orecs.view(np.uint8)).cuda()
+        d_buf, d_orecs = to_gpu(np.frombuffer(buf, np.uint8).copy()), to_gpu(orecs.view(np.uint8))
         pt_size = int(orecs["dst"][-1]) + int(orecs["len"][-1]) + 16
         d_pt = torch.zeros(pt_size, dtype=torch.uint8, device="cuda")
         d_st = torch.zeros(n, dtype=torch.int32, device="cuda")
@@ -190,7 +191,7 @@ def run_tls_case(seed, stats):
         eng.tls_open_records(iv, d_orecs.data_ptr(), n, d_buf.data_ptr(), d_pt.data_ptr(), d_st.data_ptr(),
                              d_ty.data_ptr(), conn_ptr=d_conn.data_ptr() if multi else 0)
         torch.cuda.synchronize()
-        pt, st, ty = d_pt.cpu().numpy(), d_st.cpu().numpy().view(np.uint32), d_ty.cpu().numpy()
+        pt, st, ty = to_cpu(d_pt), to_cpu(d_st).view(np.uint32), to_cpu(d_ty)
         bad = 0
         for i, w in enumerate(received):
             want = oracle.tls_open_record(key, ivs[i], seqs[i], w)

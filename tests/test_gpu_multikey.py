@@ -10,6 +10,7 @@ import oracle
 import rapido_amd as ra
 from conftest import kernel_family
 from rapido_amd import records
+from rapido_amd.hostmem import to_cpu, to_gpu
 
 pytestmark = pytest.mark.gpu
 
@@ -19,7 +20,7 @@ EXPECT = {"split": "_wins_", "window16": "_win16_", "batch": "_k4_mk"}
 
 def dev(a):
     import torch
-    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    return to_gpu(np.ascontiguousarray(a))
 
 
 def sessions(rng, nkeys, keylen):
@@ -69,7 +70,7 @@ def test_multikey_aead_vs_oracle(gpu, family, nkeys, keylen):
         d_ct = torch.zeros(len(src) + 16, dtype=torch.uint8, device="cuda")
         mk.seal_batch(d_recs.data_ptr(), d_k.data_ptr(), n, d_src.data_ptr(), d_ct.data_ptr(), d_aad.data_ptr())
         torch.cuda.synchronize()
-        got = d_ct.cpu().numpy()
+        got = to_cpu(d_ct)
         want = oracle_seal(keys, ivs, kidx, recs, src, aad)
         for i, r in enumerate(recs):
             a, b = int(r["dst"]), int(r["dst"]) + int(r["len"]) + 16
@@ -86,7 +87,7 @@ def test_multikey_aead_vs_oracle(gpu, family, nkeys, keylen):
         mk.open_batch(d_recs.data_ptr(), d_kb.data_ptr(), n, d_bad.data_ptr(), d_pt.data_ptr(), d_aad.data_ptr(),
                       d_st.data_ptr())
         torch.cuda.synchronize()
-        st, pt = d_st.cpu().numpy().view(np.uint32), d_pt.cpu().numpy()
+        st, pt = to_cpu(d_st).view(np.uint32), to_cpu(d_pt)
     for i, r in enumerate(recs):
         a, ln = int(r["dst"]), int(r["len"])
         if i in (3, 7, 11):
@@ -116,7 +117,7 @@ def test_multikey_seal_skips_out_of_range_keys(gpu, family):
         d_ct = torch.full((len(src) + 16,), 0xA5, dtype=torch.uint8, device="cuda")
         mk.seal_batch(d_recs.data_ptr(), d_k.data_ptr(), n, d_src.data_ptr(), d_ct.data_ptr(), d_aad.data_ptr())
         torch.cuda.synchronize()
-        got = d_ct.cpu().numpy()
+        got = to_cpu(d_ct)
     ok = kidx < 3
     want = oracle_seal(keys, ivs, np.where(ok, kidx, 0), recs, src, aad)
     for i, r in enumerate(recs):
@@ -168,7 +169,7 @@ def test_multikey_tls_windows_vs_oracle(gpu, family, nkeys):
         mk.tls_seal_records(d_recs.data_ptr(), d_k.data_ptr(), n, d_src.data_ptr(), d_wire.data_ptr(),
                             conn_ptr=d_c.data_ptr())
         torch.cuda.synchronize()
-        wire = d_wire.cpu().numpy()
+        wire = to_cpu(d_wire)
         for i, t in enumerate(trecs):
             frag = bytes(src[int(t["src"]): int(t["src"]) + int(t["len"])])
             want = oracle.tls_seal_record(keys[kidx[i]], conn_iv(ivs[kidx[i]], int(conn[i])), int(t["seq"]),
@@ -190,7 +191,7 @@ def test_multikey_tls_windows_vs_oracle(gpu, family, nkeys):
             mk.tls_open_records(dev(orecs.view(np.uint8)).data_ptr(), d_k.data_ptr(), n, d_w.data_ptr(), d_pt.data_ptr(),
                                 d_st.data_ptr(), d_ty.data_ptr(), conn_ptr=d_c.data_ptr(), flags=flags)
             torch.cuda.synchronize()
-            st, ty, pt = d_st.cpu().numpy().view(np.uint32), d_ty.cpu().numpy(), d_pt.cpu().numpy()
+            st, ty, pt = to_cpu(d_st).view(np.uint32), to_cpu(d_ty), to_cpu(d_pt)
             for i, t in enumerate(trecs):
                 a, ln = int(orecs[i]["dst"]), int(t["len"])
                 seg_bad = [b for b in tampered if kidx[b] == kidx[i] and conn[b] == conn[i] and b < i]
@@ -254,7 +255,7 @@ def test_multikey_ordered_launches_share_one_sort(gpu):
     mk.seal_batch(d_recs.data_ptr(), d_k.data_ptr(), n, d_src.data_ptr(), d_b.data_ptr(), d_aad.data_ptr())
     torch.cuda.synchronize()
     assert torch.equal(d_a, d_b)
-    order = d_order.cpu().numpy().view(np.uint32)
+    order = to_cpu(d_order).view(np.uint32)
     assert sorted(order.tolist()) == list(range(n)) and order[-1] == 77  # a permutation, the stray key last
     sk = np.minimum(kidx[order], nkeys)
     assert (np.diff(sk.astype(np.int64)) >= 0).all()
@@ -263,7 +264,7 @@ def test_multikey_ordered_launches_share_one_sort(gpu):
     mk.open_batch_ordered(d_recs.data_ptr(), d_k.data_ptr(), d_order.data_ptr(), n, d_a.data_ptr(), d_pt.data_ptr(),
                           d_aad.data_ptr(), d_st.data_ptr())
     torch.cuda.synchronize()
-    st, pt = d_st.cpu().numpy().view(np.uint32), d_pt.cpu().numpy()
+    st, pt = to_cpu(d_st).view(np.uint32), to_cpu(d_pt)
     for i, r in enumerate(recs):
         a, ln = int(r["dst"]), int(r["len"])
         if i == 77:

@@ -9,6 +9,7 @@ import oracle
 import rapido_amd as ra
 from conftest import FAMILIES, kernel_family
 from rapido_amd import records
+from rapido_amd.hostmem import to_cpu, to_gpu
 
 pytestmark = pytest.mark.gpu
 
@@ -24,7 +25,7 @@ def aead_kernels(request, engine_lib):
 
 def to_dev(a: np.ndarray):
     import torch
-    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    return to_gpu(np.ascontiguousarray(a))
 
 
 def run_batch(eng, is_seal, static_iv, recs, src, dst_size, aad, inplace=False):
@@ -40,7 +41,7 @@ def run_batch(eng, is_seal, static_iv, recs, src, dst_size, aad, inplace=False):
         eng.open_batch(static_iv, d_recs.data_ptr(), len(recs), d_src.data_ptr(), d_dst.data_ptr(), d_aad.data_ptr(),
                        d_st.data_ptr())
     torch.cuda.synchronize()
-    return d_dst.cpu().numpy(), d_st.cpu().numpy().view(np.uint32)
+    return to_cpu(d_dst), to_cpu(d_st).view(np.uint32)
 
 
 def random_batch(rng, n, max_len=2000, max_aad=64, unaligned=True):
@@ -349,21 +350,21 @@ def test_ordered_ragged_batch(gpu, lanes):
         eng.seal_batch_ordered(iv, d_recs.data_ptr(), d_order.data_ptr(), n, d_src.data_ptr(), d_dst.data_ptr(),
                                d_aad.data_ptr())
         torch.cuda.synchronize()
-        order = d_order.cpu().numpy().view(np.uint32)
+        order = to_cpu(d_order).view(np.uint32)
         assert sorted(order.tolist()) == list(range(n))
         work = (recs["len"].astype(np.int64) + 15) // 16 + (recs["aadlen"].astype(np.int64) + 15) // 16
         assert (np.diff(work[order]) <= 0).all()
         want = np.zeros_like(src)
         oracle.batch(True, key, iv, recs, src, want, aad)
-        got = d_dst.cpu().numpy()
+        got = to_cpu(d_dst)
         assert slices(got, recs, 16) == slices(want, recs, 16)
         d_pt = torch.zeros_like(d_src)
         d_st = torch.zeros(n, dtype=torch.int32, device="cuda")
         eng.open_batch_ordered(iv, d_recs.data_ptr(), d_order.data_ptr(), n, d_dst.data_ptr(), d_pt.data_ptr(),
                                d_aad.data_ptr(), d_st.data_ptr())
         torch.cuda.synchronize()
-        assert (d_st.cpu().numpy().view(np.uint32) == recs["len"]).all()
-        assert slices(d_pt.cpu().numpy(), recs, 0) == [bytes(src[int(r["src"]): int(r["src"]) + int(r["len"])])
+        assert (to_cpu(d_st).view(np.uint32) == recs["len"]).all()
+        assert slices(to_cpu(d_pt), recs, 0) == [bytes(src[int(r["src"]): int(r["src"]) + int(r["len"])])
                                                         for r in recs]
     finally:
         ra.set_lanes_per_record(prev)

@@ -16,6 +16,7 @@ import oracle
 import rapido_amd as ra
 from conftest import FAMILIES, kernel_family
 from rapido_amd.records import xorshift64star
+from rapido_amd.hostmem import to_cpu, to_gpu
 
 pytestmark = pytest.mark.gpu
 
@@ -332,7 +333,7 @@ def test_delivery_at_guard_edges(guards, at):
     woff = np.cumsum([0] + [len(w) for w in wires[:-1]]).astype(np.uint64)
     soff = np.cumsum([0] + [(ln + 1 + 15) // 16 * 16 for ln in lens[:-1]]).astype(np.uint64)  # 16-aligned slots
     wire = b"".join(bytes(w) for w in wires)
-    d_wire = torch.from_numpy(np.frombuffer(wire, np.uint8).copy()).cuda()
+    d_wire = to_gpu(np.frombuffer(wire, np.uint8).copy())
     d_slots = torch.zeros(int(soff[-1]) + lens[-1] + 17, dtype=torch.uint8, device="cuda")
     o = np.zeros(n, ra.TLS_RECORD_DTYPE)
     o["src"], o["dst"], o["seq"], o["len"] = woff, soff, 3 + np.arange(n), np.array(lens) + 17

@@ -13,6 +13,7 @@ import oracle
 import rapido_amd as ra
 from conftest import FAMILIES, kernel_family
 from rapido_amd.records import xorshift64star
+from rapido_amd.hostmem import to_cpu, to_gpu
 
 pytestmark = pytest.mark.gpu
 GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "tls_records.json")))
@@ -29,7 +30,7 @@ def framing_kernels(request, engine_lib):
 
 def dev(a):
     import torch
-    return torch.from_numpy(np.array(a, copy=True)).cuda()
+    return to_gpu(np.array(a, copy=True))
 
 
 def seal(eng, iv, trecs, src, wire_size, dst=None):
@@ -39,7 +40,7 @@ def seal(eng, iv, trecs, src, wire_size, dst=None):
     d_recs = dev(trecs.view(np.uint8))
     eng.tls_seal_records(iv, d_recs.data_ptr(), len(trecs), d_src.data_ptr(), d_dst.data_ptr())
     torch.cuda.synchronize()
-    return d_dst.cpu().numpy()
+    return to_cpu(d_dst)
 
 
 def open_(eng, iv, orecs, wire, pt_size, inplace=False):
@@ -52,7 +53,7 @@ def open_(eng, iv, orecs, wire, pt_size, inplace=False):
     eng.tls_open_records(iv, d_recs.data_ptr(), len(orecs), d_wire.data_ptr(), d_pt.data_ptr(), d_st.data_ptr(),
                          d_ty.data_ptr())
     torch.cuda.synchronize()
-    return d_pt.cpu().numpy(), d_st.cpu().numpy().view(np.uint32), d_ty.cpu().numpy()
+    return to_cpu(d_pt), to_cpu(d_st).view(np.uint32), to_cpu(d_ty)
 
 
 def xs(seed, n):
@@ -211,7 +212,7 @@ def test_in_place(gpu):
     d, d_recs = dev(buf), dev(trecs.view(np.uint8))  # descriptors held until the launch completes
     eng.tls_seal_records(iv, d_recs.data_ptr(), len(trecs), d.data_ptr(), d.data_ptr())
     torch.cuda.synchronize()
-    wire = d.cpu().numpy()
+    wire = to_cpu(d)
     for i, ln in enumerate(lens):
         assert wire[base[i]: base[i] + ln + 22].tobytes() == oracle.tls_seal_record(key, iv, 50 + i, 23, frags[i])
     orecs = trecs.copy()
@@ -256,7 +257,7 @@ def test_multi_connection_windows(gpu, keylen):
     eng = ra.Engine(key)
     eng.tls_seal_records(iv, d_recs.data_ptr(), len(trecs), d_src.data_ptr(), d_wire.data_ptr(), conn_ptr=d_conn.data_ptr())
     torch.cuda.synchronize()
-    wire = d_wire.cpu().numpy()
+    wire = to_cpu(d_wire)
     for t, c in zip(trecs, conn):
         frag = bytes(src[int(t["src"]): int(t["src"]) + int(t["len"])])
         want = oracle.tls_seal_record(key, conn_iv(iv, int(c)), int(t["seq"]), int(t["type"]), frag)
@@ -275,7 +276,7 @@ def test_multi_connection_windows(gpu, keylen):
         eng.tls_open_records(iv, d_orecs.data_ptr(), len(orecs), d_wire.data_ptr(), d_pt.data_ptr(), d_st.data_ptr(),
                              d_ty.data_ptr(), conn_ptr=d_ids.data_ptr())
         torch.cuda.synchronize()
-        return d_pt.cpu().numpy(), d_st.cpu().numpy().view(np.uint32), d_ty.cpu().numpy()
+        return to_cpu(d_pt), to_cpu(d_st).view(np.uint32), to_cpu(d_ty)
 
     pt, st, ty = receive(conn)
     assert (st == trecs["len"]).all() and (ty == trecs["type"]).all()
@@ -312,7 +313,7 @@ def test_many_windows_one_launch(gpu, framing_kernels):
     eng = ra.Engine(key)
     eng.tls_seal_records(iv, d_recs.data_ptr(), n, d_src.data_ptr(), d_wire.data_ptr(), conn_ptr=d_conn.data_ptr())
     torch.cuda.synchronize()
-    wire = d_wire.cpu().numpy()
+    wire = to_cpu(d_wire)
     for i in range(n):
         t = trecs[i]
         frag = bytes(src[int(t["src"]): int(t["src"]) + int(t["len"])])
@@ -329,7 +330,7 @@ def test_many_windows_one_launch(gpu, framing_kernels):
     eng.tls_open_records(iv, d_orecs.data_ptr(), n, d_wire.data_ptr(), d_pt.data_ptr(), d_st.data_ptr(), d_ty.data_ptr(),
                          conn_ptr=d_conn.data_ptr())
     torch.cuda.synchronize()
-    st, ty, pt = d_st.cpu().numpy().view(np.uint32), d_ty.cpu().numpy(), d_pt.cpu().numpy()
+    st, ty, pt = to_cpu(d_st).view(np.uint32), to_cpu(d_ty), to_cpu(d_pt)
     assert (st == trecs["len"]).all() and (ty == trecs["type"]).all()
     for i in range(n):
         a, b = int(orecs["dst"][i]), int(trecs["src"][i])
@@ -367,7 +368,7 @@ def test_open_stop_at_first_failure(gpu, multi):
     eng.tls_seal_records(iv, d_recs.data_ptr(), len(trecs), d_src.data_ptr(), d_wire.data_ptr(),
                          conn_ptr=d_conn.data_ptr() if multi else 0)
     torch.cuda.synchronize()
-    wire = d_wire.cpu().numpy().copy()
+    wire = to_cpu(d_wire).copy()
     orecs = trecs.copy()
     orecs["src"] = trecs["dst"]
     orecs["len"] = trecs["len"] + 17
@@ -385,7 +386,7 @@ def test_open_stop_at_first_failure(gpu, multi):
         eng.tls_open_records(iv, d_o.data_ptr(), len(orecs), d_w.data_ptr(), d_pt.data_ptr(), d_st.data_ptr(),
                              d_ty.data_ptr(), conn_ptr=d_ids.data_ptr() if multi else 0, flags=flags)
         torch.cuda.synchronize()
-        st, ty, pt = d_st.cpu().numpy().view(np.uint32), d_ty.cpu().numpy(), d_pt.cpu().numpy()
+        st, ty, pt = to_cpu(d_st).view(np.uint32), to_cpu(d_ty), to_cpu(d_pt)
         for ci in range(nconn):
             first_bad = min([i for i in bad if ci * per <= i < (ci + 1) * per], default=None)
             for i in range(ci * per, (ci + 1) * per):
@@ -420,7 +421,7 @@ def test_open_stop_at_failure_two_streams(gpu):
         d_recs, d_src = dev(trecs.view(np.uint8)), dev(src)  # alive until the seal has run
         eng.tls_seal_records(iv, d_recs.data_ptr(), n, d_src.data_ptr(), d_wire.data_ptr())
         torch.cuda.synchronize()
-        wire = d_wire.cpu().numpy().copy()
+        wire = to_cpu(d_wire).copy()
         wire[bad * (ln + 22) + 9] ^= 0x10
         orecs = trecs.copy()
         orecs["src"], orecs["dst"], orecs["len"] = trecs["dst"], np.arange(n, dtype=np.uint64) * (ln + 1), ln + 17
@@ -442,10 +443,10 @@ def test_open_stop_at_failure_two_streams(gpu):
                              d_ty.data_ptr(), stream=s.cuda_stream, flags=ra.OPEN_STOP_AT_FAILURE)
     torch.cuda.synchronize()
     for (orecs, _, src), (_, d_pt, d_st, _), bad in zip(jobs, outs, (41000, 37)):
-        st = d_st.cpu().numpy().view(np.uint32)
+        st = to_cpu(d_st).view(np.uint32)
         assert (st[:bad] == 1400).all() and st[bad] == ra.TLS_BAD_RECORD_MAC
         assert (st[bad + 1:] == ra.TLS_NOT_PROCESSED).all()
-        pt = d_pt.cpu().numpy().reshape(-1, 1401)
+        pt = to_cpu(d_pt).reshape(-1, 1401)
         assert pt[:bad, :1400].tobytes() == src[:bad * 1400].tobytes()
         assert not pt[bad + 1:].any()
     eng.close()

@@ -5,6 +5,7 @@ import socket
 
 import pytest
 import torch.multiprocessing as mp
+from rapido_amd.hostmem import to_cpu, to_gpu
 
 
 def _free_port():
@@ -208,10 +209,10 @@ def test_contexts_on_each_present_device(gpu):
             rec[0] = (0, 0, 0, 5, 100, 0)
             src = torch.arange(100, dtype=torch.uint8, device=f"cuda:{d}")
             dst = torch.zeros(116, dtype=torch.uint8, device=f"cuda:{d}")
-            d_rec = torch.from_numpy(rec.view(np.uint8).copy()).to(f"cuda:{d}")
+            d_rec = to_gpu(rec.view(np.uint8).copy(), f"cuda:{d}")
             eng.seal_batch(iv, d_rec.data_ptr(), 1, src.data_ptr(), dst.data_ptr(), src.data_ptr())
             torch.cuda.synchronize(d)
-            assert dst.cpu().numpy().tobytes() == oracle.seal(key, oracle.build_iv(iv, 5), b"", bytes(range(100)))
+            assert to_cpu(dst).tobytes() == oracle.seal(key, oracle.build_iv(iv, 5), b"", bytes(range(100)))
         eng.close()
     with pytest.raises(RuntimeError, match=f"device ordinal {n} is not present"):
         ra.Engine(key, device=n)
