@@ -138,16 +138,15 @@ def cpulist(cpus) -> str:
     return ",".join(out)
 
 
-def hip_pci_bus_id(dev_index: int):
-    """The GPU's PCI address ("0000:c1:00.0") from hipDeviceGetPCIBusId, or None."""
-    import ctypes
+def gpu_pci_bus_id(dev_index: int):
+    """The GPU's PCI address ("0000:c1:00.0") from torch's device properties (the process's one HIP runtime), or
+    None.  (A ctypes load of libamdhip64.so by name would bring in the system's HIP runtime beside torch's bundled
+    one: two runtimes in one process.)"""
     try:
-        hip = ctypes.CDLL("libamdhip64.so")
-        buf = ctypes.create_string_buffer(64)
-        if hip.hipDeviceGetPCIBusId(buf, 64, dev_index) != 0:
-            return None
-        return buf.value.decode().lower()
-    except OSError:
+        import torch
+        pr = torch.cuda.get_device_properties(dev_index)
+        return f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+    except Exception:
         return None
 
 
@@ -157,7 +156,7 @@ def place_rank(dev_index: int, bus_id=None, sysfs: str = "/sys/bus/pci/devices")
     within the CPUs it may use, and later allocations preferring the node's memory (set_mempolicy MPOL_PREFERRED), so the
     pinned staging and e2e_pcie buffers, touched first after this, are node-local.  Returns the fields every rank's line
     carries; a field that could not be had is None (never a guess)."""
-    bus_id = bus_id if bus_id is not None else hip_pci_bus_id(dev_index)
+    bus_id = bus_id if bus_id is not None else gpu_pci_bus_id(dev_index)
     out = {"pci_bus_id": bus_id, "numa_node": None, "cpus": None, "pinned": False, "mempolicy": None}
     if not bus_id:
         return out
