@@ -4,7 +4,9 @@ treats differently (empty, under a block, TLS sizes, 16 KiB +- a block, up to 70
 arbitrary byte offsets, records in place or not, and tampers with a few tags or ciphertext bytes before the open.
 Checked per record: the sealed bytes and tag against the oracle, the open's status, the plaintext of every verified
 record, and a zeroed output for every record that fails (fusion's open leaves nothing, lib/fusion.c:656-679).  A
-third of the cases frame TLS 1.3 records instead (run_tls_case).
+third of the cases frame TLS 1.3 records instead (run_tls_case).  About a quarter of either kind are multi-key (round
+6): 2..12 sessions of one key size in one launch (ptls_mi355x_*_multikey), every record under its session's key and
+IV, each checked against the oracle with that session's key.
 
 By default the suite runs GATE_CASES cases from a fixed seed (the same cases on every box); RAPIDO_FUZZ_SECONDS makes
 it a time-boxed campaign instead, RAPIDO_FUZZ_SEED sets the first case's seed ("random" takes it from the clock); RAPIDO_FUZZ_LOG names a file that gets the campaign's summary as one JSON line.  The seed of
@@ -58,30 +60,44 @@ def run_case(seed, stats):
     family = FAMILIES[int(rng.integers(0, len(FAMILIES)))]
     lanes = int(rng.choice([1, 2, 4, 8])) if family == "batch" else 4
     keylen = int(rng.choice([16, 32]))
-    key = rng.integers(0, 256, keylen, dtype=np.uint8).tobytes()
-    iv = rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    nkeys = int(rng.integers(2, 13)) if rng.random() < 0.25 else 1  # a multi-key launch (round 6)
+    keys = [rng.integers(0, 256, keylen, dtype=np.uint8).tobytes() for _ in range(nkeys)]
+    ivs = [rng.integers(0, 256, 12, dtype=np.uint8).tobytes() for _ in range(nkeys)]
+    key, iv = keys[0], ivs[0]
     recs, src, aad, inplace = random_case(rng)
     n = len(recs)
+    kidx = rng.integers(0, nkeys, n).astype(np.uint32)
     want = np.zeros_like(src) if not inplace else src.copy()
-    oracle.batch(True, key, iv, recs, src, want, aad)
+    for k in range(nkeys):  # each session's records under its own key and IV
+        sel = kidx == k
+        if sel.any():
+            oracle.batch(True, keys[k], ivs[k], recs[sel], src, want, aad)
     tamper = np.flatnonzero(rng.random(n) < 0.03)
     prev_k = ra.set_lanes_per_record(lanes)
     try:
         with kernel_family(family, framing=False):
-            eng = ra.Engine(key)
+            engines = [ra.Engine(k) for k in keys]
+            eng = engines[0]
+            mk = ra.MultiKey(engines, ivs) if nkeys > 1 else None
             dev = "cuda"
             d_recs = to_gpu(recs.view(np.uint8), dev)
             d_aad = to_gpu(aad, dev)
             d_src = to_gpu(src, dev)
+            d_kidx = to_gpu(kidx.view(np.int32), dev)
             d_ct = d_src.clone() if inplace else torch.zeros_like(d_src)
-            eng.seal_batch(iv, d_recs.data_ptr(), n, (d_ct if inplace else d_src).data_ptr(), d_ct.data_ptr(),
-                           d_aad.data_ptr())
+            if mk is not None:
+                mk.seal_batch(d_recs.data_ptr(), d_kidx.data_ptr(), n, (d_ct if inplace else d_src).data_ptr(),
+                              d_ct.data_ptr(), d_aad.data_ptr())
+            else:
+                eng.seal_batch(iv, d_recs.data_ptr(), n, (d_ct if inplace else d_src).data_ptr(), d_ct.data_ptr(),
+                               d_aad.data_ptr())
             torch.cuda.synchronize()
             ct = to_cpu(d_ct)
             for i, r in enumerate(recs):
                 a, ln = int(r["dst"]), int(r["len"])
                 assert bytes(ct[a:a + ln + 16]) == bytes(want[a:a + ln + 16]), \
-                    f"seed {seed}: seal of record {i} (len {ln}, aad {int(r['aadlen'])}, {family}, K={lanes}, in place {inplace})"
+                    f"seed {seed}: seal of record {i} (len {ln}, aad {int(r['aadlen'])}, {family}, K={lanes}, " \
+                    f"in place {inplace}, {nkeys} keys)"
             # tamper: flip a tag byte or a ciphertext byte of a few records
             for i in tamper:
                 a, ln = int(recs[i]["dst"]), int(recs[i]["len"])
@@ -99,23 +115,30 @@ def run_case(seed, stats):
                 d_orecs = to_gpu(open_recs.view(np.uint8), dev)
                 d_pt = torch.zeros_like(d_src)
             d_st = torch.zeros(n, dtype=torch.int32, device=dev)
-            eng.open_batch(iv, d_orecs.data_ptr(), n, d_in.data_ptr(), d_pt.data_ptr(), d_aad.data_ptr(), d_st.data_ptr())
+            if mk is not None:
+                mk.open_batch(d_orecs.data_ptr(), d_kidx.data_ptr(), n, d_in.data_ptr(), d_pt.data_ptr(),
+                              d_aad.data_ptr(), d_st.data_ptr())
+            else:
+                eng.open_batch(iv, d_orecs.data_ptr(), n, d_in.data_ptr(), d_pt.data_ptr(), d_aad.data_ptr(),
+                               d_st.data_ptr())
             torch.cuda.synchronize()
             pt, st = to_cpu(d_pt), to_cpu(d_st).view(np.uint32)
             bad = set(int(i) for i in tamper)
             for i, r in enumerate(open_recs):
                 a, ln = int(r["dst"]), int(r["len"])
-                where = f"seed {seed}: open of record {i} (len {ln}, {family}, K={lanes}, in place {inplace})"
+                where = f"seed {seed}: open of record {i} (len {ln}, {family}, K={lanes}, in place {inplace}, {nkeys} keys)"
                 if i in bad:
                     assert st[i] == FAIL, where + ": tampered record verified"
                     assert not pt[a:a + ln].any(), where + ": plaintext of a failed record released"
                 else:
                     assert st[i] == ln, where + f": status {st[i]:#x}"
                     assert bytes(pt[a:a + ln]) == bytes(src[int(recs[i]['src']):int(recs[i]['src']) + ln]), where
-            eng.close()
+            for e in engines:
+                e.close()
     finally:
         ra.set_lanes_per_record(prev_k)
     stats["cases"] += 1
+    stats["multikey_cases"] += int(nkeys > 1)
     stats["records"] += n
     stats["payload_bytes"] += int(recs["len"].sum())
     stats["tampered"] += len(tamper)
@@ -138,9 +161,12 @@ def run_tls_case(seed, stats):
     rng = np.random.default_rng(seed)
     family = FAMILIES[int(rng.integers(0, len(FAMILIES)))]
     keylen = int(rng.choice([16, 32]))
-    key = rng.integers(0, 256, keylen, dtype=np.uint8).tobytes()
-    iv = rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+    nkeys = int(rng.integers(2, 13)) if rng.random() < 0.25 else 1  # several sessions in one launch (round 6)
+    keys = [rng.integers(0, 256, keylen, dtype=np.uint8).tobytes() for _ in range(nkeys)]
+    sess_ivs = [rng.integers(0, 256, 12, dtype=np.uint8).tobytes() for _ in range(nkeys)]
+    key, iv = keys[0], sess_ivs[0]
     n = int(rng.integers(1, 4)) if rng.random() < 0.2 else int(rng.integers(1, 201))
+    kidx = rng.integers(0, nkeys, n).astype(np.uint32)
     multi = bool(rng.random() < 0.4)
     conns = rng.choice([0, 1, 7, int(rng.integers(0, 2 ** 32))], n).astype(np.uint32) if multi else np.zeros(n, np.uint32)
     cls = rng.choice(len(LEN_CLASSES) - 1, n, p=LEN_WEIGHTS[:-1] / LEN_WEIGHTS[:-1].sum())
@@ -154,25 +180,35 @@ def run_tls_case(seed, stats):
         off += ln
         woff += ln + ra.TLS_OVERHEAD
     src = rng.integers(0, 256, off + 16, dtype=np.uint8)
-    ivs = [conn_iv(iv, int(c)) for c in conns]
+    ivs = [conn_iv(sess_ivs[int(kidx[i])], int(c)) for i, c in enumerate(conns)]
+    rkeys = [keys[int(k)] for k in kidx]  # each record's session key
     with kernel_family(family, framing=True):
-        eng = ra.Engine(key)
+        engines = [ra.Engine(k) for k in keys]
+        eng = engines[0]
+        mk = ra.MultiKey(engines, sess_ivs) if nkeys > 1 else None
         d_src, d_recs = to_gpu(src), to_gpu(trecs.view(np.uint8))
         d_conn = to_gpu(conns.view(np.int32))
+        d_kidx = to_gpu(kidx.view(np.int32))
         d_wire = torch.zeros(woff + 16, dtype=torch.uint8, device="cuda")
-        eng.tls_seal_records(iv, d_recs.data_ptr(), n, d_src.data_ptr(), d_wire.data_ptr(),
-                             conn_ptr=d_conn.data_ptr() if multi else 0)
+        if mk is not None:
+            mk.tls_seal_records(d_recs.data_ptr(), d_kidx.data_ptr(), n, d_src.data_ptr(), d_wire.data_ptr(),
+                                conn_ptr=d_conn.data_ptr() if multi else 0)
+        else:
+            eng.tls_seal_records(iv, d_recs.data_ptr(), n, d_src.data_ptr(), d_wire.data_ptr(),
+                                 conn_ptr=d_conn.data_ptr() if multi else 0)
         torch.cuda.synchronize()
         wire = to_cpu(d_wire)
         received, seqs = [], []
         for i, t in enumerate(trecs):
             frag = src[int(t["src"]):int(t["src"]) + int(t["len"])].tobytes()
-            want = oracle.tls_seal_record(key, ivs[i], int(t["seq"]), int(t["type"]), frag)
+            want = oracle.tls_seal_record(rkeys[i], ivs[i], int(t["seq"]), int(t["type"]), frag)
             got = wire[int(t["dst"]):int(t["dst"]) + len(want)].tobytes()
-            assert got == want, f"seed {seed}: seal of record {i} (len {int(t['len'])}, {family}, multi {multi})"
+            assert got == want, f"seed {seed}: seal of record {i} (len {int(t['len'])}, {family}, multi {multi}, " \
+                                f"{nkeys} keys)"
             u = rng.random()
             if u < 0.1 and int(t["len"]) + 64 <= ra.TLS_MAX_FRAGMENT + 256:  # the peer padded it
-                got = oracle.tls_seal_record(key, ivs[i], int(t["seq"]), int(t["type"]), frag, int(rng.integers(1, 64)))
+                got = oracle.tls_seal_record(rkeys[i], ivs[i], int(t["seq"]), int(t["type"]), frag,
+                                             int(rng.integers(1, 64)))
             elif u < 0.13:  # damaged in flight: a ciphertext or tag byte
                 w = bytearray(got)
                 w[int(rng.integers(5, len(w)))] ^= 1 << int(rng.integers(0, 8))
@@ -188,15 +224,19 @@ def run_tls_case(seed, stats):
         d_pt = torch.zeros(pt_size, dtype=torch.uint8, device="cuda")
         d_st = torch.zeros(n, dtype=torch.int32, device="cuda")
         d_ty = torch.zeros(n, dtype=torch.uint8, device="cuda")
-        eng.tls_open_records(iv, d_orecs.data_ptr(), n, d_buf.data_ptr(), d_pt.data_ptr(), d_st.data_ptr(),
-                             d_ty.data_ptr(), conn_ptr=d_conn.data_ptr() if multi else 0)
+        if mk is not None:
+            mk.tls_open_records(d_orecs.data_ptr(), d_kidx.data_ptr(), n, d_buf.data_ptr(), d_pt.data_ptr(),
+                                d_st.data_ptr(), d_ty.data_ptr(), conn_ptr=d_conn.data_ptr() if multi else 0)
+        else:
+            eng.tls_open_records(iv, d_orecs.data_ptr(), n, d_buf.data_ptr(), d_pt.data_ptr(), d_st.data_ptr(),
+                                 d_ty.data_ptr(), conn_ptr=d_conn.data_ptr() if multi else 0)
         torch.cuda.synchronize()
         pt, st, ty = to_cpu(d_pt), to_cpu(d_st).view(np.uint32), to_cpu(d_ty)
         bad = 0
         for i, w in enumerate(received):
-            want = oracle.tls_open_record(key, ivs[i], seqs[i], w)
+            want = oracle.tls_open_record(rkeys[i], ivs[i], seqs[i], w)
             o = orecs[i]
-            where = f"seed {seed}: open of record {i} ({family}, multi {multi})"
+            where = f"seed {seed}: open of record {i} ({family}, multi {multi}, {nkeys} keys)"
             if want == oracle.TLS_BAD_MAC:
                 bad += 1
                 assert st[i] == ra.TLS_BAD_RECORD_MAC, where
@@ -206,8 +246,10 @@ def run_tls_case(seed, stats):
             else:
                 assert st[i] == len(want[0]) and ty[i] == want[1], where + f": status {st[i]:#x} type {ty[i]}"
                 assert pt[int(o["dst"]):int(o["dst"]) + int(st[i])].tobytes() == want[0], where
-        eng.close()
+        for e in engines:
+            e.close()
     stats["tls_cases"] += 1
+    stats["multikey_cases"] += int(nkeys > 1)
     stats["tls_records"] += n
     stats["tls_refused"] += bad
     stats["families"][family] = stats["families"].get(family, 0) + 1
@@ -222,7 +264,7 @@ def test_fuzz_campaign(gpu):
     seed = os.environ.get("RAPIDO_FUZZ_SEED", "20250")  # fixed by default (the suite's gate); "random": from the clock
     base = int(time.time()) & 0xFFFFFFF if seed == "random" else int(seed)
     stats = {"seed_base": base, "cases": 0, "records": 0, "payload_bytes": 0, "tampered": 0, "in_place": 0,
-             "tls_cases": 0, "tls_records": 0, "tls_refused": 0, "families": {}}
+             "tls_cases": 0, "tls_records": 0, "tls_refused": 0, "multikey_cases": 0, "families": {}}
     t0 = last = time.time()
     while (time.time() - t0 < budget) if timed else (stats["cases"] + stats["tls_cases"] < GATE_CASES):
         seed = base + stats["cases"] + stats["tls_cases"]
@@ -236,4 +278,4 @@ def test_fuzz_campaign(gpu):
     if os.environ.get("RAPIDO_FUZZ_LOG"):
         with open(os.environ["RAPIDO_FUZZ_LOG"], "a") as f:
             f.write(json.dumps(stats) + "\n")
-    assert stats["cases"] > 0
+    assert stats["cases"] > 0 and (timed or stats["multikey_cases"] > 0)
