@@ -5,7 +5,8 @@ windows over those connections (a connection may appear several times: its conse
 (empty, 1 byte, exactly 16 KiB, over 16 KiB), a transport, and damage on the receive side (a flipped ciphertext or
 tag bit, a truncated tail).  The expected bytes come from a plain model of ptls_send / ptls_receive over the oracle's
 TLS 1.3 record functions (lib/picotls.c:4969-4988 for the limit, :650-652 for the stop at the first failure), which
-tests/test_tls_records.py pins to the reference's own outputs."""
+tests/test_tls_records.py pins to the reference's own outputs.  Since round 6 a third of the sessions give every
+connection a session (key and IV) of its own, so their launches carry several keys."""
 import numpy as np
 import pytest
 
@@ -121,8 +122,14 @@ def random_session(rng, transport, keylen, case):
     nconn = int(rng.integers(1, 4))
     cids = [int(c) for c in rng.choice(1 << 16, nconn, replace=False)]
     seqs = [int(LIMIT - rng.integers(1, 6)) if rng.random() < 0.3 else int(rng.integers(0, 1 << 20)) for _ in cids]
-    tx = [ra.RecordLayer(key, conn_iv(iv, c), seq=s) for c, s in zip(cids, seqs)]
-    rx = [ra.RecordLayer(key, conn_iv(iv, c), seq=s) for c, s in zip(cids, seqs)]
+    # round 6: in a third of the sessions every connection is a session of its own (its own key and IV, one key
+    # size), so the launches below carry several keys (the multi-key framing kernels)
+    own = rng.random() < 1 / 3
+    keys = [rng.integers(0, 256, keylen, dtype=np.uint8).tobytes() if own and c else key for c in range(nconn)]
+    sivs = [rng.integers(0, 256, 12, dtype=np.uint8).tobytes() if own and c else iv for c in range(nconn)]
+    civ = [conn_iv(sivs[c], cids[c]) for c in range(nconn)]
+    tx = [ra.RecordLayer(keys[c], civ[c], seq=seqs[c]) for c in range(nconn)]
+    rx = [ra.RecordLayer(keys[c], civ[c], seq=seqs[c]) for c in range(nconn)]
     h = Host(transport, tx + rx, 1 << 23)
     # the launch: windows over the connections, some connections more than once
     order = [int(c) for c in rng.integers(0, nconn, int(rng.integers(1, 6)))]
@@ -133,7 +140,7 @@ def random_session(rng, transport, keylen, case):
     run_seq = list(seqs)
     wires = []
     for c, w, o, (wlen, n) in zip(order, windows_b, outs, got):
-        want, wn, run_seq[c] = model_seal(key, conn_iv(iv, cids[c]), run_seq[c], w)
+        want, wn, run_seq[c] = model_seal(keys[c], civ[c], run_seq[c], w)
         assert o[:wlen].tobytes() == want and n == wn, f"{case} ({transport}): seal window of connection {c}"
         wires.append(want)
     assert [t.seq for t in tx] == run_seq
@@ -164,11 +171,11 @@ def random_session(rng, transport, keylen, case):
         # (build_aad writes 03 03 itself, lib/picotls.c:621-628), so a flipped version bit leaves the stream intact
         hdr_ok = all(w[o] == 23 and 17 <= ln - 5 <= 16640 for o, ln in spans)
         if not hdr_ok:  # a flipped type or length bit: the layer's parser decides; only the delivered prefix is checked
-            assert r[1] == model_open(key, conn_iv(iv, cids[c]), exp_seq[c], w[:r[2]])[1]
+            assert r[1] == model_open(keys[c], civ[c], exp_seq[c], w[:r[2]])[1]
             exp_seq[c] += r[3]
             state[c] = "lost"
             continue
-        want = model_open(key, conn_iv(iv, cids[c]), exp_seq[c], w)
+        want = model_open(keys[c], civ[c], exp_seq[c], w)
         assert r == want, f"{case}: open window of connection {c}"
         exp_seq[c] += want[3]
         if want[3] < len(spans):
