@@ -20,7 +20,9 @@ At N=1 the same run also measures, each on its own batch and clock, the other si
 The JSON line also carries
   roofline      -- the dominant kernel's algorithmic HBM bytes per launch / its mean launch
                    time (HIP events on the launch stream) against the 8 TB/s HBM3E peak;
-                   `traffic` from rocprofv3 PMC counters (profiles/pmc_traffic.json);
+                   `traffic` = HBM bytes per launch from rocprofv3 PMC counters, measured at the end of
+                   this run by two child passes of this script under rocprofv3 (FETCH_SIZE,
+                   WRITE_SIZE; --no-live-pmc skips them and keeps profiles/pmc_traffic.json's figure);
   cpu_baseline  -- the reference engine (lib/fusion.c, built unmodified into oracle/_ref) with the
                    t/ptlsbench.c methodology: one pinned process per core, CLOCK_PROCESS_CPUTIME_ID,
                    1400 B and 16 KiB, AES-128 and AES-256, 1 core and all usable cores; measured
@@ -871,6 +873,69 @@ def record_layer_stream(key_bytes: int = 16, nwin: int = 64, depth: int = 4, tra
     return res
 
 
+def live_pmc_traffic(workload: str, timeout_s: float = 150.0) -> dict:
+    """HBM bytes per launch of `workload`'s kernels measured on THIS box in THIS run: two child passes of this script
+    under rocprofv3 (FETCH_SIZE, then WRITE_SIZE: their TCC counters do not fit one pass), 2 steps each, bytes =
+    2 x FETCH_SIZE x 1024 + WRITE_SIZE x 1024 per dispatch (gfx950: FETCH_SIZE reports half of a 16 B/lane streaming
+    read; MI355X_MICROARCH.md, HBM section), averaged over the kernel's dispatches.  The children run after every
+    timed region of this process.  -> {kernel: bytes} or {"error": ...}."""
+    import csv
+    import shutil
+    import signal
+    import tempfile
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return {"error": "rocprofv3 not found"}
+    tmp = tempfile.mkdtemp(prefix="rapido_pmc_")
+    env = dict(os.environ, TMPDIR=tmp)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    per = {}
+    try:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            out = os.path.join(tmp, counter)
+            cmd = [prof, "--pmc", counter, "--kernel-trace", "-d", out, "-o", "run", "--output-format", "csv", "--",
+                   sys.executable, os.path.abspath(__file__), "--workload", workload, "--steps", "2", "--warmup", "1",
+                   "--prewarm-ms", "0", "--check", "0", "--no-cpu-baseline", "--no-e2e", "--no-workloads",
+                   "--no-live-pmc"]
+            p = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                                 start_new_session=True)
+            try:
+                _, err = p.communicate(timeout=timeout_s)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)  # the child's own process group (rocprofv3 and the bench under it)
+                p.wait()
+                return {"error": f"{counter} pass timed out after {timeout_s:.0f} s"}
+            path = os.path.join(out, "run_counter_collection.csv")
+            if p.returncode != 0 or not os.path.exists(path):
+                tail = (err or b"").decode(errors="replace").strip().splitlines()[-1:]
+                return {"error": f"{counter} pass: exit {p.returncode} {tail}"}
+            vals = {}
+            for r in csv.DictReader(open(path)):
+                if r["Kernel_Name"].startswith("mi355x_") and r["Counter_Name"] == counter:
+                    vals.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
+            for k, v in vals.items():
+                per.setdefault(k, {})[counter] = sum(v) / len(v)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    return {k: int(2 * c["FETCH_SIZE"] * 1024 + c["WRITE_SIZE"] * 1024) for k, c in per.items()
+            if "FETCH_SIZE" in c and "WRITE_SIZE" in c}
+
+
+def apply_live_traffic(res: dict, workload: str) -> None:
+    """roofline.traffic of a result from live_pmc_traffic; the builder's committed figure stays beside it."""
+    rf = res["roofline"]
+    live = live_pmc_traffic(workload)
+    if "error" in live or rf["kernel"] not in live:
+        rf["traffic_live_error"] = live.get("error", f"no counters for {rf['kernel']}")
+        return
+    rf["traffic_builder"], rf["traffic_builder_source"] = rf["traffic"], rf["traffic_source"]
+    rf["traffic"] = live[rf["kernel"]]
+    rf["traffic_source"] = ("measured in this run on this GPU: rocprofv3 --pmc child passes of this workload "
+                            "(FETCH_SIZE, WRITE_SIZE), 2 x FETCH_SIZE + WRITE_SIZE bytes per launch of the kernel")
+    rf["traffic_over_algorithmic"] = round(rf["traffic"] / rf["algorithmic_bytes_per_launch"], 4)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -891,6 +956,8 @@ def main() -> None:
     ap.add_argument("--e2e", action="store_true", help="(the default) time the PCIe-inclusive path, every rank")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive path")
     ap.add_argument("--check", type=int, default=64, help="records checked to round-trip after timing")
+    ap.add_argument("--no-live-pmc", action="store_true",
+                    help="at N=1, skip the rocprofv3 PMC child passes that measure roofline.traffic in this run")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -1021,6 +1088,12 @@ def main() -> None:
             del ex
             torch.cuda.empty_cache()
         out["workloads"] = side
+
+    # HBM traffic measured here, after every timed region: PMC child passes under rocprofv3 (N=1 only)
+    if world == 1 and not args.no_live_pmc:
+        apply_live_traffic(out, args.workload)
+        for w, r in out.get("workloads", {}).items():
+            apply_live_traffic(r, w)
 
     if cpu is not None:
         out["cpu_baseline"] = cpu

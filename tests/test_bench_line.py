@@ -91,3 +91,52 @@ def test_clock_sampler_reports_why_it_is_off():
     summ = s.summary(0.0, 1e12)
     if s.h is None:
         assert s.err and summ["source"] is None and summ["error"]
+
+
+FAKE_ROCPROF = """#!/usr/bin/env python3
+import os, sys
+a = sys.argv[1:]
+counter, out = a[a.index("--pmc") + 1], a[a.index("-d") + 1]
+if os.environ.get("FAKE_ROCPROF_FAIL") == counter:
+    sys.exit(3)
+os.makedirs(out, exist_ok=True)
+v = {"FETCH_SIZE": (1000.0, 1002.0), "WRITE_SIZE": (500.0, 500.0)}[counter]
+with open(os.path.join(out, "run_counter_collection.csv"), "w") as f:
+    f.write("Kernel_Name,Counter_Name,Counter_Value\\n")
+    for x in v:
+        f.write(f"mi355x_gcm_seal_aes128_k4,{counter},{x}\\n")
+    f.write(f"__amd_rocclr_fillBufferAligned,{counter},7\\n")
+"""
+
+
+def _fake_rocprof(tmp_path, monkeypatch):
+    p = tmp_path / "rocprofv3"
+    p.write_text(FAKE_ROCPROF)
+    p.chmod(0o755)
+    monkeypatch.setenv("PATH", f"{tmp_path}:{os.environ['PATH']}")
+
+
+def test_live_pmc_traffic_from_two_child_passes(tmp_path, monkeypatch):
+    """roofline.traffic measured in the run: a FETCH_SIZE and a WRITE_SIZE pass (rocprofv3 children), 2 x FETCH + WRITE
+    in bytes per dispatch, averaged over the kernel's dispatches; the builder's committed figure kept beside it."""
+    import bench
+    _fake_rocprof(tmp_path, monkeypatch)
+    live = bench.live_pmc_traffic("1400")
+    assert live == {"mi355x_gcm_seal_aes128_k4": int(2 * 1001.0 * 1024 + 500.0 * 1024)}
+    res = {"roofline": {"kernel": "mi355x_gcm_seal_aes128_k4", "traffic": 123, "traffic_source": "builder",
+                        "algorithmic_bytes_per_launch": 2_000_000}}
+    bench.apply_live_traffic(res, "1400")
+    rf = res["roofline"]
+    assert rf["traffic"] == live["mi355x_gcm_seal_aes128_k4"] and rf["traffic_builder"] == 123
+    assert "measured in this run" in rf["traffic_source"] and rf["traffic_over_algorithmic"] > 1
+
+
+def test_live_pmc_traffic_failure_keeps_the_builders_figure(tmp_path, monkeypatch):
+    import bench
+    _fake_rocprof(tmp_path, monkeypatch)
+    monkeypatch.setenv("FAKE_ROCPROF_FAIL", "WRITE_SIZE")
+    res = {"roofline": {"kernel": "mi355x_gcm_seal_aes128_k4", "traffic": 123, "traffic_source": "builder",
+                        "algorithmic_bytes_per_launch": 2_000_000}}
+    bench.apply_live_traffic(res, "1400")
+    rf = res["roofline"]
+    assert rf["traffic"] == 123 and rf["traffic_source"] == "builder" and "WRITE_SIZE pass" in rf["traffic_live_error"]
