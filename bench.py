@@ -873,7 +873,10 @@ def record_layer_stream(key_bytes: int = 16, nwin: int = 64, depth: int = 4, tra
     return res
 
 
-def live_pmc_traffic(workload: str, timeout_s: float = 150.0) -> dict:
+_LIVE_PMC_FAILED = []  # the first failed pass: later workloads skip their passes (a bounded bench on any box)
+
+
+def live_pmc_traffic(workload: str, timeout_s: float = 90.0) -> dict:
     """HBM bytes per launch of `workload`'s kernels measured on THIS box in THIS run: two child passes of this script
     under rocprofv3 (FETCH_SIZE, then WRITE_SIZE: their TCC counters do not fit one pass), 2 steps each, bytes =
     2 x FETCH_SIZE x 1024 + WRITE_SIZE x 1024 per dispatch (gfx950: FETCH_SIZE reports half of a 16 B/lane streaming
@@ -883,8 +886,11 @@ def live_pmc_traffic(workload: str, timeout_s: float = 150.0) -> dict:
     import shutil
     import signal
     import tempfile
+    if _LIVE_PMC_FAILED:
+        return {"error": f"skipped after an earlier failed pass ({_LIVE_PMC_FAILED[0]})"}
     prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(prof):
+        _LIVE_PMC_FAILED.append("rocprofv3 not found")
         return {"error": "rocprofv3 not found"}
     tmp = tempfile.mkdtemp(prefix="rapido_pmc_")
     env = dict(os.environ, TMPDIR=tmp)
@@ -905,10 +911,12 @@ def live_pmc_traffic(workload: str, timeout_s: float = 150.0) -> dict:
             except subprocess.TimeoutExpired:
                 os.killpg(p.pid, signal.SIGKILL)  # the child's own process group (rocprofv3 and the bench under it)
                 p.wait()
+                _LIVE_PMC_FAILED.append(f"{counter} pass of {workload} timed out")
                 return {"error": f"{counter} pass timed out after {timeout_s:.0f} s"}
             path = os.path.join(out, "run_counter_collection.csv")
             if p.returncode != 0 or not os.path.exists(path):
                 tail = (err or b"").decode(errors="replace").strip().splitlines()[-1:]
+                _LIVE_PMC_FAILED.append(f"{counter} pass of {workload}: exit {p.returncode}")
                 return {"error": f"{counter} pass: exit {p.returncode} {tail}"}
             vals = {}
             for r in csv.DictReader(open(path)):

@@ -121,6 +121,7 @@ def test_live_pmc_traffic_from_two_child_passes(tmp_path, monkeypatch):
     in bytes per dispatch, averaged over the kernel's dispatches; the builder's committed figure kept beside it."""
     import bench
     _fake_rocprof(tmp_path, monkeypatch)
+    monkeypatch.setattr(bench, "_LIVE_PMC_FAILED", [])
     live = bench.live_pmc_traffic("1400")
     assert live == {"mi355x_gcm_seal_aes128_k4": int(2 * 1001.0 * 1024 + 500.0 * 1024)}
     res = {"roofline": {"kernel": "mi355x_gcm_seal_aes128_k4", "traffic": 123, "traffic_source": "builder",
@@ -134,9 +135,21 @@ def test_live_pmc_traffic_from_two_child_passes(tmp_path, monkeypatch):
 def test_live_pmc_traffic_failure_keeps_the_builders_figure(tmp_path, monkeypatch):
     import bench
     _fake_rocprof(tmp_path, monkeypatch)
+    monkeypatch.setattr(bench, "_LIVE_PMC_FAILED", [])
     monkeypatch.setenv("FAKE_ROCPROF_FAIL", "WRITE_SIZE")
     res = {"roofline": {"kernel": "mi355x_gcm_seal_aes128_k4", "traffic": 123, "traffic_source": "builder",
                         "algorithmic_bytes_per_launch": 2_000_000}}
     bench.apply_live_traffic(res, "1400")
     rf = res["roofline"]
     assert rf["traffic"] == 123 and rf["traffic_source"] == "builder" and "WRITE_SIZE pass" in rf["traffic_live_error"]
+
+
+def test_live_pmc_traffic_stops_after_a_failed_pass(tmp_path, monkeypatch):
+    """One failed pass ends the live passes for the run: the later workloads keep the builder's figure at once."""
+    import bench
+    _fake_rocprof(tmp_path, monkeypatch)
+    monkeypatch.setattr(bench, "_LIVE_PMC_FAILED", [])
+    monkeypatch.setenv("FAKE_ROCPROF_FAIL", "FETCH_SIZE")
+    assert "FETCH_SIZE pass" in bench.live_pmc_traffic("1400")["error"]
+    monkeypatch.delenv("FAKE_ROCPROF_FAIL")
+    assert "skipped after an earlier failed pass" in bench.live_pmc_traffic("16k")["error"]
