@@ -101,6 +101,60 @@ def test_multikey_aead_vs_oracle(gpu, family, nkeys, keylen):
         e.close()
 
 
+def test_multikey_beyond_the_counting_sort(gpu):
+    """More keys than the counting sort's LDS buckets (8191): the batch kernels' grouping falls back to hipCUB's radix
+    sort.  9000 key slots over 64 contexts (a slot's key is context k % 64, its IV its own), 20 000 records with key
+    indices over all slots and some out of range, sealed and opened against the oracle, ordered and unordered."""
+    import torch
+    rng = np.random.default_rng(9000)
+    nslots, n = 9000, 20000
+    keys, _ = sessions(rng, 64, 16)
+    engines = [ra.Engine(k) for k in keys]
+    ivs = [rng.integers(0, 256, 12, dtype=np.uint8).tobytes() for _ in range(nslots)]
+    mk = ra.MultiKey([engines[k % 64] for k in range(nslots)], ivs)
+    slot_keys = [keys[k % 64] for k in range(nslots)]
+    recs, src, aad = aead_batch(rng, n, 600)
+    kidx = rng.integers(0, nslots, n).astype(np.uint32)
+    kidx[::997] = nslots + 3  # out of range: refused
+    with kernel_family("batch", framing=False):
+        assert "_k4_mk" in ra.kernel_name_multikey(True, 16, n, False)
+        d_recs, d_src, d_aad, d_k = dev(recs.view(np.uint8)), dev(src), dev(aad), dev(kidx.view(np.int32))
+        d_ct = torch.zeros(len(src) + 16, dtype=torch.uint8, device="cuda")
+        mk.seal_batch(d_recs.data_ptr(), d_k.data_ptr(), n, d_src.data_ptr(), d_ct.data_ptr(), d_aad.data_ptr())
+        torch.cuda.synchronize()
+        got = to_cpu(d_ct)
+        ok = kidx < nslots
+        want = oracle_seal(slot_keys, ivs, np.where(ok, kidx, 0), recs, src, aad)
+        for i in np.flatnonzero(ok)[::7]:  # a seventh of the records, every slot range
+            r = recs[i]
+            a, b = int(r["dst"]), int(r["dst"]) + int(r["len"]) + 16
+            assert bytes(got[a:b]) == bytes(want[a:b]), (i, int(kidx[i]))
+        for i in np.flatnonzero(~ok):
+            r = recs[i]
+            assert not got[int(r["dst"]): int(r["dst"]) + int(r["len"]) + 16].any(), i  # seal wrote nothing
+        # open, through one by-key order shared by the launch (ptls_mi355x_order_by_key)
+        d_order = torch.zeros(n, dtype=torch.int32, device="cuda")
+        mk.order_by_key(d_k.data_ptr(), n, d_order.data_ptr())
+        d_in = dev(got)
+        d_pt = torch.zeros(len(src) + 16, dtype=torch.uint8, device="cuda")
+        d_st = torch.zeros(n, dtype=torch.int32, device="cuda")
+        mk.open_batch_ordered(d_recs.data_ptr(), d_k.data_ptr(), d_order.data_ptr(), n, d_in.data_ptr(),
+                              d_pt.data_ptr(), d_aad.data_ptr(), d_st.data_ptr())
+        torch.cuda.synchronize()
+        st, pt = to_cpu(d_st).view(np.uint32), to_cpu(d_pt)
+        order = to_cpu(d_order).view(np.uint32)
+    ks = np.where(kidx[order] < nslots, kidx[order], nslots)
+    assert (np.diff(ks.astype(np.int64)) >= 0).all() and sorted(order.tolist()) == list(range(n))
+    for i, r in enumerate(recs):
+        a, ln = int(r["dst"]), int(r["len"])
+        if not ok[i]:
+            assert st[i] == 0xFFFFFFFF, i
+        else:
+            assert st[i] == ln and bytes(pt[a:a + ln]) == bytes(src[int(r["src"]): int(r["src"]) + ln]), i
+    for e in engines:
+        e.close()
+
+
 @pytest.mark.parametrize("family", MK_FAMILIES)
 def test_multikey_seal_skips_out_of_range_keys(gpu, family):
     import torch
