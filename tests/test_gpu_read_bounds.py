@@ -310,6 +310,74 @@ def test_status_and_types_at_guard_edges(guards, family, at):
     checked()
 
 
+@pytest.mark.parametrize("family", ["split", "window16", "batch"])
+@pytest.mark.parametrize("at", ["start", "end"])
+def test_multikey_records_at_guard_edges(guards, family, at):
+    """The multi-key kernels (round 6) against the guards: eleven records of three sessions (LENS, interleaved keys),
+    back to back with their inputs, outputs and the key-index array each flush against the edge, the descriptors and
+    the statuses flush against the other; sealed, then opened separately and through a shared by-key order, every
+    byte against the oracle under its own session's key."""
+    import torch  # noqa: F401  (the device is torch's)
+    lib, gs = guards
+    IN, AUX, OUT = (Region(lib, g) for g in gs)
+    keys = [bytes((b + 17 * k) & 0xFF for b in range(16)) for k in range(3)]
+    ivs = [bytes((b + 5 * k) & 0xFF for b in range(12)) for k in range(3)]
+    engines = [ra.Engine(k) for k in keys]
+    mk = ra.MultiKey(engines, ivs)
+    other = "end" if at == "start" else "start"
+    n = len(LENS)
+    kidx = np.array([(i * 2) % 3 for i in range(n)], np.uint32)
+    pts = [xorshift64star(300 + i, ln).tobytes() for i, ln in enumerate(LENS)]
+    aad = xorshift64star(333, 13).tobytes()
+    soff = np.cumsum([0] + LENS[:-1]).astype(np.uint64)
+    coff = np.cumsum([0] + [ln + 16 for ln in LENS[:-1]]).astype(np.uint64)
+    ssize, csize = int(sum(LENS)), int(sum(LENS)) + 16 * n
+    recs = np.zeros(n, ra.RECORD_DTYPE)
+    recs["src"], recs["dst"], recs["aad"], recs["seq"], recs["len"], recs["aadlen"] = soff, coff, 0, 3 + np.arange(n), LENS, 13
+    wants = [oracle.seal(keys[int(kidx[i])], oracle.build_iv(ivs[int(kidx[i])], 3 + i), aad, p) for i, p in enumerate(pts)]
+    with kernel_family(family, framing=False):
+        for r in (IN, AUX, OUT):
+            r.clear()
+        src = IN.put(b"".join(pts), at)
+        dst = OUT.addr(csize, at)
+        d_k = AUX.put(kidx.view(np.uint8), at)
+        d_recs = AUX.put(recs.view(np.uint8), other)
+        d_aad = AUX.base + AUX.len // 2
+        assert lib.guard_h2d(d_aad, np.frombuffer(aad, np.uint8).ctypes.data, 13) == 0
+        mk.seal_batch(d_recs, d_k, n, src, dst, d_aad)
+        checked()
+        ct = OUT.get(dst, csize)
+        for i in range(n):
+            c = int(coff[i])
+            assert ct[c:c + LENS[i] + 16] == wants[i], (family, at, i)
+        # open: ciphertexts at the edge, plaintexts at the edge, statuses at the other end (the descriptors move)
+        IN.clear()
+        OUT.clear()
+        src = IN.put(ct, at)
+        dst = OUT.addr(ssize, at)
+        o = recs.copy()
+        o["src"], o["dst"] = coff, soff
+        d_o = AUX.base + AUX.len // 2 + 4096
+        assert lib.guard_h2d(d_o, o.ctypes.data, o.nbytes) == 0
+        st = AUX.addr(4 * n, other)
+        mk.open_batch(d_o, d_k, n, src, dst, d_aad, st)
+        checked()
+        assert list(np.frombuffer(AUX.get(st, 4 * n), np.uint32)) == LENS, (family, at)
+        assert OUT.get(dst, ssize) == b"".join(pts), (family, at)
+        if family == "batch":  # the by-key order flush against an edge too (the inputs' other end), read by the open
+            OUT.clear()
+            order = IN.addr(4 * n, other)
+            mk.order_by_key(d_k, n, order)
+            checked()
+            mk.open_batch_ordered(d_o, d_k, order, n, src, dst, d_aad, st)
+            checked()
+            assert list(np.frombuffer(AUX.get(st, 4 * n), np.uint32)) == LENS, (family, at, "ordered")
+            assert OUT.get(dst, ssize) == b"".join(pts), (family, at, "ordered")
+    for e in engines:
+        e.close()
+    checked()
+
+
 @pytest.mark.parametrize("at", ["start", "end"])
 def test_delivery_at_guard_edges(guards, at):
     """The delivery kernel (ptls_mi355x_tls_deliver_records, handle_input's receive loop on the device) writing each
