@@ -151,3 +151,43 @@ def test_slot_decrypt_fails_closed_on_an_injected_gpu_error(gpu):
         L.ptls_mi355x_test_inject_engine_errors(0)
         enc.free()
         dec.free()
+
+
+@pytest.mark.gpu
+def test_fault_report_describes_gpu_runtime_memory(gpu, tmp_path):
+    """On the GPU the report's address description comes from the HSA runtime (hsa_amd_pointer_info): device memory
+    and pinned host memory (hipHostMalloc) are the runtime's allocations with their extents; a range the record layer
+    registered (hipHostRegister) is NOT in the runtime's allocation map on this stack -- HIP maps it through the kernel
+    driver's shared-virtual-memory ranges, device address = host address -- so the report's record-layer table is what
+    names it; a plain heap array is unknown to the runtime and named by its /proc/self/maps line."""
+    import numpy as np
+    import torch
+    log = str(tmp_path / "fault.log")
+    d = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda")
+    pinned = torch.zeros(1 << 20, dtype=torch.uint8, pin_memory=True)
+    raw = np.zeros((4 << 20) + 4096, np.uint8)
+    off = (-raw.ctypes.data) % 4096
+    reg = raw[off:off + (4 << 20)]
+    heap = np.zeros(1 << 20, np.uint8)
+    rl = ra.RecordLayer(bytes(16), bytes(12))
+    rl.register(reg)
+    _with_report_path(log)
+    try:
+        for p in (d.data_ptr() + 4096, pinned.data_ptr() + 4096, reg.ctypes.data + 8192, heap.ctypes.data + 4096):
+            ra.fault_journal_report(p, 0x1)
+        text = open(log).read()
+    finally:
+        _with_report_path(os.environ["RAPIDO_FAULT_LOG"])
+        rl.unregister(reg)
+        rl.close()
+    reports = text.split("=== end of fault journal ===")[:4]
+    first = [next(ln for ln in r.splitlines() if "fault VA" in ln) for r in reports]
+    assert "HSA allocation" in first[0], first[0]
+    assert "HSA allocation" in first[1] or "locked" in first[1], first[1]
+    assert "unknown to the runtime" in first[2] or "locked host range" in first[2], first[2]
+    assert "unknown to the runtime" in first[3], first[3]
+    held = [ln.strip() for ln in reports[2].splitlines() if "HOLDS THE FAULTING ADDRESS" in ln]
+    # the record layer's registration table names it (and the journal's registration event)
+    assert any(ln.startswith("host ") and "+ 4194304" in ln for ln in held), reports[2]
+    assert "[heap]" in reports[3] or "maps: " in reports[3]
+    assert ra.fault_journal_faults() == 0  # reports on request are not faults
