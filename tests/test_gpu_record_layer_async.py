@@ -639,3 +639,58 @@ def test_reserved_layer_across_a_rekey(gpu, transport):
         for o, want in zip(outs, wants):
             assert o[:len(want)].tobytes() == want
     tx.close()
+
+
+@pytest.mark.parametrize("transport", ["direct", "zero_copy"])
+def test_sessions_in_one_async_launch(gpu, transport):
+    """Round 6: the windows of three sessions (each its own key and IV) in one asynchronous launch each way.  Sealed
+    bytes per session against the oracle; on the receive side session B's window stops at a bad record (alert 20, its
+    next window in the following launch completes STALE) while sessions A and C deliver in both launches; a session
+    layer named by an in-flight launch cannot be rekeyed."""
+    rng = np.random.default_rng(606)
+    keys = [rng.integers(0, 256, 16, dtype=np.uint8).tobytes() for _ in range(3)]
+    ivs = [rng.integers(0, 256, 12, dtype=np.uint8).tobytes() for _ in range(3)]
+    seqs = [5, 70, 0]
+    tx = [ra.RecordLayer(k, v, seq=s) for k, v, s in zip(keys, ivs, seqs)]
+    rx = [ra.RecordLayer(k, v, seq=s) for k, v, s in zip(keys, ivs, seqs)]
+    h = Host(transport, tx + rx, 1 << 22)
+    frags = [[[rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in (16384, 1400, 3, 9000)] for _ in range(3)]
+             for _ in range(2)]  # [launch][session] -> fragments
+    # seal: two launches of one window per session, both in flight
+    tickets = []
+    for L in range(2):
+        wins = [[h.take(len(f), f) for f in frags[L][s]] for s in range(3)]
+        outs = [h.take(sum(len(f) + ra.TLS_OVERHEAD for f in frags[L][s])) for s in range(3)]
+        tickets.append((ra.record_layer_seal_submit_multi(tx, wins, outs), outs))
+    with pytest.raises(RuntimeError):
+        tx[2].rekey(keys[2], ivs[2])  # named by a launch in flight
+    wires, run = [[None] * 3 for _ in range(2)], list(seqs)
+    for L, (t, outs) in enumerate(tickets):
+        res = tx[0].wait_multi(t, 3)
+        for s in range(3):
+            want, run[s] = oracle_window(keys[s], ivs[s], run[s], frags[L][s])
+            assert res[s][:2] == (len(want), 4) and outs[s][:len(want)].tobytes() == want, (L, s)
+            wires[L][s] = want
+    assert [t.seq for t in tx] == run
+    # open: session B's first window has a bad ciphertext byte in its third record
+    bad = bytearray(wires[0][1])
+    third = len(frags[0][1][0]) + len(frags[0][1][1]) + 2 * ra.TLS_OVERHEAD
+    bad[third + 9] ^= 4
+    tickets = []
+    for L in range(2):
+        ws = [bytes(bad) if (L, s) == (0, 1) else wires[L][s] for s in range(3)]
+        ins = [h.take(len(w), w) for w in ws]
+        outs = [h.take(len(w)) for w in ws]
+        tickets.append((ra.record_layer_open_submit_multi(rx, ins, outs)[0], outs))
+    r0 = rx[0].wait_multi(tickets[0][0], 3)
+    r1 = rx[0].wait_multi(tickets[1][0], 3)
+    for s in (0, 2):
+        for L, r in ((0, r0), (1, r1)):
+            n = sum(map(len, frags[L][s]))
+            assert r[s][:2] == (n, 4) and r[s][3] == 0 and tickets[L][1][s][:n].tobytes() == b"".join(frags[L][s])
+    assert r0[1][1] == 2 and r0[1][3] == 20  # two records delivered, then BAD_RECORD_MAC
+    assert tickets[0][1][1][:r0[1][0]].tobytes() == b"".join(frags[0][1][:2])
+    assert r1[1] == (0, 0, 0, ra.RECORD_LAYER_STALE)
+    assert rx[1].seq == seqs[1] + 2 and rx[0].seq == seqs[0] + 8 and rx[2].seq == seqs[2] + 8
+    for rl in tx + rx:
+        rl.close()
