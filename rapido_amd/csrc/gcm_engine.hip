@@ -1748,6 +1748,31 @@ extern "C" __global__ void mi355x_mk_keys(const uint32_t *__restrict__ key_idx, 
  */
 constexpr uint32_t MK_LDS_BUCKETS = 8192, MK_PER_BLOCK = 4096;
 
+/*
+ * A wave's LDS counter adds.  Same-address LDS atomics of a wave serialise, so a wave whose lanes all carry one key (a
+ * batch of one session, or a session's contiguous run) takes one atomic for the whole wave; any other wave one atomic
+ * per lane, as before (measured: serving the lanes key by key with ballots costs more than the LDS's own serialisation
+ * once a wave holds two or more keys, profiles/r06x_mk_prep.txt).  Returns the counter's value before the lane's unit
+ * (its slot in the key's run).  Called by the whole wave (uniform trip counts).
+ */
+__device__ __forceinline__ uint32_t mk_lds_add(uint32_t *h, uint32_t k, bool valid)
+{
+    const uint64_t act = __ballot(valid);
+    if (act == 0ull)
+        return 0u;
+    const int src = __builtin_ctzll(act);
+    const uint32_t k0 = (uint32_t)__shfl((int)k, src, 64);
+    if (__ballot(valid && k == k0) == act) { /* one key in the wave: one atomic */
+        const uint32_t lane = __lane_id();
+        uint32_t base = 0u;
+        if (lane == (uint32_t)src)
+            base = atomicAdd(&h[k0], (uint32_t)__popcll(act));
+        base = (uint32_t)__shfl((int)base, src, 64);
+        return base + (uint32_t)__popcll(act & ((1ull << lane) - 1ull));
+    }
+    return valid ? atomicAdd(&h[k], 1u) : 0u;
+}
+
 extern "C" __global__ __launch_bounds__(1024) void mi355x_mk_count(const uint32_t *__restrict__ key_idx, uint32_t n,
                                                                    uint32_t nkeys, uint32_t *__restrict__ counts)
 {
@@ -1757,9 +1782,11 @@ extern "C" __global__ __launch_bounds__(1024) void mi355x_mk_count(const uint32_
         h[b] = 0u;
     __syncthreads();
     const uint32_t i0 = blockIdx.x * MK_PER_BLOCK, i1 = min(n, i0 + MK_PER_BLOCK);
-    for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-        const uint32_t k = key_idx[i];
-        atomicAdd(&h[k < nkeys ? k : nkeys], 1u);
+    for (uint32_t b0 = i0; b0 < i1; b0 += blockDim.x) { /* uniform over the block: every wave calls mk_lds_add */
+        const uint32_t i = b0 + threadIdx.x;
+        const bool valid = i < i1;
+        const uint32_t k = valid ? key_idx[i] : 0u;
+        (void)mk_lds_add(h, k < nkeys ? k : nkeys, valid);
     }
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x)
@@ -1777,18 +1804,24 @@ extern "C" __global__ __launch_bounds__(1024) void mi355x_mk_scatter(const uint3
         h[b] = 0u;
     __syncthreads();
     const uint32_t i0 = blockIdx.x * MK_PER_BLOCK, i1 = min(n, i0 + MK_PER_BLOCK);
-    for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-        const uint32_t k = key_idx[i];
-        atomicAdd(&h[k < nkeys ? k : nkeys], 1u);
+    for (uint32_t b0 = i0; b0 < i1; b0 += blockDim.x) {
+        const uint32_t i = b0 + threadIdx.x;
+        const bool valid = i < i1;
+        const uint32_t k = valid ? key_idx[i] : 0u;
+        (void)mk_lds_add(h, k < nkeys ? k : nkeys, valid);
     }
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) /* this block's run of key b: one global atomic */
         if (h[b] != 0u)
             h[b] = atomicAdd(cursor + b, h[b]);
     __syncthreads();
-    for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-        const uint32_t k = key_idx[i];
-        order[atomicAdd(&h[k < nkeys ? k : nkeys], 1u)] = i;
+    for (uint32_t b0 = i0; b0 < i1; b0 += blockDim.x) {
+        const uint32_t i = b0 + threadIdx.x;
+        const bool valid = i < i1;
+        const uint32_t k = valid ? key_idx[i] : 0u;
+        const uint32_t pos = mk_lds_add(h, k < nkeys ? k : nkeys, valid);
+        if (valid)
+            order[pos] = i;
     }
 }
 
@@ -1833,6 +1866,53 @@ extern "C" __global__ void mi355x_mk_bounds(const uint32_t *__restrict__ sorted,
         keys[k].first = i;
     if (i + 1u == n || mk_sorted_key(sorted, key_idx, order, i + 1u, nkeys) != k)
         keys[k].end = i + 1u;
+}
+
+/*
+ * mi355x_mk_reset + mi355x_mk_bounds in one pass (up to MK_LDS_BUCKETS - 1 keys, so a thread's run of empty keys is
+ * short): in the sorted order, the record where a new key starts also writes the ranges of the keys skipped since the
+ * previous record's key (empty: first = end = i), the last record those above its key (first = end = n), and threads
+ * below nkeys zero the group counters.  One launch fewer per multi-key call.
+ */
+extern "C" __global__ void mi355x_mk_bounds_all(const uint32_t *__restrict__ key_idx, const uint32_t *__restrict__ order,
+                                                uint32_t n, uint32_t nkeys, MkKey *__restrict__ keys,
+                                                uint32_t *__restrict__ ctr, uint32_t *__restrict__ st,
+                                                uint8_t *__restrict__ types, uint32_t frame)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x, lane = __lane_id();
+    if (i < nkeys)
+        ctr[i] = 0u;
+    /* each record's key gathered once (key_idx[order[i]]); its neighbours' from the adjacent lanes, a wave's two edge
+     * lanes gathering their own (every lane takes part in the shuffles) */
+    const uint32_t k = i < n ? mk_sorted_key(nullptr, key_idx, order, i, nkeys) : nkeys;
+    uint32_t kp = (uint32_t)__shfl_up((int)k, 1, 64), kn = (uint32_t)__shfl_down((int)k, 1, 64);
+    if (i >= n)
+        return;
+    if (lane == 0u && i != 0u)
+        kp = mk_sorted_key(nullptr, key_idx, order, i - 1u, nkeys);
+    if (lane == 63u && i + 1u < n)
+        kn = mk_sorted_key(nullptr, key_idx, order, i + 1u, nkeys);
+    if (i == 0u || k != kp) {
+        for (uint32_t e = i == 0u ? 0u : kp + 1u; e < k && e < nkeys; ++e) { /* keys with no record */
+            keys[e].first = i;
+            keys[e].end = i;
+        }
+        if (k < nkeys)
+            keys[k].first = i;
+    }
+    if (k >= nkeys) {
+        if (frame)
+            mk_reject<true>(order[i], st, types);
+        else
+            mk_reject<false>(order[i], st, types);
+    } else if (i + 1u == n || kn != k) {
+        keys[k].end = i + 1u;
+    }
+    if (i + 1u == n)
+        for (uint32_t e = k + 1u; e < nkeys; ++e) { /* keys above the last record's */
+            keys[e].first = n;
+            keys[e].end = n;
+        }
 }
 
 /* stop-at-failure segments of a multi-key open: a connection is (key, connection id) */
@@ -3103,11 +3183,19 @@ static int launch_multikey(ptls_mi355x_aesgcm_context_t *const *ctxs, const void
     } else { /* the caller's order (ptls_mi355x_order_by_key), e.g. shared by a batch's seal and open */
         order = (uint32_t *)given_order;
     }
-    hipLaunchKernelGGL(mi355x_mk_reset, dim3(gk), dim3(256), 0, stream, tab, (uint32_t)nkeys, ctr);
-    HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(mi355x_mk_bounds, dim3(g), dim3(256), 0, stream, nullptr, key_idx, order, (uint32_t)n,
-                       (uint32_t)nkeys, tab, seal ? nullptr : status, seal ? nullptr : types, frame ? 1u : 0u);
-    HIPCHK(hipGetLastError());
+    if (nkeys + 1 <= MK_LDS_BUCKETS) { /* ranges and counters in one launch (mi355x_mk_bounds_all) */
+        const size_t th = n > nkeys ? n : nkeys;
+        hipLaunchKernelGGL(mi355x_mk_bounds_all, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, stream, key_idx, order,
+                           (uint32_t)n, (uint32_t)nkeys, tab, ctr, seal ? nullptr : status, seal ? nullptr : types,
+                           frame ? 1u : 0u);
+        HIPCHK(hipGetLastError());
+    } else {
+        hipLaunchKernelGGL(mi355x_mk_reset, dim3(gk), dim3(256), 0, stream, tab, (uint32_t)nkeys, ctr);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(mi355x_mk_bounds, dim3(g), dim3(256), 0, stream, nullptr, key_idx, order, (uint32_t)n,
+                           (uint32_t)nkeys, tab, seal ? nullptr : status, seal ? nullptr : types, frame ? 1u : 0u);
+        HIPCHK(hipGetLastError());
+    }
     /* groups: at most n / 16 + nkeys (each key's last group partial); a CU's worth of waves per workgroup */
     const uint64_t groups = n / 16 + nkeys, blocks = (groups + 15) / 16;
     const uint32_t nb = (uint32_t)(blocks < grid ? blocks : grid);
