@@ -760,7 +760,7 @@ def e2e_pcie(ra, extra, dev, steps):
     sh = extra["stream"].cuda_stream
     h_src = torch.empty(extra["src_bytes"], dtype=torch.uint8, pin_memory=True)
     h_dst = torch.empty(extra["src_bytes"], dtype=torch.uint8, pin_memory=True)
-    h_src.copy_(d_src.cpu())
+    h_src.copy_(d_src)  # device -> pinned: no pageable intermediate (rapido_amd/hostmem.py)
     torch.cuda.synchronize(dev)
     reps = max(2, steps // 4)
     t0 = time.perf_counter()
@@ -796,7 +796,7 @@ def e2e_pcie(ra, extra, dev, steps):
         pipelined()
     torch.cuda.synchronize(dev)
     piped = (time.perf_counter() - t0) / reps
-    if not torch.equal(h_dst[: int(ends[-1])], d_ct[: int(ends[-1])].cpu()):
+    if not torch.equal(h_dst[: int(ends[-1])].to(dev), d_ct[: int(ends[-1])]):  # compared on the device (pinned H2D)
         raise SystemExit("bench: pipelined PCIe seal differs from the device-resident seal -- results invalid")
     # the receive side: the sealed records (h_dst) in, opened, plaintexts and statuses back into pinned host memory
     d_pt, d_st = extra["d_pt"], extra["d_st"]
